@@ -1,0 +1,158 @@
+"""Benchmark: agent-steps/s of the batched quadrotor-swarm control step on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config, fits one GPU):
+MultiHover, 8 drones, 16 384 envs per GPU, ActionType.ONE_D_PID (learn_mappo.py
+default), Physics.DYN, fp32, synthetic random-policy rollout (Philox U(-1,1)
+actions drawn in-kernel), obs written into an on-device rollout
+buffer slot each step.  A "step" = one control step of every env on the rank
+(one fused HIP launch: action→PID→8 substeps→obs/reward/done/auto-reset).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+envs are sharded (weak scaling, 16 384 envs per rank, global env ids offset by
+rank) with no data-path collective; value = all ranks' agent-steps ÷ max-over-
+ranks wall time.
+
+Extra JSON fields:
+  roofline      the step kernel: §8(d) algorithmic bytes per agent-step (418 B,
+                C3 ONE_D_PID) × agents per launch ÷ mean launch time from HIP
+                events on the launch stream, vs 8 TB/s.
+  cpu_baseline  the oracle (C++ CPU restatement of the reference semantics,
+                fp64 like the reference) on 176 envs (README's 22-worker
+                topology) timed on this host, rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "marl-gym-pybullet-drones_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from gym_pybullet_drones_amd.envs.swarm import grid_layout  # noqa: E402
+
+METRIC = "agent-steps/sec, MultiHover 8-drone MAPPO @ 1/2/4/8 GPU vs PyBullet CPU"
+BYTES_PER_AGENT_STEP = {"one_d_pid": 418.0, "vel": 790.0, "rpm": 720.0}
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--envs", type=int, default=16384, help="envs per GPU")
+    p.add_argument("--drones", type=int, default=8)
+    p.add_argument("--act", default="one_d_pid")
+    p.add_argument("--slots", type=int, default=32, help="rollout-buffer slots the obs ring cycles through")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import qs_oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 22, os.cpu_count() or 1))
+    E = 176   # README.md:38-39: 176 envs on 22 workers
+    sim = qs_oracle.OracleSim(task="multihover", num_envs=E, num_drones=args.drones, act=args.act, precision=8,
+                              initial_xyzs=grid_layout(args.drones) if args.drones >= 6 else None)
+    sim.reset(0)
+    t0 = time.perf_counter()
+    sim.run_random(5, threads)
+    dt = time.perf_counter() - t0
+    steps = max(10, int(seconds / max(dt / 5, 1e-6)))
+    t0 = time.perf_counter()
+    sim.run_random(steps, threads)
+    dt = time.perf_counter() - t0
+    sim.close()
+    return {"value": E * args.drones * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {E} envs x "
+                      f"{args.drones} drones x {steps} random-policy ctrl steps, OpenMP {threads} threads, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from gym_pybullet_drones_amd.envs import QuadSwarm
+    E, D = args.envs, args.drones
+    sw = QuadSwarm("multihover", num_envs=E, num_drones=D, act=args.act, precision=4,
+                   initial_xyzs=grid_layout(D) if D >= 6 else None, env_offset=rank * E)
+    O, A = sw.obs_dim, sw.act_dim
+    obs_buf = torch.empty((args.slots, E, D, O), dtype=torch.float32, device=sw.device)
+    act_buf = torch.empty((args.slots, E, D, A), dtype=torch.float32, device=sw.device)
+    rew_buf = torch.empty((args.slots, E), dtype=torch.float32, device=sw.device)
+    te_buf = torch.empty((args.slots, E), dtype=torch.uint8, device=sw.device)
+    tr_buf = torch.empty((args.slots, E), dtype=torch.uint8, device=sw.device)
+    sw.reset(0, obs=obs_buf[0])
+
+    def step(t):
+        k = t % args.slots
+        sw.step(None, obs=obs_buf[k], reward=rew_buf[k], terminated=te_buf[k], truncated=tr_buf[k],
+                actions_out=act_buf[k])
+
+    for t in range(args.warmup):
+        step(t)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        ev[t][0].record(stream)
+        step(args.warmup + t)
+        ev[t][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed], device=sw.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    agents_total = E * D * world
+    value = agents_total * args.steps / elapsed
+    nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    assert sw.reset_error() == 0
+    assert torch.isfinite(obs_buf[:min(args.slots, args.steps)]).all()
+    if rank == 0:
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"MultiHover {D}-drone x {E} envs/GPU, ActionType.{args.act.upper()}, "
+                                   "Physics.DYN, random-policy rollout (C3 env config; MAPPO learner not in "
+                                   "the timed step)",
+                       "envs_per_gpu": E, "drones": D, "total_envs": E * world, "act": args.act,
+                       "physics": "dyn", "parallelism": f"env-shard x{world}", "precision": "fp32"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel_ms": kern_ms, "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    sw.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

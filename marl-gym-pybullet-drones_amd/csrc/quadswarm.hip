@@ -1,0 +1,972 @@
+// quadswarm.hip — MI355X (gfx950) batched quadrotor-swarm control step.
+//
+// One launch advances every (env, drone) of a shard by one control step:
+// action → RPM (incl. the DSL PID), PYB_STEPS_PER_CTRL rigid-body substeps,
+// readback, MultiHover/Spiral obs + reward + termination, and the vec-env
+// auto-reset.  It replaces BaseAviary.step (BaseAviary.py:259-383) driven by
+// SubprocVecEnv workers (subproc_vec_env.py:188-206); see include/quadswarm.h
+// for the per-entry-point reference mapping.
+//
+// Layout (DESIGN.md §HBM layout): per-agent state is structure-of-arrays
+// [field][N] (N = E*D, agent a = env*D + drone) so lane i of a wavefront
+// touches element i of every field — every state load/store is a fully
+// coalesced 256 B (fp32) wave access.  A workgroup owns whole envs
+// (EPB = floor(256/D) envs × D drones), so the per-env reductions (reward
+// mean, any-terminated), the O(D²) downwash neighbour scan and the reset
+// rejection search all run through LDS with no inter-workgroup traffic.
+// The path is elementwise ODE + a small PID: no contraction, so no MFMA; the
+// bound is HBM bandwidth.
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstring>
+#include <cmath>
+#include <string>
+#include <vector>
+#include <new>
+
+#include "quadswarm.h"
+
+namespace qs {
+
+constexpr int kBlock = 256;          // threads per workgroup (4 waves)
+constexpr uint32_t kMaxResetTries = 1u << 24;
+enum { STREAM_ACT = 1, STREAM_RESET = 2 };
+enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
+
+// ---------------------------------------------------------------- math utils
+template <class T> struct M;
+template <> struct M<float> {
+  __device__ static float sqrt_(float x) { return sqrtf(x); }
+  __device__ static float sin_(float x) { return sinf(x); }
+  __device__ static float cos_(float x) { return cosf(x); }
+  __device__ static float atan2_(float y, float x) { return atan2f(y, x); }
+  __device__ static float asin_(float x) { return asinf(x); }
+  __device__ static float exp_(float x) { return expf(x); }
+  __device__ static float abs_(float x) { return fabsf(x); }
+  __device__ static float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+  __device__ static float add_rn(float a, float b) { return __fadd_rn(a, b); }
+  __device__ static float sub_rn(float a, float b) { return __fsub_rn(a, b); }
+};
+template <> struct M<double> {
+  __device__ static double sqrt_(double x) { return sqrt(x); }
+  __device__ static double sin_(double x) { return sin(x); }
+  __device__ static double cos_(double x) { return cos(x); }
+  __device__ static double atan2_(double y, double x) { return atan2(y, x); }
+  __device__ static double asin_(double x) { return asin(x); }
+  __device__ static double exp_(double x) { return exp(x); }
+  __device__ static double abs_(double x) { return fabs(x); }
+  __device__ static double mul_rn(double a, double b) { return __dmul_rn(a, b); }
+  __device__ static double add_rn(double a, double b) { return __dadd_rn(a, b); }
+  __device__ static double sub_rn(double a, double b) { return __dsub_rn(a, b); }
+};
+
+template <class T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// Philox4x32-10 (Random123).  Same stream definition as the oracle.
+struct U4 { uint32_t x, y, z, w; };
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+  }
+  return c;
+}
+// 24-bit uniform in [0,1), exact in float and double.
+template <class T> __device__ __forceinline__ T u01(uint32_t x) { return T(x >> 8) * T(1.0 / 16777216.0); }
+
+// -------------------------------------------------------------- parameters
+template <class T> struct Params {
+  // sizes
+  int E, D, N, A, O, H, S, EPB;
+  int task, act_type, mode;
+  uint32_t aux, flags;
+  int pyb_freq;
+  double ep_len_sec;
+  uint32_t k0, k1;
+  long long env_offset;
+  // physics constants (BaseAviary.py:117-128, cf2x.urdf)
+  T dt, ctrl_dt, KF, KM, M, GRAVITY, Jd0, Jd1, Jd2, Ji0, Ji1, Ji2, L_SQRT2, HOVER_RPM, SPEED_LIMIT, G_PID;
+  T DRAG0, DRAG1, DRAG2, GND_COEFF, PROP_R, GND_CLIP, DW1, DW2, DW3;
+  T sp_R, sp_OMEGA, sp_VZ, sp_cx, sp_cy, sp_cz;
+  // device buffers
+  T* st;                  // [QS_AGENT_FIELDS][N]
+  int32_t* env;           // [QS_ENV_FIELDS][E]
+  float* hist;            // [H][N][A]
+  double* ep_return;      // [E]
+  const T* orig_xyz;      // [D][3]
+  qs_episode_rec* log;    // [log_cap]
+  unsigned long long* log_count;
+  long long log_cap;
+  int* err;               // [1] reset search overflow flag
+  // per-step I/O
+  const uint8_t* reset_mask;   // MODE_RESET_MASK: [E] or NULL (= all)
+  const float* act_in;
+  float* obs;
+  T* rew;
+  uint8_t* term;
+  uint8_t* trunc;
+  float* tobs;
+  uint8_t* reasons;
+  float* act_out;
+};
+
+// ---------------------------------------------------- conversions (external)
+// pybullet getMatrixFromQuaternion = btMatrix3x3::setRotation (s = 2/|q|²).
+template <class T> __device__ __forceinline__ void quat_to_rot(const T q[4], T R[9]) {
+  T x = q[0], y = q[1], z = q[2], w = q[3];
+  T d = x * x + y * y + z * z + w * w;
+  T s = T(2) / d;
+  T xs = x * s, ys = y * s, zs = z * s;
+  T wx = w * xs, wy = w * ys, wz = w * zs;
+  T xx = x * xs, xy = x * ys, xz = x * zs;
+  T yy = y * ys, yz = y * zs, zz = z * zs;
+  R[0] = T(1) - (yy + zz); R[1] = xy - wz; R[2] = xz + wy;
+  R[3] = xy + wz; R[4] = T(1) - (xx + zz); R[5] = yz - wx;
+  R[6] = xz - wy; R[7] = yz + wx; R[8] = T(1) - (xx + yy);
+}
+// pybullet getEulerFromQuaternion.
+template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T rpy[3]) {
+  using F = M<T>;
+  T sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
+  T sarg = T(-2) * (q[0] * q[2] - q[3] * q[1]);
+  if (sarg <= T(-0.99999)) {
+    rpy[0] = 0; rpy[1] = T(-0.5 * M_PI); rpy[2] = T(2) * F::atan2_(q[0], -q[1]);
+  } else if (sarg >= T(0.99999)) {
+    rpy[0] = 0; rpy[1] = T(0.5 * M_PI); rpy[2] = T(2) * F::atan2_(-q[0], q[1]);
+  } else {
+    rpy[0] = F::atan2_(T(2) * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+    rpy[1] = F::asin_(sarg);
+    rpy[2] = F::atan2_(T(2) * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+  }
+}
+
+// ------------------------------------------------------------ DSL PID
+// DSLPIDControl.computeControl (DSLPIDControl.py:82-259), one drone.
+// pid: int_pos[3], int_rpy[3], last_rpy[3] (updated in place).
+template <class T>
+__device__ void dsl_pid(const Params<T>& P, T pid[9], const T pos[3], const T q[4], const T vel[3],
+                        const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
+  using F = M<T>;
+  const T dt = P.ctrl_dt;
+  T R[9];
+  quat_to_rot(q, R);
+  T pe[3], ve[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { pe[i] = tpos[i] - pos[i]; ve[i] = tvel[i] - vel[i]; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pid[i] = clampv(pid[i] + pe[i] * dt, T(-2), T(2));
+  pid[2] = clampv(pid[2], T(-0.15), T(0.15));
+  const T PF[3] = {T(.4), T(.4), T(1.25)}, IF[3] = {T(.05), T(.05), T(.05)}, DF[3] = {T(.2), T(.2), T(.5)};
+  T tt[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tt[i] = PF[i] * pe[i] + IF[i] * pid[i] + DF[i] * ve[i];
+  tt[2] += P.G_PID;
+  T st = tt[0] * R[2] + tt[1] * R[5] + tt[2] * R[8];
+  st = st > T(0) ? st : T(0);
+  T thrust = (F::sqrt_(st / (T(4) * P.KF)) - T(4070.3)) / T(0.2685);
+  T inv = T(1) / F::sqrt_(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+  T z[3] = {tt[0] * inv, tt[1] * inv, tt[2] * inv};
+  T xc0 = F::cos_(tyaw), xc1 = F::sin_(tyaw);
+  // y = (z × x_c)/|z × x_c| with x_c = (xc0, xc1, 0)
+  T y[3] = {-z[2] * xc1, z[2] * xc0, z[0] * xc1 - z[1] * xc0};
+  T yi = T(1) / F::sqrt_(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
+  y[0] *= yi; y[1] *= yi; y[2] *= yi;
+  T x[3] = {y[1] * z[2] - y[2] * z[1], y[2] * z[0] - y[0] * z[2], y[0] * z[1] - y[1] * z[0]};
+  // target_rotation columns x,y,z (scipy XYZ round trip = identity on SO(3)).
+  // rot_e = vee(Rt^T R - R^T Rt)
+  const T* Rt0 = x; const T* Rt1 = y; const T* Rt2 = z;   // columns
+  auto Rt = [&](int i, int j) -> T { return j == 0 ? Rt0[i] : (j == 1 ? Rt1[i] : Rt2[i]); };
+  auto E = [&](int i, int j) -> T {
+    T a = Rt(0, i) * R[0 * 3 + j] + Rt(1, i) * R[1 * 3 + j] + Rt(2, i) * R[2 * 3 + j];
+    T b = R[0 * 3 + i] * Rt(0, j) + R[1 * 3 + i] * Rt(1, j) + R[2 * 3 + i] * Rt(2, j);
+    return a - b;
+  };
+  T rot_e[3] = {E(2, 1), E(0, 2), E(1, 0)};
+  T rpy[3];
+  quat_to_rpy(q, rpy);
+  T rate_e[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { rate_e[i] = T(0) - (rpy[i] - pid[6 + i]) / dt; pid[6 + i] = rpy[i]; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pid[3 + i] = clampv(pid[3 + i] - rot_e[i] * dt, T(-1500), T(1500));
+  pid[3] = clampv(pid[3], T(-1), T(1));
+  pid[4] = clampv(pid[4], T(-1), T(1));
+  const T PT[3] = {T(70000.), T(70000.), T(60000.)}, IT[3] = {T(0), T(0), T(500.)}, DT[3] = {T(20000.), T(20000.), T(12000.)};
+  T tq[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tq[i] = clampv(-PT[i] * rot_e[i] + DT[i] * rate_e[i] + IT[i] * pid[3 + i], T(-3200), T(3200));
+  // CF2X mixer (DSLPIDControl.py:48-53)
+  const T MX[4][3] = {{T(-.5), T(-.5), T(-1)}, {T(-.5), T(.5), T(1)}, {T(.5), T(.5), T(-1)}, {T(.5), T(-.5), T(1)}};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    T pwm = thrust + (MX[m][0] * tq[0] + MX[m][1] * tq[1] + MX[m][2] * tq[2]);
+    pwm = clampv(pwm, T(20000), T(65535));
+    rpm[m] = T(0.2685) * pwm + T(4070.3);
+  }
+}
+
+// --------------------------------------------------- LDS workspace layout
+template <class T> struct Shared {
+  T cand[kBlock][3];        // reset candidates / downwash snapshot positions
+  T rew[kBlock];            // per-drone reward terms
+  uint8_t bits[kBlock];     // per-drone termination reason bits
+  int reject[kBlock];       // per-group rejection flag (reset search)
+  int done[kBlock];         // per-env done flag (EPB <= kBlock)
+  int need[kBlock];         // per-env: still searching
+  uint32_t win_try[kBlock]; // per-env winning try index
+  int win_group;
+  int any;
+  uint32_t ep_bcast;
+};
+
+// Reset search (MultiHoverAviary.reset rejection loop, MH:83-102), group g
+// (= threads g*D .. g*D+D-1) evaluates `try_idx` for local env `lenv`.
+// Writes cand positions for its group and returns (via s.reject[g]).
+template <class T>
+__device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, int lenv, uint32_t try_idx,
+                               uint32_t genv, uint32_t episode, bool active) {
+  using F = M<T>;
+  const int tid = threadIdx.x;
+  if (active) {
+    U4 r = philox(U4{try_idx, genv, episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
+    T n0 = T(0.5) * u01<T>(r.x) - T(0.25), n1 = T(0.5) * u01<T>(r.y) - T(0.25), n2 = T(0.5) * u01<T>(r.z) - T(0.25);
+    T px = F::add_rn(P.orig_xyz[d * 3 + 0], n0);
+    T py = F::add_rn(P.orig_xyz[d * 3 + 1], n1);
+    T pz = F::add_rn(P.orig_xyz[d * 3 + 2], n2);
+    pz = clampv(pz, T(0.1), T(1.0));
+    s.cand[tid][0] = px; s.cand[tid][1] = py; s.cand[tid][2] = pz;
+  }
+  __syncthreads();
+  if (active) {
+    const int base = g * P.D;
+    T px = s.cand[tid][0], py = s.cand[tid][1], pz = s.cand[tid][2];
+    bool bad = pz < T(0.1);
+    for (int j = d + 1; j < P.D; ++j) {
+      T dx = F::sub_rn(px, s.cand[base + j][0]);
+      T dy = F::sub_rn(py, s.cand[base + j][1]);
+      T dz = F::sub_rn(pz, s.cand[base + j][2]);
+      T ss = F::add_rn(F::add_rn(F::mul_rn(dx, dx), F::mul_rn(dy, dy)), F::mul_rn(dz, dz));
+      if (F::sqrt_(ss) < T(0.5)) bad = true;
+    }
+    if (bad) s.reject[g] = 1;
+  }
+  __syncthreads();
+  (void)lenv;
+}
+
+// ---------------------------------------------------------------- the step
+template <class T>
+__global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
+  using F = M<T>;
+  __shared__ Shared<T> s;
+  const int tid = threadIdx.x;
+  const int D = P.D, N = P.N;
+  const int lenv = tid / D, d = tid - lenv * D;
+  const int e = blockIdx.x * P.EPB + lenv;
+  const bool valid = (lenv < P.EPB) && (e < P.E);
+  const int a = e * D + d;
+  const uint32_t genv = (uint32_t)(P.env_offset + e);
+
+  // ---------------- load state
+  T pos[3] = {0, 0, 0}, q[4] = {0, 0, 0, 1}, vel[3] = {0, 0, 0}, w[3] = {0, 0, 0}, lrpm[4] = {0, 0, 0, 0};
+  T pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
+  int32_t step_counter = 0, episode = 0, total = 0, ep_len = 0;
+  const bool has_pid = P.act_type == QS_ACT_PID || P.act_type == QS_ACT_VEL || P.act_type == QS_ACT_ONE_D_PID;
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pos[i] = P.st[(QS_F_POS + i) * N + a];
+      vel[i] = P.st[(QS_F_VEL + i) * N + a];
+      w[i] = P.st[(QS_F_RPY_RATES + i) * N + a];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = P.st[(QS_F_QUAT + i) * N + a];
+    if (P.aux & QS_AUX_DRAG) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lrpm[i] = P.st[(QS_F_LAST_RPM + i) * N + a];
+    }
+    if (has_pid) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) pid[i] = P.st[(QS_F_PID_INT_POS + i) * N + a];
+    }
+    if (P.task == QS_TASK_MULTIHOVER) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) tgt[i] = P.st[(QS_F_TARGET + i) * N + a];
+    }
+    step_counter = P.env[QS_E_STEP_COUNTER * P.E + e];
+    episode = P.env[QS_E_EPISODE * P.E + e];
+    total = P.env[QS_E_TOTAL_STEPS * P.E + e];
+    ep_len = P.env[QS_E_EP_LEN * P.E + e];
+  }
+  const int A = P.A, H = P.H, O = P.O;
+  T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
+  bool done_env = false;
+  int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
+  uint8_t bits = 0;
+  T rterm = 0;
+
+  if (P.mode == MODE_STEP) {
+    // ---------------- action (trainer-provided or synthetic random policy)
+    float act[4] = {0, 0, 0, 0};
+    if (valid) {
+      if (P.act_in) {
+        for (int k = 0; k < A; ++k) act[k] = P.act_in[(size_t)a * A + k];
+      } else {
+        U4 r = philox(U4{(uint32_t)total, genv, 0u, (uint32_t)((STREAM_ACT << 24) | d)}, P.k0, P.k1);
+        const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+        for (int k = 0; k < A; ++k) act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
+      }
+      if (P.act_out)
+        for (int k = 0; k < A; ++k) P.act_out[(size_t)a * A + k] = act[k];
+      // action_buffer.append(action) (BaseRLAviary.py:187): ring slot total % H
+      const int slot = total % H;
+      for (int k = 0; k < A; ++k) P.hist[((size_t)slot * N + a) * A + k] = act[k];
+    }
+    // ---------------- _preprocessAction (BaseRLAviary.py:188-239)
+    T rpm[4] = {0, 0, 0, 0};
+    quat_to_rpy(q, rpy);
+    if (valid) {
+      const T z3[3] = {0, 0, 0};
+      switch (P.act_type) {
+        case QS_ACT_RPM:
+#pragma unroll
+          for (int m = 0; m < 4; ++m) rpm[m] = P.HOVER_RPM * (T(1) + T(0.05) * T(act[m]));
+          break;
+        case QS_ACT_ONE_D_RPM: {
+          T r = P.HOVER_RPM * (T(1) + T(0.05) * T(act[0]));
+          rpm[0] = rpm[1] = rpm[2] = rpm[3] = r;
+        } break;
+        case QS_ACT_ONE_D_PID: {
+          T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
+          dsl_pid(P, pid, pos, q, vel, tp, T(0), z3, rpm);
+        } break;
+        case QS_ACT_VEL: {
+          T v0 = T(act[0]), v1 = T(act[1]), v2 = T(act[2]);
+          T n = F::sqrt_(v0 * v0 + v1 * v1 + v2 * v2);
+          T u0 = 0, u1 = 0, u2 = 0;
+          if (n != T(0)) { u0 = v0 / n; u1 = v1 / n; u2 = v2 / n; }
+          T sp = P.SPEED_LIMIT * F::abs_(T(act[3]));
+          T tv[3] = {sp * u0, sp * u1, sp * u2};
+          dsl_pid(P, pid, pos, q, vel, pos, rpy[2], tv, rpm);
+        } break;
+        case QS_ACT_PID: {
+          T dir[3] = {T(act[0]) - pos[0], T(act[1]) - pos[1], T(act[2]) - pos[2]};
+          T dist = F::sqrt_(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+          T np_[3];
+          if (dist <= T(1)) { np_[0] = T(act[0]); np_[1] = T(act[1]); np_[2] = T(act[2]); }
+          else { for (int i = 0; i < 3; ++i) np_[i] = pos[i] + (dir[i] / dist) * T(1); }
+          dsl_pid(P, pid, pos, q, vel, np_, T(0), z3, rpm);
+        } break;
+        default: break;
+      }
+    }
+    // ---------------- PYB_STEPS_PER_CTRL substeps (BaseAviary.py:343-372)
+    T f[4], zt[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) { f[m] = rpm[m] * rpm[m] * P.KF; zt[m] = rpm[m] * rpm[m] * P.KM; }
+    const T thrust_z = ((f[0] + f[1]) + f[2]) + f[3];
+    const T tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];
+    const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * P.L_SQRT2;
+    const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * P.L_SQRT2;
+    const bool dw = (P.aux & QS_AUX_DW) != 0;
+    for (int sub = 0; sub < P.S; ++sub) {
+      T R[9];
+      quat_to_rot(q, R);
+      T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
+      if (P.aux & QS_AUX_GND) {  // _groundEffect (BaseAviary.py:731-750)
+        T srpy[3];
+        quat_to_rpy(q, srpy);
+        if (F::abs_(srpy[0]) < T(M_PI / 2) && F::abs_(srpy[1]) < T(M_PI / 2)) {
+          const T PX[4] = {T(0.028), T(-0.028), T(-0.028), T(0.028)};
+          const T PY[4] = {T(-0.028), T(-0.028), T(0.028), T(0.028)};
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            T h = pos[2] + (R[6] * PX[m] + R[7] * PY[m]);
+            h = h < P.GND_CLIP ? P.GND_CLIP : h;
+            T ratio = P.PROP_R / (T(4) * h);
+            T g = rpm[m] * rpm[m] * P.KF * P.GND_COEFF * (ratio * ratio);
+            zb += g; txe += PY[m] * g; tye += -PX[m] * g;
+          }
+        }
+      }
+      if (P.aux & QS_AUX_DRAG) {  // _drag (BaseAviary.py:770-781), previous-substep rpm
+        T sr = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) sr += T(2 * M_PI) * lrpm[m] / T(60);
+        fwx += (T(-1) * P.DRAG0 * sr) * vel[0];
+        fwy += (T(-1) * P.DRAG1 * sr) * vel[1];
+        fwz += (T(-1) * P.DRAG2 * sr) * vel[2];
+      }
+      if (dw) {  // _downwash (BaseAviary.py:798-811): neighbours' substep-start z via LDS
+        __syncthreads();
+        s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
+        __syncthreads();
+        if (valid) {
+          const int base = lenv * D;
+          for (int j = 0; j < D; ++j) {
+            T dz = s.cand[base + j][2] - pos[2];
+            T dx = s.cand[base + j][0] - pos[0], dy = s.cand[base + j][1] - pos[1];
+            T dxy = F::sqrt_(dx * dx + dy * dy);
+            if (dz > T(0) && dxy < T(10)) {
+              T ratio = P.PROP_R / (T(4) * dz);
+              T alpha = P.DW1 * (ratio * ratio);
+              T beta = P.DW2 * dz + P.DW3;
+              T qq = dxy / beta;
+              zb += -alpha * F::exp_(T(-.5) * (qq * qq));
+            }
+          }
+        }
+      }
+      // _dynamics (BaseAviary.py:836-877)
+      T fw0 = R[2] * zb + fwx, fw1 = R[5] * zb + fwy, fw2 = (R[8] * zb - P.GRAVITY) + fwz;
+      T Jw0 = P.Jd0 * w[0], Jw1 = P.Jd1 * w[1], Jw2 = P.Jd2 * w[2];
+      T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
+      T wd0 = P.Ji0 * ((tx + txe) - c0), wd1 = P.Ji1 * ((ty + tye) - c1), wd2 = P.Ji2 * (tz - c2);
+      vel[0] = vel[0] + P.dt * (fw0 / P.M);
+      vel[1] = vel[1] + P.dt * (fw1 / P.M);
+      vel[2] = vel[2] + P.dt * (fw2 / P.M);
+      w[0] = w[0] + P.dt * wd0;
+      w[1] = w[1] + P.dt * wd1;
+      w[2] = w[2] + P.dt * wd2;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pos[i] = pos[i] + P.dt * vel[i];
+      // _integrateQ (BaseAviary.py:879-892)
+      T wn = F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+      if (!(F::abs_(wn) <= T(1e-8))) {
+        T th = wn * P.dt / T(2);
+        T c = F::cos_(th), sn = F::sin_(th);
+        T k = (T(2) / wn) * T(0.5) * sn;   // (2/|ω|)·(0.5·Λ)·sinθ
+        T p_ = w[0], q_ = w[1], r_ = w[2];
+        T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+        q[0] = c * x0 + k * (r_ * x1 - q_ * x2 + p_ * x3);
+        q[1] = c * x1 + k * (-r_ * x0 + p_ * x2 + q_ * x3);
+        q[2] = c * x2 + k * (q_ * x0 - p_ * x1 + r_ * x3);
+        q[3] = c * x3 + k * (-p_ * x0 - q_ * x1 - r_ * x2);
+      }
+      // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875)
+      angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
+      angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
+      angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
+    }
+    quat_to_rpy(q, rpy);   // readback (BaseAviary.py:374, 518)
+    total += 1;
+
+    // ---------------- reward / termination per drone
+    if (valid) {
+      if (P.task == QS_TASK_MULTIHOVER) {  // MultiHoverAviary.py:128-186, 216-241
+        T ex = pos[0] - tgt[0], ey = pos[1] - tgt[1];
+        T err_xy = F::sqrt_(ex * ex + ey * ey);
+        T err_z = pos[2] - tgt[2];
+        T vz = vel[2];
+        T r_xy = T(1) / (T(1) + err_xy);
+        T r_z = F::exp_(T(-7.5) * F::abs_(err_z));
+        T r_vel = F::abs_(err_z) < T(0.2) ? T(-1.5) * (vz * vz) : T(0);
+        T hover = (err_xy < T(0.03) && F::abs_(err_z) < T(0.03) && F::abs_(vz) < T(0.03)) ? T(0.5) : T(0);
+        rterm = ((r_xy + r_z) + r_vel) + hover;
+        if (pos[2] < T(0.03)) bits |= QS_REASON_CRASH;
+        if (F::abs_(rpy[0]) > T(1.2) || F::abs_(rpy[1]) > T(1.2)) bits |= QS_REASON_FLIP;
+        if (F::abs_(pos[0]) > T(3.0) || F::abs_(pos[1]) > T(3.0)) bits |= QS_REASON_OOB;
+      } else {  // SpiralAviary.py:82-99, 150-191
+        T t = T((double)step_counter / (double)P.pyb_freq);
+        T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
+        T prx = P.sp_cx + P.sp_R * F::cos_(ph), pry = P.sp_cy + P.sp_R * F::sin_(ph), prz = T(0.3) + P.sp_VZ * t;
+        T vrx = -P.sp_R * P.sp_OMEGA * F::sin_(ph), vry = P.sp_R * P.sp_OMEGA * F::cos_(ph), vrz = P.sp_VZ;
+        T dp0 = pos[0] - prx, dp1 = pos[1] - pry, dp2 = pos[2] - prz;
+        T dv0 = q[0] - vrx, dv1 = q[1] - vry, dv2 = q[2] - vrz;   // "vel" = quat xyz (SP:156)
+        T np_ = F::sqrt_(dp0 * dp0 + dp1 * dp1 + dp2 * dp2), nv = F::sqrt_(dv0 * dv0 + dv1 * dv1 + dv2 * dv2);
+        T r_pos = F::exp_(T(-4.0) * (np_ * np_));
+        T r_vel = F::exp_(T(-2.0) * (nv * nv));
+        T rx = pos[0] - P.sp_cx, ry = pos[1] - P.sp_cy;
+        T rn = F::sqrt_(rx * rx + ry * ry);
+        T r_tan = 0;
+        if (rn > T(1e-3)) {
+          T tnx = -(ry / rn), tny = rx / rn;
+          T vx = q[0], vy = q[1];
+          T vn = F::sqrt_(vx * vx + vy * vy);
+          if (vn > T(1e-3)) {
+            T dot = (vx / vn) * tnx + (vy / vn) * tny;
+            r_tan = dot > T(0) ? dot : T(0);
+          }
+        }
+        rterm = (T(1.0) * r_pos + T(2.0) * r_vel) + T(1.0) * r_tan;
+        if (pos[2] < T(0.05) || pos[2] > T(3.0)) bits |= QS_REASON_ZRANGE;
+      }
+    }
+    s.rew[tid] = rterm;
+    s.bits[tid] = bits;
+    __syncthreads();
+    // per-env reduction in drone order (reference: reward += ... for i in range(D))
+    if (valid && d == 0) {
+      T rsum = 0;
+      uint8_t any = 0;
+      for (int j = 0; j < D; ++j) { rsum += s.rew[tid + j]; any |= s.bits[tid + j]; }
+      T r = rsum / T(D);
+      bool te = any != 0;
+      bool tr = ((double)step_counter / (double)P.pyb_freq) > P.ep_len_sec;   // MultiHoverAviary.py:267-268
+      if (P.rew) P.rew[e] = r;
+      if (P.term) P.term[e] = te;
+      if (P.trunc) P.trunc[e] = tr;
+      double ret = P.ep_return[e] + (double)r;
+      int len = ep_len + 1;
+      bool dn = te || tr;
+      if (dn) {
+        unsigned long long slot = atomicAdd(P.log_count, 1ull);
+        qs_episode_rec rec;
+        rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
+        P.log[slot % (unsigned long long)P.log_cap] = rec;
+        ret = 0; len = 0;
+      }
+      P.ep_return[e] = ret;
+      P.env[QS_E_EP_LEN * P.E + e] = len;
+      s.done[lenv] = dn;
+    }
+    if (P.reasons && valid) P.reasons[a] = bits;
+    step_counter += P.S;   // BaseAviary.py:382
+    __syncthreads();
+    done_env = valid && s.done[lenv];
+  } else if (P.mode == MODE_RESET_ALL) {
+    // qs_reset: every env starts episode 0
+    done_env = valid;
+  } else {
+    // qs_reset_envs: env.reset() on the masked envs
+    done_env = valid && (P.reset_mask == nullptr || P.reset_mask[e] != 0);
+  }
+  // worker.step_env resets on done unless this is a single-env facade
+  const bool do_reset = done_env && !(P.mode == MODE_STEP && (P.flags & QS_FLAG_NO_AUTORESET));
+
+  // ---------------- obs writer (BaseRLAviary._computeObs + Spiral extras)
+  auto write_obs = [&](float* dst, const T* p_, const T* r_, const T* v_, const T* av_, const T* q_, int sc) {
+    float* o = dst + (size_t)a * O;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      o[i] = (float)p_[i]; o[3 + i] = (float)r_[i]; o[6 + i] = (float)v_[i]; o[9 + i] = (float)av_[i];
+    }
+    for (int i = 0; i < H; ++i) {
+      const int slot = (total + i) % H;
+      for (int k = 0; k < A; ++k) o[12 + i * A + k] = P.hist[((size_t)slot * N + a) * A + k];
+    }
+    if (P.task == QS_TASK_SPIRAL) {
+      T t = T((double)sc / (double)P.pyb_freq);
+      T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
+      T sn = F::sin_(ph), cs = F::cos_(ph);
+      T prx = P.sp_cx + P.sp_R * cs, pry = P.sp_cy + P.sp_R * sn, prz = T(0.3) + P.sp_VZ * t;
+      T vrx = -P.sp_R * P.sp_OMEGA * sn, vry = P.sp_R * P.sp_OMEGA * cs, vrz = P.sp_VZ;
+      float* x = o + 12 + H * A;
+      x[0] = (float)(prx - p_[0]); x[1] = (float)(pry - p_[1]); x[2] = (float)(prz - p_[2]);
+      x[3] = (float)(vrx - q_[0]); x[4] = (float)(vry - q_[1]); x[5] = (float)(vrz - q_[2]);
+      x[6] = (float)sn; x[7] = (float)cs;
+      x[8] = (float)vrx; x[9] = (float)vry; x[10] = (float)vrz;
+    }
+  };
+
+  if (valid && done_env && P.mode == MODE_STEP && P.tobs)
+    write_obs(P.tobs, pos, rpy, vel, angv, q, obs_sc);
+
+  // ---------------- auto-reset (worker.step_env → env.reset)
+  s.any = 0;
+  __syncthreads();
+  if (do_reset && d == 0) s.any = 1;
+  __syncthreads();
+  if (s.any) {
+    if (d == 0 && lenv < P.EPB) s.need[lenv] = do_reset ? 1 : 0;
+    if (P.mode != MODE_RESET_ALL && do_reset) episode += 1;
+    T init[3];
+    if (P.task == QS_TASK_MULTIHOVER) {
+      // Phase 1: every group tries index 0 for its own env.
+      if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
+      __syncthreads();
+      eval_candidate(P, s, lenv, d, lenv, 0u, genv, (uint32_t)episode, do_reset);
+      if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
+      __syncthreads();
+      // Phase 2: for each still-rejected env, all groups search in parallel,
+      // tries base+g; the smallest accepted index wins (= sequential order).
+      for (int k = 0; k < P.EPB; ++k) {
+        if (!s.need[k]) continue;   // block-uniform (LDS)
+        const int ek = blockIdx.x * P.EPB + k;
+        const uint32_t genv_k = (uint32_t)(P.env_offset + ek);
+        // episode number of env k lives in its drone-0 thread; broadcast via LDS
+        __syncthreads();
+        if (tid == k * D) s.ep_bcast = (uint32_t)episode;
+        __syncthreads();
+        const uint32_t epk = s.ep_bcast;
+        uint32_t base = 1;
+        for (;;) {
+          if (tid < P.EPB) s.reject[tid] = 0;
+          if (tid == 0) s.win_group = 1 << 30;
+          __syncthreads();
+          const bool act_ = lenv < P.EPB;
+          eval_candidate(P, s, lenv, d, k, base + (uint32_t)lenv, genv_k, epk, act_);
+          if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
+          __syncthreads();
+          if (s.win_group < (1 << 30) || base + P.EPB >= kMaxResetTries) {
+            if (tid == 0) {
+              if (s.win_group < (1 << 30)) s.win_try[k] = base + (uint32_t)s.win_group;
+              else { s.win_try[k] = 0; atomicExch(P.err, 1); }
+            }
+            __syncthreads();
+            break;
+          }
+          base += (uint32_t)P.EPB;
+        }
+        if (tid == 0) s.need[k] = 2;   // resolved by phase 2 (win_try holds the index)
+        __syncthreads();
+      }
+      if (do_reset) {
+        uint32_t wt = (s.need[lenv] == 2) ? s.win_try[lenv] : 0u;
+        U4 r = philox(U4{wt, genv, (uint32_t)episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
+        init[0] = F::add_rn(P.orig_xyz[d * 3 + 0], T(0.5) * u01<T>(r.x) - T(0.25));
+        init[1] = F::add_rn(P.orig_xyz[d * 3 + 1], T(0.5) * u01<T>(r.y) - T(0.25));
+        init[2] = clampv(F::add_rn(P.orig_xyz[d * 3 + 2], T(0.5) * u01<T>(r.z) - T(0.25)), T(0.1), T(1.0));
+      }
+    } else {
+      if (do_reset) { init[0] = P.orig_xyz[d * 3 + 0]; init[1] = P.orig_xyz[d * 3 + 1]; init[2] = P.orig_xyz[d * 3 + 2]; }
+    }
+    if (do_reset) {
+      // BaseAviary._housekeeping (BaseAviary.py:458-477): PID state and the
+      // action history are NOT reset (reference quirk).
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { pos[i] = init[i]; vel[i] = 0; w[i] = 0; rpy[i] = 0; angv[i] = 0; }
+      q[0] = q[1] = q[2] = 0; q[3] = 1;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) lrpm[m] = 0;
+      tgt[0] = init[0]; tgt[1] = init[1]; tgt[2] = init[2] + T(1.0 / (double)(d + 1));   // MH:106
+      step_counter = 0;
+      obs_sc = 0;
+    }
+  }
+
+  if (!valid) return;
+  if (P.obs && (P.mode != MODE_RESET_MASK || do_reset)) write_obs(P.obs, pos, rpy, vel, angv, q, obs_sc);
+
+  // ---------------- store state
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    P.st[(QS_F_POS + i) * N + a] = pos[i];
+    P.st[(QS_F_VEL + i) * N + a] = vel[i];
+    P.st[(QS_F_RPY_RATES + i) * N + a] = w[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) P.st[(QS_F_QUAT + i) * N + a] = q[i];
+  // last_clipped_action is part of the state vector (BaseAviary.py:560); it is
+  // read back only when the drag model consumes it, but always written.
+#pragma unroll
+  for (int i = 0; i < 4; ++i) P.st[(QS_F_LAST_RPM + i) * N + a] = lrpm[i];
+  if (has_pid && P.mode == MODE_STEP) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) P.st[(QS_F_PID_INT_POS + i) * N + a] = pid[i];
+  }
+  if (P.task == QS_TASK_MULTIHOVER && do_reset) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) P.st[(QS_F_TARGET + i) * N + a] = tgt[i];
+  }
+  if (d == 0) {
+    P.env[QS_E_STEP_COUNTER * P.E + e] = step_counter;
+    P.env[QS_E_EPISODE * P.E + e] = episode;
+    P.env[QS_E_TOTAL_STEPS * P.E + e] = total;
+  }
+}
+
+// Calibration kernel: dword per lane, grid-stride (MI355X_MICROARCH §HBM).
+__global__ void calib_copy_kernel(float* __restrict__ dst, const float* __restrict__ src, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+}  // namespace qs
+
+// ===========================================================================
+// Host side: the C-ABI.
+// ===========================================================================
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& m) { g_err = m; return code; }
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) return fail(QS_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// cf2x.urdf + BaseAviary.py:117-128 (same values as the oracle's Consts).
+struct HostConsts {
+  double G = 9.8, M = 0.027, L = 0.0397, T2W = 2.25, IXX = 1.4e-5, IYY = 1.4e-5, IZZ = 2.17e-5;
+  double KF = 3.16e-10, KM = 7.94e-12, COLL_H = 0.025, COLL_Z_OFF = 0.0, MAX_SPEED_KMH = 30.0;
+  double GND_EFF_COEFF = 11.36859, PROP_RADIUS = 2.31348e-2, DRAG_XY = 9.1785e-7, DRAG_Z = 10.311e-7;
+  double DW1 = 2267.18, DW2 = 0.16, DW3 = -0.11;
+};
+}  // namespace
+
+struct qs_handle {
+  qs_spec spec;
+  qs_dims dims;
+  int device = 0;
+  void* st = nullptr;          // agent SoA (real)
+  int32_t* env = nullptr;      // env int32 SoA
+  float* hist = nullptr;
+  double* ep_return = nullptr;
+  void* orig = nullptr;        // [D][3] real
+  qs_episode_rec* log = nullptr;
+  unsigned long long* log_count = nullptr;
+  long long log_cap = 0;
+  int* err = nullptr;
+  uint64_t seed = 0;
+  bool reset_done = false;
+  std::vector<double> orig_host;
+};
+
+template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P) {
+  const HostConsts C;
+  const qs_spec& s = h->spec;
+  std::memset(&P, 0, sizeof(P));
+  P.E = s.num_envs; P.D = s.num_drones; P.N = h->dims.num_agents; P.A = h->dims.act_dim; P.O = h->dims.obs_dim;
+  P.H = h->dims.hist_len; P.S = h->dims.substeps;
+  P.EPB = qs::kBlock / s.num_drones;
+  P.task = s.task; P.act_type = s.act_type; P.aux = s.aux_forces; P.flags = s.flags; P.pyb_freq = s.pyb_freq;
+  P.ep_len_sec = s.episode_len_sec;
+  P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
+  P.env_offset = s.env_offset;
+  P.dt = T(1.0 / s.pyb_freq); P.ctrl_dt = T(1.0 / s.ctrl_freq);
+  P.KF = T(C.KF); P.KM = T(C.KM); P.M = T(C.M); P.GRAVITY = T(C.G * C.M);
+  P.Jd0 = T(C.IXX); P.Jd1 = T(C.IYY); P.Jd2 = T(C.IZZ);
+  P.Ji0 = T(1.0 / C.IXX); P.Ji1 = T(1.0 / C.IYY); P.Ji2 = T(1.0 / C.IZZ);
+  P.L_SQRT2 = T(C.L / std::sqrt(2.0));
+  P.HOVER_RPM = T(std::sqrt(C.G * C.M / (4 * C.KF)));
+  P.SPEED_LIMIT = T(0.03 * C.MAX_SPEED_KMH * (1000.0 / 3600.0));
+  P.G_PID = T(9.8 * C.M);
+  P.DRAG0 = T(C.DRAG_XY); P.DRAG1 = T(C.DRAG_XY); P.DRAG2 = T(C.DRAG_Z);
+  P.GND_COEFF = T(C.GND_EFF_COEFF); P.PROP_R = T(C.PROP_RADIUS);
+  {
+    double max_rpm = std::sqrt((C.T2W * C.G * C.M) / (4 * C.KF));
+    double max_thrust = 4 * C.KF * max_rpm * max_rpm;
+    P.GND_CLIP = T(0.25 * C.PROP_RADIUS * std::sqrt((15 * max_rpm * max_rpm * C.KF * C.GND_EFF_COEFF) / max_thrust));
+  }
+  P.DW1 = T(C.DW1); P.DW2 = T(C.DW2); P.DW3 = T(C.DW3);
+  P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
+  P.sp_cx = T(s.target_center[0]); P.sp_cy = T(s.target_center[1]); P.sp_cz = T(s.target_center[2]);
+  P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.ep_return = h->ep_return; P.orig_xyz = (const T*)h->orig;
+  P.log = h->log; P.log_count = h->log_count; P.log_cap = h->log_cap; P.err = h->err;
+}
+
+template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t st) {
+  const int grid = (P.E + P.EPB - 1) / P.EPB;
+  hipLaunchKernelGGL(qs::step_kernel<T>, dim3(grid), dim3(qs::kBlock), 0, st, P);
+  HIP_TRY(hipGetLastError());
+  return QS_OK;
+}
+
+extern "C" {
+
+const char* qs_last_error(void) { return g_err.c_str(); }
+int qs_abi_version(void) { return QS_ABI_VERSION; }
+
+int qs_create(const qs_spec* spec, int device, qs_handle** out) {
+  if (!spec || !out) return fail(QS_E_INVALID, "qs_create: null argument");
+  const qs_spec& s = *spec;
+  if (s.task != QS_TASK_MULTIHOVER && s.task != QS_TASK_SPIRAL) return fail(QS_E_INVALID, "qs_create: bad task");
+  if (s.num_drones < 1 || s.num_drones > 64) return fail(QS_E_INVALID, "qs_create: num_drones must be in 1..64");
+  if (s.num_envs < 1) return fail(QS_E_INVALID, "qs_create: num_envs must be >= 1");
+  if (s.physics != QS_PHYS_DYN) return fail(QS_E_INVALID, "qs_create: only Physics.DYN is implemented (PYB is SURVEY §8(f) next-1)");
+  if (s.aux_forces & ~7u) return fail(QS_E_INVALID, "qs_create: bad aux_forces");
+  if (s.flags & ~QS_FLAG_NO_AUTORESET) return fail(QS_E_INVALID, "qs_create: bad flags");
+  if (s.pyb_freq <= 0 || s.ctrl_freq <= 0 || s.pyb_freq % s.ctrl_freq)
+    return fail(QS_E_INVALID, "qs_create: pyb_freq is not divisible by env_freq");  // BaseAviary.py:79-80
+  if (s.ctrl_freq < 2) return fail(QS_E_INVALID, "qs_create: ctrl_freq must be >= 2 (action history length ctrl_freq//2)");
+  if (s.precision != 4 && s.precision != 8) return fail(QS_E_INVALID, "qs_create: precision must be 4 or 8");
+  if (s.task == QS_TASK_MULTIHOVER && !s.initial_xyzs && s.num_drones >= 6)
+    return fail(QS_E_INVALID, "qs_create: MultiHover reset with the default diagonal layout cannot complete for "
+                              "D >= 6 (SURVEY §7 hard-2); pass initial_xyzs");
+  int A;
+  switch (s.act_type) {
+    case QS_ACT_RPM: case QS_ACT_VEL: A = 4; break;
+    case QS_ACT_PID: A = 3; break;
+    case QS_ACT_ONE_D_RPM: case QS_ACT_ONE_D_PID: A = 1; break;
+    default: return fail(QS_E_INVALID, "qs_create: bad act_type");
+  }
+  HIP_TRY(hipSetDevice(device));
+  auto* h = new (std::nothrow) qs_handle();
+  if (!h) return fail(QS_E_NOMEM, "qs_create: host allocation failed");
+  h->spec = s;
+  h->spec.initial_xyzs = nullptr;
+  h->device = device;
+  qs_dims& d = h->dims;
+  d.num_envs = s.num_envs; d.num_drones = s.num_drones; d.num_agents = s.num_envs * s.num_drones;
+  d.act_dim = A; d.hist_len = s.ctrl_freq / 2; d.substeps = s.pyb_freq / s.ctrl_freq;
+  d.obs_dim = 12 + d.hist_len * A + (s.task == QS_TASK_SPIRAL ? 11 : 0);
+  d.precision = s.precision; d.agent_fields = QS_AGENT_FIELDS; d.env_fields = QS_ENV_FIELDS;
+  // initial layout (BaseAviary.py:194-197 / SpiralAviary.py:47-53)
+  const HostConsts C;
+  h->orig_host.resize(3 * s.num_drones);
+  for (int i = 0; i < s.num_drones; ++i) {
+    double xyz[3];
+    if (s.initial_xyzs) { for (int k = 0; k < 3; ++k) xyz[k] = s.initial_xyzs[i * 3 + k]; }
+    else if (s.task == QS_TASK_SPIRAL) {
+      xyz[0] = s.spiral_radius * std::cos(2 * M_PI * i / s.num_drones);
+      xyz[1] = s.spiral_radius * std::sin(2 * M_PI * i / s.num_drones);
+      xyz[2] = 0.3;
+    } else {
+      xyz[0] = i * 4 * C.L; xyz[1] = i * 4 * C.L; xyz[2] = C.COLL_H / 2 - C.COLL_Z_OFF + .1;
+    }
+    for (int k = 0; k < 3; ++k) h->orig_host[i * 3 + k] = xyz[k];
+  }
+  const size_t rs = (size_t)s.precision;
+  const size_t N = d.num_agents;
+  h->log_cap = std::max<long long>(1 << 16, 4LL * s.num_envs);
+  auto cleanup = [&]() { qs_destroy(h); };
+  hipError_t e1 = hipMalloc(&h->st, rs * QS_AGENT_FIELDS * N);
+  hipError_t e2 = hipMalloc((void**)&h->env, sizeof(int32_t) * QS_ENV_FIELDS * s.num_envs);
+  hipError_t e3 = hipMalloc((void**)&h->hist, sizeof(float) * d.hist_len * N * A);
+  hipError_t e4 = hipMalloc((void**)&h->ep_return, sizeof(double) * s.num_envs);
+  hipError_t e5 = hipMalloc(&h->orig, rs * 3 * s.num_drones);
+  hipError_t e6 = hipMalloc((void**)&h->log, sizeof(qs_episode_rec) * h->log_cap);
+  hipError_t e7 = hipMalloc((void**)&h->log_count, sizeof(unsigned long long));
+  hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
+  if (e1 || e2 || e3 || e4 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
+  if (s.precision == 8) {
+    if (hipMemcpy(h->orig, h->orig_host.data(), 8 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }
+  } else {
+    std::vector<float> of(h->orig_host.begin(), h->orig_host.end());
+    if (hipMemcpy(h->orig, of.data(), 4 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }
+  }
+  if (hipMemset(h->st, 0, rs * QS_AGENT_FIELDS * N) || hipMemset(h->env, 0, sizeof(int32_t) * QS_ENV_FIELDS * s.num_envs) ||
+      hipMemset(h->hist, 0, sizeof(float) * d.hist_len * N * A) || hipMemset(h->ep_return, 0, sizeof(double) * s.num_envs) ||
+      hipMemset(h->log_count, 0, sizeof(unsigned long long)) || hipMemset(h->err, 0, sizeof(int))) {
+    cleanup(); return fail(QS_E_HIP, "qs_create: memset");
+  }
+  *out = h;
+  return QS_OK;
+}
+
+int qs_destroy(qs_handle* h) {
+  if (!h) return QS_OK;
+  hipSetDevice(h->device);
+  void* ptrs[] = {h->st, h->env, h->hist, h->ep_return, h->orig, h->log, h->log_count, h->err};
+  for (void* p : ptrs) if (p) hipFree(p);
+  delete h;
+  return QS_OK;
+}
+
+int qs_get_dims(const qs_handle* h, qs_dims* out) {
+  if (!h || !out) return fail(QS_E_INVALID, "qs_get_dims: null argument");
+  *out = h->dims;
+  return QS_OK;
+}
+
+int qs_reset(qs_handle* h, uint64_t seed, float* obs, void* stream) {
+  if (!h) return fail(QS_E_INVALID, "qs_reset: null handle");
+  hipStream_t st = (hipStream_t)stream;
+  const qs_dims& d = h->dims;
+  const size_t N = d.num_agents, rs = d.precision;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemsetAsync(h->st, 0, rs * QS_AGENT_FIELDS * N, st));
+  HIP_TRY(hipMemsetAsync(h->env, 0, sizeof(int32_t) * QS_ENV_FIELDS * d.num_envs, st));
+  HIP_TRY(hipMemsetAsync(h->hist, 0, sizeof(float) * d.hist_len * N * d.act_dim, st));
+  HIP_TRY(hipMemsetAsync(h->ep_return, 0, sizeof(double) * d.num_envs, st));
+  HIP_TRY(hipMemsetAsync(h->log_count, 0, sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(int), st));
+  h->seed = seed;
+  int rc;
+  if (d.precision == 8) {
+    qs::Params<double> P; fill_params(h, P); P.mode = qs::MODE_RESET_ALL; P.obs = obs;
+    rc = launch(h, P, st);
+  } else {
+    qs::Params<float> P; fill_params(h, P); P.mode = qs::MODE_RESET_ALL; P.obs = obs;
+    rc = launch(h, P, st);
+  }
+  if (rc == QS_OK) h->reset_done = true;
+  return rc;
+}
+
+int qs_reset_envs(qs_handle* h, const uint8_t* mask, float* obs, void* stream) {
+  if (!h) return fail(QS_E_INVALID, "qs_reset_envs: null handle");
+  if (!h->reset_done) return fail(QS_E_STATE, "qs_reset_envs: call qs_reset first");
+  hipStream_t st = (hipStream_t)stream;
+  if (h->dims.precision == 8) {
+    qs::Params<double> P; fill_params(h, P); P.mode = qs::MODE_RESET_MASK; P.reset_mask = mask; P.obs = obs;
+    return launch(h, P, st);
+  }
+  qs::Params<float> P; fill_params(h, P); P.mode = qs::MODE_RESET_MASK; P.reset_mask = mask; P.obs = obs;
+  return launch(h, P, st);
+}
+
+int qs_step(qs_handle* h, const float* actions, const qs_step_out* out, void* stream) {
+  if (!h) return fail(QS_E_INVALID, "qs_step: null handle");
+  if (!h->reset_done) return fail(QS_E_STATE, "qs_step: call qs_reset first");
+  hipStream_t st = (hipStream_t)stream;
+  qs_step_out o{};
+  if (out) o = *out;
+  if (h->dims.precision == 8) {
+    qs::Params<double> P; fill_params(h, P); P.mode = qs::MODE_STEP;
+    P.act_in = actions; P.obs = o.obs; P.rew = (double*)o.reward; P.term = o.terminated; P.trunc = o.truncated;
+    P.tobs = o.terminal_obs; P.reasons = o.reasons; P.act_out = o.actions_out;
+    return launch(h, P, st);
+  }
+  qs::Params<float> P; fill_params(h, P); P.mode = qs::MODE_STEP;
+  P.act_in = actions; P.obs = o.obs; P.rew = (float*)o.reward; P.term = o.terminated; P.trunc = o.truncated;
+  P.tobs = o.terminal_obs; P.reasons = o.reasons; P.act_out = o.actions_out;
+  return launch(h, P, st);
+}
+
+int qs_state_io(qs_handle* h, int block, void* buf, int dir, void* stream) {
+  if (!h || !buf) return fail(QS_E_INVALID, "qs_state_io: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const qs_dims& d = h->dims;
+  void* src = nullptr;
+  size_t bytes = 0;
+  switch (block) {
+    case QS_STATE_AGENT: src = h->st; bytes = (size_t)d.precision * QS_AGENT_FIELDS * d.num_agents; break;
+    case QS_STATE_ENV: src = h->env; bytes = sizeof(int32_t) * QS_ENV_FIELDS * d.num_envs; break;
+    case QS_STATE_HISTORY: src = h->hist; bytes = sizeof(float) * d.hist_len * d.num_agents * d.act_dim; break;
+    case QS_STATE_EP_RETURN: src = h->ep_return; bytes = sizeof(double) * d.num_envs; break;
+    default: return fail(QS_E_INVALID, "qs_state_io: bad block");
+  }
+  HIP_TRY(hipSetDevice(h->device));
+  if (dir) HIP_TRY(hipMemcpyAsync(src, buf, bytes, hipMemcpyDeviceToDevice, st));
+  else HIP_TRY(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToDevice, st));
+  if (dir) h->reset_done = true;
+  return QS_OK;
+}
+
+int qs_episode_log(qs_handle* h, qs_episode_rec* dst, int64_t cap, int64_t* total, void* stream) {
+  if (!h || !total) return fail(QS_E_INVALID, "qs_episode_log: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(h->device));
+  unsigned long long cnt = 0;
+  HIP_TRY(hipMemcpyAsync(&cnt, h->log_count, sizeof(cnt), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *total = (int64_t)cnt;
+  if (!dst || cap <= 0 || cnt == 0) return QS_OK;
+  const long long avail = std::min<long long>((long long)cnt, h->log_cap);
+  const long long k = std::min<long long>(avail, cap);
+  // most recent k records, in ring order, wrapped
+  const long long first = (long long)cnt - k;
+  for (long long done = 0; done < k;) {
+    long long idx = (first + done) % h->log_cap;
+    long long run = std::min<long long>(k - done, h->log_cap - idx);
+    HIP_TRY(hipMemcpyAsync(dst + done, h->log + idx, sizeof(qs_episode_rec) * run, hipMemcpyDeviceToDevice, st));
+    done += run;
+  }
+  return QS_OK;
+}
+
+int qs_reset_error(qs_handle* h, int* out) {
+  if (!h || !out) return fail(QS_E_INVALID, "qs_reset_error: null argument");
+  HIP_TRY(hipMemcpy(out, h->err, sizeof(int), hipMemcpyDeviceToHost));
+  return QS_OK;
+}
+
+int qs_calib_copy(float* dst, const float* src, int64_t n, void* stream) {
+  if (!dst || !src || n < 0) return fail(QS_E_INVALID, "qs_calib_copy: bad argument");
+  long long blocks = std::min<long long>((n + 255) / 256, 256LL * 8);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(qs::calib_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dst, src, (long long)n);
+  HIP_TRY(hipGetLastError());
+  return QS_OK;
+}
+
+}  // extern "C"

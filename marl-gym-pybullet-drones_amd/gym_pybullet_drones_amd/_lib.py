@@ -1,0 +1,111 @@
+"""ctypes binding of libquadswarm.so — the C-ABI declared in include/quadswarm.h.
+
+This is exactly the binding a maintainer would add on the reference side
+(INTEGRATION.md): plain pointers, sizes and a hipStream_t, no torch types.
+The library must be built in-tree (``__graft_entry__.build()``); importing the
+product path without it raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libquadswarm.so")
+
+QS_OK = 0
+TASK_MULTIHOVER, TASK_SPIRAL = 0, 1
+ACT_RPM, ACT_PID, ACT_VEL, ACT_ONE_D_RPM, ACT_ONE_D_PID = 0, 1, 2, 3, 4
+PHYS_DYN = 1
+AUX_GND, AUX_DRAG, AUX_DW = 1, 2, 4
+AGENT_FIELDS, ENV_FIELDS = 29, 4
+STATE_AGENT, STATE_ENV, STATE_HISTORY, STATE_EP_RETURN = 0, 1, 2, 3
+FLAG_NO_AUTORESET = 1
+REASON_CRASH, REASON_FLIP, REASON_OOB, REASON_ZRANGE = 1, 2, 4, 8
+
+# agent field offsets (include/quadswarm.h)
+F_POS, F_QUAT, F_VEL, F_RPY_RATES, F_LAST_RPM = 0, 3, 7, 10, 13
+F_PID_INT_POS, F_PID_INT_RPY, F_PID_LAST_RPY, F_TARGET = 17, 20, 23, 26
+E_STEP_COUNTER, E_EPISODE, E_TOTAL_STEPS, E_EP_LEN = 0, 1, 2, 3
+
+
+class QsSpec(ctypes.Structure):
+    _fields_ = [
+        ("task", ctypes.c_int32), ("num_envs", ctypes.c_int32), ("num_drones", ctypes.c_int32),
+        ("act_type", ctypes.c_int32), ("physics", ctypes.c_int32), ("aux_forces", ctypes.c_uint32),
+        ("pyb_freq", ctypes.c_int32), ("ctrl_freq", ctypes.c_int32), ("precision", ctypes.c_int32),
+        ("flags", ctypes.c_uint32), ("env_offset", ctypes.c_int64), ("episode_len_sec", ctypes.c_double),
+        ("initial_xyzs", ctypes.POINTER(ctypes.c_double)), ("spiral_radius", ctypes.c_double),
+        ("spiral_period", ctypes.c_double), ("height_rate", ctypes.c_double),
+        ("target_center", ctypes.c_double * 3),
+    ]
+
+
+class QsDims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "num_envs", "num_drones", "num_agents", "act_dim", "obs_dim", "hist_len", "substeps",
+        "precision", "agent_fields", "env_fields")]
+
+
+class QsStepOut(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
+                ("truncated", ctypes.c_void_p), ("terminal_obs", ctypes.c_void_p), ("reasons", ctypes.c_void_p),
+                ("actions_out", ctypes.c_void_p)]
+
+
+EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq", "<i8")])
+
+# Every symbol include/quadswarm.h declares (tests check the .so exports them).
+EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
+           "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy")
+
+_lib = None
+
+
+class QuadSwarmError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libquadswarm.so (after torch, so both share one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise QuadSwarmError(
+            f"{LIB_PATH} is missing: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    try:
+        import torch  # noqa: F401  (registers libamdhip64.so.7 first)
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    L.qs_last_error.restype = ctypes.c_char_p
+    L.qs_abi_version.restype = i32
+    L.qs_create.argtypes = [ctypes.POINTER(QsSpec), i32, ctypes.POINTER(vp)]
+    L.qs_destroy.argtypes = [vp]
+    L.qs_get_dims.argtypes = [vp, ctypes.POINTER(QsDims)]
+    L.qs_reset.argtypes = [vp, ctypes.c_uint64, vp, vp]
+    L.qs_reset_envs.argtypes = [vp, vp, vp, vp]
+    L.qs_step.argtypes = [vp, vp, ctypes.POINTER(QsStepOut), vp]
+    L.qs_state_io.argtypes = [vp, i32, vp, i32, vp]
+    L.qs_episode_log.argtypes = [vp, vp, i64, ctypes.POINTER(i64), vp]
+    L.qs_reset_error.argtypes = [vp, ctypes.POINTER(i32)]
+    L.qs_calib_copy.argtypes = [vp, vp, i64, vp]
+    for name in EXPORTS:
+        if name != "qs_last_error":
+            getattr(L, name).restype = i32
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != QS_OK:
+        msg = load().qs_last_error()
+        raise QuadSwarmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())

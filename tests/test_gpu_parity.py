@@ -1,0 +1,242 @@
+"""Parity of the HIP step kernel (through the C-ABI) against the CPU oracle.
+
+Both sides consume the same seeded inputs: identical Philox-drawn resets and
+random-policy actions (or identical trainer-style actions), same constants.
+
+Two methodologies:
+ 1. Teacher-forced one-step parity over long horizons (≥ 2 episodes, crossing the
+    242/578-step truncation and many auto-resets): before every step the oracle's
+    full state (agent SoA, env counters, history, episode returns) is injected into
+    the kernel, both step once, all outputs are compared.  This bounds the per-step
+    error to single-step rounding, free of chaotic amplification.
+      fp64: obs |Δ| ≤ 1e-7 + 2e-7·|x| (float32 obs rounding of fp64 values),
+            reward rel 1e-12, state rel 1e-12 + 1e-12 abs
+      fp32: obs |Δ| ≤ 1e-4 + 1e-4·|x|, reward 1e-5, state 1e-4 + 1e-4·|x|
+      flags, reasons, actions, reset draws: exact.
+ 2. Free-running trajectories, 30 control steps open loop:
+      fp32: |Δpos| ≤ 1e-4 m, |Δquat| ≤ 1e-4, |Δvel| ≤ 1e-3 m/s; fp64: 1e-9 / 1e-9 / 1e-8.
+"""
+import numpy as np
+import pytest
+import torch
+
+import qs_oracle
+
+pytestmark = pytest.mark.gpu
+
+from gym_pybullet_drones_amd.envs.swarm import grid_layout  # noqa: E402
+
+GRID8 = grid_layout(8).tolist()
+GRID16 = grid_layout(16).tolist()
+
+CONFIGS = {
+    # id: (oracle/QuadSwarm kwargs)
+    "C2_mh_rpm_d4": dict(task="multihover", num_drones=4, act="rpm"),
+    "C3_mh_onedpid_d8": dict(task="multihover", num_drones=8, act="one_d_pid", initial_xyzs=GRID8),
+    "C3v_mh_vel_d8": dict(task="multihover", num_drones=8, act="vel", initial_xyzs=GRID8),
+    "C4_spiral_vel_d5": dict(task="spiral", num_drones=5, act="vel"),
+    "C5_mh_dw_d16": dict(task="multihover", num_drones=16, act="one_d_pid", initial_xyzs=GRID16, aux=("dw",)),
+    "mh_onedrpm_d2": dict(task="multihover", num_drones=2, act="one_d_rpm"),
+    "mh_pid_d3": dict(task="multihover", num_drones=3, act="pid"),
+    "mh_gnd_drag_d4": dict(task="multihover", num_drones=4, act="one_d_pid", aux=("gnd", "drag", "dw")),
+}
+
+
+def make_pair(cfg, E, precision, env_offset=0):
+    from gym_pybullet_drones_amd.envs import QuadSwarm
+    from gym_pybullet_drones_amd.utils.enums import Physics
+    kw = dict(cfg)
+    aux = tuple(kw.pop("aux", ()))
+    phys = {(): Physics.DYN, ("dw",): Physics.PYB_DW, ("gnd", "drag", "dw"): Physics.PYB_GND_DRAG_DW}[aux]
+    sw = QuadSwarm(num_envs=E, precision=precision, physics=phys, env_offset=env_offset, **kw)
+    orc = qs_oracle.OracleSim(num_envs=E, precision=precision, aux=aux, env_offset=env_offset, **kw)
+    return sw, orc
+
+
+OBS_TOL = {8: (1e-7, 2e-7), 4: (1e-4, 1e-4)}
+STATE_TOL = {8: (1e-12, 1e-12), 4: (1e-4, 1e-4)}
+REW_TOL = {8: 1e-12, 4: 1e-5}
+
+
+def assert_close(name, got, want, tol):
+    atol, rtol = tol
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    err = np.abs(got - want)
+    lim = atol + rtol * np.abs(want)
+    bad = err > lim
+    assert not bad.any(), (f"{name}: {bad.sum()} / {bad.size} elements out of tolerance; max err "
+                           f"{err.max():.3e} at {np.unravel_index(err.argmax(), err.shape)}: "
+                           f"got {got.flat[err.argmax()]!r} want {want.flat[err.argmax()]!r}")
+
+
+def inject(sw, orc):
+    for block in (0, 1, 2, 3):
+        sw.set_state(block, torch.as_tensor(orc.get_state(block)))
+
+
+def teacher_forced(cfg, E, precision, steps, seed=3, actions_fn=None):
+    sw, orc = make_pair(cfg, E, precision)
+    o_g = sw.reset(seed).cpu().numpy()
+    o_c = orc.reset(seed)
+    np.testing.assert_array_equal(o_g[..., :3], o_c[..., :3])   # reset draws bit-identical
+    assert_close("reset obs", o_g, o_c, OBS_TOL[precision])
+    n_done = 0
+    for t in range(steps):
+        inject(sw, orc)
+        acts = None if actions_fn is None else actions_fn(t, sw)
+        r = sw.step(None if acts is None else torch.as_tensor(acts, device=sw.device), want_terminal=True,
+                    want_reasons=True, actions_out=torch.zeros((E, sw.num_drones, sw.act_dim), device=sw.device))
+        c = orc.step(acts)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(r.actions.cpu().numpy(), c["actions"], err_msg=f"actions t={t}")
+        np.testing.assert_array_equal(r.truncated.cpu().numpy(), c["truncated"], err_msg=f"truncated t={t}")
+        np.testing.assert_array_equal(r.terminated.cpu().numpy(), c["terminated"], err_msg=f"terminated t={t}")
+        np.testing.assert_array_equal(r.reasons.cpu().numpy(), c["reasons"], err_msg=f"reasons t={t}")
+        done = (c["terminated"] | c["truncated"]).astype(bool)
+        n_done += int(done.sum())
+        assert_close(f"obs t={t}", r.obs.cpu().numpy(), c["obs"], OBS_TOL[precision])
+        assert_close(f"reward t={t}", r.reward.cpu().numpy(), c["reward"], (REW_TOL[precision],) * 2)
+        if done.any():
+            assert_close(f"terminal obs t={t}", r.terminal_obs.cpu().numpy()[done], c["terminal_obs"][done],
+                         OBS_TOL[precision])
+        assert_close(f"agent state t={t}", sw.get_state(0).cpu().numpy(), orc.get_state(0), STATE_TOL[precision])
+        np.testing.assert_array_equal(sw.get_state(1).cpu().numpy(), orc.get_state(1), err_msg=f"env t={t}")
+        np.testing.assert_array_equal(sw.get_state(2).cpu().numpy(), orc.get_state(2), err_msg=f"hist t={t}")
+    assert sw.reset_error() == 0
+    sw.close()
+    return n_done
+
+
+def free_running(cfg, E, precision, steps=30, seed=11):
+    """Open-loop trajectories.  fp64: kernel vs fp64 oracle within 1e-7.  fp32:
+    precision-consistent — the kernel's RMS deviation from the fp64 oracle (the
+    reference's precision) must stay within 3x the fp32 oracle's own deviation
+    (+1e-5), i.e. the kernel is as close to the fp64 truth as fp32 arithmetic allows."""
+    sw, orc = make_pair(cfg, E, precision)
+    kw = dict(cfg)
+    aux = tuple(kw.pop("aux", ()))
+    truth = qs_oracle.OracleSim(num_envs=E, precision=8, aux=aux, **kw)
+    sw.reset(seed)
+    orc.reset(seed)
+    truth.reset(seed)
+    alive = np.ones(E, bool)
+    for t in range(steps):
+        r = sw.step(None)
+        c = orc.step(None)
+        tr = truth.step(None)
+        torch.cuda.synchronize()
+        # an env that terminates in any of the three runs is dropped from then on
+        alive &= ~(r.terminated.cpu().numpy().astype(bool) | c["terminated"].astype(bool)
+                   | tr["terminated"].astype(bool))
+        cols = np.repeat(alive, sw.num_drones)
+        g, o, T = sw.get_state(0).cpu().numpy()[:, cols], orc.get_state(0)[:, cols], truth.get_state(0)[:, cols]
+        for name, sl in (("pos", slice(0, 3)), ("quat", slice(3, 7)), ("vel", slice(7, 10))):
+            if precision == 8:
+                assert_close(f"{name} t={t}", g[sl], o[sl], (1e-7, 1e-7))
+            else:
+                rms_g = np.sqrt(np.mean((g[sl] - T[sl]) ** 2)) if g.size else 0.0
+                rms_o = np.sqrt(np.mean((o[sl].astype(np.float64) - T[sl]) ** 2)) if g.size else 0.0
+                assert rms_g <= 3 * rms_o + 1e-5, f"{name} t={t}: kernel rms {rms_g:.3e} vs fp32 oracle {rms_o:.3e}"
+        if t == 0:
+            assert alive.any()
+    sw.close()
+
+
+@pytest.mark.parametrize("precision", [8, 4])
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_teacher_forced_parity(name, precision):
+    """One-step parity at every step of a 300-step (Spiral: 600-step) random-policy run."""
+    steps = 600 if CONFIGS[name]["task"] == "spiral" else 300
+    n_done = teacher_forced(CONFIGS[name], E=16, precision=precision, steps=steps)
+    assert n_done > 0
+
+
+@pytest.mark.parametrize("precision", [8, 4])
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_free_running_parity(name, precision):
+    free_running(CONFIGS[name], E=16, precision=precision)
+
+
+def test_given_actions_parity():
+    """Trainer-provided actions (not the in-kernel RNG), including |a| > 1 (raw Normal samples)."""
+    rng = np.random.default_rng(0)
+    fn = lambda t, sw: (rng.normal(size=(sw.num_envs, sw.num_drones, sw.act_dim)) * 0.7).astype(np.float32)
+    teacher_forced(CONFIGS["C3v_mh_vel_d8"], E=12, precision=8, steps=120, actions_fn=fn)
+
+
+def test_episode_log_parity():
+    cfg = CONFIGS["C2_mh_rpm_d4"]
+    sw, orc = make_pair(cfg, E=32, precision=8)
+    sw.reset(2)
+    orc.reset(2)
+    for _ in range(120):
+        sw.step(None)
+        orc.step(None)
+    recs_g, tot_g = sw.episode_log()
+    recs_c, tot_c = orc.episode_log()
+    assert tot_g == tot_c and tot_g > 0
+    np.testing.assert_array_equal(recs_g["env"], recs_c["env"])
+    np.testing.assert_array_equal(recs_g["len"], recs_c["len"])
+    np.testing.assert_array_equal(recs_g["seq"], recs_c["seq"])
+    np.testing.assert_allclose(recs_g["ret"], recs_c["ret"], rtol=1e-9)
+
+
+def test_env_offset_shard_equivalence():
+    """A shard with env_offset=k reproduces envs k.. of the unsharded run (multi-GPU RNG contract)."""
+    from gym_pybullet_drones_amd.envs import QuadSwarm
+    cfg = CONFIGS["C3_mh_onedpid_d8"]
+    full = QuadSwarm(num_envs=32, precision=8, **cfg)
+    shard = QuadSwarm(num_envs=16, precision=8, env_offset=16, **cfg)
+    a = full.reset(5)
+    b = shard.reset(5)
+    for _ in range(20):
+        a = full.step(None).obs
+        b = shard.step(None).obs
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a[16:].cpu().numpy(), b.cpu().numpy())
+
+
+def test_state_injection_and_reset_envs():
+    """qs_state_io round trip and env.reset() semantics (PID + history persist)."""
+    cfg = CONFIGS["C3_mh_onedpid_d8"]
+    sw, orc = make_pair(cfg, E=8, precision=8)
+    sw.reset(1)
+    orc.reset(1)
+    for _ in range(5):
+        sw.step(None)
+        orc.step(None)
+    mask = np.array([1, 0, 1, 0, 0, 0, 0, 1], np.uint8)
+    og = sw.reset_envs(torch.as_tensor(mask, device=sw.device)).cpu().numpy()
+    oc = orc.reset_envs(mask)
+    sel = mask.astype(bool)
+    assert_close("reset_envs obs", og[sel], oc[sel], OBS_TOL[8])
+    np.testing.assert_array_equal(sw.get_state(1).cpu().numpy(), orc.get_state(1))
+    # inject a perturbed state into both and keep stepping
+    st = orc.get_state(0)
+    st[7] += 0.05   # vel x
+    sw.set_state(0, torch.as_tensor(st))
+    orc.set_state(0, st)
+    for t in range(10):
+        r = sw.step(None)
+        c = orc.step(None)
+        torch.cuda.synchronize()
+        assert_close(f"after injection t={t}", r.obs.cpu().numpy(), c["obs"], (1e-6, 1e-6))
+
+
+def test_no_autoreset_facade():
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    env = MultiHoverAviary(num_drones=2, act=ActionType.ONE_D_RPM, precision=8)
+    obs, info = env.reset()
+    assert obs.shape == (2, 27) and info == {"answer": 42, "termination_reasons": []}
+    done = False
+    n = 0
+    while not done and n < 300:
+        obs, rew, term, trunc, info = env.step(-20 * np.ones((2, 1), np.float32))   # rpm 0: free fall
+        done = term or trunc
+        n += 1
+    assert term and any("crashed" in s for s in info["termination_reasons"])
+    z = obs[:, 2]
+    assert (z < 0.03).any()
+    env.close()
