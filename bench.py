@@ -103,25 +103,38 @@ def main():
         sw.step(None, obs=obs_buf[k], reward=rew_buf[k], terminated=te_buf[k], truncated=tr_buf[k],
                 actions_out=act_buf[k])
 
+    # The rollout loop is captured once as a HIP graph of `slots` step launches
+    # (one per rollout-buffer slot) and replayed: the host launches one graph
+    # per `slots` steps instead of one kernel per step.
     for t in range(args.warmup):
         step(t)
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=stream):
+        for k in range(args.slots):
+            step(k)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    n_rep = (args.steps + args.slots - 1) // args.slots
+    steps = n_rep * args.slots
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_rep)]
+    cur = torch.cuda.current_stream()
     t0 = time.perf_counter()
-    for t in range(args.steps):
-        ev[t][0].record(stream)
-        step(args.warmup + t)
-        ev[t][1].record(stream)
+    for r in range(n_rep):
+        ev[r][0].record(cur)
+        graph.replay()
+        ev[r][1].record(cur)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # mean step-kernel duration on the launch stream: graph time / launches per graph
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) / args.slots
+    args.steps = steps
     if dist:
         t = torch.tensor([elapsed], device=sw.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

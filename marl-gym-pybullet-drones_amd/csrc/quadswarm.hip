@@ -11,7 +11,7 @@
 // [field][N] (N = E*D, agent a = env*D + drone) so lane i of a wavefront
 // touches element i of every field — every state load/store is a fully
 // coalesced 256 B (fp32) wave access.  A workgroup owns whole envs
-// (EPB = floor(256/D) envs × D drones), so the per-env reductions (reward
+// (EPB = floor(64/D) envs × D drones, one wavefront), so the per-env reductions (reward
 // mean, any-terminated), the O(D²) downwash neighbour scan and the reset
 // rejection search all run through LDS with no inter-workgroup traffic.
 // The path is elementwise ODE + a small PID: no contraction, so no MFMA; the
@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <cmath>
 #include <string>
@@ -29,7 +30,10 @@
 
 namespace qs {
 
-constexpr int kBlock = 256;          // threads per workgroup (4 waves)
+// One wavefront per workgroup: a wave owns floor(64/D) whole envs, so every
+// per-env reduction, neighbour scan and reset search stays inside one wave and
+// the workgroup barriers below cost nothing (no inter-wave coupling).
+constexpr int kBlock = 64;
 constexpr uint32_t kMaxResetTries = 1u << 24;
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
 enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
@@ -63,7 +67,27 @@ template <> struct M<double> {
 
 template <class T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// sin/cos of the exp-map half angle θ = |ω|·dt/2 (BaseAviary.py:890-891).  θ is
+// small in flight (|ω| ≲ 100 rad/s ⇒ θ ≲ 0.21); a degree-9/10 Taylor series is
+// then exact to < 1e-13 relative, far below fp32 rounding, and ~6× cheaper
+// than the range-reduced library sin/cos.  Large θ falls back to the library.
+template <class T> __device__ __forceinline__ void half_angle_sincos(T th, T& sn, T& cs) {
+  if (th < T(0.25)) {
+    const T t2 = th * th;
+    sn = th * (T(1) - t2 * (T(1) / T(6)) * (T(1) - t2 * (T(1) / T(20)) * (T(1) - t2 * (T(1) / T(42)) *
+                                                                           (T(1) - t2 * (T(1) / T(72))))));
+    cs = T(1) - t2 * T(0.5) * (T(1) - t2 * (T(1) / T(12)) * (T(1) - t2 * (T(1) / T(30)) *
+                                                          (T(1) - t2 * (T(1) / T(56)))));
+  } else {
+    sn = M<T>::sin_(th);
+    cs = M<T>::cos_(th);
+  }
+}
+
 // Philox4x32-10 (Random123).  Same stream definition as the oracle.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* g_ptr_t;
+
 struct U4 { uint32_t x, y, z, w; };
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -102,6 +126,9 @@ template <class T> struct Params {
   unsigned long long* log_count;
   long long log_cap;
   int* err;               // [1] reset search overflow flag
+  int stage_rows;         // obs rows staged in LDS per pass
+  int ablate;             // dev-only phase ablation (QS_ABLATE env var), 0 in production
+  unsigned long long* stamps;   // dev-only phase timestamps (QS_STAMPS env var), null in production
   // per-step I/O
   const uint8_t* reset_mask;   // MODE_RESET_MASK: [E] or NULL (= all)
   const float* act_in;
@@ -258,6 +285,12 @@ __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, i
   (void)lenv;
 }
 
+template <class T> __device__ __forceinline__ int valid_rows_in_block(const Params<T>& P) {
+  const int e0 = blockIdx.x * P.EPB;
+  const int ne = min(P.EPB, P.E - e0);
+  return ne * P.D;
+}
+
 // ---------------------------------------------------------------- the step
 template <class T>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
@@ -270,6 +303,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const bool valid = (lenv < P.EPB) && (e < P.E);
   const int a = e * D + d;
   const uint32_t genv = (uint32_t)(P.env_offset + e);
+#define QS_STAMP(k)                                                                         \
+  do {                                                                                      \
+    if (P.stamps && tid == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  QS_STAMP(0);
 
   // ---------------- load state
   T pos[3] = {0, 0, 0}, q[4] = {0, 0, 0, 1}, vel[3] = {0, 0, 0}, w[3] = {0, 0, 0}, lrpm[4] = {0, 0, 0, 0};
@@ -303,15 +341,48 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     ep_len = P.env[QS_E_EP_LEN * P.E + e];
   }
   const int A = P.A, H = P.H, O = P.O;
+  // ---------------- async prefetch of the H-1 older action-history entries the
+  // obs rows need (BaseRLAviary.py:317-318), straight into LDS by LDS-DMA, issued
+  // together with the state loads so the ring read costs no extra latency phase.
+  // LDS image is lane-linear [entry][lane][A] (DMA destination = base + lane*size).
+  extern __shared__ float dyn_lds[];
+  float* const hist_pref = dyn_lds;
+  float* const stage = dyn_lds + (size_t)(H - 1) * kBlock * A;
+  const bool want_obs = (P.obs != nullptr) || (P.tobs != nullptr);
+  if (want_obs) {
+    const int a_src = valid ? a : blockIdx.x * P.EPB * D;   // idle lanes read a valid row
+    const int tot_obs = total + (P.mode == MODE_STEP ? 1 : 0);
+    for (int i = 0; i < H - 1; ++i) {
+      const int slot = (tot_obs + i) % H;
+      const float* src = P.hist + ((size_t)slot * N + a_src) * A;
+      lds_ptr_t dst = (lds_ptr_t)(hist_pref + (size_t)i * kBlock * A);
+      if (A == 1) {
+        __builtin_amdgcn_global_load_lds((g_ptr_t)src, dst, 4, 0, 0);
+      } else if (A == 3) {   // [entry][k][lane]: dwordx3 DMA does not land lane-linear at 12 B
+        for (int k = 0; k < 3; ++k)
+          __builtin_amdgcn_global_load_lds((g_ptr_t)(src + k), (lds_ptr_t)(hist_pref + ((size_t)i * 3 + k) * kBlock),
+                                           4, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds((g_ptr_t)src, dst, 16, 0, 0);
+      }
+    }
+  }
   T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
   bool done_env = false;
   int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
   uint8_t bits = 0;
   T rterm = 0;
 
+  float cur_act[4] = {0, 0, 0, 0};   // this step's action (newest history entry)
+  if (P.mode != MODE_STEP && valid && total > 0) {
+    const int slot = (total - 1) % H;
+    for (int k = 0; k < A; ++k) cur_act[k] = P.hist[((size_t)slot * N + a) * A + k];
+  }
+  if (P.stamps) { volatile T sink = pos[0] + q[3] + pid[0] + tgt[0] + (T)total; (void)sink; }
+  QS_STAMP(1);
   if (P.mode == MODE_STEP) {
     // ---------------- action (trainer-provided or synthetic random policy)
-    float act[4] = {0, 0, 0, 0};
+    float* act = cur_act;
     if (valid) {
       if (P.act_in) {
         for (int k = 0; k < A; ++k) act[k] = P.act_in[(size_t)a * A + k];
@@ -329,7 +400,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // ---------------- _preprocessAction (BaseRLAviary.py:188-239)
     T rpm[4] = {0, 0, 0, 0};
     quat_to_rpy(q, rpy);
-    if (valid) {
+    if (valid && (P.ablate & 1)) { rpm[0] = rpm[1] = rpm[2] = rpm[3] = P.HOVER_RPM; }
+    else if (valid) {
       const T z3[3] = {0, 0, 0};
       switch (P.act_type) {
         case QS_ACT_RPM:
@@ -364,6 +436,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         default: break;
       }
     }
+    QS_STAMP(2);
     // ---------------- PYB_STEPS_PER_CTRL substeps (BaseAviary.py:343-372)
     T f[4], zt[4];
 #pragma unroll
@@ -373,7 +446,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * P.L_SQRT2;
     const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * P.L_SQRT2;
     const bool dw = (P.aux & QS_AUX_DW) != 0;
-    for (int sub = 0; sub < P.S; ++sub) {
+    const int nsub = (P.ablate & 2) ? 1 : P.S;
+    for (int sub = 0; sub < nsub; ++sub) {
       T R[9];
       quat_to_rot(q, R);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
@@ -436,9 +510,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       for (int i = 0; i < 3; ++i) pos[i] = pos[i] + P.dt * vel[i];
       // _integrateQ (BaseAviary.py:879-892)
       T wn = F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-      if (!(F::abs_(wn) <= T(1e-8))) {
+      if (!(F::abs_(wn) <= T(1e-8)) && !(P.ablate & 8)) {
         T th = wn * P.dt / T(2);
-        T c = F::cos_(th), sn = F::sin_(th);
+        T c, sn;
+        half_angle_sincos(th, sn, c);
         T k = (T(2) / wn) * T(0.5) * sn;   // (2/|ω|)·(0.5·Λ)·sinθ
         T p_ = w[0], q_ = w[1], r_ = w[2];
         T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
@@ -456,6 +531,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
     quat_to_rpy(q, rpy);   // readback (BaseAviary.py:374, 518)
     total += 1;
+    QS_STAMP(3);
 
     // ---------------- reward / termination per drone
     if (valid) {
@@ -541,16 +617,16 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const bool do_reset = done_env && !(P.mode == MODE_STEP && (P.flags & QS_FLAG_NO_AUTORESET));
 
   // ---------------- obs writer (BaseRLAviary._computeObs + Spiral extras)
-  auto write_obs = [&](float* dst, const T* p_, const T* r_, const T* v_, const T* av_, const T* q_, int sc) {
-    float* o = dst + (size_t)a * O;
+  auto write_obs_row = [&](float* o, const T* p_, const T* r_, const T* v_, const T* av_, const T* q_, int sc) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       o[i] = (float)p_[i]; o[3 + i] = (float)r_[i]; o[6 + i] = (float)v_[i]; o[9 + i] = (float)av_[i];
     }
-    for (int i = 0; i < H; ++i) {
-      const int slot = (total + i) % H;
-      for (int k = 0; k < A; ++k) o[12 + i * A + k] = P.hist[((size_t)slot * N + a) * A + k];
-    }
+    for (int i = 0; i < H - 1 && !(P.ablate & 16); ++i)   // older entries, prefetched into LDS
+      for (int k = 0; k < A; ++k)
+        o[12 + i * A + k] = (A == 3) ? hist_pref[((size_t)i * 3 + k) * kBlock + tid]
+                                     : hist_pref[((size_t)i * kBlock + tid) * A + k];
+    for (int k = 0; k < A; ++k) o[12 + (H - 1) * A + k] = cur_act[k];   // newest = this step's action
     if (P.task == QS_TASK_SPIRAL) {
       T t = T((double)sc / (double)P.pyb_freq);
       T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
@@ -565,8 +641,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
   };
 
+  QS_STAMP(4);
+  if (want_obs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // history LDS-DMA landed
   if (valid && done_env && P.mode == MODE_STEP && P.tobs)
-    write_obs(P.tobs, pos, rpy, vel, angv, q, obs_sc);
+    write_obs_row(P.tobs + (size_t)a * O, pos, rpy, vel, angv, q, obs_sc);
 
   // ---------------- auto-reset (worker.step_env → env.reset)
   s.any = 0;
@@ -641,8 +719,38 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
   }
 
+  QS_STAMP(5);
+  // ---------------- obs output
+  if (P.obs && !(P.ablate & 4)) {
+    if (P.mode == MODE_RESET_MASK) {
+      if (valid && do_reset) write_obs_row(P.obs + (size_t)a * O, pos, rpy, vel, angv, q, obs_sc);
+    } else {
+      // The block's obs rows are one contiguous span of HBM: build them in LDS
+      // and store the span with 16-byte coalesced stores (a per-lane row store
+      // touches 64 lines per wave instruction and doubled the write traffic).
+      const int nvalid = valid_rows_in_block(P);
+      const long long row0 = (long long)blockIdx.x * P.EPB * D;
+      for (int p0 = 0; p0 < nvalid; p0 += P.stage_rows) {   // block-uniform
+        const int p1 = min(nvalid, p0 + P.stage_rows);
+        if (tid >= p0 && tid < p1) write_obs_row(stage + (size_t)(tid - p0) * O, pos, rpy, vel, angv, q, obs_sc);
+        __syncthreads();
+        const long long g0 = (row0 + p0) * O, g1 = (row0 + p1) * O;
+        long long head = (g0 + 3) & ~3LL;
+        if (head > g1) head = g1;
+        long long tail = g1 & ~3LL;
+        if (tail < head) tail = head;
+        for (long long i = g0 + tid; i < head; i += kBlock) P.obs[i] = stage[i - g0];
+        for (long long i = head + 4LL * tid; i < tail; i += 4LL * kBlock) {
+          const long long j = i - g0;
+          *reinterpret_cast<float4*>(P.obs + i) = make_float4(stage[j], stage[j + 1], stage[j + 2], stage[j + 3]);
+        }
+        for (long long i = tail + tid; i < g1; i += kBlock) P.obs[i] = stage[i - g0];
+        __syncthreads();
+      }
+    }
+  }
+  QS_STAMP(6);
   if (!valid) return;
-  if (P.obs && (P.mode != MODE_RESET_MASK || do_reset)) write_obs(P.obs, pos, rpy, vel, angv, q, obs_sc);
 
   // ---------------- store state
 #pragma unroll
@@ -715,6 +823,7 @@ struct qs_handle {
   unsigned long long* log_count = nullptr;
   long long log_cap = 0;
   int* err = nullptr;
+  unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
   uint64_t seed = 0;
   bool reset_done = false;
   std::vector<double> orig_host;
@@ -751,11 +860,18 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.sp_cx = T(s.target_center[0]); P.sp_cy = T(s.target_center[1]); P.sp_cz = T(s.target_center[2]);
   P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.ep_return = h->ep_return; P.orig_xyz = (const T*)h->orig;
   P.log = h->log; P.log_count = h->log_count; P.log_cap = h->log_cap; P.err = h->err;
+  static const int ablate = getenv("QS_ABLATE") ? atoi(getenv("QS_ABLATE")) : 0;   // dev experiments only
+  P.ablate = ablate;
+  P.stamps = h->stamps;
 }
 
 template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t st) {
   const int grid = (P.E + P.EPB - 1) / P.EPB;
-  hipLaunchKernelGGL(qs::step_kernel<T>, dim3(grid), dim3(qs::kBlock), 0, st, P);
+  // obs staging: as many rows per pass as fit a 64 KiB LDS budget
+  const int rows = P.EPB * P.D;
+  P.stage_rows = std::max(1, std::min(rows, (48 * 1024) / (4 * P.O)));
+  const size_t lds = ((size_t)P.stage_rows * P.O + (size_t)(P.H - 1) * qs::kBlock * P.A) * sizeof(float);
+  hipLaunchKernelGGL(qs::step_kernel<T>, dim3(grid), dim3(qs::kBlock), lds, st, P);
   HIP_TRY(hipGetLastError());
   return QS_OK;
 }
@@ -838,14 +954,27 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
       hipMemset(h->log_count, 0, sizeof(unsigned long long)) || hipMemset(h->err, 0, sizeof(int))) {
     cleanup(); return fail(QS_E_HIP, "qs_create: memset");
   }
+  if (getenv("QS_STAMPS")) {   // dev-only phase timestamps
+    const int grid = (s.num_envs + qs::kBlock / s.num_drones - 1) / (qs::kBlock / s.num_drones);
+    if (hipMalloc((void**)&h->stamps, sizeof(unsigned long long) * 8 * grid) == hipSuccess)
+      hipMemset(h->stamps, 0, sizeof(unsigned long long) * 8 * grid);
+  }
   *out = h;
+  return QS_OK;
+}
+
+// dev-only: copy the per-wave phase timestamps (8 per workgroup) to host.
+extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n) {
+  if (!h || !h->stamps) return fail(QS_E_STATE, "QS_STAMPS not enabled");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(host, h->stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
   return QS_OK;
 }
 
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
   hipSetDevice(h->device);
-  void* ptrs[] = {h->st, h->env, h->hist, h->ep_return, h->orig, h->log, h->log_count, h->err};
+  void* ptrs[] = {h->st, h->env, h->hist, h->ep_return, h->orig, h->log, h->log_count, h->err, h->stamps};
   for (void* p : ptrs) if (p) hipFree(p);
   delete h;
   return QS_OK;

@@ -1,0 +1,28 @@
+"""Dev: per-wave phase timestamps of the step kernel (QS_STAMPS=1)."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "marl-gym-pybullet-drones_amd"))
+os.environ["QS_STAMPS"] = "1"
+import numpy as np, torch
+from gym_pybullet_drones_amd import _lib as L
+from gym_pybullet_drones_amd.envs import QuadSwarm, grid_layout
+E, D = 16384, 8
+sw = QuadSwarm("multihover", num_envs=E, num_drones=D, act="one_d_pid", precision=4, initial_xyzs=grid_layout(D))
+obs = torch.empty((E, D, sw.obs_dim), device="cuda"); act = torch.empty((E, D, 1), device="cuda")
+sw.reset(0, obs=obs)
+for t in range(20):
+    sw.step(None, obs=obs, actions_out=act)
+torch.cuda.synchronize()
+G = E // (64 // D)
+buf = np.zeros(G * 8, np.uint64)
+lib = L.load(); lib.qs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+L.check(lib.qs_debug_stamps(sw._h, buf.ctypes.data_as(ctypes.c_void_p), G * 8), "stamps")
+st = buf.reshape(G, 8).astype(np.float64) * 10e-3   # 100 MHz → µs
+t0 = st[:, 0].min()
+names = ["start", "loads used", "action/pid done", "substeps done", "reward/reset done", "obs waited", "obs stored"]
+print("phase (µs, relative to first wave start): p10 / median / p90")
+for k in range(7):
+    v = st[:, k] - t0
+    print(f"{names[k]:20s} {np.percentile(v,10):7.2f} {np.median(v):7.2f} {np.percentile(v,90):7.2f}")
+d = np.diff(st[:, :7], axis=1)
+print("per-wave phase durations median:", np.round(np.median(d, axis=0), 2))
