@@ -57,7 +57,9 @@ EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq"
 
 # Every symbol include/quadswarm.h declares (tests check the .so exports them).
 EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
-           "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy")
+           "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
+           # include/qs_learner.h
+           "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_learner_last_error")
 
 _lib = None
 
@@ -93,8 +95,14 @@ def load():
     L.qs_episode_log.argtypes = [vp, vp, i64, ctypes.POINTER(i64), vp]
     L.qs_reset_error.argtypes = [vp, ctypes.POINTER(i32)]
     L.qs_calib_copy.argtypes = [vp, vp, i64, vp]
+    L.qs_gae.argtypes = [ctypes.c_int32, i64, vp, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_int32,
+                         vp, vp, vp]
+    f32 = ctypes.c_float
+    L.qs_adam_gated.argtypes = [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, f32, vp]
+    L.qs_adam_commit.argtypes = [vp, vp, f32, vp]
+    L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
-        if name != "qs_last_error":
+        if name not in ("qs_last_error", "qs_learner_last_error"):
             getattr(L, name).restype = i32
     _lib = L
     return L
@@ -102,7 +110,8 @@ def load():
 
 def check(rc, what=""):
     if rc != QS_OK:
-        msg = load().qs_last_error()
+        lib = load()
+        msg = lib.qs_learner_last_error() if what.startswith(("qs_gae", "qs_adam")) else lib.qs_last_error()
         raise QuadSwarmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
 
 

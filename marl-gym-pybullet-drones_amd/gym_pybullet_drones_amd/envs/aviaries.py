@@ -51,7 +51,16 @@ class _SingleEnvAviary:
         self.ACTION_BUFFER_SIZE = ctrl_freq // 2
         self.EPISODE_LEN_SEC = self.swarm.episode_len_sec
         self._started = False
+        self._vec_spec = dict(task=self.TASK, num_drones=num_drones, act=ActionType(act), physics=Physics(physics),
+                              pyb_freq=pyb_freq, ctrl_freq=ctrl_freq, precision=precision,
+                              initial_xyzs=None if initial_xyzs is None else np.asarray(initial_xyzs, np.float64),
+                              **task_kw)
         self.swarm.reset(0)
+
+    def vec_spec(self):
+        """Constructor kwargs that rebuild this env as a batched SwarmVecEnv (used by MAPPO
+        in place of make_vec_envs(env_func, ...), vectorized_env/__init__.py:42-66)."""
+        return dict(self._vec_spec)
 
     @property
     def step_counter(self):

@@ -1,0 +1,394 @@
+"""MAPPO agent: shared-weight Gaussian actor + centralized critic, PPO update on device.
+
+Same model and loss semantics as gym_pybullet_drones/mappo/agent.py:
+  MLP (safe_control_gym/math_and_models/neural_networks.py:18-54, default init)
+  MLPActor AG:87-148 (logstd init -0.5, Normal(mean, exp(logstd)))
+  CentralizedCritic AG:164-223 (D·O → hidden → hidden → 1 on concatenated obs)
+  MAPPOActorCritic.step AG:389-415 (batched sample; v returned as zeros)
+  compute_policy_loss AG:602-640, compute_value_loss AG:642-700, update AG:702-772
+  (actor Adam step only if approx_kl <= 1.5·target_kl; critic step always;
+  max_grad_norm configured but not applied — as in the reference)
+
+MI355X-specific structure:
+  * actor and critic parameters/gradients live in one flat fp32 buffer each;
+    autograd accumulates into `.grad` views of it, so one RCCL all-reduce per
+    model and one fused Adam launch (qs_adam_gated, HIP) update everything;
+  * the KL gate is evaluated on the device by that kernel — no host sync per
+    minibatch — so a whole update iteration (gather, forward, backward, both
+    optimizer steps, stats) is captured once as a HIP graph and replayed;
+  * under torch.distributed, approx_kl and the gradients are averaged across
+    ranks before the gate/step, so every rank takes the same branch.
+"""
+import ctypes
+import math
+from collections import defaultdict
+
+import torch
+import torch.distributed as tdist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib as L
+
+
+def get_activation(name):
+    return getattr(torch, name) if name in ("tanh", "relu", "sigmoid") else (getattr(F, name) if name else (lambda x: x))
+
+
+class MLP(nn.Module):
+    """neural_networks.py:18-54 (nn.Linear default init; init_weights=False there)."""
+
+    def __init__(self, input_dim, output_dim, hidden_dims=(), act='relu', output_act=None, **kwargs):
+        super().__init__()
+        dims = [input_dim] + list(hidden_dims) + [output_dim]
+        self.fcs = nn.ModuleList([nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1)])
+        self.act = get_activation(act)
+        self.output_act = get_activation(output_act)
+
+    def forward(self, x):
+        out = x
+        for fc in self.fcs[:-1]:
+            out = self.act(fc(out))
+        return self.output_act(self.fcs[-1](out))
+
+
+class Normal(torch.distributions.Normal):
+    """distributions.py:9-33: log_prob summed over the last axis (keepdim), entropy summed, mode = mean."""
+
+    def __init__(self, loc, scale):
+        super().__init__(loc, scale, validate_args=False)   # validation would force host syncs
+
+    def log_prob(self, actions):
+        return super().log_prob(actions).sum(-1, keepdim=True)
+
+    def entropy(self):
+        return super().entropy().sum(-1)
+
+    def mode(self):
+        return self.mean
+
+    def sample(self, sample_shape=torch.Size()):
+        # torch.normal(loc, scale) validates scale >= 0 with a device→host read, which
+        # cannot be captured in a graph; loc + scale·ε is the same distribution
+        shape = self._extended_shape(sample_shape)
+        with torch.no_grad():
+            return self.loc.expand(shape) + self.scale.expand(shape) * torch.randn(shape, dtype=self.loc.dtype,
+                                                                                 device=self.loc.device)
+
+
+class MLPActor(nn.Module):
+    def __init__(self, obs_dim, act_dim, hidden_dims, activation, discrete=False, action_scale=1.0):
+        super().__init__()
+        if discrete:
+            raise NotImplementedError("discrete actions are not used by the drone tasks")
+        self.pi_net = MLP(obs_dim, act_dim, hidden_dims, activation)
+        self.discrete = discrete
+        self.action_scale = action_scale
+        self.logstd = nn.Parameter(-0.5 * torch.ones(act_dim))
+
+    def dist(self, obs):
+        return Normal(self.pi_net(obs) * self.action_scale, self.logstd.exp())
+
+    def forward(self, obs, act=None):
+        dist = self.dist(obs)
+        return dist, (dist.log_prob(act) if act is not None else None)
+
+    def get_scaled_action(self, obs, deterministic=False):
+        dist = self.dist(obs)
+        return dist.mode() if deterministic else dist.sample()
+
+
+class CentralizedCritic(nn.Module):
+    def __init__(self, global_obs_dim, hidden_dims, activation, include_actions=False, action_dim=0):
+        super().__init__()
+        self.include_actions = include_actions
+        self.v_net = MLP(global_obs_dim + (action_dim if include_actions else 0), 1, hidden_dims, activation)
+
+    def forward(self, global_obs, actions=None):
+        x = global_obs.reshape(global_obs.shape[0], -1) if global_obs.dim() == 3 else global_obs
+        if self.include_actions and actions is not None:
+            x = torch.cat([x, actions.reshape(x.shape[0], -1)], dim=-1)
+        return self.v_net(x)
+
+
+class MAPPOActorCritic(nn.Module):
+    def __init__(self, obs_space, act_space, hidden_dims=(64, 64), activation='tanh', share_actor_weights=True,
+                 centralized_critic=True, include_actions_in_critic=False, global_state_dim=None, action_scale=1.0):
+        super().__init__()
+        obs_shape, act_shape = tuple(obs_space.shape), tuple(act_space.shape)
+        if len(obs_shape) == 1:
+            num_agents, obs_dim = 1, obs_shape[0]
+        else:
+            num_agents, obs_dim = obs_shape
+        act_dim = act_shape[-1]
+        if len(act_shape) == 2 and num_agents == 1:
+            num_agents = act_shape[0]
+        if not share_actor_weights or not centralized_critic:
+            raise NotImplementedError("only share_actor_weights=True with centralized_critic=True (the configuration "
+                                      "of both reference MAPPO scripts) is implemented")
+        self.num_agents, self.obs_dim, self.act_dim = num_agents, obs_dim, act_dim
+        self.share_actor_weights, self.centralized_critic = share_actor_weights, centralized_critic
+        self.include_actions_in_critic = include_actions_in_critic
+        self.action_scale = action_scale
+        self.actor = MLPActor(obs_dim, act_dim, list(hidden_dims), activation, False, action_scale)
+        gdim = global_state_dim if global_state_dim is not None else num_agents * obs_dim
+        self.critic = CentralizedCritic(gdim, list(hidden_dims), activation, include_actions_in_critic,
+                                        num_agents * act_dim if include_actions_in_critic else 0)
+
+    def get_actor(self, agent_idx=None):
+        return self.actor
+
+    @torch.no_grad()
+    def step(self, obs, get_global_obs_fn=None):
+        """Batched branch of AG:389-415 on device tensors: obs (E, D, O) or (E·D, O)."""
+        shape = obs.shape
+        flat = obs.reshape(-1, self.obs_dim)
+        dist = self.actor.dist(flat)
+        act = dist.sample()
+        if self.action_scale != 1.0:
+            act = act * self.action_scale
+        logp = dist.log_prob(act)
+        if len(shape) == 3:
+            E, D = shape[0], shape[1]
+        else:
+            D = self.num_agents
+            E = flat.shape[0] // D
+        return act.reshape(E, D, -1), torch.zeros(E, D, 1, device=obs.device), logp.reshape(E, D, 1)
+
+    @torch.no_grad()
+    def act(self, obs):
+        """Deterministic actions (dist.mode) for evaluation (AG:425-449)."""
+        return self.actor.dist(obs.reshape(-1, self.obs_dim)).mode().reshape(*obs.shape[:-1], self.act_dim)
+
+    def get_value(self, global_obs, actions=None, agent_idx=None):
+        return self.critic(global_obs, actions)
+
+    def get_actor_logp(self, obs, act, agent_idx=None):
+        return self.actor(obs, act)[1]
+
+    def get_entropy(self, obs, agent_idx=None):
+        return self.actor(obs)[0].entropy()
+
+
+class FlatBuffers:
+    """Parameters, gradients and Adam moments of one module in flat fp32 buffers."""
+
+    def __init__(self, module, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.params = [p for p in module.parameters()]
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.n = n
+        self.flat = torch.zeros(n, device=dev)
+        self.grad = torch.zeros(n, device=dev)
+        self.exp_avg = torch.zeros(n, device=dev)
+        self.exp_avg_sq = torch.zeros(n, device=dev)
+        self.step = torch.zeros(1, device=dev)
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            self.offsets.append((off, k))
+            off += k
+        self.lr, self.betas, self.eps = lr, betas, eps
+
+    def adam(self, gate_val=None, gate_thr=0.0):
+        lib = L.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.check(lib.qs_adam_gated(self.n, L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.exp_avg),
+                                  L.ptr(self.exp_avg_sq), L.ptr(self.step), self.lr, self.betas[0], self.betas[1],
+                                  self.eps, L.ptr(gate_val), float(gate_thr), st), "qs_adam_gated")
+        L.check(lib.qs_adam_commit(L.ptr(self.step), L.ptr(gate_val), float(gate_thr), st), "qs_adam_commit")
+
+    # torch.optim.Adam state_dict format (checkpoint compatibility, MP:203-229)
+    def state_dict(self):
+        state = {}
+        for i, (off, k) in enumerate(self.offsets):
+            if float(self.step.item()) > 0:
+                state[i] = {'step': self.step.detach().cpu().reshape(()).clone(),
+                            'exp_avg': self.exp_avg[off:off + k].view_as(self.params[i]).detach().clone(),
+                            'exp_avg_sq': self.exp_avg_sq[off:off + k].view_as(self.params[i]).detach().clone()}
+        group = {'lr': self.lr, 'betas': self.betas, 'eps': self.eps, 'weight_decay': 0, 'amsgrad': False,
+                 'maximize': False, 'foreach': None, 'capturable': False, 'differentiable': False, 'fused': None,
+                 'params': list(range(len(self.params)))}
+        return {'state': state, 'param_groups': [group]}
+
+    def load_state_dict(self, sd):
+        g = sd['param_groups'][0]
+        self.lr, self.betas, self.eps = g['lr'], tuple(g['betas']), g['eps']
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        self.step.zero_()
+        for i, s in sd['state'].items():
+            off, k = self.offsets[int(i)]
+            self.exp_avg[off:off + k].copy_(s['exp_avg'].reshape(-1))
+            self.exp_avg_sq[off:off + k].copy_(s['exp_avg_sq'].reshape(-1))
+            self.step.fill_(float(s['step']))
+
+
+def _dist_world():
+    return tdist.get_world_size() if (tdist.is_available() and tdist.is_initialized()) else 1
+
+
+class MAPPOAgent:
+    """AG:501-772 with the update on device (flat buffers, gated HIP Adam, optional graph)."""
+
+    def __init__(self, obs_space, act_space, hidden_dim=256, use_clipped_value=False, clip_param=0.2, target_kl=0.01,
+                 entropy_coef=0.01, actor_lr=0.0003, critic_lr=0.001, opt_epochs=10, mini_batch_size=64,
+                 activation='tanh', share_actor_weights=True, centralized_critic=True, include_actions_in_critic=False,
+                 global_state_dim=None, action_scale=1.0, use_graphs=True, device='cuda', **kwargs):
+        self.obs_space, self.act_space = obs_space, act_space
+        self.use_clipped_value, self.clip_param, self.target_kl = use_clipped_value, clip_param, target_kl
+        self.entropy_coef, self.opt_epochs, self.mini_batch_size = entropy_coef, opt_epochs, mini_batch_size
+        self.activation = activation
+        self.share_actor_weights, self.centralized_critic = share_actor_weights, centralized_critic
+        self.include_actions_in_critic = include_actions_in_critic
+        self.action_scale = action_scale
+        self.use_graphs = use_graphs
+        self.device = torch.device(device)
+        self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
+                                   share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
+                                   include_actions_in_critic=include_actions_in_critic,
+                                   global_state_dim=global_state_dim, action_scale=action_scale)
+        self.actor_lr, self.critic_lr = actor_lr, critic_lr
+        self._opt_ready = False
+        self._graph = None
+        self.to(self.device)
+
+    # ------------------------------------------------------------ plumbing
+    def to(self, device):
+        self.device = torch.device(device)
+        self.ac.to(self.device)
+        if self.device.type == 'cuda':
+            self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr)
+            self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr)
+            if _dist_world() > 1:   # identical initial weights on every rank
+                tdist.broadcast(self.actor_opt.flat, 0)
+                tdist.broadcast(self.critic_opt.flat, 0)
+            self._opt_ready = True
+            self._graph = None
+
+    def train(self):
+        self.ac.train()
+
+    def eval(self):
+        self.ac.eval()
+
+    def state_dict(self):
+        return {'ac': self.ac.state_dict(), 'actor_opt': self.actor_opt.state_dict(),
+                'critic_opt': self.critic_opt.state_dict()}
+
+    def load_state_dict(self, state_dict):
+        self.ac.load_state_dict(state_dict['ac'])   # copies into the flat-buffer views in place
+        self.actor_opt.load_state_dict(state_dict['actor_opt'])
+        self.critic_opt.load_state_dict(state_dict['critic_opt'])
+
+    # ------------------------------------------------------------- losses
+    def compute_policy_loss(self, batch, agent_idx=None):
+        """AG:602-640."""
+        obs, act, logp_old, adv = batch['obs'], batch['act'], batch['logp'], batch['adv']
+        dist = self.ac.actor.dist(obs)
+        logp = dist.log_prob(act)
+        ratio = torch.exp(logp - logp_old)
+        clip_adv = torch.clamp(ratio, 1 - self.clip_param, 1 + self.clip_param) * adv
+        policy_loss = -torch.min(ratio * adv, clip_adv).mean()
+        entropy_loss = -dist.entropy().mean()   # the reference re-runs the actor; same value
+        approx_kl = (logp_old - logp).mean()
+        return policy_loss, entropy_loss, approx_kl
+
+    def compute_value_loss(self, batch, agent_idx=None):
+        """AG:642-683 (centralized critic, ret averaged over agents)."""
+        global_obs, ret = batch['global_obs'], batch['ret']
+        v_cur = self.ac.get_value(global_obs, batch.get('act') if self.include_actions_in_critic else None)
+        if ret.dim() == 3:
+            ret = ret.mean(dim=1, keepdim=True)
+        if v_cur.shape != ret.shape:
+            ret = ret.reshape(v_cur.shape)
+        if self.use_clipped_value:
+            v_old = batch.get('v', torch.zeros_like(v_cur)).mean(dim=1) if batch.get('v') is not None else 0 * v_cur
+            v_old = v_old.reshape(v_cur.shape)
+            v_old_clipped = v_old + (v_cur - v_old).clamp(-self.clip_param, self.clip_param)
+            return 0.5 * torch.max((v_cur - ret).pow(2), (v_old_clipped - ret).pow(2)).mean()
+        return 0.5 * (v_cur - ret).pow(2).mean()
+
+    # ------------------------------------------------------------- update
+    def _iteration(self, batch, acc):
+        """One minibatch: actor step (KL-gated on device), critic step, stat accumulation."""
+        world = _dist_world()
+        policy_loss, entropy_loss, approx_kl = self.compute_policy_loss(batch)
+        self.actor_opt.grad.zero_()
+        (policy_loss + self.entropy_coef * entropy_loss).backward()
+        kl = approx_kl.detach().float().reshape(1)
+        if world > 1:
+            tdist.all_reduce(self.actor_opt.grad)
+            self.actor_opt.grad.div_(world)
+            tdist.all_reduce(kl)
+            kl = kl / world
+        gate = kl if self.target_kl > 0 else None
+        self.actor_opt.adam(gate, 1.5 * self.target_kl)
+        value_loss = self.compute_value_loss(batch)
+        self.critic_opt.grad.zero_()
+        value_loss.backward()
+        if world > 1:
+            tdist.all_reduce(self.critic_opt.grad)
+            self.critic_opt.grad.div_(world)
+        self.critic_opt.adam(None, 0.0)
+        acc += torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
+                            entropy_loss.detach().double(), approx_kl.detach().double()])
+
+    def _capture(self, rollouts):
+        """Capture one update iteration as a HIP graph over static index/accumulator tensors."""
+        mb = self.mini_batch_size
+        self._g_idx = torch.zeros(mb, dtype=torch.long, device=self.device)
+        self._g_acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self._g_rollouts = rollouts
+        # warm-up on a side stream (torch.cuda.graph requirement), with a snapshot/restore of
+        # the parameters and optimizer state so the warm-up leaves no trace
+        snap = [t.clone() for t in (self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq,
+                                    self.actor_opt.step, self.critic_opt.flat, self.critic_opt.exp_avg,
+                                    self.critic_opt.exp_avg_sq, self.critic_opt.step)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._iteration(rollouts.sample(self._g_idx), self._g_acc)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._iteration(rollouts.sample(self._g_idx), self._g_acc)
+        for t, v in zip((self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq, self.actor_opt.step,
+                         self.critic_opt.flat, self.critic_opt.exp_avg, self.critic_opt.exp_avg_sq,
+                         self.critic_opt.step), snap):
+            t.copy_(v)
+        self._graph = g
+
+    def update(self, rollouts, device='cuda', generator=None):
+        """AG:702-772: opt_epochs × minibatches; per-epoch means of the loss stats."""
+        results = defaultdict(list)
+        total_steps = rollouts.max_length * rollouts.batch_size
+        num_mini_batch = total_steps // self.mini_batch_size
+        assert num_mini_batch != 0, 'num_mini_batch is 0'
+        graphs = self.use_graphs and self.device.type == 'cuda' and _dist_world() == 1
+        if graphs and (self._graph is None or self._g_rollouts is not rollouts):
+            self._capture(rollouts)
+        per_epoch = []
+        for epoch in range(self.opt_epochs):
+            perm = torch.randperm(total_steps, device=self.device, generator=generator)
+            if graphs:
+                self._g_acc.zero_()
+                for i in range(num_mini_batch):
+                    self._g_idx.copy_(perm[i * self.mini_batch_size:(i + 1) * self.mini_batch_size])
+                    self._graph.replay()
+                per_epoch.append(self._g_acc.clone())
+            else:
+                acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+                for i in range(num_mini_batch):
+                    self._iteration(rollouts.sample(perm[i * self.mini_batch_size:(i + 1) * self.mini_batch_size]),
+                                    acc)
+                per_epoch.append(acc)
+        stats = (torch.stack(per_epoch) / num_mini_batch).cpu()   # one host sync per update
+        for j, k in enumerate(['policy_loss', 'value_loss', 'entropy_loss', 'approx_kl']):
+            results[k] = float(stats[:, j].mean())
+        return dict(results)

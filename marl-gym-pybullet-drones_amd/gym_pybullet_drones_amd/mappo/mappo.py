@@ -1,0 +1,454 @@
+"""MAPPO controller with the rollout, GAE and PPO update resident on the GPU.
+
+Same constructor, attributes and methods as gym_pybullet_drones/mappo/mappo.py
+(MAPPO MP:23-1349): MAPPO(env_func, training, checkpoint_path, output_dir,
+use_gpu, seed, **MAPPO_CONFIG) with reset / learn / train_step / run /
+select_action / save / load / close.
+
+What changes:
+  * `env_func(seed=...)` is called once to obtain the env description (one of
+    this package's aviaries); the `rollout_batch_size` training envs are then a
+    single SwarmVecEnv on the GPU (no SubprocVecEnv / num_workers pool).  Under
+    torch.distributed every rank owns `rollout_batch_size` envs with global env
+    ids offset by rank (weak scaling), gradients are averaged over ranks.
+  * The rollout writes obs/actions/logp straight into the (T, E, D, ·) device
+    buffer; with `use_graphs` the whole T-step rollout (actor forward, Normal
+    sample, simulator step, reward/mask bookkeeping) is one HIP graph replay.
+  * total_steps counts env-steps over all ranks.
+Reference quirks kept (SURVEY §7 hard-5): v placeholders are zeros, terminal_v
+is zero (TimeLimit.truncated is never set), rewards are the per-env mean tiled
+over agents, termination_counts stay empty because auto-reset replaces the info
+(subproc_vec_env.py:195-206), obs are normalised twice on a done when
+norm_obs=True and reference_compat=True (MP:804, 1037).
+"""
+import os
+import random
+import time
+from collections import defaultdict, deque
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+from ..utils.enums import ActionType, Physics
+from ..vec_env import SwarmVecEnv, VecRecordEpisodeStatistics
+from .agent import MAPPOAgent
+from .buffer import MAPPOBuffer, normalize_advantages
+from .config import MAPPO_CONFIG
+from .normalization import BaseNormalizer, MeanStdNormalizer, RewardStdNormalizer
+
+
+def get_random_state():
+    """safe_control_gym/utils/utils.py:82-88 (+ the torch CUDA generator)."""
+    st = {'random': random.getstate(), 'numpy': np.random.get_state(), 'torch': torch.get_rng_state()}
+    if torch.cuda.is_available():
+        st['torch_cuda'] = torch.cuda.get_rng_state()
+    return st
+
+
+def set_random_state(st):
+    random.setstate(st['random'])
+    np.random.set_state(st['numpy'])
+    torch.set_rng_state(st['torch'])
+    if 'torch_cuda' in st and torch.cuda.is_available():
+        torch.cuda.set_rng_state(st['torch_cuda'])
+
+
+class ExperimentLogger:
+    """Minimal stand-in for safe_control_gym's ExperimentLogger (observability is out
+    of scope): stdout + one CSV of scalars per log_step."""
+
+    def __init__(self, log_dir, log_file_out=True, use_tensorboard=False):
+        self.log_dir = log_dir
+        self.rows = []
+        self.file = None
+        if log_file_out:
+            os.makedirs(log_dir, exist_ok=True)
+            self.file = open(os.path.join(log_dir, 'scalars.csv'), 'a')
+
+    def info(self, msg):
+        print(msg)
+
+    def add_scalars(self, data, step, prefix=None):
+        for k, v in data.items():
+            name = f"{prefix}/{k}" if prefix else k
+            self.rows.append((step, name, float(v)))
+
+    def dump_scalars(self):
+        if self.file:
+            for s, k, v in self.rows:
+                self.file.write(f"{s},{k},{v}\n")
+            self.file.flush()
+        self.rows = []
+
+    def close(self):
+        if self.file:
+            self.file.close()
+            self.file = None
+
+
+class RecordEpisodeStatistics:
+    """Single-env episode statistics (record_episode_statistics.py:13-94) for run()."""
+
+    def __init__(self, env, deque_size=None):
+        self.env = env
+        self.deque_size = deque_size
+        self.episode_return = 0.0
+        self.episode_length = 0
+        self.return_queue = deque(maxlen=deque_size)
+        self.length_queue = deque(maxlen=deque_size)
+        self.episode_stats, self.accumulated_stats, self.queued_stats = {}, {}, {}
+
+    def add_tracker(self, name, init_value, mode='accumulate'):
+        self.episode_stats[name] = init_value
+        if mode == 'accumulate':
+            self.accumulated_stats[name] = init_value
+        else:
+            self.queued_stats[name] = deque(maxlen=self.deque_size)
+
+    def reset(self, **kwargs):
+        self.episode_return, self.episode_length = 0.0, 0
+        for k in self.episode_stats:
+            self.episode_stats[k] *= 0
+        return self.env.reset(**kwargs)
+
+    def step(self, action):
+        obs, reward, terminated, truncated, info = self.env.step(action)
+        self.episode_return += reward
+        self.episode_length += 1
+        for k in self.episode_stats:
+            if k in info:
+                self.episode_stats[k] += info[k]
+        if terminated or truncated:
+            info['episode'] = {'r': self.episode_return, 'l': self.episode_length}
+            self.return_queue.append(self.episode_return)
+            self.length_queue.append(self.episode_length)
+            for k in self.episode_stats:
+                info['episode'][k] = self.episode_stats[k]
+                if k in self.queued_stats:
+                    self.queued_stats[k].append(self.episode_stats[k])
+                self.episode_stats[k] *= 0
+            self.episode_return, self.episode_length = 0.0, 0
+        return obs, reward, terminated, truncated, info
+
+    def __getattr__(self, name):
+        if name.startswith('_'):
+            raise AttributeError(name)
+        return getattr(self.env, name)
+
+
+def _env_spec(proto):
+    if isinstance(proto, dict):
+        return dict(proto)
+    if hasattr(proto, 'vec_spec'):
+        return proto.vec_spec()
+    raise TypeError("env_func must return one of gym_pybullet_drones_amd.envs' aviaries (or a dict spec)")
+
+
+class MAPPO:
+    '''Multi-Agent PPO with centralized training and decentralized execution (MP:23).'''
+
+    def __init__(self, env_func, training=True, checkpoint_path='model_latest.pt', output_dir='temp', use_gpu=False,
+                 seed=0, **kwargs):
+        config = MAPPO_CONFIG.copy()
+        config.update(kwargs)
+        config.setdefault('use_graphs', True)
+        config.setdefault('reference_compat', True)
+        for k, v in config.items():   # BaseController: kwargs → attributes
+            setattr(self, k, v)
+        self.env_func, self.training = env_func, training
+        self.checkpoint_path, self.output_dir, self.use_gpu, self.seed = checkpoint_path, output_dir, use_gpu, seed
+        if not torch.cuda.is_available():
+            raise RuntimeError("this MAPPO runs on the GPU only (the simulator is a HIP kernel)")
+        self.dist = tdist.is_available() and tdist.is_initialized()
+        self.rank = tdist.get_rank() if self.dist else 0
+        self.world = tdist.get_world_size() if self.dist else 1
+        self.device = torch.device('cuda', torch.cuda.current_device())
+        torch.manual_seed(seed + self.rank)
+        np.random.seed(seed + self.rank)
+        random.seed(seed + self.rank)
+        self.eval_env = None
+        proto = env_func(seed=seed)
+        spec = _env_spec(proto)
+        if training:
+            E = int(getattr(self, 'rollout_batch_size', 1))
+            venv = SwarmVecEnv(num_envs=E, seed=seed, device=self.device, env_offset=self.rank * E, **spec)
+            self.env = VecRecordEpisodeStatistics(venv, self.deque_size)
+            self.eval_env = RecordEpisodeStatistics(proto, self.deque_size)
+        else:
+            self.env = RecordEpisodeStatistics(proto)
+        self.is_vectorized = hasattr(self.env, 'num_envs')
+        self.num_envs = self.env.num_envs if self.is_vectorized else 1
+        obs_shape = self.env.observation_space.shape
+        self.num_agents, self.obs_dim = (1, obs_shape[0]) if len(obs_shape) == 1 else obs_shape
+        self.global_state_dim = self.num_agents * self.obs_dim
+        self.agent = MAPPOAgent(self.env.observation_space, self.env.action_space, hidden_dim=self.hidden_dim,
+                                use_clipped_value=self.use_clipped_value, clip_param=self.clip_param,
+                                target_kl=self.target_kl, entropy_coef=self.entropy_coef, actor_lr=self.actor_lr,
+                                critic_lr=self.critic_lr, opt_epochs=self.opt_epochs,
+                                mini_batch_size=self.mini_batch_size, activation=self.activation,
+                                share_actor_weights=self.share_actor_weights,
+                                centralized_critic=self.centralized_critic,
+                                include_actions_in_critic=self.include_actions_in_critic,
+                                global_state_dim=self.global_state_dim, use_graphs=self.use_graphs,
+                                device=self.device)
+        self.obs_normalizer = BaseNormalizer()
+        if self.norm_obs:
+            self.obs_normalizer = MeanStdNormalizer(shape=obs_shape, clip=self.clip_obs, epsilon=1e-8,
+                                                    device=self.device)
+        self.reward_normalizer = BaseNormalizer()
+        if self.norm_reward:
+            self.reward_normalizer = RewardStdNormalizer(gamma=self.gamma, clip=self.clip_reward, epsilon=1e-8,
+                                                         device=self.device)
+        self.logger = ExperimentLogger(output_dir, log_file_out=training and self.rank == 0)
+        self._rollouts = None
+        self._rollout_graph = None
+        self.total_steps = 0
+
+    # ----------------------------------------------------------------- misc
+    def reset(self):
+        '''MP:147-167.'''
+        if self.training:
+            self.total_steps = 0
+            if self.eval_env is not None:
+                self.eval_env.add_tracker('constraint_violation', 0, mode='queue')
+                self.eval_env.add_tracker('mse', 0, mode='queue')
+            obs = self.env.venv.reset_t() if self.is_vectorized else self.env.reset()[0]
+            self.obs = self.obs_normalizer(obs) if self.norm_obs else obs.clone()
+            self.episode_return = 0
+            self.episode_length = 0
+        else:
+            self.env.add_tracker('constraint_violation', 0, mode='queue')
+            self.env.add_tracker('constraint_values', 0, mode='queue')
+            self.env.add_tracker('mse', 0, mode='queue')
+
+    def close(self):
+        for env in (getattr(self, 'env', None), getattr(self, 'eval_env', None)):
+            try:
+                if env is not None:
+                    env.close()
+            except Exception:
+                pass
+        if getattr(self, 'logger', None) is not None:
+            self.logger.close()
+
+    def save(self, path):
+        '''MP:203-229 (same keys).'''
+        if self.rank != 0:
+            return
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        state_dict = {'agent': self.agent.state_dict(), 'obs_normalizer': self.obs_normalizer.state_dict(),
+                      'reward_normalizer': self.reward_normalizer.state_dict()}
+        if self.training:
+            env_random_state = self.env.get_env_random_state() if hasattr(self.env, 'get_env_random_state') else None
+            state_dict.update({'total_steps': self.total_steps,
+                               'obs': self.obs.detach().cpu() if torch.is_tensor(self.obs) else self.obs,
+                               'random_state': get_random_state(), 'env_random_state': env_random_state})
+        torch.save(state_dict, path)
+
+    def load(self, path):
+        '''MP:231-270.  Checkpoints written by this class contain only tensors, numpy arrays and
+        RNG tuples; loading them needs weights_only=False like the reference.'''
+        state = torch.load(path, map_location=self.device, weights_only=False)
+        self.agent.load_state_dict(state['agent'])
+        self.obs_normalizer.load_state_dict(state['obs_normalizer'])
+        self.reward_normalizer.load_state_dict(state['reward_normalizer'])
+        if self.training:
+            self.total_steps = state['total_steps']
+            self.obs = torch.as_tensor(state['obs'], device=self.device)
+            if 'random_state' in state:
+                try:
+                    set_random_state(state['random_state'])
+                except Exception as e:
+                    print(f"Warning: could not restore random state: {e}")
+            if state.get('env_random_state') is not None and hasattr(self.env, 'set_env_random_state'):
+                self.env.set_env_random_state(state['env_random_state'])
+
+    def select_action(self, obs, info=None):
+        '''MP:272-287: deterministic (dist.mode) actions for evaluation.'''
+        with torch.inference_mode():
+            o = torch.as_tensor(np.asarray(obs) if not torch.is_tensor(obs) else obs, dtype=torch.float32,
+                                device=self.device)
+            return self.agent.ac.act(o).cpu().numpy().astype(np.float32)
+
+    # ------------------------------------------------------------ rollout
+    def _buffer(self):
+        if self._rollouts is None:
+            self._rollouts = MAPPOBuffer(self.env.observation_space, self.env.action_space, self.rollout_steps,
+                                         batch_size=self.num_envs, include_global_state=self.centralized_critic,
+                                         global_state_dim=self.global_state_dim, device=self.device)
+            E, D = self.num_envs, self.num_agents
+            self._rew_raw = torch.zeros((self.rollout_steps, E), device=self.device)
+            self._te = torch.zeros((self.rollout_steps, E), dtype=torch.uint8, device=self.device)
+            self._tr = torch.zeros((self.rollout_steps, E), dtype=torch.uint8, device=self.device)
+            self._raw_obs = torch.zeros((E, D, self.obs_dim), device=self.device)
+        return self._rollouts
+
+    def _rollout_step(self, rollouts, t, warmup=False):
+        """One control step of every env, entirely on the device (MP:647-1027)."""
+        swarm = self.env.venv.swarm
+        obs_t = rollouts.next_obs_slots[t]
+        act, _, logp = self.agent.ac.step(obs_t)
+        rollouts.act[t].copy_(act)
+        rollouts.logp[t].copy_(logp)
+        target = self._raw_obs if self.norm_obs else rollouts.next_obs_slots[t + 1]
+        if not warmup:
+            swarm.step(rollouts.act[t], obs=target, reward=self._rew_raw[t], terminated=self._te[t],
+                       truncated=self._tr[t])
+        done = (self._te[t] | self._tr[t]).float()
+        rew = self._rew_raw[t]
+        if self.norm_obs:
+            rollouts.next_obs_slots[t + 1].copy_(self.obs_normalizer(self._raw_obs))
+        if self.norm_reward:
+            rew = self.reward_normalizer(rew, done)
+        rollouts.rew_env[t].copy_(rew)
+        rollouts.mask_env[t].copy_(1 - done)
+
+    def _capture_rollout(self, rollouts):
+        # warm-up: load every torch kernel of the step outside the capture (lazy module
+        # loads are not allowed while capturing); the simulator call is skipped and the
+        # RNG state restored, so the warm-up has no effect on the run
+        rng = torch.cuda.get_rng_state()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._rollout_step(rollouts, 0, warmup=True)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        torch.cuda.set_rng_state(rng)
+        rollouts.next_obs_slots[0].copy_(self.obs)
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for t in range(self.rollout_steps):
+                self._rollout_step(rollouts, t)
+        torch.cuda.current_stream().wait_stream(s)
+        self._rollout_graph = g
+
+    def train_step(self):
+        '''MP:619-1184: rollout (T steps × E envs) → last value → GAE → advantage
+        normalisation → PPO update.'''
+        self.agent.train()
+        self.obs_normalizer.unset_read_only()
+        rollouts = self._buffer()
+        rollouts.reset()
+        start = time.time()
+        rollouts.next_obs_slots[0].copy_(self.obs)
+        # the quirk path (norm_obs + double normalisation on done) needs a host branch per step
+        graph_ok = self.use_graphs and self.world == 1 and not self.norm_obs and not self.norm_reward
+        if graph_ok:
+            if self._rollout_graph is None:
+                # the capture records the T steps; the stream runs them only at replay
+                self._capture_rollout(rollouts)
+            self._rollout_graph.replay()
+        else:
+            for t in range(self.rollout_steps):
+                self._rollout_step(rollouts, t)
+                if self.norm_obs and self.reference_compat:
+                    done = self._te[t] | self._tr[t]
+                    if bool(done.any()):   # MP:1037: re-normalise (and re-update stats) on any done
+                        rollouts.next_obs_slots[t + 1].copy_(self.obs_normalizer(rollouts.next_obs_slots[t + 1]))
+        rollouts.t, rollouts.full = 0, True
+        self.obs = rollouts.next_obs_slots[self.rollout_steps].clone()
+        self.total_steps += self.rollout_steps * self.num_envs * self.world
+        with torch.inference_mode():
+            E, D = self.num_envs, self.num_agents
+            last_vals = self.agent.ac.get_value(self.obs.reshape(E, D * self.obs_dim))       # (E, 1)
+            last_val = last_vals.reshape(E, 1, 1).expand(E, D, 1)
+        rollouts.compute_returns_and_advantages(last_val, gamma=self.gamma, use_gae=self.use_gae,
+                                                gae_lambda=self.gae_lambda)
+        rollouts.adv = normalize_advantages(rollouts.adv)
+        results = self.agent.update(rollouts, self.device)
+        self.env.sync_from_device()
+        step_means = self._rew_raw.mean(dim=1).double().cpu().numpy()
+        results.update({'step': self.total_steps, 'elapsed_time': time.time() - start,
+                        'step_reward_mean': step_means.mean(), 'step_reward_std': step_means.std(),
+                        'step_reward_total': step_means.sum(),
+                        'termination_counts': defaultdict(int)})
+        rew_sum = float(rollouts.rew_env.double().sum().item()) * self.num_agents
+        self.episode_return += rew_sum / self.rollout_steps
+        self.episode_length += self.rollout_steps
+        return results
+
+    # -------------------------------------------------------------- learn
+    def learn(self, env=None, **kwargs):
+        '''MP:289-532 (training loop with checkpoints and periodic evaluation).'''
+        if self.num_checkpoints > 0:
+            step_interval = np.linspace(0, self.max_env_steps, self.num_checkpoints)
+            interval_save = np.zeros_like(step_interval, dtype=bool)
+        while self.total_steps < self.max_env_steps:
+            results = self.train_step()
+            if self.log_interval and self.total_steps % self.log_interval == 0 and self.rank == 0:
+                ep_returns = np.asarray(self.env.return_queue)
+                ep_lengths = np.asarray(self.env.length_queue)
+                print(f"{self.total_steps:10d} return {ep_returns.mean() if len(ep_returns) else 0:10.2f} "
+                      f"length {ep_lengths.mean() if len(ep_lengths) else 0:7.1f} "
+                      f"vloss {results['value_loss']:.4f} ploss {results['policy_loss']:.4f} "
+                      f"ent {results['entropy_loss']:.4f} kl {results['approx_kl']:.4f}")
+            should_save = (self.total_steps >= self.max_env_steps
+                           or (self.save_interval and self.total_steps % self.save_interval == 0)
+                           or not hasattr(self, '_first_checkpoint_saved'))
+            if should_save:
+                self.save(self.checkpoint_path)
+                self.save(os.path.join(self.output_dir, 'checkpoints', f'model_{self.total_steps}.pt'))
+                self._first_checkpoint_saved = True
+            if self.num_checkpoints > 0:
+                interval_id = np.argmin(np.abs(np.array(step_interval) - self.total_steps))
+                if not interval_save[interval_id]:
+                    self.save(os.path.join(self.output_dir, 'checkpoints', f'model_{self.total_steps}.pt'))
+                    interval_save[interval_id] = True
+            if self.eval_interval and self.total_steps % self.eval_interval == 0 and self.eval_env is not None:
+                results['eval'] = self.run(env=self.eval_env, n_episodes=self.eval_batch_size)
+                score = results['eval']['ep_returns'].mean()
+                if self.eval_save_best and getattr(self, 'eval_best_score', -np.inf) < score:
+                    self.eval_best_score = score
+                    self.save(os.path.join(self.output_dir, 'model_best.pt'))
+            if self.log_interval and self.total_steps % self.log_interval == 0:
+                self.log_step(results)
+
+    def run(self, env=None, render=False, n_episodes=10, verbose=False):
+        '''MP:534-581: deterministic evaluation on a single env.'''
+        self.agent.eval()
+        self.obs_normalizer.set_read_only()
+        env = self.eval_env if env is None else env
+        if not isinstance(env, RecordEpisodeStatistics):
+            env = RecordEpisodeStatistics(env, n_episodes)
+        obs, info = env.reset()
+        obs = self._norm_np(obs)
+        ep_returns, ep_lengths = [], []
+        while len(ep_returns) < n_episodes:
+            action = self.select_action(obs=obs, info=info)
+            obs, _, terminated, truncated, info = env.step(action)
+            if terminated or truncated:
+                ep_returns.append(info['episode']['r'])
+                ep_lengths.append(info['episode']['l'])
+                obs, _ = env.reset()
+            obs = self._norm_np(obs)
+        out = {'ep_returns': np.asarray(ep_returns), 'ep_lengths': np.asarray(ep_lengths)}
+        if len(env.queued_stats) > 0:
+            out.update({k: np.asarray(v) for k, v in env.queued_stats.items()})
+        return out
+
+    def _norm_np(self, obs):
+        if not self.norm_obs:
+            return obs
+        t = torch.as_tensor(np.asarray(obs), dtype=torch.float32, device=self.device).unsqueeze(0)
+        return self.obs_normalizer(t)[0].cpu().numpy()
+
+    def log_step(self, results):
+        '''MP:1186-1350 (scalars only).'''
+        step = results['step']
+        self.logger.add_scalars({'step': step, 'step_time': results['elapsed_time'],
+                                 'progress': step / self.max_env_steps}, step, prefix='time')
+        self.logger.add_scalars({k: results[k] for k in ['policy_loss', 'value_loss', 'entropy_loss', 'approx_kl']},
+                                step, prefix='loss')
+        self.logger.add_scalars({k: results[k] for k in ['step_reward_mean', 'step_reward_std', 'step_reward_total']},
+                                step, prefix='reward')
+        ep_returns = np.asarray(self.env.return_queue)
+        ep_lengths = np.asarray(self.env.length_queue)
+        if len(ep_returns):
+            self.logger.add_scalars({'ep_length': ep_lengths.mean(), 'ep_return': ep_returns.mean(),
+                                     'ep_return_std': ep_returns.std()}, step, prefix='stat')
+        self.logger.dump_scalars()
