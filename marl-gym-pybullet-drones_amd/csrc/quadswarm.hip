@@ -38,6 +38,32 @@ constexpr uint32_t kMaxResetTries = 1u << 24;
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
 enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
 
+// ------------------------------------------------------- CF2X constants
+// cf2x.urdf:5, 11-12, 34 and BaseAviary.py:117-128, as compile-time literals so
+// they fold into the instruction stream (no kernel-argument SGPRs, no spills).
+// The three square-root-derived values are the correctly rounded doubles of
+// their defining expressions; qs_create re-derives them with std::sqrt and
+// refuses to run if any differs (check_consts below).
+namespace cf2x {
+constexpr double G = 9.8, M = 0.027, L = 0.0397, KF = 3.16e-10, KM = 7.94e-12;
+constexpr double IXX = 1.4e-5, IYY = 1.4e-5, IZZ = 2.17e-5;
+constexpr double GRAVITY = G * M;                       // BaseAviary.py:117
+constexpr double L_SQRT2 = 0.028072139213105935;        // L / sqrt(2)      (BA:849-850)
+constexpr double HOVER_RPM = 14468.429183500699;        // sqrt(G M / 4 KF) (BA:118)
+constexpr double GND_CLIP = 0.037763713492095015;       // BaseAviary.py:125-126
+constexpr double SPEED_LIMIT = 0.03 * 30.0 * (1000.0 / 3600.0);   // BaseRLAviary.py:88
+constexpr double G_PID = 9.8 * M;                       // DSLPIDControl.py:43 (GRAVITY)
+constexpr double DRAG_XY = 9.1785e-7, DRAG_Z = 10.311e-7;
+constexpr double GND_COEFF = 11.36859, PROP_R = 2.31348e-2;
+constexpr double DW1 = 2267.18, DW2 = 0.16, DW3 = -0.11;
+}  // namespace cf2x
+
+// Compile-time shape of an action type (BaseRLAviary.py:262-277).
+template <int ACT> struct Act {
+  static constexpr int A = (ACT == QS_ACT_RPM || ACT == QS_ACT_VEL) ? 4 : (ACT == QS_ACT_PID ? 3 : 1);
+  static constexpr bool pid = ACT == QS_ACT_PID || ACT == QS_ACT_VEL || ACT == QS_ACT_ONE_D_PID;
+};
+
 // ---------------------------------------------------------------- math utils
 template <class T> struct M;
 template <> struct M<float> {
@@ -48,6 +74,7 @@ template <> struct M<float> {
   __device__ static float asin_(float x) { return asinf(x); }
   __device__ static float exp_(float x) { return expf(x); }
   __device__ static float abs_(float x) { return fabsf(x); }
+  __device__ static float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
   __device__ static float mul_rn(float a, float b) { return __fmul_rn(a, b); }
   __device__ static float add_rn(float a, float b) { return __fadd_rn(a, b); }
   __device__ static float sub_rn(float a, float b) { return __fsub_rn(a, b); }
@@ -60,6 +87,7 @@ template <> struct M<double> {
   __device__ static double asin_(double x) { return asin(x); }
   __device__ static double exp_(double x) { return exp(x); }
   __device__ static double abs_(double x) { return fabs(x); }
+  __device__ static double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
   __device__ static double mul_rn(double a, double b) { return __dmul_rn(a, b); }
   __device__ static double add_rn(double a, double b) { return __dadd_rn(a, b); }
   __device__ static double sub_rn(double a, double b) { return __dsub_rn(a, b); }
@@ -67,20 +95,32 @@ template <> struct M<double> {
 
 template <class T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-// sin/cos of the exp-map half angle θ = |ω|·dt/2 (BaseAviary.py:890-891).  θ is
-// small in flight (|ω| ≲ 100 rad/s ⇒ θ ≲ 0.21); a degree-9/10 Taylor series is
-// then exact to < 1e-13 relative, far below fp32 rounding, and ~6× cheaper
-// than the range-reduced library sin/cos.  Large θ falls back to the library.
-template <class T> __device__ __forceinline__ void half_angle_sincos(T th, T& sn, T& cs) {
-  if (th < T(0.25)) {
-    const T t2 = th * th;
-    sn = th * (T(1) - t2 * (T(1) / T(6)) * (T(1) - t2 * (T(1) / T(20)) * (T(1) - t2 * (T(1) / T(42)) *
-                                                                           (T(1) - t2 * (T(1) / T(72))))));
-    cs = T(1) - t2 * T(0.5) * (T(1) - t2 * (T(1) / T(12)) * (T(1) - t2 * (T(1) / T(30)) *
-                                                          (T(1) - t2 * (T(1) / T(56)))));
+// cos θ and sin θ / |ω| for the exp-map update (BaseAviary.py:889-891), with
+// θ = |ω|·dt/2, from u = θ² = |ω|²·(dt/2)² — no square root and no division
+// in flight (θ < 0.25, i.e. |ω| < 120 rad/s at 240 Hz).  Taylor series in u,
+// truncated where the next term is < 1e-10 of an fp32 ulp (fp32) or < 1e-4 of
+// an fp64 ulp (fp64).  Larger θ falls back to the library sin/cos.
+template <class T> __device__ __forceinline__ void expmap_coeffs(T wn2, T hdt, T hdt2, T& c, T& k) {
+  using F = M<T>;
+  const T u = wn2 * hdt2;
+  if (u < T(0.0625)) {
+    T s, cc;
+    if constexpr (sizeof(T) == 4) {
+      s = F::fma_(u, F::fma_(u, F::fma_(u, T(-1.0 / 5040), T(1.0 / 120)), T(-1.0 / 6)), T(1));
+      cc = F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, T(1.0 / 40320), T(-1.0 / 720)), T(1.0 / 24)), T(-0.5)), T(1));
+    } else {
+      s = F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, T(1.0 / 6227020800.0), T(-1.0 / 39916800.0)),
+                                                           T(1.0 / 362880)), T(-1.0 / 5040)), T(1.0 / 120)), T(-1.0 / 6)), T(1));
+      cc = F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, T(1.0 / 479001600.0), T(-1.0 / 3628800.0)),
+                                                            T(1.0 / 40320)), T(-1.0 / 720)), T(1.0 / 24)), T(-0.5)), T(1));
+    }
+    c = cc;
+    k = hdt * s;             // sin θ / |ω| = (dt/2) · sinc θ
   } else {
-    sn = M<T>::sin_(th);
-    cs = M<T>::cos_(th);
+    const T wn = F::sqrt_(wn2);
+    const T th = wn * hdt;
+    c = F::cos_(th);
+    k = F::sin_(th) / wn;
   }
 }
 
@@ -105,16 +145,14 @@ template <class T> __device__ __forceinline__ T u01(uint32_t x) { return T(x >> 
 // -------------------------------------------------------------- parameters
 template <class T> struct Params {
   // sizes
-  int E, D, N, A, O, H, S, EPB;
-  int task, act_type, mode;
+  int E, D, N, O, H, S, EPB;
+  int mode;
   uint32_t aux, flags;
   int pyb_freq;
   double ep_len_sec;
   uint32_t k0, k1;
   long long env_offset;
-  // physics constants (BaseAviary.py:117-128, cf2x.urdf)
-  T dt, ctrl_dt, KF, KM, M, GRAVITY, Jd0, Jd1, Jd2, Ji0, Ji1, Ji2, L_SQRT2, HOVER_RPM, SPEED_LIMIT, G_PID;
-  T DRAG0, DRAG1, DRAG2, GND_COEFF, PROP_R, GND_CLIP, DW1, DW2, DW3;
+  T dt, hdt, hdt2, ctrl_dt;      // PYB_TIMESTEP, dt/2, (dt/2)², CTRL_TIMESTEP
   T sp_R, sp_OMEGA, sp_VZ, sp_cx, sp_cy, sp_cz;
   // device buffers
   T* st;                  // [QS_AGENT_FIELDS][N]
@@ -127,8 +165,7 @@ template <class T> struct Params {
   long long log_cap;
   int* err;               // [1] reset search overflow flag
   int stage_rows;         // obs rows staged in LDS per pass
-  int ablate;             // dev-only phase ablation (QS_ABLATE env var), 0 in production
-  unsigned long long* stamps;   // dev-only phase timestamps (QS_STAMPS env var), null in production
+  unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
   // per-step I/O
   const uint8_t* reset_mask;   // MODE_RESET_MASK: [E] or NULL (= all)
   const float* act_in;
@@ -155,6 +192,17 @@ template <class T> __device__ __forceinline__ void quat_to_rot(const T q[4], T R
   R[3] = xy + wz; R[4] = T(1) - (xx + zz); R[5] = yz - wx;
   R[6] = xz - wy; R[7] = yz + wx; R[8] = T(1) - (xx + yy);
 }
+// Third column of the same matrix (the body z axis): all the force model of a
+// DYN substep needs.  Same operations as quat_to_rot, so bit-identical.
+template <class T> __device__ __forceinline__ void quat_to_zaxis(const T q[4], T& r2, T& r5, T& r8) {
+  T x = q[0], y = q[1], z = q[2], w = q[3];
+  T d = x * x + y * y + z * z + w * w;
+  T s = T(2) / d;
+  T xs = x * s, ys = y * s, zs = z * s;
+  r2 = x * zs + w * ys;
+  r5 = y * zs - w * xs;
+  r8 = T(1) - (x * xs + y * ys);
+}
 // pybullet getEulerFromQuaternion.
 template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T rpy[3]) {
   using F = M<T>;
@@ -173,12 +221,13 @@ template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T r
 
 // ------------------------------------------------------------ DSL PID
 // DSLPIDControl.computeControl (DSLPIDControl.py:82-259), one drone.
-// pid: int_pos[3], int_rpy[3], last_rpy[3] (updated in place).
+// pid: int_pos[3], int_rpy[3], last_rpy[3] (updated in place); rpy = the
+// current attitude (computed once by the caller, DSLPIDControl.py:240).
 template <class T>
-__device__ void dsl_pid(const Params<T>& P, T pid[9], const T pos[3], const T q[4], const T vel[3],
-                        const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
+__device__ __forceinline__ void dsl_pid(T ctrl_dt, T pid[9], const T pos[3], const T q[4], const T vel[3],
+                                        const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
   using F = M<T>;
-  const T dt = P.ctrl_dt;
+  const T dt = ctrl_dt;
   T R[9];
   quat_to_rot(q, R);
   T pe[3], ve[3];
@@ -191,10 +240,10 @@ __device__ void dsl_pid(const Params<T>& P, T pid[9], const T pos[3], const T q[
   T tt[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) tt[i] = PF[i] * pe[i] + IF[i] * pid[i] + DF[i] * ve[i];
-  tt[2] += P.G_PID;
+  tt[2] += T(cf2x::G_PID);
   T st = tt[0] * R[2] + tt[1] * R[5] + tt[2] * R[8];
   st = st > T(0) ? st : T(0);
-  T thrust = (F::sqrt_(st / (T(4) * P.KF)) - T(4070.3)) / T(0.2685);
+  T thrust = (F::sqrt_(st / (T(4) * T(cf2x::KF))) - T(4070.3)) / T(0.2685);
   T inv = T(1) / F::sqrt_(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
   T z[3] = {tt[0] * inv, tt[1] * inv, tt[2] * inv};
   T xc0 = F::cos_(tyaw), xc1 = F::sin_(tyaw);
@@ -213,8 +262,6 @@ __device__ void dsl_pid(const Params<T>& P, T pid[9], const T pos[3], const T q[
     return a - b;
   };
   T rot_e[3] = {E(2, 1), E(0, 2), E(1, 0)};
-  T rpy[3];
-  quat_to_rpy(q, rpy);
   T rate_e[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) { rate_e[i] = T(0) - (rpy[i] - pid[6 + i]) / dt; pid[6 + i] = rpy[i]; }
@@ -251,10 +298,10 @@ template <class T> struct Shared {
 };
 
 // Reset search (MultiHoverAviary.reset rejection loop, MH:83-102), group g
-// (= threads g*D .. g*D+D-1) evaluates `try_idx` for local env `lenv`.
-// Writes cand positions for its group and returns (via s.reject[g]).
+// (= threads g*D .. g*D+D-1) evaluates `try_idx` for its env.
+// Writes cand positions for its group and flags rejection in s.reject[g].
 template <class T>
-__device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, int lenv, uint32_t try_idx,
+__device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, uint32_t try_idx,
                                uint32_t genv, uint32_t episode, bool active) {
   using F = M<T>;
   const int tid = threadIdx.x;
@@ -282,38 +329,41 @@ __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, i
     if (bad) s.reject[g] = 1;
   }
   __syncthreads();
-  (void)lenv;
 }
 
-template <class T> __device__ __forceinline__ int valid_rows_in_block(const Params<T>& P) {
-  const int e0 = blockIdx.x * P.EPB;
-  const int ne = min(P.EPB, P.E - e0);
-  return ne * P.D;
-}
+#ifdef QS_STAMPS_BUILD
+#define QS_STAMP(k)                                                                         \
+  do {                                                                                      \
+    if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define QS_STAMP(k) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------- the step
-template <class T>
+// TASK (qs_task) and ACT (qs_action_type) are compile-time: each launch runs
+// a kernel with only its own task's obs/reward code and its own action
+// preprocessing, with the action width A folded into every index.
+template <class T, int TASK, int ACT>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   using F = M<T>;
+  constexpr int A = Act<ACT>::A;
+  constexpr bool kPid = Act<ACT>::pid;
+  constexpr bool kHover = TASK == QS_TASK_MULTIHOVER;
   __shared__ Shared<T> s;
   const int tid = threadIdx.x;
-  const int D = P.D, N = P.N;
+  const int D = P.D, N = P.N, H = P.H, O = P.O;
   const int lenv = tid / D, d = tid - lenv * D;
   const int e = blockIdx.x * P.EPB + lenv;
   const bool valid = (lenv < P.EPB) && (e < P.E);
   const int a = e * D + d;
   const uint32_t genv = (uint32_t)(P.env_offset + e);
-#define QS_STAMP(k)                                                                         \
-  do {                                                                                      \
-    if (P.stamps && tid == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
   QS_STAMP(0);
 
   // ---------------- load state
   T pos[3] = {0, 0, 0}, q[4] = {0, 0, 0, 1}, vel[3] = {0, 0, 0}, w[3] = {0, 0, 0}, lrpm[4] = {0, 0, 0, 0};
   T pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
   int32_t step_counter = 0, episode = 0, total = 0, ep_len = 0;
-  const bool has_pid = P.act_type == QS_ACT_PID || P.act_type == QS_ACT_VEL || P.act_type == QS_ACT_ONE_D_PID;
   if (valid) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -327,11 +377,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) lrpm[i] = P.st[(QS_F_LAST_RPM + i) * N + a];
     }
-    if (has_pid) {
+    if constexpr (kPid) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) pid[i] = P.st[(QS_F_PID_INT_POS + i) * N + a];
     }
-    if (P.task == QS_TASK_MULTIHOVER) {
+    if constexpr (kHover) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) tgt[i] = P.st[(QS_F_TARGET + i) * N + a];
     }
@@ -340,192 +390,198 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     total = P.env[QS_E_TOTAL_STEPS * P.E + e];
     ep_len = P.env[QS_E_EP_LEN * P.E + e];
   }
-  const int A = P.A, H = P.H, O = P.O;
+  // history ring head: this step's action goes to slot total % H; the obs of
+  // this step lists the H-1 older entries starting at slot (total+1) % H.
+  const int wslot = total % H;
   // ---------------- async prefetch of the H-1 older action-history entries the
   // obs rows need (BaseRLAviary.py:317-318), straight into LDS by LDS-DMA, issued
   // together with the state loads so the ring read costs no extra latency phase.
   // LDS image is lane-linear [entry][lane][A] (DMA destination = base + lane*size).
-  extern __shared__ float dyn_lds[];
+  extern __shared__ float4 dyn_lds4[];   // float4: 16-B aligned staging for the obs stores
+  float* const dyn_lds = reinterpret_cast<float*>(dyn_lds4);
   float* const hist_pref = dyn_lds;
   float* const stage = dyn_lds + (size_t)(H - 1) * kBlock * A;
   const bool want_obs = (P.obs != nullptr) || (P.tobs != nullptr);
   if (want_obs) {
     const int a_src = valid ? a : blockIdx.x * P.EPB * D;   // idle lanes read a valid row
-    const int tot_obs = total + (P.mode == MODE_STEP ? 1 : 0);
+    int slot = P.mode == MODE_STEP ? wslot + 1 : wslot;
+    if (slot == H) slot = 0;
     for (int i = 0; i < H - 1; ++i) {
-      const int slot = (tot_obs + i) % H;
       const float* src = P.hist + ((size_t)slot * N + a_src) * A;
-      lds_ptr_t dst = (lds_ptr_t)(hist_pref + (size_t)i * kBlock * A);
-      if (A == 1) {
-        __builtin_amdgcn_global_load_lds((g_ptr_t)src, dst, 4, 0, 0);
-      } else if (A == 3) {   // [entry][k][lane]: dwordx3 DMA does not land lane-linear at 12 B
+      if (++slot == H) slot = 0;
+      if constexpr (A == 1) {
+        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + i * kBlock), 4, 0, 0);
+      } else if constexpr (A == 3) {   // [entry][k][lane]: dwordx3 DMA does not land lane-linear at 12 B
         for (int k = 0; k < 3; ++k)
-          __builtin_amdgcn_global_load_lds((g_ptr_t)(src + k), (lds_ptr_t)(hist_pref + ((size_t)i * 3 + k) * kBlock),
-                                           4, 0, 0);
+          __builtin_amdgcn_global_load_lds((g_ptr_t)(src + k), (lds_ptr_t)(hist_pref + (i * 3 + k) * kBlock), 4, 0, 0);
       } else {
-        __builtin_amdgcn_global_load_lds((g_ptr_t)src, dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + i * kBlock * 4), 16, 0, 0);
       }
     }
   }
   T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
   bool done_env = false;
   int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
-  uint8_t bits = 0;
-  T rterm = 0;
 
-  float cur_act[4] = {0, 0, 0, 0};   // this step's action (newest history entry)
+  float cur_act[A];            // this step's action (newest history entry)
+#pragma unroll
+  for (int k = 0; k < A; ++k) cur_act[k] = 0.f;
   if (P.mode != MODE_STEP && valid && total > 0) {
-    const int slot = (total - 1) % H;
+    const int slot = wslot == 0 ? H - 1 : wslot - 1;
+#pragma unroll
     for (int k = 0; k < A; ++k) cur_act[k] = P.hist[((size_t)slot * N + a) * A + k];
   }
-  if (P.stamps) { volatile T sink = pos[0] + q[3] + pid[0] + tgt[0] + (T)total; (void)sink; }
   QS_STAMP(1);
   if (P.mode == MODE_STEP) {
     // ---------------- action (trainer-provided or synthetic random policy)
     float* act = cur_act;
     if (valid) {
       if (P.act_in) {
+#pragma unroll
         for (int k = 0; k < A; ++k) act[k] = P.act_in[(size_t)a * A + k];
       } else {
         U4 r = philox(U4{(uint32_t)total, genv, 0u, (uint32_t)((STREAM_ACT << 24) | d)}, P.k0, P.k1);
         const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
         for (int k = 0; k < A; ++k) act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
       }
-      if (P.act_out)
+      if (P.act_out) {
+#pragma unroll
         for (int k = 0; k < A; ++k) P.act_out[(size_t)a * A + k] = act[k];
+      }
       // action_buffer.append(action) (BaseRLAviary.py:187): ring slot total % H
-      const int slot = total % H;
-      for (int k = 0; k < A; ++k) P.hist[((size_t)slot * N + a) * A + k] = act[k];
+#pragma unroll
+      for (int k = 0; k < A; ++k) P.hist[((size_t)wslot * N + a) * A + k] = act[k];
     }
     // ---------------- _preprocessAction (BaseRLAviary.py:188-239)
     T rpm[4] = {0, 0, 0, 0};
-    quat_to_rpy(q, rpy);
-    if (valid && (P.ablate & 1)) { rpm[0] = rpm[1] = rpm[2] = rpm[3] = P.HOVER_RPM; }
-    else if (valid) {
+    if (valid) {
       const T z3[3] = {0, 0, 0};
-      switch (P.act_type) {
-        case QS_ACT_RPM:
+      if constexpr (ACT == QS_ACT_RPM) {
 #pragma unroll
-          for (int m = 0; m < 4; ++m) rpm[m] = P.HOVER_RPM * (T(1) + T(0.05) * T(act[m]));
-          break;
-        case QS_ACT_ONE_D_RPM: {
-          T r = P.HOVER_RPM * (T(1) + T(0.05) * T(act[0]));
-          rpm[0] = rpm[1] = rpm[2] = rpm[3] = r;
-        } break;
-        case QS_ACT_ONE_D_PID: {
+        for (int m = 0; m < 4; ++m) rpm[m] = T(cf2x::HOVER_RPM) * (T(1) + T(0.05) * T(act[m]));
+      } else if constexpr (ACT == QS_ACT_ONE_D_RPM) {
+        T r = T(cf2x::HOVER_RPM) * (T(1) + T(0.05) * T(act[0]));
+        rpm[0] = rpm[1] = rpm[2] = rpm[3] = r;
+      } else {
+        quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
+        if constexpr (ACT == QS_ACT_ONE_D_PID) {
           T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
-          dsl_pid(P, pid, pos, q, vel, tp, T(0), z3, rpm);
-        } break;
-        case QS_ACT_VEL: {
+          dsl_pid(P.ctrl_dt, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
+        } else if constexpr (ACT == QS_ACT_VEL) {
           T v0 = T(act[0]), v1 = T(act[1]), v2 = T(act[2]);
           T n = F::sqrt_(v0 * v0 + v1 * v1 + v2 * v2);
           T u0 = 0, u1 = 0, u2 = 0;
           if (n != T(0)) { u0 = v0 / n; u1 = v1 / n; u2 = v2 / n; }
-          T sp = P.SPEED_LIMIT * F::abs_(T(act[3]));
+          T sp = T(cf2x::SPEED_LIMIT) * F::abs_(T(act[3]));
           T tv[3] = {sp * u0, sp * u1, sp * u2};
-          dsl_pid(P, pid, pos, q, vel, pos, rpy[2], tv, rpm);
-        } break;
-        case QS_ACT_PID: {
+          dsl_pid(P.ctrl_dt, pid, pos, q, vel, rpy, pos, rpy[2], tv, rpm);
+        } else {   // QS_ACT_PID: _calculateNextStep (BaseAviary.py:1108-1150)
           T dir[3] = {T(act[0]) - pos[0], T(act[1]) - pos[1], T(act[2]) - pos[2]};
           T dist = F::sqrt_(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
           T np_[3];
           if (dist <= T(1)) { np_[0] = T(act[0]); np_[1] = T(act[1]); np_[2] = T(act[2]); }
           else { for (int i = 0; i < 3; ++i) np_[i] = pos[i] + (dir[i] / dist) * T(1); }
-          dsl_pid(P, pid, pos, q, vel, np_, T(0), z3, rpm);
-        } break;
-        default: break;
+          dsl_pid(P.ctrl_dt, pid, pos, q, vel, rpy, np_, T(0), z3, rpm);
+        }
       }
     }
     QS_STAMP(2);
     // ---------------- PYB_STEPS_PER_CTRL substeps (BaseAviary.py:343-372)
     T f[4], zt[4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) { f[m] = rpm[m] * rpm[m] * P.KF; zt[m] = rpm[m] * rpm[m] * P.KM; }
+    for (int m = 0; m < 4; ++m) { f[m] = rpm[m] * rpm[m] * T(cf2x::KF); zt[m] = rpm[m] * rpm[m] * T(cf2x::KM); }
     const T thrust_z = ((f[0] + f[1]) + f[2]) + f[3];
     const T tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];
-    const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * P.L_SQRT2;
-    const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * P.L_SQRT2;
-    const bool dw = (P.aux & QS_AUX_DW) != 0;
-    const int nsub = (P.ablate & 2) ? 1 : P.S;
-    for (int sub = 0; sub < nsub; ++sub) {
-      T R[9];
-      quat_to_rot(q, R);
+    const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
+    const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
+    const T dt = P.dt;
+    for (int sub = 0; sub < P.S; ++sub) {
+      T R2, R5, R8;
+      quat_to_zaxis(q, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
-      if (P.aux & QS_AUX_GND) {  // _groundEffect (BaseAviary.py:731-750)
-        T srpy[3];
-        quat_to_rpy(q, srpy);
-        if (F::abs_(srpy[0]) < T(M_PI / 2) && F::abs_(srpy[1]) < T(M_PI / 2)) {
-          const T PX[4] = {T(0.028), T(-0.028), T(-0.028), T(0.028)};
-          const T PY[4] = {T(-0.028), T(-0.028), T(0.028), T(0.028)};
+      if (P.aux) {
+        if (P.aux & QS_AUX_GND) {  // _groundEffect (BaseAviary.py:731-750)
+          T srpy[3], R[9];
+          quat_to_rpy(q, srpy);
+          quat_to_rot(q, R);
+          if (F::abs_(srpy[0]) < T(M_PI / 2) && F::abs_(srpy[1]) < T(M_PI / 2)) {
+            const T PX[4] = {T(0.028), T(-0.028), T(-0.028), T(0.028)};
+            const T PY[4] = {T(-0.028), T(-0.028), T(0.028), T(0.028)};
 #pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            T h = pos[2] + (R[6] * PX[m] + R[7] * PY[m]);
-            h = h < P.GND_CLIP ? P.GND_CLIP : h;
-            T ratio = P.PROP_R / (T(4) * h);
-            T g = rpm[m] * rpm[m] * P.KF * P.GND_COEFF * (ratio * ratio);
-            zb += g; txe += PY[m] * g; tye += -PX[m] * g;
+            for (int m = 0; m < 4; ++m) {
+              T h = pos[2] + (R[6] * PX[m] + R[7] * PY[m]);
+              h = h < T(cf2x::GND_CLIP) ? T(cf2x::GND_CLIP) : h;
+              T ratio = T(cf2x::PROP_R) / (T(4) * h);
+              T g = rpm[m] * rpm[m] * T(cf2x::KF) * T(cf2x::GND_COEFF) * (ratio * ratio);
+              zb += g; txe += PY[m] * g; tye += -PX[m] * g;
+            }
           }
         }
-      }
-      if (P.aux & QS_AUX_DRAG) {  // _drag (BaseAviary.py:770-781), previous-substep rpm
-        T sr = 0;
+        if (P.aux & QS_AUX_DRAG) {  // _drag (BaseAviary.py:770-781), previous-substep rpm
+          T sr = 0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) sr += T(2 * M_PI) * lrpm[m] / T(60);
-        fwx += (T(-1) * P.DRAG0 * sr) * vel[0];
-        fwy += (T(-1) * P.DRAG1 * sr) * vel[1];
-        fwz += (T(-1) * P.DRAG2 * sr) * vel[2];
-      }
-      if (dw) {  // _downwash (BaseAviary.py:798-811): neighbours' substep-start z via LDS
-        __syncthreads();
-        s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
-        __syncthreads();
-        if (valid) {
-          const int base = lenv * D;
-          for (int j = 0; j < D; ++j) {
-            T dz = s.cand[base + j][2] - pos[2];
-            T dx = s.cand[base + j][0] - pos[0], dy = s.cand[base + j][1] - pos[1];
-            T dxy = F::sqrt_(dx * dx + dy * dy);
-            if (dz > T(0) && dxy < T(10)) {
-              T ratio = P.PROP_R / (T(4) * dz);
-              T alpha = P.DW1 * (ratio * ratio);
-              T beta = P.DW2 * dz + P.DW3;
-              T qq = dxy / beta;
-              zb += -alpha * F::exp_(T(-.5) * (qq * qq));
+          for (int m = 0; m < 4; ++m) sr += T(2 * M_PI) * lrpm[m] / T(60);
+          fwx += (T(-1) * T(cf2x::DRAG_XY) * sr) * vel[0];
+          fwy += (T(-1) * T(cf2x::DRAG_XY) * sr) * vel[1];
+          fwz += (T(-1) * T(cf2x::DRAG_Z) * sr) * vel[2];
+        }
+        if (P.aux & QS_AUX_DW) {  // _downwash (BaseAviary.py:798-811): neighbours' substep-start z via LDS
+          __syncthreads();
+          s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
+          __syncthreads();
+          if (valid) {
+            const int base = lenv * D;
+            for (int j = 0; j < D; ++j) {
+              T dz = s.cand[base + j][2] - pos[2];
+              T dx = s.cand[base + j][0] - pos[0], dy = s.cand[base + j][1] - pos[1];
+              T dxy = F::sqrt_(dx * dx + dy * dy);
+              if (dz > T(0) && dxy < T(10)) {
+                T ratio = T(cf2x::PROP_R) / (T(4) * dz);
+                T alpha = T(cf2x::DW1) * (ratio * ratio);
+                T beta = T(cf2x::DW2) * dz + T(cf2x::DW3);
+                T qq = dxy / beta;
+                zb += -alpha * F::exp_(T(-.5) * (qq * qq));
+              }
             }
           }
         }
       }
       // _dynamics (BaseAviary.py:836-877)
-      T fw0 = R[2] * zb + fwx, fw1 = R[5] * zb + fwy, fw2 = (R[8] * zb - P.GRAVITY) + fwz;
-      T Jw0 = P.Jd0 * w[0], Jw1 = P.Jd1 * w[1], Jw2 = P.Jd2 * w[2];
+      T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
+      T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
       T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
-      T wd0 = P.Ji0 * ((tx + txe) - c0), wd1 = P.Ji1 * ((ty + tye) - c1), wd2 = P.Ji2 * (tz - c2);
-      vel[0] = vel[0] + P.dt * (fw0 / P.M);
-      vel[1] = vel[1] + P.dt * (fw1 / P.M);
-      vel[2] = vel[2] + P.dt * (fw2 / P.M);
-      w[0] = w[0] + P.dt * wd0;
-      w[1] = w[1] + P.dt * wd1;
-      w[2] = w[2] + P.dt * wd2;
+      T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
+      T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
+      vel[0] = vel[0] + dt * (fw0 / T(cf2x::M));
+      vel[1] = vel[1] + dt * (fw1 / T(cf2x::M));
+      vel[2] = vel[2] + dt * (fw2 / T(cf2x::M));
+      w[0] = w[0] + dt * wd0;
+      w[1] = w[1] + dt * wd1;
+      w[2] = w[2] + dt * wd2;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) pos[i] = pos[i] + P.dt * vel[i];
-      // _integrateQ (BaseAviary.py:879-892)
-      T wn = F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-      if (!(F::abs_(wn) <= T(1e-8)) && !(P.ablate & 8)) {
-        T th = wn * P.dt / T(2);
-        T c, sn;
-        half_angle_sincos(th, sn, c);
-        T k = (T(2) / wn) * T(0.5) * sn;   // (2/|ω|)·(0.5·Λ)·sinθ
-        T p_ = w[0], q_ = w[1], r_ = w[2];
-        T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+      for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
+      if (sub == P.S - 1) {
+        // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875);
+        // only the last substep's value reaches the obs.
+        T R[9];
+        quat_to_rot(q, R);
+        angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
+        angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
+        angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
+      }
+      // _integrateQ (BaseAviary.py:879-892); np.isclose(|ω|, 0) ⇔ |ω| <= 1e-8
+      const T wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+      if (wn2 > T(1e-16)) {
+        T c, k;
+        expmap_coeffs(wn2, P.hdt, P.hdt2, c, k);
+        const T p_ = w[0], q_ = w[1], r_ = w[2];
+        const T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
         q[0] = c * x0 + k * (r_ * x1 - q_ * x2 + p_ * x3);
         q[1] = c * x1 + k * (-r_ * x0 + p_ * x2 + q_ * x3);
         q[2] = c * x2 + k * (q_ * x0 - p_ * x1 + r_ * x3);
         q[3] = c * x3 + k * (-p_ * x0 - q_ * x1 - r_ * x2);
       }
-      // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875)
-      angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
-      angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
-      angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
 #pragma unroll
       for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
     }
@@ -534,8 +590,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     QS_STAMP(3);
 
     // ---------------- reward / termination per drone
+    T rterm = 0;
+    uint8_t bits = 0;
     if (valid) {
-      if (P.task == QS_TASK_MULTIHOVER) {  // MultiHoverAviary.py:128-186, 216-241
+      if constexpr (kHover) {  // MultiHoverAviary.py:128-186, 216-241
         T ex = pos[0] - tgt[0], ey = pos[1] - tgt[1];
         T err_xy = F::sqrt_(ex * ex + ey * ey);
         T err_z = pos[2] - tgt[2];
@@ -617,25 +675,27 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const bool do_reset = done_env && !(P.mode == MODE_STEP && (P.flags & QS_FLAG_NO_AUTORESET));
 
   // ---------------- obs writer (BaseRLAviary._computeObs + Spiral extras)
-  auto write_obs_row = [&](float* o, const T* p_, const T* r_, const T* v_, const T* av_, const T* q_, int sc) {
+  auto write_obs_row = [&](float* o, int sc) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      o[i] = (float)p_[i]; o[3 + i] = (float)r_[i]; o[6 + i] = (float)v_[i]; o[9 + i] = (float)av_[i];
+      o[i] = (float)pos[i]; o[3 + i] = (float)rpy[i]; o[6 + i] = (float)vel[i]; o[9 + i] = (float)angv[i];
     }
-    for (int i = 0; i < H - 1 && !(P.ablate & 16); ++i)   // older entries, prefetched into LDS
+    for (int i = 0; i < H - 1; ++i) {   // older entries, prefetched into LDS
+#pragma unroll
       for (int k = 0; k < A; ++k)
-        o[12 + i * A + k] = (A == 3) ? hist_pref[((size_t)i * 3 + k) * kBlock + tid]
-                                     : hist_pref[((size_t)i * kBlock + tid) * A + k];
+        o[12 + i * A + k] = (A == 3) ? hist_pref[(i * 3 + k) * kBlock + tid] : hist_pref[(i * kBlock + tid) * A + k];
+    }
+#pragma unroll
     for (int k = 0; k < A; ++k) o[12 + (H - 1) * A + k] = cur_act[k];   // newest = this step's action
-    if (P.task == QS_TASK_SPIRAL) {
+    if constexpr (!kHover) {
       T t = T((double)sc / (double)P.pyb_freq);
       T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
       T sn = F::sin_(ph), cs = F::cos_(ph);
       T prx = P.sp_cx + P.sp_R * cs, pry = P.sp_cy + P.sp_R * sn, prz = T(0.3) + P.sp_VZ * t;
       T vrx = -P.sp_R * P.sp_OMEGA * sn, vry = P.sp_R * P.sp_OMEGA * cs, vrz = P.sp_VZ;
       float* x = o + 12 + H * A;
-      x[0] = (float)(prx - p_[0]); x[1] = (float)(pry - p_[1]); x[2] = (float)(prz - p_[2]);
-      x[3] = (float)(vrx - q_[0]); x[4] = (float)(vry - q_[1]); x[5] = (float)(vrz - q_[2]);
+      x[0] = (float)(prx - pos[0]); x[1] = (float)(pry - pos[1]); x[2] = (float)(prz - pos[2]);
+      x[3] = (float)(vrx - q[0]); x[4] = (float)(vry - q[1]); x[5] = (float)(vrz - q[2]);
       x[6] = (float)sn; x[7] = (float)cs;
       x[8] = (float)vrx; x[9] = (float)vry; x[10] = (float)vrz;
     }
@@ -643,8 +703,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
   QS_STAMP(4);
   if (want_obs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // history LDS-DMA landed
-  if (valid && done_env && P.mode == MODE_STEP && P.tobs)
-    write_obs_row(P.tobs + (size_t)a * O, pos, rpy, vel, angv, q, obs_sc);
+  if (valid && done_env && P.mode == MODE_STEP && P.tobs) write_obs_row(P.tobs + (size_t)a * O, obs_sc);
 
   // ---------------- auto-reset (worker.step_env → env.reset)
   s.any = 0;
@@ -655,11 +714,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     if (d == 0 && lenv < P.EPB) s.need[lenv] = do_reset ? 1 : 0;
     if (P.mode != MODE_RESET_ALL && do_reset) episode += 1;
     T init[3];
-    if (P.task == QS_TASK_MULTIHOVER) {
+    if constexpr (kHover) {
       // Phase 1: every group tries index 0 for its own env.
       if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
       __syncthreads();
-      eval_candidate(P, s, lenv, d, lenv, 0u, genv, (uint32_t)episode, do_reset);
+      eval_candidate(P, s, lenv, d, 0u, genv, (uint32_t)episode, do_reset);
       if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
       __syncthreads();
       // Phase 2: for each still-rejected env, all groups search in parallel,
@@ -679,7 +738,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           if (tid == 0) s.win_group = 1 << 30;
           __syncthreads();
           const bool act_ = lenv < P.EPB;
-          eval_candidate(P, s, lenv, d, k, base + (uint32_t)lenv, genv_k, epk, act_);
+          eval_candidate(P, s, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
           if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
           __syncthreads();
           if (s.win_group < (1 << 30) || base + P.EPB >= kMaxResetTries) {
@@ -721,30 +780,34 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
   QS_STAMP(5);
   // ---------------- obs output
-  if (P.obs && !(P.ablate & 4)) {
+  if (P.obs) {
     if (P.mode == MODE_RESET_MASK) {
-      if (valid && do_reset) write_obs_row(P.obs + (size_t)a * O, pos, rpy, vel, angv, q, obs_sc);
+      if (valid && do_reset) write_obs_row(P.obs + (size_t)a * O, obs_sc);
     } else {
       // The block's obs rows are one contiguous span of HBM: build them in LDS
       // and store the span with 16-byte coalesced stores (a per-lane row store
       // touches 64 lines per wave instruction and doubled the write traffic).
-      const int nvalid = valid_rows_in_block(P);
-      const long long row0 = (long long)blockIdx.x * P.EPB * D;
+      const int nvalid = [&] { const int e0 = blockIdx.x * P.EPB; return min(P.EPB, P.E - e0) * D; }();
+      float* const blk = P.obs + (size_t)blockIdx.x * P.EPB * D * O;
       for (int p0 = 0; p0 < nvalid; p0 += P.stage_rows) {   // block-uniform
         const int p1 = min(nvalid, p0 + P.stage_rows);
-        if (tid >= p0 && tid < p1) write_obs_row(stage + (size_t)(tid - p0) * O, pos, rpy, vel, angv, q, obs_sc);
+        if (tid >= p0 && tid < p1) write_obs_row(stage + (tid - p0) * O, obs_sc);
         __syncthreads();
-        const long long g0 = (row0 + p0) * O, g1 = (row0 + p1) * O;
-        long long head = (g0 + 3) & ~3LL;
-        if (head > g1) head = g1;
-        long long tail = g1 & ~3LL;
-        if (tail < head) tail = head;
-        for (long long i = g0 + tid; i < head; i += kBlock) P.obs[i] = stage[i - g0];
-        for (long long i = head + 4LL * tid; i < tail; i += 4LL * kBlock) {
-          const long long j = i - g0;
-          *reinterpret_cast<float4*>(P.obs + i) = make_float4(stage[j], stage[j + 1], stage[j + 2], stage[j + 3]);
+        float* const g = blk + (size_t)p0 * O;                 // span start
+        const int n = (p1 - p0) * O;                          // floats in the span
+        const int head = min(n, (int)((4 - (((uintptr_t)g >> 2) & 3)) & 3));   // floats to 16-B alignment
+        if (tid < head) g[tid] = stage[tid];
+        const int nv = (n - head) >> 2;
+        if ((head & 3) == 0) {
+          for (int i = tid; i < nv; i += kBlock)
+            *reinterpret_cast<float4*>(g + 4 * i) = *reinterpret_cast<const float4*>(stage + 4 * i);
+        } else {
+          for (int i = tid; i < nv; i += kBlock) {
+            const float* src = stage + head + 4 * i;
+            *reinterpret_cast<float4*>(g + head + 4 * i) = make_float4(src[0], src[1], src[2], src[3]);
+          }
         }
-        for (long long i = tail + tid; i < g1; i += kBlock) P.obs[i] = stage[i - g0];
+        for (int i = head + 4 * nv + tid; i < n; i += kBlock) g[i] = stage[i];
         __syncthreads();
       }
     }
@@ -765,11 +828,13 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   // read back only when the drag model consumes it, but always written.
 #pragma unroll
   for (int i = 0; i < 4; ++i) P.st[(QS_F_LAST_RPM + i) * N + a] = lrpm[i];
-  if (has_pid && P.mode == MODE_STEP) {
+  if constexpr (kPid) {
+    if (P.mode == MODE_STEP) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) P.st[(QS_F_PID_INT_POS + i) * N + a] = pid[i];
+      for (int i = 0; i < 9; ++i) P.st[(QS_F_PID_INT_POS + i) * N + a] = pid[i];
+    }
   }
-  if (P.task == QS_TASK_MULTIHOVER && do_reset) {
+  if (kHover && do_reset) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) P.st[(QS_F_TARGET + i) * N + a] = tgt[i];
   }
@@ -830,49 +895,83 @@ struct qs_handle {
 };
 
 template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P) {
-  const HostConsts C;
   const qs_spec& s = h->spec;
   std::memset(&P, 0, sizeof(P));
-  P.E = s.num_envs; P.D = s.num_drones; P.N = h->dims.num_agents; P.A = h->dims.act_dim; P.O = h->dims.obs_dim;
+  P.E = s.num_envs; P.D = s.num_drones; P.N = h->dims.num_agents; P.O = h->dims.obs_dim;
   P.H = h->dims.hist_len; P.S = h->dims.substeps;
   P.EPB = qs::kBlock / s.num_drones;
-  P.task = s.task; P.act_type = s.act_type; P.aux = s.aux_forces; P.flags = s.flags; P.pyb_freq = s.pyb_freq;
+  P.aux = s.aux_forces; P.flags = s.flags; P.pyb_freq = s.pyb_freq;
   P.ep_len_sec = s.episode_len_sec;
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
   P.env_offset = s.env_offset;
-  P.dt = T(1.0 / s.pyb_freq); P.ctrl_dt = T(1.0 / s.ctrl_freq);
-  P.KF = T(C.KF); P.KM = T(C.KM); P.M = T(C.M); P.GRAVITY = T(C.G * C.M);
-  P.Jd0 = T(C.IXX); P.Jd1 = T(C.IYY); P.Jd2 = T(C.IZZ);
-  P.Ji0 = T(1.0 / C.IXX); P.Ji1 = T(1.0 / C.IYY); P.Ji2 = T(1.0 / C.IZZ);
-  P.L_SQRT2 = T(C.L / std::sqrt(2.0));
-  P.HOVER_RPM = T(std::sqrt(C.G * C.M / (4 * C.KF)));
-  P.SPEED_LIMIT = T(0.03 * C.MAX_SPEED_KMH * (1000.0 / 3600.0));
-  P.G_PID = T(9.8 * C.M);
-  P.DRAG0 = T(C.DRAG_XY); P.DRAG1 = T(C.DRAG_XY); P.DRAG2 = T(C.DRAG_Z);
-  P.GND_COEFF = T(C.GND_EFF_COEFF); P.PROP_R = T(C.PROP_RADIUS);
-  {
-    double max_rpm = std::sqrt((C.T2W * C.G * C.M) / (4 * C.KF));
-    double max_thrust = 4 * C.KF * max_rpm * max_rpm;
-    P.GND_CLIP = T(0.25 * C.PROP_RADIUS * std::sqrt((15 * max_rpm * max_rpm * C.KF * C.GND_EFF_COEFF) / max_thrust));
-  }
-  P.DW1 = T(C.DW1); P.DW2 = T(C.DW2); P.DW3 = T(C.DW3);
+  const double dt = 1.0 / s.pyb_freq;
+  P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq);
   P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
   P.sp_cx = T(s.target_center[0]); P.sp_cy = T(s.target_center[1]); P.sp_cz = T(s.target_center[2]);
   P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.ep_return = h->ep_return; P.orig_xyz = (const T*)h->orig;
   P.log = h->log; P.log_count = h->log_count; P.log_cap = h->log_cap; P.err = h->err;
-  static const int ablate = getenv("QS_ABLATE") ? atoi(getenv("QS_ABLATE")) : 0;   // dev experiments only
-  P.ablate = ablate;
   P.stamps = h->stamps;
+}
+
+// LDS per workgroup: the history prefetch image plus as many obs rows as fit.
+static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 4096, kStageBudget = 48 * 1024;
+static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
+  const size_t hist = (size_t)(d.hist_len - 1) * qs::kBlock * d.act_dim * sizeof(float);
+  const size_t row = (size_t)d.obs_dim * sizeof(float);
+  if (hist + row + kLdsStatic > kLdsBytes) return QS_E_INVALID;
+  const size_t budget = std::min(kStageBudget, kLdsBytes - kLdsStatic - hist);
+  const int rows = (qs::kBlock / d.num_drones) * d.num_drones;
+  *stage_rows = (int)std::max<size_t>(1, std::min<size_t>(rows, budget / row));
+  *bytes = hist + (size_t)*stage_rows * row;
+  return QS_OK;
+}
+
+template <class T, int TASK, int ACT> static void launch_one(int grid, size_t lds, hipStream_t st, const qs::Params<T>& P) {
+  hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+}
+
+template <class T, int TASK> static int launch_act(int act, int grid, size_t lds, hipStream_t st, const qs::Params<T>& P) {
+  switch (act) {
+    case QS_ACT_RPM: launch_one<T, TASK, QS_ACT_RPM>(grid, lds, st, P); break;
+    case QS_ACT_PID: launch_one<T, TASK, QS_ACT_PID>(grid, lds, st, P); break;
+    case QS_ACT_VEL: launch_one<T, TASK, QS_ACT_VEL>(grid, lds, st, P); break;
+    case QS_ACT_ONE_D_RPM: launch_one<T, TASK, QS_ACT_ONE_D_RPM>(grid, lds, st, P); break;
+    case QS_ACT_ONE_D_PID: launch_one<T, TASK, QS_ACT_ONE_D_PID>(grid, lds, st, P); break;
+    default: return fail(QS_E_INVALID, "launch: bad act_type");
+  }
+  return QS_OK;
 }
 
 template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t st) {
   const int grid = (P.E + P.EPB - 1) / P.EPB;
-  // obs staging: as many rows per pass as fit a 64 KiB LDS budget
-  const int rows = P.EPB * P.D;
-  P.stage_rows = std::max(1, std::min(rows, (48 * 1024) / (4 * P.O)));
-  const size_t lds = ((size_t)P.stage_rows * P.O + (size_t)(P.H - 1) * qs::kBlock * P.A) * sizeof(float);
-  hipLaunchKernelGGL(qs::step_kernel<T>, dim3(grid), dim3(qs::kBlock), lds, st, P);
+  size_t lds = 0;
+  if (lds_plan(h->dims, &P.stage_rows, &lds) != QS_OK)
+    return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
+  const int rc = h->spec.task == QS_TASK_MULTIHOVER
+                     ? launch_act<T, QS_TASK_MULTIHOVER>(h->spec.act_type, grid, lds, st, P)
+                     : launch_act<T, QS_TASK_SPIRAL>(h->spec.act_type, grid, lds, st, P);
+  if (rc != QS_OK) return rc;
   HIP_TRY(hipGetLastError());
+  return QS_OK;
+}
+
+// The device code folds the CF2X constants as literals (qs::cf2x); re-derive
+// them here from the URDF values exactly as the oracle does and refuse to run
+// if any literal is not the correctly rounded value.
+static int check_consts() {
+  const HostConsts C;
+  namespace K = qs::cf2x;
+  const bool ok = K::G == C.G && K::M == C.M && K::L == C.L && K::KF == C.KF && K::KM == C.KM &&
+                  K::IXX == C.IXX && K::IYY == C.IYY && K::IZZ == C.IZZ &&
+                  K::L_SQRT2 == C.L / std::sqrt(2.0) &&
+                  K::HOVER_RPM == std::sqrt(C.G * C.M / (4 * C.KF)) &&
+                  K::SPEED_LIMIT == 0.03 * C.MAX_SPEED_KMH * (1000.0 / 3600.0) &&
+                  K::DRAG_XY == C.DRAG_XY && K::DRAG_Z == C.DRAG_Z && K::GND_COEFF == C.GND_EFF_COEFF &&
+                  K::PROP_R == C.PROP_RADIUS && K::DW1 == C.DW1 && K::DW2 == C.DW2 && K::DW3 == C.DW3;
+  const double max_rpm = std::sqrt((C.T2W * C.G * C.M) / (4 * C.KF));
+  const double max_thrust = 4 * C.KF * max_rpm * max_rpm;
+  const double gnd_clip = 0.25 * C.PROP_RADIUS * std::sqrt((15 * max_rpm * max_rpm * C.KF * C.GND_EFF_COEFF) / max_thrust);
+  if (!ok || K::GND_CLIP != gnd_clip) return fail(QS_E_INVALID, "qs_create: CF2X device constants disagree with the URDF derivation");
   return QS_OK;
 }
 
@@ -894,6 +993,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
     return fail(QS_E_INVALID, "qs_create: pyb_freq is not divisible by env_freq");  // BaseAviary.py:79-80
   if (s.ctrl_freq < 2) return fail(QS_E_INVALID, "qs_create: ctrl_freq must be >= 2 (action history length ctrl_freq//2)");
   if (s.precision != 4 && s.precision != 8) return fail(QS_E_INVALID, "qs_create: precision must be 4 or 8");
+  if (check_consts() != QS_OK) return QS_E_INVALID;
   if (s.task == QS_TASK_MULTIHOVER && !s.initial_xyzs && s.num_drones >= 6)
     return fail(QS_E_INVALID, "qs_create: MultiHover reset with the default diagonal layout cannot complete for "
                               "D >= 6 (SURVEY §7 hard-2); pass initial_xyzs");
@@ -915,6 +1015,13 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   d.act_dim = A; d.hist_len = s.ctrl_freq / 2; d.substeps = s.pyb_freq / s.ctrl_freq;
   d.obs_dim = 12 + d.hist_len * A + (s.task == QS_TASK_SPIRAL ? 11 : 0);
   d.precision = s.precision; d.agent_fields = QS_AGENT_FIELDS; d.env_fields = QS_ENV_FIELDS;
+  {
+    int rows; size_t bytes;
+    if (lds_plan(d, &rows, &bytes) != QS_OK) {
+      delete h;
+      return fail(QS_E_INVALID, "qs_create: action history (ctrl_freq // 2 entries) does not fit in LDS");
+    }
+  }
   // initial layout (BaseAviary.py:194-197 / SpiralAviary.py:47-53)
   const HostConsts C;
   h->orig_host.resize(3 * s.num_drones);
@@ -954,11 +1061,13 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
       hipMemset(h->log_count, 0, sizeof(unsigned long long)) || hipMemset(h->err, 0, sizeof(int))) {
     cleanup(); return fail(QS_E_HIP, "qs_create: memset");
   }
+#ifdef QS_STAMPS_BUILD
   if (getenv("QS_STAMPS")) {   // dev-only phase timestamps
     const int grid = (s.num_envs + qs::kBlock / s.num_drones - 1) / (qs::kBlock / s.num_drones);
     if (hipMalloc((void**)&h->stamps, sizeof(unsigned long long) * 8 * grid) == hipSuccess)
       hipMemset(h->stamps, 0, sizeof(unsigned long long) * 8 * grid);
   }
+#endif
   *out = h;
   return QS_OK;
 }
