@@ -78,6 +78,11 @@ template <> struct M<float> {
   __device__ static float mul_rn(float a, float b) { return __fmul_rn(a, b); }
   __device__ static float add_rn(float a, float b) { return __fadd_rn(a, b); }
   __device__ static float sub_rn(float a, float b) { return __fsub_rn(a, b); }
+  // fp32 hot path: hardware reciprocal / reciprocal square root (≤1 ulp) in place
+  // of the scaled division sequences; constant divisors become multiplies.
+  __device__ static float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+  __device__ static float rsqrt(float x) { return __builtin_amdgcn_rsqf(x); }
+  __device__ static float divc(float x, double c) { return x * float(1.0 / c); }
 };
 template <> struct M<double> {
   __device__ static double sqrt_(double x) { return sqrt(x); }
@@ -91,6 +96,10 @@ template <> struct M<double> {
   __device__ static double mul_rn(double a, double b) { return __dmul_rn(a, b); }
   __device__ static double add_rn(double a, double b) { return __dadd_rn(a, b); }
   __device__ static double sub_rn(double a, double b) { return __dsub_rn(a, b); }
+  // fp64 keeps the reference's exact divisions (the tight fp64 parity gate).
+  __device__ static double rcp(double x) { return 1.0 / x; }
+  __device__ static double rsqrt(double x) { return 1.0 / sqrt(x); }
+  __device__ static double divc(double x, double c) { return x / c; }
 };
 
 template <class T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
@@ -152,7 +161,7 @@ template <class T> struct Params {
   double ep_len_sec;
   uint32_t k0, k1;
   long long env_offset;
-  T dt, hdt, hdt2, ctrl_dt;      // PYB_TIMESTEP, dt/2, (dt/2)², CTRL_TIMESTEP
+  T dt, hdt, hdt2, ctrl_dt, ctrl_hz;   // PYB_TIMESTEP, dt/2, (dt/2)², CTRL_TIMESTEP, CTRL_FREQ
   T sp_R, sp_OMEGA, sp_VZ, sp_cx, sp_cy, sp_cz;
   // device buffers
   T* st;                  // [QS_AGENT_FIELDS][N]
@@ -183,7 +192,7 @@ template <class T> struct Params {
 template <class T> __device__ __forceinline__ void quat_to_rot(const T q[4], T R[9]) {
   T x = q[0], y = q[1], z = q[2], w = q[3];
   T d = x * x + y * y + z * z + w * w;
-  T s = T(2) / d;
+  T s = T(2) * M<T>::rcp(d);
   T xs = x * s, ys = y * s, zs = z * s;
   T wx = w * xs, wy = w * ys, wz = w * zs;
   T xx = x * xs, xy = x * ys, xz = x * zs;
@@ -197,7 +206,7 @@ template <class T> __device__ __forceinline__ void quat_to_rot(const T q[4], T R
 template <class T> __device__ __forceinline__ void quat_to_zaxis(const T q[4], T& r2, T& r5, T& r8) {
   T x = q[0], y = q[1], z = q[2], w = q[3];
   T d = x * x + y * y + z * z + w * w;
-  T s = T(2) / d;
+  T s = T(2) * M<T>::rcp(d);
   T xs = x * s, ys = y * s, zs = z * s;
   r2 = x * zs + w * ys;
   r5 = y * zs - w * xs;
@@ -224,7 +233,7 @@ template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T r
 // pid: int_pos[3], int_rpy[3], last_rpy[3] (updated in place); rpy = the
 // current attitude (computed once by the caller, DSLPIDControl.py:240).
 template <class T>
-__device__ __forceinline__ void dsl_pid(T ctrl_dt, T pid[9], const T pos[3], const T q[4], const T vel[3],
+__device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T pos[3], const T q[4], const T vel[3],
                                         const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
   using F = M<T>;
   const T dt = ctrl_dt;
@@ -243,13 +252,13 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T pid[9], const T pos[3], con
   tt[2] += T(cf2x::G_PID);
   T st = tt[0] * R[2] + tt[1] * R[5] + tt[2] * R[8];
   st = st > T(0) ? st : T(0);
-  T thrust = (F::sqrt_(st / (T(4) * T(cf2x::KF))) - T(4070.3)) / T(0.2685);
-  T inv = T(1) / F::sqrt_(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
+  T thrust = F::divc(F::sqrt_(F::divc(st, 4 * cf2x::KF)) - T(4070.3), 0.2685);
+  T inv = F::rsqrt(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
   T z[3] = {tt[0] * inv, tt[1] * inv, tt[2] * inv};
   T xc0 = F::cos_(tyaw), xc1 = F::sin_(tyaw);
   // y = (z × x_c)/|z × x_c| with x_c = (xc0, xc1, 0)
   T y[3] = {-z[2] * xc1, z[2] * xc0, z[0] * xc1 - z[1] * xc0};
-  T yi = T(1) / F::sqrt_(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
+  T yi = F::rsqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
   y[0] *= yi; y[1] *= yi; y[2] *= yi;
   T x[3] = {y[1] * z[2] - y[2] * z[1], y[2] * z[0] - y[0] * z[2], y[0] * z[1] - y[1] * z[0]};
   // target_rotation columns x,y,z (scipy XYZ round trip = identity on SO(3)).
@@ -264,7 +273,12 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T pid[9], const T pos[3], con
   T rot_e[3] = {E(2, 1), E(0, 2), E(1, 0)};
   T rate_e[3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) { rate_e[i] = T(0) - (rpy[i] - pid[6 + i]) / dt; pid[6 + i] = rpy[i]; }
+  for (int i = 0; i < 3; ++i) {
+    const T drpy = rpy[i] - pid[6 + i];
+    if constexpr (sizeof(T) == 4) rate_e[i] = -(drpy * ctrl_hz);
+    else rate_e[i] = T(0) - drpy / dt;
+    pid[6 + i] = rpy[i];
+  }
 #pragma unroll
   for (int i = 0; i < 3; ++i) pid[3 + i] = clampv(pid[3 + i] - rot_e[i] * dt, T(-1500), T(1500));
   pid[3] = clampv(pid[3], T(-1), T(1));
@@ -301,16 +315,16 @@ template <class T> struct Shared {
 // (= threads g*D .. g*D+D-1) evaluates `try_idx` for its env.
 // Writes cand positions for its group and flags rejection in s.reject[g].
 template <class T>
-__device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, uint32_t try_idx,
+__device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3], int g, int d, uint32_t try_idx,
                                uint32_t genv, uint32_t episode, bool active) {
   using F = M<T>;
   const int tid = threadIdx.x;
   if (active) {
     U4 r = philox(U4{try_idx, genv, episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
     T n0 = T(0.5) * u01<T>(r.x) - T(0.25), n1 = T(0.5) * u01<T>(r.y) - T(0.25), n2 = T(0.5) * u01<T>(r.z) - T(0.25);
-    T px = F::add_rn(P.orig_xyz[d * 3 + 0], n0);
-    T py = F::add_rn(P.orig_xyz[d * 3 + 1], n1);
-    T pz = F::add_rn(P.orig_xyz[d * 3 + 2], n2);
+    T px = F::add_rn(orig[0], n0);
+    T py = F::add_rn(orig[1], n1);
+    T pz = F::add_rn(orig[2], n2);
     pz = clampv(pz, T(0.1), T(1.0));
     s.cand[tid][0] = px; s.cand[tid][1] = py; s.cand[tid][2] = pz;
   }
@@ -330,6 +344,38 @@ __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, int g, int d, u
   }
   __syncthreads();
 }
+
+// Raw-buffer access to the SoA state: descriptor over the whole [F][N] array
+// (wave-uniform, from kernel arguments), field base in soffset (SGPR), lane's
+// 32-bit byte offset in voffset — one buffer instruction per field, no 64-bit
+// per-lane address arithmetic (cdna_hip_programming.md T8).
+template <class T> struct SoA {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned fstride;   // bytes per field = N * sizeof(T)
+  unsigned voff;      // lane's byte offset = a * sizeof(T)
+  __device__ __forceinline__ T ld(int f) const {
+    if constexpr (sizeof(T) == 4) {
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff, (int)(f * fstride), 0));
+    } else {
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, (int)(f * fstride), 0));
+    }
+  }
+  __device__ __forceinline__ void st(int f, T v) const {
+    if constexpr (sizeof(T) == 4) {
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc, (int)voff, (int)(f * fstride), 0);
+    } else {
+      typedef unsigned v2u __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), rsrc, (int)voff, (int)(f * fstride), 0);
+    }
+  }
+};
+
+// s_waitcnt vmcnt(0) as a real instruction (not inline asm), so the compiler's
+// wait-count tracking knows every earlier load has landed and does not insert
+// conservative vmcnt(0) waits later — those would also wait for the early
+// state stores to drain (vmcnt retires loads and stores in issue order).
+// gfx9 encoding: vmcnt[3:0]=0, expcnt[6:4]=7, lgkmcnt[11:8]=15, vmcnt_hi[15:14]=0.
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 #ifdef QS_STAMPS_BUILD
 #define QS_STAMP(k)                                                                         \
@@ -358,6 +404,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const bool valid = (lenv < P.EPB) && (e < P.E);
   const int a = e * D + d;
   const uint32_t genv = (uint32_t)(P.env_offset + e);
+  SoA<T> S;
+  S.rsrc = __builtin_amdgcn_make_buffer_rsrc(P.st, 0, (int)((unsigned)QS_AGENT_FIELDS * (unsigned)N * sizeof(T)), 0x00020000);
+  S.fstride = (unsigned)N * (unsigned)sizeof(T);
+  S.voff = (unsigned)a * (unsigned)sizeof(T);
   QS_STAMP(0);
 
   // ---------------- load state
@@ -367,31 +417,63 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   if (valid) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      pos[i] = P.st[(QS_F_POS + i) * N + a];
-      vel[i] = P.st[(QS_F_VEL + i) * N + a];
-      w[i] = P.st[(QS_F_RPY_RATES + i) * N + a];
+      pos[i] = S.ld(QS_F_POS + i);
+      vel[i] = S.ld(QS_F_VEL + i);
+      w[i] = S.ld(QS_F_RPY_RATES + i);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = P.st[(QS_F_QUAT + i) * N + a];
+    for (int i = 0; i < 4; ++i) q[i] = S.ld(QS_F_QUAT + i);
     if (P.aux & QS_AUX_DRAG) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) lrpm[i] = P.st[(QS_F_LAST_RPM + i) * N + a];
+      for (int i = 0; i < 4; ++i) lrpm[i] = S.ld(QS_F_LAST_RPM + i);
     }
     if constexpr (kPid) {
 #pragma unroll
-      for (int i = 0; i < 9; ++i) pid[i] = P.st[(QS_F_PID_INT_POS + i) * N + a];
+      for (int i = 0; i < 9; ++i) pid[i] = S.ld(QS_F_PID_INT_POS + i);
     }
     if constexpr (kHover) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) tgt[i] = P.st[(QS_F_TARGET + i) * N + a];
+      for (int i = 0; i < 3; ++i) tgt[i] = S.ld(QS_F_TARGET + i);
     }
     step_counter = P.env[QS_E_STEP_COUNTER * P.E + e];
     episode = P.env[QS_E_EPISODE * P.E + e];
     total = P.env[QS_E_TOTAL_STEPS * P.E + e];
     ep_len = P.env[QS_E_EP_LEN * P.E + e];
   }
+  // Every other global read of the launch is issued here too: vmcnt retires
+  // loads and stores in issue order, so a load issued after the early state
+  // stores below would make its consumer wait for those stores to drain.
+  float act_in[Act<ACT>::A];
+  double ep_ret0 = 0;
+  T orig[3] = {0, 0, 0};
+  bool masked = true;
+  if (valid) {
+    if (P.mode == MODE_STEP && P.act_in) {
+#pragma unroll
+      for (int k = 0; k < Act<ACT>::A; ++k) act_in[k] = P.act_in[(size_t)a * Act<ACT>::A + k];
+    }
+    if (P.mode == MODE_STEP && d == 0) ep_ret0 = P.ep_return[e];
+    if (P.mode == MODE_RESET_MASK && P.reset_mask) masked = P.reset_mask[e] != 0;
+  }
+  if (lenv < P.EPB) {   // every search group, also those past the last env (reset phase 2)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) orig[i] = P.orig_xyz[d * 3 + i];
+  }
   // history ring head: this step's action goes to slot total % H; the obs of
   // this step lists the H-1 older entries starting at slot (total+1) % H.
+  // kinematic state + last_clipped_action (BaseAviary.py:509-519, 560)
+  auto store_kin = [&]() {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      S.st(QS_F_POS + i, pos[i]);
+      S.st(QS_F_VEL + i, vel[i]);
+      S.st(QS_F_RPY_RATES + i, w[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S.st(QS_F_QUAT + i, q[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S.st(QS_F_LAST_RPM + i, lrpm[i]);
+  };
   const int wslot = total % H;
   // ---------------- async prefetch of the H-1 older action-history entries the
   // obs rows need (BaseRLAviary.py:317-318), straight into LDS by LDS-DMA, issued
@@ -431,6 +513,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
     for (int k = 0; k < A; ++k) cur_act[k] = P.hist[((size_t)slot * N + a) * A + k];
   }
+#ifdef QS_STAMPS_BUILD
+  if (P.stamps) { volatile T sink = pos[0] + q[3] + pid[0] + tgt[0] + (T)total; (void)sink; }
+#endif
+  // Every load of the launch (and the history LDS-DMA) has landed before the
+  // first store: no later wait is held up by the stores (see wait_vm0).
+  wait_vm0();
   QS_STAMP(1);
   if (P.mode == MODE_STEP) {
     // ---------------- action (trainer-provided or synthetic random policy)
@@ -438,13 +526,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     if (valid) {
       if (P.act_in) {
 #pragma unroll
-        for (int k = 0; k < A; ++k) act[k] = P.act_in[(size_t)a * A + k];
+        for (int k = 0; k < A; ++k) act[k] = act_in[k];
       } else {
         U4 r = philox(U4{(uint32_t)total, genv, 0u, (uint32_t)((STREAM_ACT << 24) | d)}, P.k0, P.k1);
         const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
         for (int k = 0; k < A; ++k) act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
       }
+    }
+    if (valid) {
       if (P.act_out) {
 #pragma unroll
         for (int k = 0; k < A; ++k) P.act_out[(size_t)a * A + k] = act[k];
@@ -467,7 +557,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
         if constexpr (ACT == QS_ACT_ONE_D_PID) {
           T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
-          dsl_pid(P.ctrl_dt, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
+          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
         } else if constexpr (ACT == QS_ACT_VEL) {
           T v0 = T(act[0]), v1 = T(act[1]), v2 = T(act[2]);
           T n = F::sqrt_(v0 * v0 + v1 * v1 + v2 * v2);
@@ -475,15 +565,21 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           if (n != T(0)) { u0 = v0 / n; u1 = v1 / n; u2 = v2 / n; }
           T sp = T(cf2x::SPEED_LIMIT) * F::abs_(T(act[3]));
           T tv[3] = {sp * u0, sp * u1, sp * u2};
-          dsl_pid(P.ctrl_dt, pid, pos, q, vel, rpy, pos, rpy[2], tv, rpm);
+          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, pos, rpy[2], tv, rpm);
         } else {   // QS_ACT_PID: _calculateNextStep (BaseAviary.py:1108-1150)
           T dir[3] = {T(act[0]) - pos[0], T(act[1]) - pos[1], T(act[2]) - pos[2]};
           T dist = F::sqrt_(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
           T np_[3];
           if (dist <= T(1)) { np_[0] = T(act[0]); np_[1] = T(act[1]); np_[2] = T(act[2]); }
           else { for (int i = 0; i < 3; ++i) np_[i] = pos[i] + (dir[i] / dist) * T(1); }
-          dsl_pid(P.ctrl_dt, pid, pos, q, vel, rpy, np_, T(0), z3, rpm);
+          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, np_, T(0), z3, rpm);
         }
+      }
+    }
+    if constexpr (kPid) {   // PID integrators are final: store now, drains under the substeps
+      if (valid) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) S.st(QS_F_PID_INT_POS + i, pid[i]);
       }
     }
     QS_STAMP(2);
@@ -553,9 +649,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
       T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
       T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
-      vel[0] = vel[0] + dt * (fw0 / T(cf2x::M));
-      vel[1] = vel[1] + dt * (fw1 / T(cf2x::M));
-      vel[2] = vel[2] + dt * (fw2 / T(cf2x::M));
+      vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
+      vel[1] = vel[1] + dt * F::divc(fw1, cf2x::M);
+      vel[2] = vel[2] + dt * F::divc(fw2, cf2x::M);
       w[0] = w[0] + dt * wd0;
       w[1] = w[1] + dt * wd1;
       w[2] = w[2] + dt * wd2;
@@ -587,6 +683,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
     quat_to_rpy(q, rpy);   // readback (BaseAviary.py:374, 518)
     total += 1;
+    // Kinematic state is final unless this env auto-resets (rewritten below):
+    // store now so the writes drain under the reward / obs phases.
+    if (valid) store_kin();
     QS_STAMP(3);
 
     // ---------------- reward / termination per drone
@@ -598,7 +697,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         T err_xy = F::sqrt_(ex * ex + ey * ey);
         T err_z = pos[2] - tgt[2];
         T vz = vel[2];
-        T r_xy = T(1) / (T(1) + err_xy);
+        T r_xy = F::rcp(T(1) + err_xy);
         T r_z = F::exp_(T(-7.5) * F::abs_(err_z));
         T r_vel = F::abs_(err_z) < T(0.2) ? T(-1.5) * (vz * vz) : T(0);
         T hover = (err_xy < T(0.03) && F::abs_(err_z) < T(0.03) && F::abs_(vz) < T(0.03)) ? T(0.5) : T(0);
@@ -636,6 +735,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     s.bits[tid] = bits;
     __syncthreads();
     // per-env reduction in drone order (reference: reward += ... for i in range(D))
+    bool dn = false;
+    double ret = 0;
+    int len = 0;
     if (valid && d == 0) {
       T rsum = 0;
       uint8_t any = 0;
@@ -646,19 +748,23 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       if (P.rew) P.rew[e] = r;
       if (P.term) P.term[e] = te;
       if (P.trunc) P.trunc[e] = tr;
-      double ret = P.ep_return[e] + (double)r;
-      int len = ep_len + 1;
-      bool dn = te || tr;
+      ret = ep_ret0 + (double)r;
+      len = ep_len + 1;
+      dn = te || tr;
+      P.ep_return[e] = dn ? 0.0 : ret;
+      P.env[QS_E_EP_LEN * P.E + e] = dn ? 0 : len;
+      s.done[lenv] = dn;
+    }
+    // Episode log (VecRecordEpisodeStatistics, record_episode_statistics.py:155-166).
+    // The atomic's returned slot makes a wave wait for all its outstanding
+    // stores, so only waves holding a finished episode take this branch.
+    if (__ballot(dn) != 0ull) {
       if (dn) {
         unsigned long long slot = atomicAdd(P.log_count, 1ull);
         qs_episode_rec rec;
         rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
         P.log[slot % (unsigned long long)P.log_cap] = rec;
-        ret = 0; len = 0;
       }
-      P.ep_return[e] = ret;
-      P.env[QS_E_EP_LEN * P.E + e] = len;
-      s.done[lenv] = dn;
     }
     if (P.reasons && valid) P.reasons[a] = bits;
     step_counter += P.S;   // BaseAviary.py:382
@@ -669,7 +775,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     done_env = valid;
   } else {
     // qs_reset_envs: env.reset() on the masked envs
-    done_env = valid && (P.reset_mask == nullptr || P.reset_mask[e] != 0);
+    done_env = valid && masked;
   }
   // worker.step_env resets on done unless this is a single-env facade
   const bool do_reset = done_env && !(P.mode == MODE_STEP && (P.flags & QS_FLAG_NO_AUTORESET));
@@ -702,7 +808,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   };
 
   QS_STAMP(4);
-  if (want_obs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // history LDS-DMA landed
   if (valid && done_env && P.mode == MODE_STEP && P.tobs) write_obs_row(P.tobs + (size_t)a * O, obs_sc);
 
   // ---------------- auto-reset (worker.step_env → env.reset)
@@ -718,7 +823,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       // Phase 1: every group tries index 0 for its own env.
       if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
       __syncthreads();
-      eval_candidate(P, s, lenv, d, 0u, genv, (uint32_t)episode, do_reset);
+      eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset);
       if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
       __syncthreads();
       // Phase 2: for each still-rejected env, all groups search in parallel,
@@ -738,7 +843,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           if (tid == 0) s.win_group = 1 << 30;
           __syncthreads();
           const bool act_ = lenv < P.EPB;
-          eval_candidate(P, s, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
+          eval_candidate(P, s, orig, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
           if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
           __syncthreads();
           if (s.win_group < (1 << 30) || base + P.EPB >= kMaxResetTries) {
@@ -757,12 +862,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       if (do_reset) {
         uint32_t wt = (s.need[lenv] == 2) ? s.win_try[lenv] : 0u;
         U4 r = philox(U4{wt, genv, (uint32_t)episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
-        init[0] = F::add_rn(P.orig_xyz[d * 3 + 0], T(0.5) * u01<T>(r.x) - T(0.25));
-        init[1] = F::add_rn(P.orig_xyz[d * 3 + 1], T(0.5) * u01<T>(r.y) - T(0.25));
-        init[2] = clampv(F::add_rn(P.orig_xyz[d * 3 + 2], T(0.5) * u01<T>(r.z) - T(0.25)), T(0.1), T(1.0));
+        init[0] = F::add_rn(orig[0], T(0.5) * u01<T>(r.x) - T(0.25));
+        init[1] = F::add_rn(orig[1], T(0.5) * u01<T>(r.y) - T(0.25));
+        init[2] = clampv(F::add_rn(orig[2], T(0.5) * u01<T>(r.z) - T(0.25)), T(0.1), T(1.0));
       }
     } else {
-      if (do_reset) { init[0] = P.orig_xyz[d * 3 + 0]; init[1] = P.orig_xyz[d * 3 + 1]; init[2] = P.orig_xyz[d * 3 + 2]; }
+      if (do_reset) { init[0] = orig[0]; init[1] = orig[1]; init[2] = orig[2]; }
     }
     if (do_reset) {
       // BaseAviary._housekeeping (BaseAviary.py:458-477): PID state and the
@@ -815,28 +920,13 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   QS_STAMP(6);
   if (!valid) return;
 
-  // ---------------- store state
+  // ---------------- store state of the envs that (auto-)reset
+  if (do_reset) {
+    store_kin();
+    if constexpr (kHover) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    P.st[(QS_F_POS + i) * N + a] = pos[i];
-    P.st[(QS_F_VEL + i) * N + a] = vel[i];
-    P.st[(QS_F_RPY_RATES + i) * N + a] = w[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) P.st[(QS_F_QUAT + i) * N + a] = q[i];
-  // last_clipped_action is part of the state vector (BaseAviary.py:560); it is
-  // read back only when the drag model consumes it, but always written.
-#pragma unroll
-  for (int i = 0; i < 4; ++i) P.st[(QS_F_LAST_RPM + i) * N + a] = lrpm[i];
-  if constexpr (kPid) {
-    if (P.mode == MODE_STEP) {
-#pragma unroll
-      for (int i = 0; i < 9; ++i) P.st[(QS_F_PID_INT_POS + i) * N + a] = pid[i];
+      for (int i = 0; i < 3; ++i) S.st(QS_F_TARGET + i, tgt[i]);
     }
-  }
-  if (kHover && do_reset) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) P.st[(QS_F_TARGET + i) * N + a] = tgt[i];
   }
   if (d == 0) {
     P.env[QS_E_STEP_COUNTER * P.E + e] = step_counter;
@@ -905,7 +995,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
   P.env_offset = s.env_offset;
   const double dt = 1.0 / s.pyb_freq;
-  P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq);
+  P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq); P.ctrl_hz = T(s.ctrl_freq);
   P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
   P.sp_cx = T(s.target_center[0]); P.sp_cy = T(s.target_center[1]); P.sp_cz = T(s.target_center[2]);
   P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.ep_return = h->ep_return; P.orig_xyz = (const T*)h->orig;
