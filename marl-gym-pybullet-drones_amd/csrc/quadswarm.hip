@@ -416,8 +416,12 @@ __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70);
 // ---------------------------------------------------------------- the step
 // TASK (qs_task) and ACT (qs_action_type) are compile-time: each launch runs
 // a kernel with only its own task's obs/reward code and its own action
-// preprocessing, with the action width A folded into every index.
-template <class T, int TASK, int ACT>
+// preprocessing, with the action width A folded into every index.  CF is the
+// control frequency when it is the task's default at pyb_freq 240 (MultiHover
+// 30 Hz, Spiral 48 Hz): the substep count, history length and obs width are
+// then constants (fully unrolled substeps, constant obs offsets); CF = 0 reads
+// them from P.
+template <class T, int TASK, int ACT, int CF>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   using F = M<T>;
   constexpr int A = Act<ACT>::A;
@@ -425,16 +429,19 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   constexpr bool kHover = TASK == QS_TASK_MULTIHOVER;
   __shared__ Shared<T> s;
   const int tid = threadIdx.x;
-  const int D = P.D, N = P.N, H = P.H, O = P.O;
+  const int D = P.D, N = P.N;
+  const int H = CF ? CF / 2 : P.H;
+  const int S = CF ? 240 / CF : P.S;
+  const int O = CF ? 12 + (CF / 2) * A + (kHover ? 0 : 11) : P.O;
   const int lenv = tid / D, d = tid - lenv * D;
   const int e = blockIdx.x * P.EPB + lenv;
   const bool valid = (lenv < P.EPB) && (e < P.E);
   const int a = e * D + d;
   const uint32_t genv = (uint32_t)(P.env_offset + e);
-  SoA<T> S;
-  S.rsrc = __builtin_amdgcn_make_buffer_rsrc(P.st, 0, (int)((unsigned)QS_AGENT_FIELDS * (unsigned)N * sizeof(T)), 0x00020000);
-  S.fstride = (unsigned)N * (unsigned)sizeof(T);
-  S.voff = (unsigned)a * (unsigned)sizeof(T);
+  SoA<T> SA;
+  SA.rsrc = __builtin_amdgcn_make_buffer_rsrc(P.st, 0, (int)((unsigned)QS_AGENT_FIELDS * (unsigned)N * sizeof(T)), 0x00020000);
+  SA.fstride = (unsigned)N * (unsigned)sizeof(T);
+  SA.voff = (unsigned)a * (unsigned)sizeof(T);
   QS_STAMP(0);
 
   // ---------------- load state
@@ -444,23 +451,23 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   if (valid) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      pos[i] = S.ld(QS_F_POS + i);
-      vel[i] = S.ld(QS_F_VEL + i);
-      w[i] = S.ld(QS_F_RPY_RATES + i);
+      pos[i] = SA.ld(QS_F_POS + i);
+      vel[i] = SA.ld(QS_F_VEL + i);
+      w[i] = SA.ld(QS_F_RPY_RATES + i);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = S.ld(QS_F_QUAT + i);
+    for (int i = 0; i < 4; ++i) q[i] = SA.ld(QS_F_QUAT + i);
     if (P.aux & QS_AUX_DRAG) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) lrpm[i] = S.ld(QS_F_LAST_RPM + i);
+      for (int i = 0; i < 4; ++i) lrpm[i] = SA.ld(QS_F_LAST_RPM + i);
     }
     if constexpr (kPid) {
 #pragma unroll
-      for (int i = 0; i < 9; ++i) pid[i] = S.ld(QS_F_PID_INT_POS + i);
+      for (int i = 0; i < 9; ++i) pid[i] = SA.ld(QS_F_PID_INT_POS + i);
     }
     if constexpr (kHover) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) tgt[i] = S.ld(QS_F_TARGET + i);
+      for (int i = 0; i < 3; ++i) tgt[i] = SA.ld(QS_F_TARGET + i);
     }
     step_counter = P.env[QS_E_STEP_COUNTER * P.E + e];
     episode = P.env[QS_E_EPISODE * P.E + e];
@@ -492,14 +499,14 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   auto store_kin = [&]() {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      S.st(QS_F_POS + i, pos[i]);
-      S.st(QS_F_VEL + i, vel[i]);
-      S.st(QS_F_RPY_RATES + i, w[i]);
+      SA.st(QS_F_POS + i, pos[i]);
+      SA.st(QS_F_VEL + i, vel[i]);
+      SA.st(QS_F_RPY_RATES + i, w[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) S.st(QS_F_QUAT + i, q[i]);
+    for (int i = 0; i < 4; ++i) SA.st(QS_F_QUAT + i, q[i]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) S.st(QS_F_LAST_RPM + i, lrpm[i]);
+    for (int i = 0; i < 4; ++i) SA.st(QS_F_LAST_RPM + i, lrpm[i]);
   };
   const int wslot = total % H;
   // ---------------- async prefetch of the H-1 older action-history entries the
@@ -606,7 +613,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     if constexpr (kPid) {   // PID integrators are final: store now, drains under the substeps
       if (valid) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) S.st(QS_F_PID_INT_POS + i, pid[i]);
+        for (int i = 0; i < 9; ++i) SA.st(QS_F_PID_INT_POS + i, pid[i]);
       }
     }
     QS_STAMP(2);
@@ -619,7 +626,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
     const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
     const T dt = P.dt;
-    for (int sub = 0; sub < P.S; ++sub) {
+#ifdef QS_SUB_NOUNROLL
+#pragma unroll 1
+#else
+#pragma unroll
+#endif
+    for (int sub = 0; sub < S; ++sub) {
       T R2, R5, R8;
       quat_to_zaxis(q, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
@@ -684,7 +696,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       w[2] = w[2] + dt * wd2;
 #pragma unroll
       for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
-      if (sub == P.S - 1) {
+      if (sub == S - 1) {
         // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875);
         // only the last substep's value reaches the obs.
         T R[9];
@@ -794,7 +806,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       }
     }
     if (P.reasons && valid) P.reasons[a] = bits;
-    step_counter += P.S;   // BaseAviary.py:382
+    step_counter += S;   // BaseAviary.py:382
     __syncthreads();
     done_env = valid && s.done[lenv];
   } else if (P.mode == MODE_RESET_ALL) {
@@ -952,7 +964,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     store_kin();
     if constexpr (kHover) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) S.st(QS_F_TARGET + i, tgt[i]);
+      for (int i = 0; i < 3; ++i) SA.st(QS_F_TARGET + i, tgt[i]);
     }
   }
   if (d == 0) {
@@ -1043,17 +1055,23 @@ static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
   return QS_OK;
 }
 
-template <class T, int TASK, int ACT> static void launch_one(int grid, size_t lds, hipStream_t st, const qs::Params<T>& P) {
-  hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+template <class T, int TASK, int ACT> static void launch_one(int grid, size_t lds, hipStream_t st, const qs::Params<T>& P,
+                                                             int ctrl_freq, int pyb_freq) {
+  constexpr int kCF = TASK == QS_TASK_MULTIHOVER ? 30 : 48;   // MultiHoverAviary.py:20, SpiralAviary.py:28
+  if (ctrl_freq == kCF && pyb_freq == 240)
+    hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, kCF>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+  else
+    hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, 0>), dim3(grid), dim3(qs::kBlock), lds, st, P);
 }
 
-template <class T, int TASK> static int launch_act(int act, int grid, size_t lds, hipStream_t st, const qs::Params<T>& P) {
+template <class T, int TASK> static int launch_act(int act, int grid, size_t lds, hipStream_t st, const qs::Params<T>& P,
+                                                   int cf, int pf) {
   switch (act) {
-    case QS_ACT_RPM: launch_one<T, TASK, QS_ACT_RPM>(grid, lds, st, P); break;
-    case QS_ACT_PID: launch_one<T, TASK, QS_ACT_PID>(grid, lds, st, P); break;
-    case QS_ACT_VEL: launch_one<T, TASK, QS_ACT_VEL>(grid, lds, st, P); break;
-    case QS_ACT_ONE_D_RPM: launch_one<T, TASK, QS_ACT_ONE_D_RPM>(grid, lds, st, P); break;
-    case QS_ACT_ONE_D_PID: launch_one<T, TASK, QS_ACT_ONE_D_PID>(grid, lds, st, P); break;
+    case QS_ACT_RPM: launch_one<T, TASK, QS_ACT_RPM>(grid, lds, st, P, cf, pf); break;
+    case QS_ACT_PID: launch_one<T, TASK, QS_ACT_PID>(grid, lds, st, P, cf, pf); break;
+    case QS_ACT_VEL: launch_one<T, TASK, QS_ACT_VEL>(grid, lds, st, P, cf, pf); break;
+    case QS_ACT_ONE_D_RPM: launch_one<T, TASK, QS_ACT_ONE_D_RPM>(grid, lds, st, P, cf, pf); break;
+    case QS_ACT_ONE_D_PID: launch_one<T, TASK, QS_ACT_ONE_D_PID>(grid, lds, st, P, cf, pf); break;
     default: return fail(QS_E_INVALID, "launch: bad act_type");
   }
   return QS_OK;
@@ -1065,8 +1083,8 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (lds_plan(h->dims, &P.stage_rows, &lds) != QS_OK)
     return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
   const int rc = h->spec.task == QS_TASK_MULTIHOVER
-                     ? launch_act<T, QS_TASK_MULTIHOVER>(h->spec.act_type, grid, lds, st, P)
-                     : launch_act<T, QS_TASK_SPIRAL>(h->spec.act_type, grid, lds, st, P);
+                     ? launch_act<T, QS_TASK_MULTIHOVER>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq, h->spec.pyb_freq)
+                     : launch_act<T, QS_TASK_SPIRAL>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq, h->spec.pyb_freq);
   if (rc != QS_OK) return rc;
   HIP_TRY(hipGetLastError());
   return QS_OK;
