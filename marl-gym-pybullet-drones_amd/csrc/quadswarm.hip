@@ -369,6 +369,9 @@ __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3]
 // and the end-of-launch write-back then runs as a serial tail; non-temporal
 // (nt) stores stream to HBM while the launch computes (C3: 17.5 → 13.2 µs,
 // profiles/).  aux = 2 is the nt bit of buffer/global_load_lds instructions.
+#ifndef QS_SUB_CONTRACT
+#define QS_SUB_CONTRACT 1
+#endif
 #ifndef QS_STATE_STORE_AUX
 #define QS_STATE_STORE_AUX 2
 #endif
@@ -653,6 +656,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
 #endif
     for (int sub = 0; sub < S; ++sub) {
+#if QS_SUB_CONTRACT
+      // a*b+c → fma inside the substep (≈25 % fewer instructions).  The one
+      // sum whose exact cancellation matters — the gyroscopic ω × Jω, zero
+      // about a symmetric axis — is written with non-contractable _rn ops.
+#pragma clang fp contract(fast)
+#endif
       T R2, R5, R8;
       quat_to_zaxis(q, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
@@ -706,7 +715,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       // _dynamics (BaseAviary.py:836-877)
       T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
       T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
-      T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
+      T c0 = F::sub_rn(F::mul_rn(w[1], Jw2), F::mul_rn(w[2], Jw1));
+      T c1 = F::sub_rn(F::mul_rn(w[2], Jw0), F::mul_rn(w[0], Jw2));
+      T c2 = F::sub_rn(F::mul_rn(w[0], Jw1), F::mul_rn(w[1], Jw0));
       T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
       T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
       vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
