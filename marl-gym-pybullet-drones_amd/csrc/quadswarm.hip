@@ -425,6 +425,9 @@ template <class T> struct SoA {
 // state stores to drain (vmcnt retires loads and stores in issue order).
 // gfx9 encoding: vmcnt[3:0]=0, expcnt[6:4]=7, lgkmcnt[11:8]=15, vmcnt_hi[15:14]=0.
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// Keeps the loads on either side in source order (the scheduler would
+// interleave them), so operands needed first are issued first.
+__device__ __forceinline__ void issue_fence() { __asm__ volatile("" ::: "memory"); }
 
 #ifdef QS_STAMPS_BUILD
 #define QS_STAMP(k)                                                                         \
@@ -466,59 +469,111 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   SA.voff = (unsigned)a * (unsigned)sizeof(T);
   QS_STAMP(0);
 
-  // ---------------- load state
-  T pos[3] = {0, 0, 0}, q[4] = {0, 0, 0, 1}, vel[3] = {0, 0, 0}, w[3] = {0, 0, 0}, lrpm[4] = {0, 0, 0, 0};
-  T pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
-  int32_t step_counter = 0, episode = 0, total = 0, ep_len = 0;
-  if (valid) {
-    // env counters first: the synthetic action draw needs only `total` and runs
-    // while the state loads are still in flight
-    step_counter = P.env[QS_E_STEP_COUNTER * P.E + e];
-    episode = P.env[QS_E_EPISODE * P.E + e];
-    total = P.env[QS_E_TOTAL_STEPS * P.E + e];
-    ep_len = P.env[QS_E_EP_LEN * P.E + e];
+  // ---------------- loads
+  // Every global read of the launch is issued here, unconditionally and
+  // branch-free: buffer loads return 0 out of range, so idle lanes (offset
+  // kOOB) and absent optional inputs (zero-size descriptor) need no branch.
+  // With straight-line issue the compiler's wait counts stay exact, so each
+  // phase waits only for its own operands (vmcnt retires in issue order).
+  // Nothing is read after the first store (see wait_vm0).
+  constexpr unsigned kOOB = 0x80000000u;
+  auto rsrc = [](const void* ptr, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), 0, (int)bytes, 0x00020000);
+  };
+  SA.voff = valid ? SA.voff : kOOB;
+  const unsigned E = (unsigned)P.E;
+  // env counters first: the synthetic action draw needs only `total`
+  const __amdgpu_buffer_rsrc_t env_r = rsrc(P.env, (unsigned)QS_ENV_FIELDS * E * 4u);
+  const unsigned ev = valid ? (unsigned)e * 4u : kOOB;
+  auto ld_env = [&](int f) { return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(env_r, (int)ev, (int)(f * E * 4u), 0); };
+  int32_t step_counter = ld_env(QS_E_STEP_COUNTER), episode = ld_env(QS_E_EPISODE);
+  int32_t total = ld_env(QS_E_TOTAL_STEPS), ep_len = ld_env(QS_E_EP_LEN);
+  issue_fence();
+  T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      pos[i] = SA.ld(QS_F_POS + i);
-      vel[i] = SA.ld(QS_F_VEL + i);
-      w[i] = SA.ld(QS_F_RPY_RATES + i);
+  for (int i = 0; i < 3; ++i) {
+    pos[i] = SA.ld(QS_F_POS + i);
+    vel[i] = SA.ld(QS_F_VEL + i);
+    w[i] = SA.ld(QS_F_RPY_RATES + i);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = SA.ld(QS_F_QUAT + i);
+  {   // last rpm: read only by the drag model (zero offset range otherwise: no traffic)
+    SoA<T> LR = SA;
+    LR.voff = (P.aux & QS_AUX_DRAG) ? SA.voff : kOOB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lrpm[i] = LR.ld(QS_F_LAST_RPM + i);
+  }
+  if constexpr (kPid) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) pid[i] = SA.ld(QS_F_PID_INT_POS + i);
+  }
+  if constexpr (kHover) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tgt[i] = SA.ld(QS_F_TARGET + i);
+  }
+  // trainer actions (absent: zero-size descriptor), episode return, reset mask
+  float act_in[A];
+  {
+    const __amdgpu_buffer_rsrc_t r = rsrc(P.act_in, P.act_in ? (unsigned)N * A * 4u : 0u);
+    const unsigned v = valid ? (unsigned)a * A * 4u : kOOB;
+#pragma unroll
+    for (int k = 0; k < A; ++k) act_in[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)v, k * 4, 0));
+  }
+  const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+      rsrc(P.ep_return, E * 8u), valid ? (int)((unsigned)e * 8u) : (int)kOOB, 0, 0));
+  const uint8_t mask_v = __builtin_amdgcn_raw_buffer_load_b8(
+      rsrc(P.reset_mask, P.reset_mask ? E : 0u), valid ? e : (int)kOOB, 0, 0);
+  const bool masked = P.reset_mask == nullptr || mask_v != 0;
+  T orig[3];   // every search group needs it, also those past the last env (reset phase 2)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) orig[i] = P.orig_xyz[d * 3 + i];
+  issue_fence();
+  // ---------------- the whole action-history ring (BaseRLAviary.py:66, 187,
+  // 317-318): all H slots, so the addresses do not depend on the loaded ring
+  // head and the reads issue with the state loads.  With the default control
+  // frequency (CF != 0, H constant) the ring goes into registers with plain
+  // buffer loads, issued last: the compiler's exact wait counts then let the
+  // PID start as soon as the state has landed while the ring still streams.
+  // Otherwise it goes into LDS by LDS-DMA, lane-linear [slot][lane][A] (A = 3
+  // as [slot][k][lane]: a dwordx3 DMA does not land lane-linear at 12 B).
+  extern __shared__ float4 dyn_lds4[];   // float4: 16-B aligned staging for the obs stores
+  float* const dyn_lds = reinterpret_cast<float*>(dyn_lds4);
+  float* const hist_pref = dyn_lds;
+  float* const stage = dyn_lds + (CF ? 0 : (size_t)H * kBlock * A);
+  constexpr int HR = CF ? CF / 2 : 1;
+  float hreg[HR][A];
+  if constexpr (CF != 0) {
+    const __amdgpu_buffer_rsrc_t hr = rsrc(P.hist, (unsigned)HR * (unsigned)N * A * 4u);
+    const unsigned hv = valid ? (unsigned)a * A * 4u : kOOB;
+#pragma unroll
+    for (int sl = 0; sl < HR; ++sl) {
+      const int so = (int)((unsigned)sl * (unsigned)N * A * 4u);
+      // (dword loads: ROCm 7.2's clang lowers __builtin_amdgcn_raw_buffer_load_b128
+      // to a single dword load; adjacent dwords are merged by the backend)
+#pragma unroll
+      for (int k = 0; k < A; ++k)
+        hreg[sl][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (int)hv, so + 4 * k, 0));
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = SA.ld(QS_F_QUAT + i);
-    if (P.aux & QS_AUX_DRAG) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) lrpm[i] = SA.ld(QS_F_LAST_RPM + i);
-    }
-    if constexpr (kPid) {
-#pragma unroll
-      for (int i = 0; i < 9; ++i) pid[i] = SA.ld(QS_F_PID_INT_POS + i);
-    }
-    if constexpr (kHover) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) tgt[i] = SA.ld(QS_F_TARGET + i);
+  } else {
+    const int a_src = valid ? a : blockIdx.x * P.EPB * D;   // idle lanes read a valid row
+    for (int sl = 0; sl < H; ++sl) {
+      const float* src = P.hist + ((size_t)sl * N + a_src) * A;
+      if constexpr (A == 1) {
+        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + sl * kBlock), 4, 0, QS_HIST_DMA_AUX);
+      } else if constexpr (A == 3) {
+        for (int k = 0; k < 3; ++k)
+          __builtin_amdgcn_global_load_lds((g_ptr_t)(src + k), (lds_ptr_t)(hist_pref + (sl * 3 + k) * kBlock), 4, 0, QS_HIST_DMA_AUX);
+      } else {
+        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + sl * kBlock * 4), 16, 0, QS_HIST_DMA_AUX);
+      }
     }
   }
-  // Every other global read of the launch is issued here too: vmcnt retires
-  // loads and stores in issue order, so a load issued after the early state
-  // stores below would make its consumer wait for those stores to drain.
-  float act_in[Act<ACT>::A];
-  double ep_ret0 = 0;
-  T orig[3] = {0, 0, 0};
-  bool masked = true;
-  if (valid) {
-    if (P.mode == MODE_STEP && P.act_in) {
-#pragma unroll
-      for (int k = 0; k < Act<ACT>::A; ++k) act_in[k] = P.act_in[(size_t)a * Act<ACT>::A + k];
-    }
-    if (P.mode == MODE_STEP && d == 0) ep_ret0 = P.ep_return[e];
-    if (P.mode == MODE_RESET_MASK && P.reset_mask) masked = P.reset_mask[e] != 0;
-  }
-  if (lenv < P.EPB) {   // every search group, also those past the last env (reset phase 2)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) orig[i] = P.orig_xyz[d * 3 + i];
-  }
-  // history ring head: this step's action goes to slot total % H; the obs of
-  // this step lists the H-1 older entries starting at slot (total+1) % H.
+  auto hist_at = [&](int sl, int k) -> float {   // LDS image (CF == 0): ring slot sl, component k, this lane
+    return A == 3 ? hist_pref[(sl * 3 + k) * kBlock + tid] : hist_pref[(sl * kBlock + tid) * A + k];
+  };
+  // history ring head: this step's action goes to slot total % H
+  const int wslot = total % H;
   // kinematic state + last_clipped_action (BaseAviary.py:509-519, 560)
   auto store_kin = [&]() {
 #pragma unroll
@@ -532,33 +587,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) SA.st(QS_F_LAST_RPM + i, lrpm[i]);
   };
-  const int wslot = total % H;
-  // ---------------- async prefetch of the H-1 older action-history entries the
-  // obs rows need (BaseRLAviary.py:317-318), straight into LDS by LDS-DMA, issued
-  // together with the state loads so the ring read costs no extra latency phase.
-  // LDS image is lane-linear [entry][lane][A] (DMA destination = base + lane*size).
-  extern __shared__ float4 dyn_lds4[];   // float4: 16-B aligned staging for the obs stores
-  float* const dyn_lds = reinterpret_cast<float*>(dyn_lds4);
-  float* const hist_pref = dyn_lds;
-  float* const stage = dyn_lds + (size_t)(H - 1) * kBlock * A;
-  const bool want_obs = (P.obs != nullptr) || (P.tobs != nullptr);
-  if (want_obs) {
-    const int a_src = valid ? a : blockIdx.x * P.EPB * D;   // idle lanes read a valid row
-    int slot = P.mode == MODE_STEP ? wslot + 1 : wslot;
-    if (slot == H) slot = 0;
-    for (int i = 0; i < H - 1; ++i) {
-      const float* src = P.hist + ((size_t)slot * N + a_src) * A;
-      if (++slot == H) slot = 0;
-      if constexpr (A == 1) {
-        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + i * kBlock), 4, 0, QS_HIST_DMA_AUX);
-      } else if constexpr (A == 3) {   // [entry][k][lane]: dwordx3 DMA does not land lane-linear at 12 B
-        for (int k = 0; k < 3; ++k)
-          __builtin_amdgcn_global_load_lds((g_ptr_t)(src + k), (lds_ptr_t)(hist_pref + (i * 3 + k) * kBlock), 4, 0, QS_HIST_DMA_AUX);
-      } else {
-        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + i * kBlock * 4), 16, 0, QS_HIST_DMA_AUX);
-      }
-    }
-  }
   T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
   bool done_env = false;
   int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
@@ -566,16 +594,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   float cur_act[A];            // this step's action (newest history entry)
 #pragma unroll
   for (int k = 0; k < A; ++k) cur_act[k] = 0.f;
-  if (P.mode != MODE_STEP && valid && total > 0) {
-    const int slot = wslot == 0 ? H - 1 : wslot - 1;
-#pragma unroll
-    for (int k = 0; k < A; ++k) cur_act[k] = P.hist[((size_t)slot * N + a) * A + k];
-  }
 #ifdef QS_STAMPS_BUILD
   if (P.stamps) { volatile T sink = pos[0] + q[3] + pid[0] + tgt[0] + (T)total; (void)sink; }
 #endif
   // ---------------- action (trainer-provided or synthetic random policy)
-  if (P.mode == MODE_STEP && valid) {
+  if (P.mode == MODE_STEP) {
     if (P.act_in) {
 #pragma unroll
       for (int k = 0; k < A; ++k) cur_act[k] = act_in[k];
@@ -586,21 +609,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       for (int k = 0; k < A; ++k) cur_act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
     }
   }
-  // Every load of the launch (and the history LDS-DMA) has landed before the
-  // first store: no later wait is held up by the stores (see wait_vm0).
-  wait_vm0();
   QS_STAMP(1);
   if (P.mode == MODE_STEP) {
     const float* act = cur_act;
-    if (valid) {
-      if (P.act_out) {
-#pragma unroll
-        for (int k = 0; k < A; ++k) nt_store(P.act_out + (size_t)a * A + k, act[k]);
-      }
-      // action_buffer.append(action) (BaseRLAviary.py:187): ring slot total % H
-#pragma unroll
-      for (int k = 0; k < A; ++k) nt_store(P.hist + ((size_t)wslot * N + a) * A + k, act[k]);
-    }
     // ---------------- _preprocessAction (BaseRLAviary.py:188-239)
     T rpm[4] = {0, 0, 0, 0};
     if (valid) {
@@ -634,8 +645,20 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         }
       }
     }
-    if constexpr (kPid) {   // PID integrators are final: store now, drains under the substeps
-      if (valid) {
+    // Every load of the launch has landed before the first store, so no later
+    // wait is held up by the stores (see wait_vm0).  The compiler's own waits
+    // let the action draw and the PID start as soon as the state loads land,
+    // with the history LDS-DMA (issued last) still streaming.
+    wait_vm0();
+    if (valid) {
+      if (P.act_out) {
+#pragma unroll
+        for (int k = 0; k < A; ++k) nt_store(P.act_out + (size_t)a * A + k, act[k]);
+      }
+      // action_buffer.append(action) (BaseRLAviary.py:187): ring slot total % H
+#pragma unroll
+      for (int k = 0; k < A; ++k) nt_store(P.hist + ((size_t)wslot * N + a) * A + k, act[k]);
+      if constexpr (kPid) {   // PID integrators are final: store now, drains under the substeps
 #pragma unroll
         for (int i = 0; i < 9; ++i) SA.st(QS_F_PID_INT_POS + i, pid[i]);
       }
@@ -666,6 +689,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       quat_to_zaxis(q, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
       if (P.aux) {
+        // no contraction here: the four ground-effect torque arms cancel exactly
+        // for a level drone only in plain multiply-then-add arithmetic
+#pragma clang fp contract(off)
         if (P.aux & QS_AUX_GND) {  // _groundEffect (BaseAviary.py:731-750)
           T srpy[3], R[9];
           quat_to_rpy(q, srpy);
@@ -842,10 +868,25 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     __syncthreads();
     done_env = valid && s.done[lenv];
   } else if (P.mode == MODE_RESET_ALL) {
-    // qs_reset: every env starts episode 0
+    wait_vm0();
+    // qs_reset: every env starts episode 0 (history is zero after qs_reset)
     done_env = valid;
   } else {
-    // qs_reset_envs: env.reset() on the masked envs
+    wait_vm0();
+    // qs_reset_envs: env.reset() on the masked envs; the obs lists the latest
+    // action (ring slot wslot-1) last
+    if (total > 0) {   // (no global read here: it would blur the step path's wait counts)
+      const int sl = wslot == 0 ? H - 1 : wslot - 1;
+      if constexpr (CF != 0) {
+#pragma unroll
+        for (int r = 0; r < HR; ++r)
+#pragma unroll
+          for (int k = 0; k < A; ++k) cur_act[k] = r == sl ? hreg[r][k] : cur_act[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < A; ++k) cur_act[k] = hist_at(sl, k);
+      }
+    }
     done_env = valid && masked;
   }
   // worker.step_env resets on done unless this is a single-env facade
@@ -857,10 +898,26 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     for (int i = 0; i < 3; ++i) {
       o[i] = (float)pos[i]; o[3 + i] = (float)rpy[i]; o[6 + i] = (float)vel[i]; o[9 + i] = (float)angv[i];
     }
-    for (int i = 0; i < H - 1; ++i) {   // older entries, prefetched into LDS
+    // history, oldest first: ring slots base .. base+H-2 (mod H), then this
+    // step's action (BaseRLAviary.py:317-318)
+    const int base = P.mode == MODE_STEP ? wslot + 1 : wslot;
+    if constexpr (CF != 0) {   // register ring: slot sl goes to column (sl - base) mod H
 #pragma unroll
-      for (int k = 0; k < A; ++k)
-        o[12 + i * A + k] = (A == 3) ? hist_pref[(i * 3 + k) * kBlock + tid] : hist_pref[(i * kBlock + tid) * A + k];
+      for (int sl = 0; sl < HR; ++sl) {
+        int col = sl - base;
+        col += col < 0 ? HR : 0;
+        if (col != HR - 1) {
+#pragma unroll
+          for (int k = 0; k < A; ++k) o[12 + col * A + k] = hreg[sl][k];
+        }
+      }
+    } else {
+      int sl = base >= H ? base - H : base;
+      for (int i = 0; i < H - 1; ++i) {
+#pragma unroll
+        for (int k = 0; k < A; ++k) o[12 + i * A + k] = hist_at(sl, k);
+        if (++sl == H) sl = 0;
+      }
     }
 #pragma unroll
     for (int k = 0; k < A; ++k) o[12 + (H - 1) * A + k] = cur_act[k];   // newest = this step's action
@@ -1077,7 +1134,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
 // LDS per workgroup: the history prefetch image plus as many obs rows as fit.
 static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 4096, kStageBudget = 48 * 1024;
 static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
-  const size_t hist = (size_t)(d.hist_len - 1) * qs::kBlock * d.act_dim * sizeof(float);
+  const size_t hist = (size_t)d.hist_len * qs::kBlock * d.act_dim * sizeof(float);
   const size_t row = (size_t)d.obs_dim * sizeof(float);
   if (hist + row + kLdsStatic > kLdsBytes) return QS_E_INVALID;
   const size_t budget = std::min(kStageBudget, kLdsBytes - kLdsStatic - hist);
