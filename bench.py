@@ -13,6 +13,11 @@ rank) with no data-path collective; value = all ranks' agent-steps ÷ max-over-
 ranks wall time.
 
 Extra JSON fields:
+  mappo         full MAPPO on the same C3 envs (BASELINE config 3): agent-steps/s of
+                MAPPO.train_step = T-step rollout with the shared actor + simulator,
+                last value, GAE, advantage normalisation and the PPO update
+                (opt_epochs x minibatches, centralized critic) — SURVEY §8(d)'s
+                "full MAPPO" figure; with N ranks the gradients are all-reduced.
   roofline      the step kernel: §8(d) algorithmic bytes per agent-step (418 B,
                 C3 ONE_D_PID) × agents per launch ÷ mean launch time from HIP
                 events on the launch stream, vs 8 TB/s.
@@ -50,6 +55,10 @@ def parse():
     p.add_argument("--slots", type=int, default=32, help="rollout-buffer slots the obs ring cycles through")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--mappo", type=int, default=1, help="also time full MAPPO train steps (0 = skip)")
+    p.add_argument("--mappo-steps", type=int, default=32, help="rollout_steps T of the MAPPO leg")
+    p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO leg")
+    p.add_argument("--mappo-iters", type=int, default=3, help="timed train steps (after one warm-up)")
     return p.parse_args()
 
 
@@ -74,6 +83,67 @@ def cpu_baseline(args, seconds):
             "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {E} envs x "
                       f"{args.drones} drones x {steps} random-policy ctrl steps, OpenMP {threads} threads, "
                       f"{dt:.1f} s"}
+
+
+def pmc_traffic(E, D, act):
+    """HBM bytes per step-kernel launch from the newest committed PMC summary of this
+    workload (profiles/rNN_pmc_traffic.json: FETCH_SIZE/WRITE_SIZE passes, calibrated;
+    scripts/gpu_prof.sh).  The counters need rocprofv3 around the process, so the
+    bench reports the committed measurement of the same kernel and names its source."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == {"envs": E, "drones": D, "act": act}:
+            best = (f, d)
+    if best is None:
+        return None, None
+    return best[1]["step_traffic_bytes"], os.path.relpath(best[0], ROOT)
+
+
+def mappo_leg(args, rank, world, dist):
+    """Full MAPPO train steps on the bench's C3 envs (learn_mappo.py:196-203 hyper-parameters,
+    hidden 256, opt_epochs 10; minibatch scaled to the 128x larger env batch)."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    D, E = args.drones, args.envs
+    act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[args.act]
+    env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act,
+                                               initial_xyzs=grid_layout(D) if D >= 6 else None)
+    m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
+              rollout_steps=args.mappo_steps, rollout_batch_size=E, opt_epochs=10,
+              mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
+    m.reset()
+    m.train_step()   # warm-up: graph capture, lazy kernel loads
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.mappo_iters):
+        m.train_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.mappo_iters
+    if dist:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    m.close()
+    T = args.mappo_steps
+    return {"value": T * E * D * world / dt, "unit": "agent-steps/s", "ms_per_train_step": dt * 1e3,
+            "train_steps": args.mappo_iters,
+            "config": {"rollout_steps": T, "envs_per_gpu": E, "drones": D, "hidden": 256, "opt_epochs": 10,
+                       "mini_batch_size": args.mappo_mb,
+                       "minibatches_per_epoch": T * E // args.mappo_mb,
+                       "graphs": world == 1, "grad_allreduce": "one fused all-reduce per minibatch" if world > 1
+                       else None}}
 
 
 def main():
@@ -145,8 +215,12 @@ def main():
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
     assert sw.reset_error() == 0
     assert torch.isfinite(obs_buf[:min(args.slots, args.steps)]).all()
+    del graph
+    sw.close()
+    mappo = mappo_leg(args, rank, world, dist) if args.mappo else None
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
+        traffic, traffic_src = pmc_traffic(E, D, args.act)
         line = {
             "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -157,12 +231,14 @@ def main():
                        "envs_per_gpu": E, "drones": D, "total_envs": E * world, "act": args.act,
                        "physics": "dyn", "parallelism": f"env-shard x{world}", "precision": "fp32"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": nbytes,
                          "kernel_ms": kern_ms, "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act)},
             "cpu_baseline": cpu,
+            "mappo": mappo,
         }
         print(json.dumps(line), flush=True)
-    sw.close()
     if dist:
         dist.destroy_process_group()
 

@@ -173,13 +173,15 @@ class MAPPOActorCritic(nn.Module):
 class FlatBuffers:
     """Parameters, gradients and Adam moments of one module in flat fp32 buffers."""
 
-    def __init__(self, module, lr, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, module, lr, betas=(0.9, 0.999), eps=1e-8, grad=None):
+        """grad: optional external flat gradient view (MAPPOAgent packs the actor and
+        critic gradients plus approx_kl into one buffer, so one all-reduce serves all)."""
         self.params = [p for p in module.parameters()]
         dev = self.params[0].device
         n = sum(p.numel() for p in self.params)
         self.n = n
         self.flat = torch.zeros(n, device=dev)
-        self.grad = torch.zeros(n, device=dev)
+        self.grad = torch.zeros(n, device=dev) if grad is None else grad
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.step = torch.zeros(1, device=dev)
@@ -262,8 +264,13 @@ class MAPPOAgent:
         self.device = torch.device(device)
         self.ac.to(self.device)
         if self.device.type == 'cuda':
-            self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr)
-            self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr)
+            na = sum(p.numel() for p in self.ac.actor.parameters())
+            nc = sum(p.numel() for p in self.ac.critic.parameters())
+            # [actor grads | critic grads | approx_kl]: the one buffer every rank all-reduces
+            self._reduce_buf = torch.zeros(na + nc + 1, device=self.device)
+            self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[:na])
+            self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr, grad=self._reduce_buf[na:na + nc])
+            self._kl = self._reduce_buf[na + nc:]
             if _dist_world() > 1:   # identical initial weights on every rank
                 tdist.broadcast(self.actor_opt.flat, 0)
                 tdist.broadcast(self.critic_opt.flat, 0)
@@ -315,25 +322,25 @@ class MAPPOAgent:
 
     # ------------------------------------------------------------- update
     def _iteration(self, batch, acc):
-        """One minibatch: actor step (KL-gated on device), critic step, stat accumulation."""
+        """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.
+
+        The reference steps the actor, then computes the value loss and steps the
+        critic (AG:717-760).  The value loss does not depend on the actor's
+        parameters, so both losses are formed first and one backward fills both
+        gradient buffers; with several ranks the actor gradient, the critic
+        gradient and approx_kl then travel in ONE all-reduce (gradient mean and
+        the KL mean every rank gates on, AG:731)."""
         world = _dist_world()
         policy_loss, entropy_loss, approx_kl = self.compute_policy_loss(batch)
-        self.actor_opt.grad.zero_()
-        (policy_loss + self.entropy_coef * entropy_loss).backward()
-        kl = approx_kl.detach().float().reshape(1)
-        if world > 1:
-            tdist.all_reduce(self.actor_opt.grad)
-            self.actor_opt.grad.div_(world)
-            tdist.all_reduce(kl)
-            kl = kl / world
-        gate = kl if self.target_kl > 0 else None
-        self.actor_opt.adam(gate, 1.5 * self.target_kl)
         value_loss = self.compute_value_loss(batch)
-        self.critic_opt.grad.zero_()
-        value_loss.backward()
+        self._reduce_buf.zero_()
+        (policy_loss + self.entropy_coef * entropy_loss + value_loss).backward()
+        self._kl.copy_(approx_kl.detach().float().reshape(1))
         if world > 1:
-            tdist.all_reduce(self.critic_opt.grad)
-            self.critic_opt.grad.div_(world)
+            tdist.all_reduce(self._reduce_buf)
+            self._reduce_buf.div_(world)
+        gate = self._kl if self.target_kl > 0 else None
+        self.actor_opt.adam(gate, 1.5 * self.target_kl)
         self.critic_opt.adam(None, 0.0)
         acc += torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
                             entropy_loss.detach().double(), approx_kl.detach().double()])

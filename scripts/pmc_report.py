@@ -25,7 +25,7 @@ def per_kernel(rows, counter):
     return acc
 
 
-def main(fetch_dir, write_dir, calib_bytes, agents, alg_bytes):
+def main(fetch_dir, write_dir, calib_bytes, agents, alg_bytes, envs=16384, drones=8, act="one_d_pid"):
     f = per_kernel(load(fetch_dir), "FETCH_SIZE")
     w = per_kernel(load(write_dir), "WRITE_SIZE")
     cal = [k for k in f if "calib_copy" in k][0]
@@ -36,9 +36,11 @@ def main(fetch_dir, write_dir, calib_bytes, agents, alg_bytes):
     sw = sorted(w[step])[len(w[step]) // 2] * 1024 * cw
     out = {"fetch_scale": cf, "write_scale": cw, "step_fetch_bytes": sf, "step_write_bytes": sw,
            "step_traffic_bytes": sf + sw, "traffic_per_agent_step": (sf + sw) / agents,
-           "algorithmic_per_agent_step": alg_bytes, "launches": len(f[step])}
+           "algorithmic_per_agent_step": alg_bytes, "launches": len(f[step]),
+           "workload": {"envs": envs, "drones": drones, "act": act}}
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], float(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5]))
+    main(sys.argv[1], sys.argv[2], float(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5]),
+         *(int(x) for x in sys.argv[6:8]), *sys.argv[8:9])
