@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include <cmath>
@@ -221,11 +222,9 @@ template <class T> __device__ __forceinline__ void quat_to_rot(const T q[4], T R
   R[6] = xz - wy; R[7] = yz + wx; R[8] = T(1) - (xx + yy);
 }
 // Third column of the same matrix (the body z axis): all the force model of a
-// DYN substep needs.  Same operations as quat_to_rot, so bit-identical.
-template <class T> __device__ __forceinline__ void quat_to_zaxis(const T q[4], T& r2, T& r5, T& r8) {
+// DYN substep needs; s = 2/|q|² supplied by the caller.
+template <class T> __device__ __forceinline__ void quat_to_zaxis_s(const T q[4], T s, T& r2, T& r5, T& r8) {
   T x = q[0], y = q[1], z = q[2], w = q[3];
-  T d = x * x + y * y + z * z + w * w;
-  T s = T(2) * M<T>::rcp(d);
   T xs = x * s, ys = y * s, zs = z * s;
   r2 = x * zs + w * ys;
   r5 = y * zs - w * xs;
@@ -673,6 +672,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
     const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
     const T dt = P.dt;
+    // The exp-map update preserves |q| (cos²θ + sin²θ = 1), so in fp32 Bullet's
+    // s = 2/|q|² (getMatrixFromQuaternion) is formed once per control step; it
+    // moves by rounding only between substeps.
+    const T s2 = T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    // One substep (BaseAviary.py:343-372).  kAux: ground effect / drag /
+    // downwash enabled; the common force-free path is compiled separately.
 #ifdef QS_SUB_NOUNROLL
 #pragma unroll 1
 #else
@@ -686,7 +691,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma clang fp contract(fast)
 #endif
       T R2, R5, R8;
-      quat_to_zaxis(q, R2, R5, R8);
+      // fp64 (the tight-parity path) re-forms s every substep exactly as Bullet does
+      const T sq = sizeof(T) == 8 ? T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) : s2;
+      quat_to_zaxis_s(q, sq, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
       if (P.aux) {
         // no contraction here: the four ground-effect torque arms cancel exactly

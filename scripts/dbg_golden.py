@@ -19,7 +19,9 @@ for t in range(mg.STEPS):
     o = r.obs.cpu().numpy(); g = GOLD[f"{name}/obs"][t]
     bad = np.argwhere(np.abs(o - g) > 2e-6 + 2e-6 * np.abs(g))
     if len(bad):
-        print("step", t, "nbad", len(bad), "cols", sorted(set(bad[:, 2].tolist()))[:40])
+        print("step", t, "nbad", len(bad), "cols", sorted(set(bad[:, 2].tolist()))[:40], "reset_error", sw.reset_error())
+        print("term", r.terminated.cpu().numpy(), "trunc", r.truncated.cpu().numpy())
+        print("pos got", o[:, :, 0:3].round(4).tolist()); print("pos want", g[:, :, 0:3].round(4).tolist())
         e, d, c = bad[0]
         print("env", e, "drone", d, "row got", np.round(o[e, d, 12:], 4).tolist())
         print("               want", np.round(g[e, d, 12:], 4).tolist())
