@@ -109,10 +109,10 @@ def mappo_leg(args, rank, world, dist):
     hidden 256, opt_epochs 10; minibatch scaled to the 128x larger env batch)."""
     from gym_pybullet_drones_amd.envs import MultiHoverAviary
     from gym_pybullet_drones_amd.mappo import MAPPO
-    from gym_pybullet_drones_amd.utils.enums import ActionType
+    from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
     D, E = args.drones, args.envs
     act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[args.act]
-    env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act,
+    env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act, physics=Physics.DYN,
                                                initial_xyzs=grid_layout(D) if D >= 6 else None)
     m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
               rollout_steps=args.mappo_steps, rollout_batch_size=E, opt_epochs=10,

@@ -73,12 +73,16 @@ typedef enum {            /* ActionType (enums.py:35-41)                   */
 } qs_action_type;
 
 typedef enum {            /* Physics (enums.py:13-21)                      */
+  QS_PHYS_PYB = 0,        /* Bullet's step of BaseAviary._physics forces
+                             (BA:679-711, 369-370), restated */
   QS_PHYS_DYN = 1         /* BaseAviary._dynamics (BA:815-892)            */
 } qs_physics;
 
-/* Extra force models added to the DYN force/torque sum (build-defined
- * combination, SURVEY §8 "Physics-mode note"): BaseAviary._groundEffect
- * (BA:715-750), _drag (BA:754-781), _downwash (BA:785-811).              */
+/* Extra force models: BaseAviary._groundEffect (BA:715-750), _drag
+ * (BA:754-781), _downwash (BA:785-811).  With QS_PHYS_PYB they give the
+ * reference's PYB_GND / PYB_DRAG / PYB_DW / PYB_GND_DRAG_DW; with
+ * QS_PHYS_DYN they are added to the DYN force/torque sum (build-defined
+ * combination, SURVEY §8 "Physics-mode note").                           */
 #define QS_AUX_GND 1u
 #define QS_AUX_DRAG 2u
 #define QS_AUX_DW 4u

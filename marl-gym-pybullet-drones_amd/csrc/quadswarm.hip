@@ -58,6 +58,10 @@ constexpr double DRAG_XY = 9.1785e-7, DRAG_Z = 10.311e-7;
 constexpr double GND_COEFF = 11.36859, PROP_R = 2.31348e-2;
 constexpr double DW1 = 2267.18, DW2 = 0.16, DW3 = -0.11;
 }  // namespace cf2x
+// Prop-link COM offsets (assets/cf2x.urdf:42-79), Bullet's default multibody
+// damping (linear = angular = 0.04) and the collision cylinder (cf2x.urdf:32-35).
+constexpr double kPropX[4] = {0.028, -0.028, -0.028, 0.028}, kPropY[4] = {-0.028, -0.028, 0.028, 0.028};
+constexpr double kPybDamping = 0.04, kCylR = 0.06, kCylHalfLen = 0.0125;
 
 // Compile-time shape of an action type (BaseRLAviary.py:262-277).
 template <int ACT> struct Act {
@@ -445,7 +449,7 @@ __device__ __forceinline__ void issue_fence() { __asm__ volatile("" ::: "memory"
 // 30 Hz, Spiral 48 Hz): the substep count, history length and obs width are
 // then constants (fully unrolled substeps, constant obs offsets); CF = 0 reads
 // them from P.
-template <class T, int TASK, int ACT, int CF>
+template <class T, int TASK, int ACT, int CF, int PHYS>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   using F = M<T>;
   constexpr int A = Act<ACT>::A;
@@ -671,6 +675,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const T tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];
     const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
     const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
+    // PYB: the four prop forces act at their links' COMs (assets/cf2x.urdf:42-79)
+    const T pbx = (((T(kPropY[0]) * f[0]) + T(kPropY[1]) * f[1]) + T(kPropY[2]) * f[2]) + T(kPropY[3]) * f[3];
+    const T pby = (((-T(kPropX[0]) * f[0]) + -T(kPropX[1]) * f[1]) + -T(kPropX[2]) * f[2]) + -T(kPropX[3]) * f[3];
     const T dt = P.dt;
     // The exp-map update preserves |q| (cos²θ + sin²θ = 1), so in fp32 Bullet's
     // s = 2/|q|² (getMatrixFromQuaternion) is formed once per control step; it
@@ -704,8 +711,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           quat_to_rpy(q, srpy);
           quat_to_rot(q, R);
           if (F::abs_(srpy[0]) < T(M_PI / 2) && F::abs_(srpy[1]) < T(M_PI / 2)) {
-            const T PX[4] = {T(0.028), T(-0.028), T(-0.028), T(0.028)};
-            const T PY[4] = {T(-0.028), T(-0.028), T(0.028), T(0.028)};
+            const T PX[4] = {T(kPropX[0]), T(kPropX[1]), T(kPropX[2]), T(kPropX[3])};
+            const T PY[4] = {T(kPropY[0]), T(kPropY[1]), T(kPropY[2]), T(kPropY[3])};
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
               T h = pos[2] + (R[6] * PX[m] + R[7] * PY[m]);
@@ -745,42 +752,102 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           }
         }
       }
-      // _dynamics (BaseAviary.py:836-877)
-      T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
-      T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
-      T c0 = F::sub_rn(F::mul_rn(w[1], Jw2), F::mul_rn(w[2], Jw1));
-      T c1 = F::sub_rn(F::mul_rn(w[2], Jw0), F::mul_rn(w[0], Jw2));
-      T c2 = F::sub_rn(F::mul_rn(w[0], Jw1), F::mul_rn(w[1], Jw0));
-      T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
-      T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
-      vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
-      vel[1] = vel[1] + dt * F::divc(fw1, cf2x::M);
-      vel[2] = vel[2] + dt * F::divc(fw2, cf2x::M);
-      w[0] = w[0] + dt * wd0;
-      w[1] = w[1] + dt * wd1;
-      w[2] = w[2] + dt * wd2;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
-      if (sub == S - 1) {
-        // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875);
-        // only the last substep's value reaches the obs.
+      if constexpr (PHYS == QS_PHYS_PYB) {
+        // Bullet's step of the _physics forces (BA:679-711, 369-370), restated
+        // as the oracle's pyb_dynamics.  No contraction: the
+        // prop-torque sums cancel exactly for equal rotors only without FMA.
+#pragma clang fp contract(off)
         T R[9];
         quat_to_rot(q, R);
-        angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
-        angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
-        angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
-      }
-      // _integrateQ (BaseAviary.py:879-892); np.isclose(|ω|, 0) ⇔ |ω| <= 1e-8
-      const T wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-      if (wn2 > T(1e-16)) {
-        T c, k;
-        expmap_coeffs(wn2, P.hdt, P.hdt2, c, k);
-        const T p_ = w[0], q_ = w[1], r_ = w[2];
+        const T k = T(kPybDamping);
+        T fw0 = R[2] * zb + fwx, fw1 = R[5] * zb + fwy, fw2 = (R[8] * zb - T(cf2x::GRAVITY)) + fwz;
+        const T vd = k + k * F::sqrt_(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
+        const T a0 = fw0 / T(cf2x::M) - vd * vel[0], a1 = fw1 / T(cf2x::M) - vd * vel[1];
+        const T a2 = fw2 / T(cf2x::M) - vd * vel[2];
+        T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
+        T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
+        const T wdm = k + k * F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        T wd0 = T(1.0 / cf2x::IXX) * (((pbx + txe) - c0) - wdm * Jw0);
+        T wd1 = T(1.0 / cf2x::IYY) * (((pby + tye) - c1) - wdm * Jw1);
+        T wd2 = T(1.0 / cf2x::IZZ) * ((tz - c2) - wdm * Jw2);
+        vel[0] = vel[0] + dt * a0;
+        vel[1] = vel[1] + dt * a1;
+        vel[2] = vel[2] + dt * a2;
+        w[0] = w[0] + dt * wd0;
+        w[1] = w[1] + dt * wd1;
+        w[2] = w[2] + dt * wd2;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
+        // exp map of the world angular velocity (|ω|dt clamped to π/4), renormalised
+        const T ww0 = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
+        const T ww1 = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
+        const T ww2 = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
+        T ang2 = ww0 * ww0 + ww1 * ww1 + ww2 * ww2;
+        const T amax = T(0.25 * M_PI) / dt;
+        if (ang2 > amax * amax) ang2 = amax * amax;
+        T c, kk;
+        expmap_coeffs(ang2, P.hdt, P.hdt2, c, kk);   // cos(|ω|dt/2), sin(|ω|dt/2)/|ω|
+        const T e0 = ww0 * kk, e1 = ww1 * kk, e2 = ww2 * kk;
         const T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
-        q[0] = c * x0 + k * (r_ * x1 - q_ * x2 + p_ * x3);
-        q[1] = c * x1 + k * (-r_ * x0 + p_ * x2 + q_ * x3);
-        q[2] = c * x2 + k * (q_ * x0 - p_ * x1 + r_ * x3);
-        q[3] = c * x3 + k * (-p_ * x0 - q_ * x1 - r_ * x2);
+        T n0 = ((c * x0 + e0 * x3) + e1 * x2) - e2 * x1;
+        T n1 = ((c * x1 - e0 * x2) + e1 * x3) + e2 * x0;
+        T n2 = ((c * x2 + e0 * x1) - e1 * x0) + e2 * x3;
+        T n3 = ((c * x3 - e0 * x0) - e1 * x1) - e2 * x2;
+        const T qn = F::sqrt_(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
+        q[0] = n0 / qn; q[1] = n1 / qn; q[2] = n2 / qn; q[3] = n3 / qn;
+        // ground plane vs the collision cylinder (cf2x.urdf:32-35)
+        T Rn[9];
+        quat_to_rot(q, Rn);
+        const T cz = F::abs_(Rn[8]);
+        const T sz = F::sqrt_(T(1) - Rn[8] * Rn[8] > T(0) ? T(1) - Rn[8] * Rn[8] : T(0));
+        const T zmin = pos[2] - (T(kCylHalfLen) * cz + T(kCylR) * sz);
+        if (zmin < T(0)) {
+          pos[2] = pos[2] - zmin;
+          if (vel[2] < T(0)) vel[2] = T(0);
+        }
+        if (sub == S - 1) {   // getBaseVelocity: world angular velocity at the new pose
+          angv[0] = Rn[0] * w[0] + Rn[1] * w[1] + Rn[2] * w[2];
+          angv[1] = Rn[3] * w[0] + Rn[4] * w[1] + Rn[5] * w[2];
+          angv[2] = Rn[6] * w[0] + Rn[7] * w[1] + Rn[8] * w[2];
+        }
+      } else {
+        // _dynamics (BaseAviary.py:836-877)
+        T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
+        T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
+        T c0 = F::sub_rn(F::mul_rn(w[1], Jw2), F::mul_rn(w[2], Jw1));
+        T c1 = F::sub_rn(F::mul_rn(w[2], Jw0), F::mul_rn(w[0], Jw2));
+        T c2 = F::sub_rn(F::mul_rn(w[0], Jw1), F::mul_rn(w[1], Jw0));
+        T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
+        T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
+        vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
+        vel[1] = vel[1] + dt * F::divc(fw1, cf2x::M);
+        vel[2] = vel[2] + dt * F::divc(fw2, cf2x::M);
+        w[0] = w[0] + dt * wd0;
+        w[1] = w[1] + dt * wd1;
+        w[2] = w[2] + dt * wd2;
+  #pragma unroll
+        for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
+        if (sub == S - 1) {
+          // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875);
+          // only the last substep's value reaches the obs.
+          T R[9];
+          quat_to_rot(q, R);
+          angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
+          angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
+          angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
+        }
+        // _integrateQ (BaseAviary.py:879-892); np.isclose(|ω|, 0) ⇔ |ω| <= 1e-8
+        const T wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+        if (wn2 > T(1e-16)) {
+          T c, k;
+          expmap_coeffs(wn2, P.hdt, P.hdt2, c, k);
+          const T p_ = w[0], q_ = w[1], r_ = w[2];
+          const T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+          q[0] = c * x0 + k * (r_ * x1 - q_ * x2 + p_ * x3);
+          q[1] = c * x1 + k * (-r_ * x0 + p_ * x2 + q_ * x3);
+          q[2] = c * x2 + k * (q_ * x0 - p_ * x1 + r_ * x3);
+          q[3] = c * x3 + k * (-p_ * x0 - q_ * x1 - r_ * x2);
+        }
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
@@ -1152,22 +1219,26 @@ static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
 }
 
 template <class T, int TASK, int ACT> static void launch_one(int grid, size_t lds, hipStream_t st, const qs::Params<T>& P,
-                                                             int ctrl_freq, int pyb_freq) {
+                                                             int ctrl_freq, int pyb_freq, int phys) {
   constexpr int kCF = TASK == QS_TASK_MULTIHOVER ? 30 : 48;   // MultiHoverAviary.py:20, SpiralAviary.py:28
-  if (ctrl_freq == kCF && pyb_freq == 240)
-    hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, kCF>), dim3(grid), dim3(qs::kBlock), lds, st, P);
-  else
-    hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, 0>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+  const bool cf = ctrl_freq == kCF && pyb_freq == 240;
+  if (phys == QS_PHYS_DYN) {
+    if (cf) hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+    else hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+  } else {
+    if (cf) hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+    else hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB>), dim3(grid), dim3(qs::kBlock), lds, st, P);
+  }
 }
 
 template <class T, int TASK> static int launch_act(int act, int grid, size_t lds, hipStream_t st, const qs::Params<T>& P,
-                                                   int cf, int pf) {
+                                                   int cf, int pf, int ph) {
   switch (act) {
-    case QS_ACT_RPM: launch_one<T, TASK, QS_ACT_RPM>(grid, lds, st, P, cf, pf); break;
-    case QS_ACT_PID: launch_one<T, TASK, QS_ACT_PID>(grid, lds, st, P, cf, pf); break;
-    case QS_ACT_VEL: launch_one<T, TASK, QS_ACT_VEL>(grid, lds, st, P, cf, pf); break;
-    case QS_ACT_ONE_D_RPM: launch_one<T, TASK, QS_ACT_ONE_D_RPM>(grid, lds, st, P, cf, pf); break;
-    case QS_ACT_ONE_D_PID: launch_one<T, TASK, QS_ACT_ONE_D_PID>(grid, lds, st, P, cf, pf); break;
+    case QS_ACT_RPM: launch_one<T, TASK, QS_ACT_RPM>(grid, lds, st, P, cf, pf, ph); break;
+    case QS_ACT_PID: launch_one<T, TASK, QS_ACT_PID>(grid, lds, st, P, cf, pf, ph); break;
+    case QS_ACT_VEL: launch_one<T, TASK, QS_ACT_VEL>(grid, lds, st, P, cf, pf, ph); break;
+    case QS_ACT_ONE_D_RPM: launch_one<T, TASK, QS_ACT_ONE_D_RPM>(grid, lds, st, P, cf, pf, ph); break;
+    case QS_ACT_ONE_D_PID: launch_one<T, TASK, QS_ACT_ONE_D_PID>(grid, lds, st, P, cf, pf, ph); break;
     default: return fail(QS_E_INVALID, "launch: bad act_type");
   }
   return QS_OK;
@@ -1179,8 +1250,10 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (lds_plan(h->dims, &P.stage_rows, &lds) != QS_OK)
     return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
   const int rc = h->spec.task == QS_TASK_MULTIHOVER
-                     ? launch_act<T, QS_TASK_MULTIHOVER>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq, h->spec.pyb_freq)
-                     : launch_act<T, QS_TASK_SPIRAL>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq, h->spec.pyb_freq);
+                     ? launch_act<T, QS_TASK_MULTIHOVER>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq,
+                                                         h->spec.pyb_freq, h->spec.physics)
+                     : launch_act<T, QS_TASK_SPIRAL>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq,
+                                                     h->spec.pyb_freq, h->spec.physics);
   if (rc != QS_OK) return rc;
   HIP_TRY(hipGetLastError());
   return QS_OK;
@@ -1217,7 +1290,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   if (s.task != QS_TASK_MULTIHOVER && s.task != QS_TASK_SPIRAL) return fail(QS_E_INVALID, "qs_create: bad task");
   if (s.num_drones < 1 || s.num_drones > 64) return fail(QS_E_INVALID, "qs_create: num_drones must be in 1..64");
   if (s.num_envs < 1) return fail(QS_E_INVALID, "qs_create: num_envs must be >= 1");
-  if (s.physics != QS_PHYS_DYN) return fail(QS_E_INVALID, "qs_create: only Physics.DYN is implemented (PYB is SURVEY §8(f) next-1)");
+  if (s.physics != QS_PHYS_DYN && s.physics != QS_PHYS_PYB) return fail(QS_E_INVALID, "qs_create: bad physics");
   if (s.aux_forces & ~7u) return fail(QS_E_INVALID, "qs_create: bad aux_forces");
   if (s.flags & ~QS_FLAG_NO_AUTORESET) return fail(QS_E_INVALID, "qs_create: bad flags");
   if (s.pyb_freq <= 0 || s.ctrl_freq <= 0 || s.pyb_freq % s.ctrl_freq)

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libquadswarm.so")
 QS_OK = 0
 TASK_MULTIHOVER, TASK_SPIRAL = 0, 1
 ACT_RPM, ACT_PID, ACT_VEL, ACT_ONE_D_RPM, ACT_ONE_D_PID = 0, 1, 2, 3, 4
-PHYS_DYN = 1
+PHYS_PYB, PHYS_DYN = 0, 1
 AUX_GND, AUX_DRAG, AUX_DW = 1, 2, 4
 AGENT_FIELDS, ENV_FIELDS = 29, 4
 STATE_AGENT, STATE_ENV, STATE_HISTORY, STATE_EP_RETURN = 0, 1, 2, 3

@@ -7,9 +7,8 @@ envs/BaseAviary.py:220-383) over an E=1 slice of the HIP QuadSwarm with the
 vec-env auto-reset disabled (BaseAviary.step never resets by itself).
 gymnasium is not installed here, so the class is duck-typed.
 
-Deviation: the reference default physics is Physics.PYB (Bullet); the
-Bullet-equivalent mode is SURVEY §8(f) next-1, so the facades default to
-Physics.DYN.
+Physics defaults to Physics.PYB like the reference (MH:18, SP:26): the kernel's
+restatement of Bullet's step (parity unpinned against pybullet).
 """
 import numpy as np
 import torch
@@ -23,7 +22,7 @@ class _SingleEnvAviary:
     TASK = None
 
     def __init__(self, drone_model=DroneModel.CF2X, num_drones=2, neighbourhood_radius=np.inf, initial_xyzs=None,
-                 initial_rpys=None, physics=Physics.DYN, pyb_freq=240, ctrl_freq=30, gui=False, record=False,
+                 initial_rpys=None, physics=Physics.PYB, pyb_freq=240, ctrl_freq=30, gui=False, record=False,
                  obs=ObservationType.KIN, act=ActionType.RPM, device=None, precision=4, **task_kw):
         if gui or record:
             raise NotImplementedError("GUI/recording are out of scope (SURVEY §2)")
@@ -115,7 +114,7 @@ class MultiHoverAviary(_SingleEnvAviary):
     TASK = "multihover"
 
     def __init__(self, drone_model=DroneModel.CF2X, num_drones=2, neighbourhood_radius=np.inf, initial_xyzs=None,
-                 initial_rpys=None, physics=Physics.DYN, pyb_freq=240, ctrl_freq=30, gui=False, record=False,
+                 initial_rpys=None, physics=Physics.PYB, pyb_freq=240, ctrl_freq=30, gui=False, record=False,
                  obs=ObservationType.KIN, act=ActionType.RPM, **kw):
         super().__init__(drone_model, num_drones, neighbourhood_radius, initial_xyzs, initial_rpys, physics,
                          pyb_freq, ctrl_freq, gui, record, obs, act, **kw)
@@ -133,7 +132,7 @@ class SpiralFormationAviary(_SingleEnvAviary):
     TASK = "spiral"
 
     def __init__(self, drone_model=DroneModel.CF2X, num_drones=3, neighbourhood_radius=np.inf, initial_xyzs=None,
-                 initial_rpys=None, physics=Physics.DYN, pyb_freq=240, ctrl_freq=48, gui=False, record=False,
+                 initial_rpys=None, physics=Physics.PYB, pyb_freq=240, ctrl_freq=48, gui=False, record=False,
                  obs=ObservationType.KIN, act=ActionType.VEL, spiral_radius=0.4, spiral_period=10.0,
                  height_rate=0.05, target_center=np.array([0.0, 0.0, 0.0]), **kw):
         self.R = spiral_radius

@@ -25,9 +25,12 @@ from ..utils.enums import ActionType, DroneModel, Physics
 
 _ACT = {ActionType.RPM: L.ACT_RPM, ActionType.PID: L.ACT_PID, ActionType.VEL: L.ACT_VEL,
         ActionType.ONE_D_RPM: L.ACT_ONE_D_RPM, ActionType.ONE_D_PID: L.ACT_ONE_D_PID}
-# Physics → aux force bits on top of the DYN integrator.
-_AUX = {Physics.DYN: 0, Physics.PYB_GND: L.AUX_GND, Physics.PYB_DRAG: L.AUX_DRAG, Physics.PYB_DW: L.AUX_DW,
-        Physics.PYB_GND_DRAG_DW: L.AUX_GND | L.AUX_DRAG | L.AUX_DW}
+# Physics → (integrator, aux force bits) (enums.py:13-21, BA:352-367).
+_PHYS = {Physics.DYN: (L.PHYS_DYN, 0), Physics.PYB: (L.PHYS_PYB, 0),
+         Physics.PYB_GND: (L.PHYS_PYB, L.AUX_GND), Physics.PYB_DRAG: (L.PHYS_PYB, L.AUX_DRAG),
+         Physics.PYB_DW: (L.PHYS_PYB, L.AUX_DW),
+         Physics.PYB_GND_DRAG_DW: (L.PHYS_PYB, L.AUX_GND | L.AUX_DRAG | L.AUX_DW)}
+_AUX_NAMES = {"gnd": L.AUX_GND, "drag": L.AUX_DRAG, "dw": L.AUX_DW}
 TASKS = {"multihover": L.TASK_MULTIHOVER, "spiral": L.TASK_SPIRAL}
 
 
@@ -66,7 +69,11 @@ class QuadSwarm:
     def __init__(self, task="multihover", num_envs=1, num_drones=2, act=ActionType.RPM, physics=Physics.DYN,
                  pyb_freq=240, ctrl_freq=None, precision=4, device=None, env_offset=0, initial_xyzs=None,
                  episode_len_sec=None, autoreset=True, drone_model=DroneModel.CF2X,
-                 spiral_radius=0.4, spiral_period=10.0, height_rate=0.05, target_center=(0.0, 0.0, 0.0)):
+                 spiral_radius=0.4, spiral_period=10.0, height_rate=0.05, target_center=(0.0, 0.0, 0.0),
+                 aux=()):
+        """aux: extra force models ("gnd", "drag", "dw") added on top of `physics`;
+        with Physics.DYN this is the build-defined DYN + aux combination (SURVEY §8
+        physics-mode note), e.g. C5's DYN + downwash."""
         if task not in TASKS:
             raise ValueError(f"unknown task {task!r}")
         act = _as_enum(act, ActionType)
@@ -74,9 +81,8 @@ class QuadSwarm:
         drone_model = _as_enum(drone_model, DroneModel)
         if drone_model != DroneModel.CF2X:
             raise NotImplementedError("only DroneModel.CF2X is implemented (the MAPPO tasks' model)")
-        if physics not in _AUX:
-            raise NotImplementedError(
-                "Physics.PYB (Bullet-integrated) is not implemented yet (SURVEY §8(f) next-1); use Physics.DYN")
+        if any(a not in _AUX_NAMES for a in aux):
+            raise ValueError(f"unknown aux force model in {aux!r} (gnd, drag, dw)")
         if not torch.cuda.is_available():
             raise L.QuadSwarmError("QuadSwarm needs a ROCm GPU: the step runs only as a HIP kernel (no CPU path)")
         self.lib = L.load()
@@ -93,8 +99,9 @@ class QuadSwarm:
         spec.num_envs = int(num_envs)
         spec.num_drones = int(num_drones)
         spec.act_type = _ACT[act]
-        spec.physics = L.PHYS_DYN
-        spec.aux_forces = _AUX[physics]
+        phys_id, aux_bits = _PHYS[physics]
+        spec.physics = phys_id
+        spec.aux_forces = aux_bits | sum(_AUX_NAMES[a] for a in set(aux))
         spec.pyb_freq = int(pyb_freq)
         spec.ctrl_freq = int(ctrl_freq)
         spec.precision = int(precision)

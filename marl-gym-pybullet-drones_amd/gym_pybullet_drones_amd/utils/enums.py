@@ -12,11 +12,11 @@ class DroneModel(Enum):
 class Physics(Enum):
     """Physics implementations.
 
-    DYN is the explicit dynamics model (BaseAviary._dynamics, BA:815-892) and is
-    what the HIP integrator implements.  The PYB_* modes are Bullet-integrated in
-    the reference; here PYB_GND / PYB_DRAG / PYB_DW / PYB_GND_DRAG_DW map to DYN
-    plus the corresponding force models (build-defined) and
-    PYB itself is not implemented yet.
+    DYN is the explicit dynamics model (BaseAviary._dynamics, BA:815-892).  PYB
+    and PYB_GND / PYB_DRAG / PYB_DW / PYB_GND_DRAG_DW are the kernel's
+    restatement of Bullet's step of the _physics forces (plus the named force
+    models); DYN plus force models is available through
+    QuadSwarm(aux=...) (build-defined, SURVEY §8 physics-mode note).
     """
     PYB = "pyb"
     DYN = "dyn"

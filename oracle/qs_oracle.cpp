@@ -148,7 +148,7 @@ template <class R> struct Drone {
 };
 
 template <class R> struct Params {
-  int task, D, E, A, H, S, act_type, O;
+  int task, D, E, A, H, S, act_type, O, physics;
   uint32_t aux, flags;
   R dt, ctrl_dt, ep_len_sec;
   int pyb_freq;
@@ -349,6 +349,140 @@ void dynamics(const Params<R>& P, Drone<R>& d, const R rpm[4], const Snap<R>* sn
   // resetBaseVelocity(vel, R_old·ω) (BA:871-875); rpy_rates stored (BA:877)
   for (int i = 0; i < 3; ++i) {
     d.ang_v[i] = rot[i][0] * w[0] + rot[i][1] * w[1] + rot[i][2] * w[2];
+    d.rpy_rates[i] = w[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Physics.PYB: the drone as Bullet integrates it (p.stepSimulation, BA:369-370)
+// after BaseAviary._physics (BA:679-711) applied its forces.  Restated from the
+// published btMultiBody algorithm (pybullet 3.2.7, external — unverified here,
+// parity unpinned):
+//  * cf2x.urdf loads as one rigid body (the prop and COM links are fixed and
+//    massless): mass M, inertia diag(IXX, IYY, IZZ) about the base COM.
+//  * each prop force [0,0,f_i] acts in LINK_FRAME at its link's COM
+//    (assets/cf2x.urdf:42-79) → body torque r_i × f_i; the yaw torque acts on
+//    link 4 (the COM) in LINK_FRAME; gravity [0,0,-G·M] (BA:479).
+//  * btMultiBody's default damping (linear = angular = 0.04, not removed by
+//    BA:492-494) as its bias force m·v·(k + k|v|), I·ω·(k + k|ω|), and the
+//    gyroscopic term ω × Iω, evaluated at the step's starting velocities.
+//  * semi-implicit Euler: velocities first, then the position with the new
+//    velocity, then the orientation by the exponential map of the world
+//    angular velocity (btMultiBody::stepPositionsMultiDof: |ω|dt clamped to
+//    π/4, sinc Taylor branch below |ω| = 0.001), renormalised.
+//  * ground plane z = 0 (plane.urdf) against the drone's collision cylinder
+//    (r 0.06, length 0.025, cf2x.urdf:32-35): a penetrating lowest point is
+//    pushed back to z = 0 and the downward normal velocity removed
+//    (inelastic, frictionless — Bullet's contact solver is not restated).
+// With aux forces (PYB_GND / PYB_DRAG / PYB_DW) the same external forces as
+// DYN's aux path are applied (BA:715-811).
+// ---------------------------------------------------------------------------
+constexpr double kPybDamping = 0.04;
+constexpr double kCylR = 0.06, kCylHalfLen = 0.0125;
+
+template <class R>
+void pyb_dynamics(const Params<R>& P, Drone<R>& d, const R rpm[4], const Snap<R>* snaps, int self) {
+  R rot[3][3];
+  quat_to_matrix(d.quat, rot);
+  R f[4], zt[4];
+  for (int m = 0; m < 4; ++m) { f[m] = rpm[m] * rpm[m] * P.KF; zt[m] = rpm[m] * rpm[m] * P.KM; }
+  // body-frame force (z) and torque of the prop forces at the prop-link COMs
+  R fzb = ((f[0] + f[1]) + f[2]) + f[3];
+  R tb[3] = {0, 0, ((-zt[0] + zt[1]) - zt[2]) + zt[3]};
+  for (int m = 0; m < 4; ++m) { tb[0] += P.PROP_XY[m][1] * f[m]; tb[1] += -P.PROP_XY[m][0] * f[m]; }
+  R fw_extra[3] = {0, 0, 0};
+  if (P.aux & QS_AUX_GND) {  // _groundEffect (BA:731-750): LINK_FRAME forces at the props
+    const Snap<R>& sn = snaps[self];
+    if (std::fabs(sn.rpy[0]) < R(M_PI / 2) && std::fabs(sn.rpy[1]) < R(M_PI / 2)) {
+      R srot[3][3];
+      quat_to_matrix(sn.quat, srot);
+      for (int m = 0; m < 4; ++m) {
+        R h = sn.pos[2] + (srot[2][0] * P.PROP_XY[m][0] + srot[2][1] * P.PROP_XY[m][1]);
+        h = h < P.GND_CLIP ? P.GND_CLIP : h;
+        R ratio = P.PROP_R / (R(4) * h);
+        R g = rpm[m] * rpm[m] * P.KF * P.GND_COEFF * (ratio * ratio);
+        fzb += g;
+        tb[0] += P.PROP_XY[m][1] * g;
+        tb[1] += -P.PROP_XY[m][0] * g;
+      }
+    }
+  }
+  if (P.aux & QS_AUX_DRAG) {  // _drag (BA:770-781): world force from the previous rpm
+    const Snap<R>& sn = snaps[self];
+    R srpm = 0;
+    for (int m = 0; m < 4; ++m) srpm += R(2 * M_PI) * d.last_rpm[m] / R(60);
+    for (int i = 0; i < 3; ++i) fw_extra[i] += (R(-1) * P.DRAG[i] * srpm) * sn.vel[i];
+  }
+  if (P.aux & QS_AUX_DW) {  // _downwash (BA:798-811): LINK_FRAME z force on link 4 (the COM)
+    const Snap<R>& me = snaps[self];
+    for (int j = 0; j < P.D; ++j) {
+      R dz = snaps[j].pos[2] - me.pos[2];
+      R dx = snaps[j].pos[0] - me.pos[0], dy = snaps[j].pos[1] - me.pos[1];
+      R dxy = std::sqrt(dx * dx + dy * dy);
+      if (dz > R(0) && dxy < R(10)) {
+        R ratio = P.PROP_R / (R(4) * dz);
+        R alpha = P.DW1 * (ratio * ratio);
+        R beta = P.DW2 * dz + P.DW3;
+        R q = dxy / beta;
+        fzb += -alpha * std::exp(R(-.5) * (q * q));
+      }
+    }
+  }
+  const R k = R(kPybDamping);
+  // linear: world force, damping, semi-implicit velocity update
+  R Fw[3] = {rot[0][2] * fzb + fw_extra[0], rot[1][2] * fzb + fw_extra[1],
+             (rot[2][2] * fzb - P.GRAVITY_DYN) + fw_extra[2]};
+  R vn = norm3(d.vel);
+  R vd = k + k * vn;
+  R acc[3];
+  for (int i = 0; i < 3; ++i) acc[i] = Fw[i] / P.M - vd * d.vel[i];
+  // angular (body frame): torque − gyroscopic − damping
+  R w[3] = {d.rpy_rates[0], d.rpy_rates[1], d.rpy_rates[2]};
+  R Jw[3] = {P.Jd[0] * w[0], P.Jd[1] * w[1], P.Jd[2] * w[2]};
+  R wxJw[3];
+  cross3(w, Jw, wxJw);
+  R wd = k + k * norm3(w);
+  R wdot[3];
+  for (int i = 0; i < 3; ++i) wdot[i] = P.Jinv[i] * ((tb[i] - wxJw[i]) - wd * Jw[i]);
+  for (int i = 0; i < 3; ++i) d.vel[i] = d.vel[i] + P.dt * acc[i];
+  for (int i = 0; i < 3; ++i) w[i] = w[i] + P.dt * wdot[i];
+  for (int i = 0; i < 3; ++i) d.pos[i] = d.pos[i] + P.dt * d.vel[i];
+  // orientation: exp map of the world angular velocity, then renormalise
+  R ww[3];
+  for (int i = 0; i < 3; ++i) ww[i] = rot[i][0] * w[0] + rot[i][1] * w[1] + rot[i][2] * w[2];
+  R ang = norm3(ww);
+  const R kMaxAng = R(0.25 * M_PI);
+  if (ang * P.dt > kMaxAng) ang = kMaxAng / P.dt;
+  R ax[3];
+  if (ang < R(0.001)) {
+    R c = R(0.5) * P.dt - (P.dt * P.dt * P.dt) * R(0.020833333333) * ang * ang;
+    for (int i = 0; i < 3; ++i) ax[i] = ww[i] * c;
+  } else {
+    R c = std::sin(R(0.5) * ang * P.dt) / ang;
+    for (int i = 0; i < 3; ++i) ax[i] = ww[i] * c;
+  }
+  R dw_ = std::cos(ang * P.dt * R(0.5));
+  const R* q = d.quat;
+  // Hamilton product dq ⊗ q, quaternions stored (x, y, z, w)
+  R nq[4] = {dw_ * q[0] + ax[0] * q[3] + ax[1] * q[2] - ax[2] * q[1],
+             dw_ * q[1] - ax[0] * q[2] + ax[1] * q[3] + ax[2] * q[0],
+             dw_ * q[2] + ax[0] * q[1] - ax[1] * q[0] + ax[2] * q[3],
+             dw_ * q[3] - ax[0] * q[0] - ax[1] * q[1] - ax[2] * q[2]};
+  R qn = std::sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+  for (int i = 0; i < 4; ++i) d.quat[i] = nq[i] / qn;
+  // ground plane: keep the collision cylinder's lowest point at z >= 0
+  R nrot[3][3];
+  quat_to_matrix(d.quat, nrot);
+  R cz = std::fabs(nrot[2][2]);
+  R sz = std::sqrt(std::max(R(0), R(1) - nrot[2][2] * nrot[2][2]));
+  R zmin = d.pos[2] - (R(kCylHalfLen) * cz + R(kCylR) * sz);
+  if (zmin < R(0)) {
+    d.pos[2] -= zmin;
+    if (d.vel[2] < R(0)) d.vel[2] = R(0);
+  }
+  // readback: getBaseVelocity's world angular velocity (BA:514-515) at the new pose
+  for (int i = 0; i < 3; ++i) {
+    d.ang_v[i] = nrot[i][0] * w[0] + nrot[i][1] * w[1] + nrot[i][2] * w[2];
     d.rpy_rates[i] = w[i];
   }
 }
@@ -571,7 +705,10 @@ template <class R> struct Sim {
         euler_from_quat(dr.quat, dr.rpy);
         for (int i = 0; i < 3; ++i) snaps[d].rpy[i] = dr.rpy[i];
       }
-      for (int d = 0; d < D; ++d) dynamics(P, drones[e * D + d], &rpm[d * 4], snaps.data(), d);
+      for (int d = 0; d < D; ++d) {
+        if (P.physics == QS_PHYS_PYB) pyb_dynamics(P, drones[e * D + d], &rpm[d * 4], snaps.data(), d);
+        else dynamics(P, drones[e * D + d], &rpm[d * 4], snaps.data(), d);
+      }
       for (int d = 0; d < D; ++d)  // last_clipped_action = clipped_action (BA:372)
         for (int m = 0; m < 4; ++m) drones[e * D + d].last_rpm[m] = rpm[d * 4 + m];
     }
@@ -620,10 +757,11 @@ template <class R> int make_params(const qs_spec* s, Params<R>& P) {
   if (s->task != QS_TASK_MULTIHOVER && s->task != QS_TASK_SPIRAL) return fail(QS_E_INVALID, "bad task");
   if (s->num_drones < 1 || s->num_drones > 64) return fail(QS_E_INVALID, "num_drones must be 1..64");
   if (s->num_envs < 1) return fail(QS_E_INVALID, "num_envs must be >= 1");
-  if (s->physics != QS_PHYS_DYN) return fail(QS_E_INVALID, "only Physics.DYN is implemented");
+  if (s->physics != QS_PHYS_DYN && s->physics != QS_PHYS_PYB) return fail(QS_E_INVALID, "bad physics");
   if (s->pyb_freq <= 0 || s->ctrl_freq <= 0 || s->pyb_freq % s->ctrl_freq)
     return fail(QS_E_INVALID, "pyb_freq is not divisible by env_freq");   // BA:79-80
   P.task = s->task; P.D = s->num_drones; P.E = s->num_envs; P.act_type = s->act_type; P.aux = s->aux_forces;
+  P.physics = s->physics;
   P.flags = s->flags;
   switch (s->act_type) {
     case QS_ACT_RPM: case QS_ACT_VEL: P.A = 4; break;

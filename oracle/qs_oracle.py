@@ -92,7 +92,7 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def make_spec(task="multihover", num_envs=1, num_drones=2, act="rpm", aux=(), ctrl_freq=None, pyb_freq=240,
+def make_spec(task="multihover", num_envs=1, num_drones=2, act="rpm", aux=(), physics="dyn", ctrl_freq=None, pyb_freq=240,
               precision=8, env_offset=0, episode_len_sec=None, initial_xyzs=None, autoreset=True,
               spiral_radius=0.4, spiral_period=10.0, height_rate=0.05, target_center=(0.0, 0.0, 0.0)):
     s = QsSpec()
@@ -100,7 +100,7 @@ def make_spec(task="multihover", num_envs=1, num_drones=2, act="rpm", aux=(), ct
     s.num_envs = num_envs
     s.num_drones = num_drones
     s.act_type = ACT[act]
-    s.physics = 1
+    s.physics = {"pyb": 0, "dyn": 1}[physics]
     s.aux_forces = sum(AUX[a] for a in aux)
     s.pyb_freq = pyb_freq
     s.ctrl_freq = ctrl_freq if ctrl_freq is not None else (30 if task == "multihover" else 48)

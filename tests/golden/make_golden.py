@@ -21,6 +21,8 @@ CASES = {
     "mh_vel_d3": dict(task="multihover", num_drones=3, act="vel"),
     "spiral_vel_d5": dict(task="spiral", num_drones=5, act="vel"),
     "mh_dw_d16": dict(task="multihover", num_drones=16, act="one_d_pid", initial_xyzs=grid_layout(16), aux=("dw",)),
+    "mh_onedpid_d8_pyb": dict(task="multihover", num_drones=8, act="one_d_pid", initial_xyzs=grid_layout(8),
+                              physics="pyb"),
 }
 E, STEPS, SEED = 3, 40, 123
 

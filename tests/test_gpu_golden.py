@@ -20,7 +20,8 @@ def test_kernel_replays_golden(name, precision):
     from gym_pybullet_drones_amd.utils.enums import Physics
     kw = dict(mg.CASES[name])
     aux = kw.pop("aux", ())
-    sw = QuadSwarm(num_envs=mg.E, precision=precision, physics=Physics.PYB_DW if aux else Physics.DYN, **kw)
+    phys = Physics.PYB if kw.pop("physics", "dyn") == "pyb" else Physics.DYN
+    sw = QuadSwarm(num_envs=mg.E, precision=precision, physics=phys, aux=aux, **kw)
     np.testing.assert_allclose(sw.reset(mg.SEED).cpu().numpy(), GOLD[f"{name}/obs0"], atol=1e-7)
     act = torch.zeros((mg.E, sw.num_drones, sw.act_dim), device=sw.device)
     steps = mg.STEPS if precision == 8 else 10   # fp32: short open-loop horizon
