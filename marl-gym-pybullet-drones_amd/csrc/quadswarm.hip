@@ -1,25 +1,10 @@
-// quadswarm.hip — MI355X (gfx950) batched quadrotor-swarm control step.
-//
-// One launch advances every (env, drone) of a shard by one control step:
-// action → RPM (incl. the DSL PID), PYB_STEPS_PER_CTRL rigid-body substeps,
-// readback, MultiHover/Spiral obs + reward + termination, and the vec-env
-// auto-reset.  It replaces BaseAviary.step (BaseAviary.py:259-383) driven by
-// SubprocVecEnv workers (subproc_vec_env.py:188-206); see include/quadswarm.h
-// for the per-entry-point reference mapping.
-//
-// Layout (DESIGN.md §HBM layout): per-agent state is structure-of-arrays
-// [field][N] (N = E*D, agent a = env*D + drone) so lane i of a wavefront
-// touches element i of every field — every state load/store is a fully
-// coalesced 256 B (fp32) wave access.  A workgroup owns whole envs
-// (EPB = floor(64/D) envs × D drones, one wavefront), so the per-env reductions (reward
-// mean, any-terminated), the O(D²) downwash neighbour scan and the reset
-// rejection search all run through LDS with no inter-workgroup traffic.
-// The path is elementwise ODE + a small PID: no contraction, so no MFMA; the
-// bound is HBM bandwidth.
-
+// quadswarm.hip — host side of the MI355X quadrotor-swarm step: the C-ABI of
+// include/quadswarm.h (handle, state buffers, launches).  The device code is
+// csrc/step_kernel.h; the kernels are instantiated per task family in
+// step_mh.hip / step_spiral.hip / step_generic.hip.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
-#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include <cmath>
@@ -28,1115 +13,9 @@
 #include <new>
 
 #include "quadswarm.h"
+#include "step_launch.h"
 
 namespace qs {
-
-// One wavefront per workgroup: a wave owns floor(64/D) whole envs, so every
-// per-env reduction, neighbour scan and reset search stays inside one wave and
-// the workgroup barriers below cost nothing (no inter-wave coupling).
-constexpr int kBlock = 64;
-constexpr uint32_t kMaxResetTries = 1u << 24;
-enum { STREAM_ACT = 1, STREAM_RESET = 2 };
-enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
-
-// ------------------------------------------------------- CF2X constants
-// cf2x.urdf:5, 11-12, 34 and BaseAviary.py:117-128, as compile-time literals so
-// they fold into the instruction stream (no kernel-argument SGPRs, no spills).
-// The three square-root-derived values are the correctly rounded doubles of
-// their defining expressions; qs_create re-derives them with std::sqrt and
-// refuses to run if any differs (check_consts below).
-namespace cf2x {
-constexpr double G = 9.8, M = 0.027, L = 0.0397, KF = 3.16e-10, KM = 7.94e-12;
-constexpr double IXX = 1.4e-5, IYY = 1.4e-5, IZZ = 2.17e-5;
-constexpr double GRAVITY = G * M;                       // BaseAviary.py:117
-constexpr double L_SQRT2 = 0.028072139213105935;        // L / sqrt(2)      (BA:849-850)
-constexpr double HOVER_RPM = 14468.429183500699;        // sqrt(G M / 4 KF) (BA:118)
-constexpr double GND_CLIP = 0.037763713492095015;       // BaseAviary.py:125-126
-constexpr double SPEED_LIMIT = 0.03 * 30.0 * (1000.0 / 3600.0);   // BaseRLAviary.py:88
-constexpr double G_PID = 9.8 * M;                       // DSLPIDControl.py:43 (GRAVITY)
-constexpr double DRAG_XY = 9.1785e-7, DRAG_Z = 10.311e-7;
-constexpr double GND_COEFF = 11.36859, PROP_R = 2.31348e-2;
-constexpr double DW1 = 2267.18, DW2 = 0.16, DW3 = -0.11;
-}  // namespace cf2x
-// Prop-link COM offsets (assets/cf2x.urdf:42-79), Bullet's default multibody
-// damping (linear = angular = 0.04) and the collision cylinder (cf2x.urdf:32-35).
-constexpr double kPropX[4] = {0.028, -0.028, -0.028, 0.028}, kPropY[4] = {-0.028, -0.028, 0.028, 0.028};
-constexpr double kPybDamping = 0.04, kCylR = 0.06, kCylHalfLen = 0.0125;
-
-// Compile-time shape of an action type (BaseRLAviary.py:262-277).
-template <int ACT> struct Act {
-  static constexpr int A = (ACT == QS_ACT_RPM || ACT == QS_ACT_VEL) ? 4 : (ACT == QS_ACT_PID ? 3 : 1);
-  static constexpr bool pid = ACT == QS_ACT_PID || ACT == QS_ACT_VEL || ACT == QS_ACT_ONE_D_PID;
-};
-
-// ---------------------------------------------------------------- math utils
-template <class T> struct M;
-template <> struct M<float> {
-  __device__ static float sqrt_(float x) { return sqrtf(x); }
-  __device__ static float sin_(float x) { return sinf(x); }
-  __device__ static float cos_(float x) { return cosf(x); }
-  // atan2 on the fp32 hot path: reduction to [0,1] with one hardware reciprocal
-  // and a degree-7 polynomial in a² (fitted here; |error| ≤ 2e-7 rad, ~3 ulp),
-  // about a third of the instructions of the library atan2f.
-  __device__ static float atan2_(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
-    const float z = a * a;
-    float p = __builtin_fmaf(z, -0.004785229451954365f, 0.02457403391599655f);
-    p = __builtin_fmaf(z, p, -0.059928297996520996f);
-    p = __builtin_fmaf(z, p, 0.0994439497590065f);
-    p = __builtin_fmaf(z, p, -0.14030005037784576f);
-    p = __builtin_fmaf(z, p, 0.1997147500514984f);
-    p = __builtin_fmaf(z, p, -0.3333210051059723f);
-    p = __builtin_fmaf(z, p, 0.9999999403953552f);
-    float r = a * p;
-    if (ay > ax) r = 1.57079637f - r;
-    if (x < 0.f) r = 3.14159274f - r;
-    return copysignf(r, y);
-  }
-  __device__ static float asin_(float x) { return asinf(x); }
-  __device__ static float exp_(float x) { return expf(x); }
-  __device__ static float abs_(float x) { return fabsf(x); }
-  __device__ static float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-  __device__ static float mul_rn(float a, float b) { return __fmul_rn(a, b); }
-  __device__ static float add_rn(float a, float b) { return __fadd_rn(a, b); }
-  __device__ static float sub_rn(float a, float b) { return __fsub_rn(a, b); }
-  // fp32 hot path: hardware reciprocal / reciprocal square root (≤1 ulp) in place
-  // of the scaled division sequences; constant divisors become multiplies.
-  __device__ static float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-  __device__ static float rsqrt(float x) { return __builtin_amdgcn_rsqf(x); }
-  __device__ static float divc(float x, double c) { return x * float(1.0 / c); }
-};
-template <> struct M<double> {
-  __device__ static double sqrt_(double x) { return sqrt(x); }
-  __device__ static double sin_(double x) { return sin(x); }
-  __device__ static double cos_(double x) { return cos(x); }
-  __device__ static double atan2_(double y, double x) { return atan2(y, x); }
-  __device__ static double asin_(double x) { return asin(x); }
-  __device__ static double exp_(double x) { return exp(x); }
-  __device__ static double abs_(double x) { return fabs(x); }
-  __device__ static double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
-  __device__ static double mul_rn(double a, double b) { return __dmul_rn(a, b); }
-  __device__ static double add_rn(double a, double b) { return __dadd_rn(a, b); }
-  __device__ static double sub_rn(double a, double b) { return __dsub_rn(a, b); }
-  // fp64 keeps the reference's exact divisions (the tight fp64 parity gate).
-  __device__ static double rcp(double x) { return 1.0 / x; }
-  __device__ static double rsqrt(double x) { return 1.0 / sqrt(x); }
-  __device__ static double divc(double x, double c) { return x / c; }
-};
-
-template <class T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
-
-// cos θ and sin θ / |ω| for the exp-map update (BaseAviary.py:889-891), with
-// θ = |ω|·dt/2, from u = θ² = |ω|²·(dt/2)² — no square root and no division
-// in flight (θ < 0.25, i.e. |ω| < 120 rad/s at 240 Hz).  Taylor series in u,
-// truncated where the next term is < 1e-10 of an fp32 ulp (fp32) or < 1e-4 of
-// an fp64 ulp (fp64).  Larger θ falls back to the library sin/cos.
-template <class T> __device__ __forceinline__ void expmap_coeffs(T wn2, T hdt, T hdt2, T& c, T& k) {
-  using F = M<T>;
-  const T u = wn2 * hdt2;
-  if (u < T(0.0625)) {
-    T s, cc;
-    if constexpr (sizeof(T) == 4) {
-      s = F::fma_(u, F::fma_(u, F::fma_(u, T(-1.0 / 5040), T(1.0 / 120)), T(-1.0 / 6)), T(1));
-      cc = F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, T(1.0 / 40320), T(-1.0 / 720)), T(1.0 / 24)), T(-0.5)), T(1));
-    } else {
-      s = F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, T(1.0 / 6227020800.0), T(-1.0 / 39916800.0)),
-                                                           T(1.0 / 362880)), T(-1.0 / 5040)), T(1.0 / 120)), T(-1.0 / 6)), T(1));
-      cc = F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, F::fma_(u, T(1.0 / 479001600.0), T(-1.0 / 3628800.0)),
-                                                            T(1.0 / 40320)), T(-1.0 / 720)), T(1.0 / 24)), T(-0.5)), T(1));
-    }
-    c = cc;
-    k = hdt * s;             // sin θ / |ω| = (dt/2) · sinc θ
-  } else {
-    const T wn = F::sqrt_(wn2);
-    const T th = wn * hdt;
-    c = F::cos_(th);
-    k = F::sin_(th) / wn;
-  }
-}
-
-// Philox4x32-10 (Random123).  Same stream definition as the oracle.
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(1))) void* g_ptr_t;
-
-struct U4 { uint32_t x, y, z, w; };
-__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
-  }
-  return c;
-}
-// 24-bit uniform in [0,1), exact in float and double.
-template <class T> __device__ __forceinline__ T u01(uint32_t x) { return T(x >> 8) * T(1.0 / 16777216.0); }
-
-// -------------------------------------------------------------- parameters
-template <class T> struct Params {
-  // sizes
-  int E, D, N, O, H, S, EPB;
-  int mode;
-  uint32_t aux, flags;
-  int pyb_freq;
-  double ep_len_sec;
-  uint32_t k0, k1;
-  long long env_offset;
-  T dt, hdt, hdt2, ctrl_dt, ctrl_hz;   // PYB_TIMESTEP, dt/2, (dt/2)², CTRL_TIMESTEP, CTRL_FREQ
-  T sp_R, sp_OMEGA, sp_VZ, sp_cx, sp_cy, sp_cz;
-  // device buffers
-  T* st;                  // [QS_AGENT_FIELDS][N]
-  int32_t* env;           // [QS_ENV_FIELDS][E]
-  float* hist;            // [H][N][A]
-  double* ep_return;      // [E]
-  const T* orig_xyz;      // [D][3]
-  qs_episode_rec* log;    // [log_cap]
-  unsigned long long* log_count;
-  long long log_cap;
-  int* err;               // [1] reset search overflow flag
-  int stage_rows;         // obs rows staged in LDS per pass
-  unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
-  // per-step I/O
-  const uint8_t* reset_mask;   // MODE_RESET_MASK: [E] or NULL (= all)
-  const float* act_in;
-  float* obs;
-  T* rew;
-  uint8_t* term;
-  uint8_t* trunc;
-  float* tobs;
-  uint8_t* reasons;
-  float* act_out;
-};
-
-// ---------------------------------------------------- conversions (external)
-// pybullet getMatrixFromQuaternion = btMatrix3x3::setRotation (s = 2/|q|²).
-template <class T> __device__ __forceinline__ void quat_to_rot(const T q[4], T R[9]) {
-  T x = q[0], y = q[1], z = q[2], w = q[3];
-  T d = x * x + y * y + z * z + w * w;
-  T s = T(2) * M<T>::rcp(d);
-  T xs = x * s, ys = y * s, zs = z * s;
-  T wx = w * xs, wy = w * ys, wz = w * zs;
-  T xx = x * xs, xy = x * ys, xz = x * zs;
-  T yy = y * ys, yz = y * zs, zz = z * zs;
-  R[0] = T(1) - (yy + zz); R[1] = xy - wz; R[2] = xz + wy;
-  R[3] = xy + wz; R[4] = T(1) - (xx + zz); R[5] = yz - wx;
-  R[6] = xz - wy; R[7] = yz + wx; R[8] = T(1) - (xx + yy);
-}
-// Third column of the same matrix (the body z axis): all the force model of a
-// DYN substep needs; s = 2/|q|² supplied by the caller.
-template <class T> __device__ __forceinline__ void quat_to_zaxis_s(const T q[4], T s, T& r2, T& r5, T& r8) {
-  T x = q[0], y = q[1], z = q[2], w = q[3];
-  T xs = x * s, ys = y * s, zs = z * s;
-  r2 = x * zs + w * ys;
-  r5 = y * zs - w * xs;
-  r8 = T(1) - (x * xs + y * ys);
-}
-// pybullet getEulerFromQuaternion.
-template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T rpy[3]) {
-  using F = M<T>;
-  T sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
-  T sarg = T(-2) * (q[0] * q[2] - q[3] * q[1]);
-  if (sarg <= T(-0.99999)) {
-    rpy[0] = 0; rpy[1] = T(-0.5 * M_PI); rpy[2] = T(2) * F::atan2_(q[0], -q[1]);
-  } else if (sarg >= T(0.99999)) {
-    rpy[0] = 0; rpy[1] = T(0.5 * M_PI); rpy[2] = T(2) * F::atan2_(-q[0], q[1]);
-  } else {
-    rpy[0] = F::atan2_(T(2) * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
-    rpy[1] = F::asin_(sarg);
-    rpy[2] = F::atan2_(T(2) * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
-  }
-}
-
-// ------------------------------------------------------------ DSL PID
-// DSLPIDControl.computeControl (DSLPIDControl.py:82-259), one drone.
-// pid: int_pos[3], int_rpy[3], last_rpy[3] (updated in place); rpy = the
-// current attitude (computed once by the caller, DSLPIDControl.py:240).
-template <class T>
-__device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T pos[3], const T q[4], const T vel[3],
-                                        const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
-  using F = M<T>;
-  const T dt = ctrl_dt;
-  T R[9];
-  quat_to_rot(q, R);
-  T pe[3], ve[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) { pe[i] = tpos[i] - pos[i]; ve[i] = tvel[i] - vel[i]; }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) pid[i] = clampv(pid[i] + pe[i] * dt, T(-2), T(2));
-  pid[2] = clampv(pid[2], T(-0.15), T(0.15));
-  const T PF[3] = {T(.4), T(.4), T(1.25)}, IF[3] = {T(.05), T(.05), T(.05)}, DF[3] = {T(.2), T(.2), T(.5)};
-  T tt[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) tt[i] = PF[i] * pe[i] + IF[i] * pid[i] + DF[i] * ve[i];
-  tt[2] += T(cf2x::G_PID);
-  T st = tt[0] * R[2] + tt[1] * R[5] + tt[2] * R[8];
-  st = st > T(0) ? st : T(0);
-  T thrust = F::divc(F::sqrt_(F::divc(st, 4 * cf2x::KF)) - T(4070.3), 0.2685);
-  T inv = F::rsqrt(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
-  T z[3] = {tt[0] * inv, tt[1] * inv, tt[2] * inv};
-  T xc0 = F::cos_(tyaw), xc1 = F::sin_(tyaw);
-  // y = (z × x_c)/|z × x_c| with x_c = (xc0, xc1, 0)
-  T y[3] = {-z[2] * xc1, z[2] * xc0, z[0] * xc1 - z[1] * xc0};
-  T yi = F::rsqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
-  y[0] *= yi; y[1] *= yi; y[2] *= yi;
-  T x[3] = {y[1] * z[2] - y[2] * z[1], y[2] * z[0] - y[0] * z[2], y[0] * z[1] - y[1] * z[0]};
-  // target_rotation columns x,y,z (scipy XYZ round trip = identity on SO(3)).
-  // rot_e = vee(Rt^T R - R^T Rt)
-  const T* Rt0 = x; const T* Rt1 = y; const T* Rt2 = z;   // columns
-  auto Rt = [&](int i, int j) -> T { return j == 0 ? Rt0[i] : (j == 1 ? Rt1[i] : Rt2[i]); };
-  auto E = [&](int i, int j) -> T {
-    T a = Rt(0, i) * R[0 * 3 + j] + Rt(1, i) * R[1 * 3 + j] + Rt(2, i) * R[2 * 3 + j];
-    T b = R[0 * 3 + i] * Rt(0, j) + R[1 * 3 + i] * Rt(1, j) + R[2 * 3 + i] * Rt(2, j);
-    return a - b;
-  };
-  T rot_e[3] = {E(2, 1), E(0, 2), E(1, 0)};
-  T rate_e[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const T drpy = rpy[i] - pid[6 + i];
-    if constexpr (sizeof(T) == 4) rate_e[i] = -(drpy * ctrl_hz);
-    else rate_e[i] = T(0) - drpy / dt;
-    pid[6 + i] = rpy[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) pid[3 + i] = clampv(pid[3 + i] - rot_e[i] * dt, T(-1500), T(1500));
-  pid[3] = clampv(pid[3], T(-1), T(1));
-  pid[4] = clampv(pid[4], T(-1), T(1));
-  const T PT[3] = {T(70000.), T(70000.), T(60000.)}, IT[3] = {T(0), T(0), T(500.)}, DT[3] = {T(20000.), T(20000.), T(12000.)};
-  T tq[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) tq[i] = clampv(-PT[i] * rot_e[i] + DT[i] * rate_e[i] + IT[i] * pid[3 + i], T(-3200), T(3200));
-  // CF2X mixer (DSLPIDControl.py:48-53)
-  const T MX[4][3] = {{T(-.5), T(-.5), T(-1)}, {T(-.5), T(.5), T(1)}, {T(.5), T(.5), T(-1)}, {T(.5), T(-.5), T(1)}};
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    T pwm = thrust + (MX[m][0] * tq[0] + MX[m][1] * tq[1] + MX[m][2] * tq[2]);
-    pwm = clampv(pwm, T(20000), T(65535));
-    rpm[m] = T(0.2685) * pwm + T(4070.3);
-  }
-}
-
-// --------------------------------------------------- LDS workspace layout
-template <class T> struct Shared {
-  T cand[kBlock][3];        // reset candidates / downwash snapshot positions
-  T rew[kBlock];            // per-drone reward terms
-  uint8_t bits[kBlock];     // per-drone termination reason bits
-  int reject[kBlock];       // per-group rejection flag (reset search)
-  int done[kBlock];         // per-env done flag (EPB <= kBlock)
-  int need[kBlock];         // per-env: still searching
-  uint32_t win_try[kBlock]; // per-env winning try index
-  int win_group;
-  int any;
-  uint32_t ep_bcast;
-};
-
-// Reset search (MultiHoverAviary.reset rejection loop, MH:83-102), group g
-// (= threads g*D .. g*D+D-1) evaluates `try_idx` for its env.
-// Writes cand positions for its group and flags rejection in s.reject[g].
-template <class T>
-__device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3], int g, int d, uint32_t try_idx,
-                               uint32_t genv, uint32_t episode, bool active) {
-  using F = M<T>;
-  const int tid = threadIdx.x;
-  if (active) {
-    U4 r = philox(U4{try_idx, genv, episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
-    T n0 = T(0.5) * u01<T>(r.x) - T(0.25), n1 = T(0.5) * u01<T>(r.y) - T(0.25), n2 = T(0.5) * u01<T>(r.z) - T(0.25);
-    T px = F::add_rn(orig[0], n0);
-    T py = F::add_rn(orig[1], n1);
-    T pz = F::add_rn(orig[2], n2);
-    pz = clampv(pz, T(0.1), T(1.0));
-    s.cand[tid][0] = px; s.cand[tid][1] = py; s.cand[tid][2] = pz;
-  }
-  __syncthreads();
-  if (active) {
-    const int base = g * P.D;
-    T px = s.cand[tid][0], py = s.cand[tid][1], pz = s.cand[tid][2];
-    bool bad = pz < T(0.1);
-    for (int j = d + 1; j < P.D; ++j) {
-      T dx = F::sub_rn(px, s.cand[base + j][0]);
-      T dy = F::sub_rn(py, s.cand[base + j][1]);
-      T dz = F::sub_rn(pz, s.cand[base + j][2]);
-      T ss = F::add_rn(F::add_rn(F::mul_rn(dx, dx), F::mul_rn(dy, dy)), F::mul_rn(dz, dz));
-      if (F::sqrt_(ss) < T(0.5)) bad = true;
-    }
-    if (bad) s.reject[g] = 1;
-  }
-  __syncthreads();
-}
-
-// Cache policy.  Every byte the step touches is streamed: read once, written
-// once per launch.  Default-policy stores leave ~30 MB dirty in the eight L2s
-// and the end-of-launch write-back then runs as a serial tail; non-temporal
-// (nt) stores stream to HBM while the launch computes (C3: 17.5 → 13.2 µs,
-// profiles/).  aux = 2 is the nt bit of buffer/global_load_lds instructions.
-#ifndef QS_SUB_CONTRACT
-#define QS_SUB_CONTRACT 1
-#endif
-#ifndef QS_STATE_STORE_AUX
-#define QS_STATE_STORE_AUX 2
-#endif
-#ifndef QS_STATE_LOAD_AUX
-#define QS_STATE_LOAD_AUX 0
-#endif
-#ifndef QS_HIST_DMA_AUX
-#define QS_HIST_DMA_AUX 0
-#endif
-#ifndef QS_NT_OBS
-#define QS_NT_OBS 1
-#endif
-typedef float f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void obs_store4(float4* p, float4 v) {
-  if constexpr (QS_NT_OBS) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
-  else *p = v;
-}
-template <class V> __device__ __forceinline__ void nt_store(V* p, V v) {
-  if constexpr (QS_NT_OBS) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
-// Raw-buffer access to the SoA state: descriptor over the whole [F][N] array
-// (wave-uniform, from kernel arguments), field base in soffset (SGPR), lane's
-// 32-bit byte offset in voffset — one buffer instruction per field, no 64-bit
-// per-lane address arithmetic (cdna_hip_programming.md T8).
-template <class T> struct SoA {
-  __amdgpu_buffer_rsrc_t rsrc;
-  unsigned fstride;   // bytes per field = N * sizeof(T)
-  unsigned voff;      // lane's byte offset = a * sizeof(T)
-  __device__ __forceinline__ T ld(int f) const {
-    if constexpr (sizeof(T) == 4) {
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff, (int)(f * fstride), QS_STATE_LOAD_AUX));
-    } else {
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, (int)(f * fstride), QS_STATE_LOAD_AUX));
-    }
-  }
-  __device__ __forceinline__ void st(int f, T v) const {
-    if constexpr (sizeof(T) == 4) {
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc, (int)voff, (int)(f * fstride), QS_STATE_STORE_AUX);
-    } else {
-      typedef unsigned v2u __attribute__((ext_vector_type(2)));
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), rsrc, (int)voff, (int)(f * fstride), QS_STATE_STORE_AUX);
-    }
-  }
-};
-
-// s_waitcnt vmcnt(0) as a real instruction (not inline asm), so the compiler's
-// wait-count tracking knows every earlier load has landed and does not insert
-// conservative vmcnt(0) waits later — those would also wait for the early
-// state stores to drain (vmcnt retires loads and stores in issue order).
-// gfx9 encoding: vmcnt[3:0]=0, expcnt[6:4]=7, lgkmcnt[11:8]=15, vmcnt_hi[15:14]=0.
-__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-// Keeps the loads on either side in source order (the scheduler would
-// interleave them), so operands needed first are issued first.
-__device__ __forceinline__ void issue_fence() { __asm__ volatile("" ::: "memory"); }
-
-#ifdef QS_STAMPS_BUILD
-#define QS_STAMP(k)                                                                         \
-  do {                                                                                      \
-    if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define QS_STAMP(k) do { } while (0)
-#endif
-
-// ---------------------------------------------------------------- the step
-// TASK (qs_task) and ACT (qs_action_type) are compile-time: each launch runs
-// a kernel with only its own task's obs/reward code and its own action
-// preprocessing, with the action width A folded into every index.  CF is the
-// control frequency when it is the task's default at pyb_freq 240 (MultiHover
-// 30 Hz, Spiral 48 Hz): the substep count, history length and obs width are
-// then constants (fully unrolled substeps, constant obs offsets); CF = 0 reads
-// them from P.
-template <class T, int TASK, int ACT, int CF, int PHYS>
-__global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
-  using F = M<T>;
-  constexpr int A = Act<ACT>::A;
-  constexpr bool kPid = Act<ACT>::pid;
-  constexpr bool kHover = TASK == QS_TASK_MULTIHOVER;
-  __shared__ Shared<T> s;
-  const int tid = threadIdx.x;
-  const int D = P.D, N = P.N;
-  const int H = CF ? CF / 2 : P.H;
-  const int S = CF ? 240 / CF : P.S;
-  const int O = CF ? 12 + (CF / 2) * A + (kHover ? 0 : 11) : P.O;
-  const int lenv = tid / D, d = tid - lenv * D;
-  const int e = blockIdx.x * P.EPB + lenv;
-  const bool valid = (lenv < P.EPB) && (e < P.E);
-  const int a = e * D + d;
-  const uint32_t genv = (uint32_t)(P.env_offset + e);
-  SoA<T> SA;
-  SA.rsrc = __builtin_amdgcn_make_buffer_rsrc(P.st, 0, (int)((unsigned)QS_AGENT_FIELDS * (unsigned)N * sizeof(T)), 0x00020000);
-  SA.fstride = (unsigned)N * (unsigned)sizeof(T);
-  SA.voff = (unsigned)a * (unsigned)sizeof(T);
-  QS_STAMP(0);
-
-  // ---------------- loads
-  // Every global read of the launch is issued here, unconditionally and
-  // branch-free: buffer loads return 0 out of range, so idle lanes (offset
-  // kOOB) and absent optional inputs (zero-size descriptor) need no branch.
-  // With straight-line issue the compiler's wait counts stay exact, so each
-  // phase waits only for its own operands (vmcnt retires in issue order).
-  // Nothing is read after the first store (see wait_vm0).
-  constexpr unsigned kOOB = 0x80000000u;
-  auto rsrc = [](const void* ptr, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), 0, (int)bytes, 0x00020000);
-  };
-  SA.voff = valid ? SA.voff : kOOB;
-  const unsigned E = (unsigned)P.E;
-  // env counters first: the synthetic action draw needs only `total`
-  const __amdgpu_buffer_rsrc_t env_r = rsrc(P.env, (unsigned)QS_ENV_FIELDS * E * 4u);
-  const unsigned ev = valid ? (unsigned)e * 4u : kOOB;
-  auto ld_env = [&](int f) { return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(env_r, (int)ev, (int)(f * E * 4u), 0); };
-  int32_t step_counter = ld_env(QS_E_STEP_COUNTER), episode = ld_env(QS_E_EPISODE);
-  int32_t total = ld_env(QS_E_TOTAL_STEPS), ep_len = ld_env(QS_E_EP_LEN);
-  issue_fence();
-  T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    pos[i] = SA.ld(QS_F_POS + i);
-    vel[i] = SA.ld(QS_F_VEL + i);
-    w[i] = SA.ld(QS_F_RPY_RATES + i);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) q[i] = SA.ld(QS_F_QUAT + i);
-  {   // last rpm: read only by the drag model (zero offset range otherwise: no traffic)
-    SoA<T> LR = SA;
-    LR.voff = (P.aux & QS_AUX_DRAG) ? SA.voff : kOOB;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) lrpm[i] = LR.ld(QS_F_LAST_RPM + i);
-  }
-  if constexpr (kPid) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) pid[i] = SA.ld(QS_F_PID_INT_POS + i);
-  }
-  if constexpr (kHover) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) tgt[i] = SA.ld(QS_F_TARGET + i);
-  }
-  // trainer actions (absent: zero-size descriptor), episode return, reset mask
-  float act_in[A];
-  {
-    const __amdgpu_buffer_rsrc_t r = rsrc(P.act_in, P.act_in ? (unsigned)N * A * 4u : 0u);
-    const unsigned v = valid ? (unsigned)a * A * 4u : kOOB;
-#pragma unroll
-    for (int k = 0; k < A; ++k) act_in[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)v, k * 4, 0));
-  }
-  const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-      rsrc(P.ep_return, E * 8u), valid ? (int)((unsigned)e * 8u) : (int)kOOB, 0, 0));
-  const uint8_t mask_v = __builtin_amdgcn_raw_buffer_load_b8(
-      rsrc(P.reset_mask, P.reset_mask ? E : 0u), valid ? e : (int)kOOB, 0, 0);
-  const bool masked = P.reset_mask == nullptr || mask_v != 0;
-  T orig[3];   // every search group needs it, also those past the last env (reset phase 2)
-#pragma unroll
-  for (int i = 0; i < 3; ++i) orig[i] = P.orig_xyz[d * 3 + i];
-  issue_fence();
-  // ---------------- the whole action-history ring (BaseRLAviary.py:66, 187,
-  // 317-318): all H slots, so the addresses do not depend on the loaded ring
-  // head and the reads issue with the state loads.  With the default control
-  // frequency (CF != 0, H constant) the ring goes into registers with plain
-  // buffer loads, issued last: the compiler's exact wait counts then let the
-  // PID start as soon as the state has landed while the ring still streams.
-  // Otherwise it goes into LDS by LDS-DMA, lane-linear [slot][lane][A] (A = 3
-  // as [slot][k][lane]: a dwordx3 DMA does not land lane-linear at 12 B).
-  extern __shared__ float4 dyn_lds4[];   // float4: 16-B aligned staging for the obs stores
-  float* const dyn_lds = reinterpret_cast<float*>(dyn_lds4);
-  float* const hist_pref = dyn_lds;
-  float* const stage = dyn_lds + (CF ? 0 : (size_t)H * kBlock * A);
-  constexpr int HR = CF ? CF / 2 : 1;
-  float hreg[HR][A];
-  if constexpr (CF != 0) {
-    const __amdgpu_buffer_rsrc_t hr = rsrc(P.hist, (unsigned)HR * (unsigned)N * A * 4u);
-    const unsigned hv = valid ? (unsigned)a * A * 4u : kOOB;
-#pragma unroll
-    for (int sl = 0; sl < HR; ++sl) {
-      const int so = (int)((unsigned)sl * (unsigned)N * A * 4u);
-      // (dword loads: ROCm 7.2's clang lowers __builtin_amdgcn_raw_buffer_load_b128
-      // to a single dword load; adjacent dwords are merged by the backend)
-#pragma unroll
-      for (int k = 0; k < A; ++k)
-        hreg[sl][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (int)hv, so + 4 * k, 0));
-    }
-  } else {
-    const int a_src = valid ? a : blockIdx.x * P.EPB * D;   // idle lanes read a valid row
-    for (int sl = 0; sl < H; ++sl) {
-      const float* src = P.hist + ((size_t)sl * N + a_src) * A;
-      if constexpr (A == 1) {
-        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + sl * kBlock), 4, 0, QS_HIST_DMA_AUX);
-      } else if constexpr (A == 3) {
-        for (int k = 0; k < 3; ++k)
-          __builtin_amdgcn_global_load_lds((g_ptr_t)(src + k), (lds_ptr_t)(hist_pref + (sl * 3 + k) * kBlock), 4, 0, QS_HIST_DMA_AUX);
-      } else {
-        __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(hist_pref + sl * kBlock * 4), 16, 0, QS_HIST_DMA_AUX);
-      }
-    }
-  }
-  auto hist_at = [&](int sl, int k) -> float {   // LDS image (CF == 0): ring slot sl, component k, this lane
-    return A == 3 ? hist_pref[(sl * 3 + k) * kBlock + tid] : hist_pref[(sl * kBlock + tid) * A + k];
-  };
-  // history ring head: this step's action goes to slot total % H
-  const int wslot = total % H;
-  // kinematic state + last_clipped_action (BaseAviary.py:509-519, 560)
-  auto store_kin = [&]() {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      SA.st(QS_F_POS + i, pos[i]);
-      SA.st(QS_F_VEL + i, vel[i]);
-      SA.st(QS_F_RPY_RATES + i, w[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) SA.st(QS_F_QUAT + i, q[i]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) SA.st(QS_F_LAST_RPM + i, lrpm[i]);
-  };
-  T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
-  bool done_env = false;
-  int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
-
-  float cur_act[A];            // this step's action (newest history entry)
-#pragma unroll
-  for (int k = 0; k < A; ++k) cur_act[k] = 0.f;
-#ifdef QS_STAMPS_BUILD
-  if (P.stamps) { volatile T sink = pos[0] + q[3] + pid[0] + tgt[0] + (T)total; (void)sink; }
-#endif
-  // ---------------- action (trainer-provided or synthetic random policy)
-  if (P.mode == MODE_STEP) {
-    if (P.act_in) {
-#pragma unroll
-      for (int k = 0; k < A; ++k) cur_act[k] = act_in[k];
-    } else {
-      U4 r = philox(U4{(uint32_t)total, genv, 0u, (uint32_t)((STREAM_ACT << 24) | d)}, P.k0, P.k1);
-      const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-      for (int k = 0; k < A; ++k) cur_act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
-    }
-  }
-  QS_STAMP(1);
-  if (P.mode == MODE_STEP) {
-    const float* act = cur_act;
-    // ---------------- _preprocessAction (BaseRLAviary.py:188-239)
-    T rpm[4] = {0, 0, 0, 0};
-    if (valid) {
-      const T z3[3] = {0, 0, 0};
-      if constexpr (ACT == QS_ACT_RPM) {
-#pragma unroll
-        for (int m = 0; m < 4; ++m) rpm[m] = T(cf2x::HOVER_RPM) * (T(1) + T(0.05) * T(act[m]));
-      } else if constexpr (ACT == QS_ACT_ONE_D_RPM) {
-        T r = T(cf2x::HOVER_RPM) * (T(1) + T(0.05) * T(act[0]));
-        rpm[0] = rpm[1] = rpm[2] = rpm[3] = r;
-      } else {
-        quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
-        if constexpr (ACT == QS_ACT_ONE_D_PID) {
-          T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
-          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
-        } else if constexpr (ACT == QS_ACT_VEL) {
-          T v0 = T(act[0]), v1 = T(act[1]), v2 = T(act[2]);
-          T n = F::sqrt_(v0 * v0 + v1 * v1 + v2 * v2);
-          T u0 = 0, u1 = 0, u2 = 0;
-          if (n != T(0)) { u0 = v0 / n; u1 = v1 / n; u2 = v2 / n; }
-          T sp = T(cf2x::SPEED_LIMIT) * F::abs_(T(act[3]));
-          T tv[3] = {sp * u0, sp * u1, sp * u2};
-          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, pos, rpy[2], tv, rpm);
-        } else {   // QS_ACT_PID: _calculateNextStep (BaseAviary.py:1108-1150)
-          T dir[3] = {T(act[0]) - pos[0], T(act[1]) - pos[1], T(act[2]) - pos[2]};
-          T dist = F::sqrt_(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
-          T np_[3];
-          if (dist <= T(1)) { np_[0] = T(act[0]); np_[1] = T(act[1]); np_[2] = T(act[2]); }
-          else { for (int i = 0; i < 3; ++i) np_[i] = pos[i] + (dir[i] / dist) * T(1); }
-          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, np_, T(0), z3, rpm);
-        }
-      }
-    }
-    // Every load of the launch has landed before the first store, so no later
-    // wait is held up by the stores (see wait_vm0).  The compiler's own waits
-    // let the action draw and the PID start as soon as the state loads land,
-    // with the history LDS-DMA (issued last) still streaming.
-    wait_vm0();
-    if (valid) {
-      if (P.act_out) {
-#pragma unroll
-        for (int k = 0; k < A; ++k) nt_store(P.act_out + (size_t)a * A + k, act[k]);
-      }
-      // action_buffer.append(action) (BaseRLAviary.py:187): ring slot total % H
-#pragma unroll
-      for (int k = 0; k < A; ++k) nt_store(P.hist + ((size_t)wslot * N + a) * A + k, act[k]);
-      if constexpr (kPid) {   // PID integrators are final: store now, drains under the substeps
-#pragma unroll
-        for (int i = 0; i < 9; ++i) SA.st(QS_F_PID_INT_POS + i, pid[i]);
-      }
-    }
-    QS_STAMP(2);
-    // ---------------- PYB_STEPS_PER_CTRL substeps (BaseAviary.py:343-372)
-    T f[4], zt[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) { f[m] = rpm[m] * rpm[m] * T(cf2x::KF); zt[m] = rpm[m] * rpm[m] * T(cf2x::KM); }
-    const T thrust_z = ((f[0] + f[1]) + f[2]) + f[3];
-    const T tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];
-    const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
-    const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
-    // PYB: the four prop forces act at their links' COMs (assets/cf2x.urdf:42-79)
-    const T pbx = (((T(kPropY[0]) * f[0]) + T(kPropY[1]) * f[1]) + T(kPropY[2]) * f[2]) + T(kPropY[3]) * f[3];
-    const T pby = (((-T(kPropX[0]) * f[0]) + -T(kPropX[1]) * f[1]) + -T(kPropX[2]) * f[2]) + -T(kPropX[3]) * f[3];
-    const T dt = P.dt;
-    // The exp-map update preserves |q| (cos²θ + sin²θ = 1), so in fp32 Bullet's
-    // s = 2/|q|² (getMatrixFromQuaternion) is formed once per control step; it
-    // moves by rounding only between substeps.
-    const T s2 = T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    // One substep (BaseAviary.py:343-372).  kAux: ground effect / drag /
-    // downwash enabled; the common force-free path is compiled separately.
-#ifdef QS_SUB_NOUNROLL
-#pragma unroll 1
-#else
-#pragma unroll
-#endif
-    for (int sub = 0; sub < S; ++sub) {
-#if QS_SUB_CONTRACT
-      // a*b+c → fma inside the substep (≈25 % fewer instructions).  The one
-      // sum whose exact cancellation matters — the gyroscopic ω × Jω, zero
-      // about a symmetric axis — is written with non-contractable _rn ops.
-#pragma clang fp contract(fast)
-#endif
-      T R2, R5, R8;
-      // fp64 (the tight-parity path) re-forms s every substep exactly as Bullet does
-      const T sq = sizeof(T) == 8 ? T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) : s2;
-      quat_to_zaxis_s(q, sq, R2, R5, R8);
-      T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
-      if (P.aux) {
-        // no contraction here: the four ground-effect torque arms cancel exactly
-        // for a level drone only in plain multiply-then-add arithmetic
-#pragma clang fp contract(off)
-        if (P.aux & QS_AUX_GND) {  // _groundEffect (BaseAviary.py:731-750)
-          T srpy[3], R[9];
-          quat_to_rpy(q, srpy);
-          quat_to_rot(q, R);
-          if (F::abs_(srpy[0]) < T(M_PI / 2) && F::abs_(srpy[1]) < T(M_PI / 2)) {
-            const T PX[4] = {T(kPropX[0]), T(kPropX[1]), T(kPropX[2]), T(kPropX[3])};
-            const T PY[4] = {T(kPropY[0]), T(kPropY[1]), T(kPropY[2]), T(kPropY[3])};
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-              T h = pos[2] + (R[6] * PX[m] + R[7] * PY[m]);
-              h = h < T(cf2x::GND_CLIP) ? T(cf2x::GND_CLIP) : h;
-              T ratio = T(cf2x::PROP_R) / (T(4) * h);
-              T g = rpm[m] * rpm[m] * T(cf2x::KF) * T(cf2x::GND_COEFF) * (ratio * ratio);
-              zb += g; txe += PY[m] * g; tye += -PX[m] * g;
-            }
-          }
-        }
-        if (P.aux & QS_AUX_DRAG) {  // _drag (BaseAviary.py:770-781), previous-substep rpm
-          T sr = 0;
-#pragma unroll
-          for (int m = 0; m < 4; ++m) sr += T(2 * M_PI) * lrpm[m] / T(60);
-          fwx += (T(-1) * T(cf2x::DRAG_XY) * sr) * vel[0];
-          fwy += (T(-1) * T(cf2x::DRAG_XY) * sr) * vel[1];
-          fwz += (T(-1) * T(cf2x::DRAG_Z) * sr) * vel[2];
-        }
-        if (P.aux & QS_AUX_DW) {  // _downwash (BaseAviary.py:798-811): neighbours' substep-start z via LDS
-          __syncthreads();
-          s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
-          __syncthreads();
-          if (valid) {
-            const int base = lenv * D;
-            for (int j = 0; j < D; ++j) {
-              T dz = s.cand[base + j][2] - pos[2];
-              T dx = s.cand[base + j][0] - pos[0], dy = s.cand[base + j][1] - pos[1];
-              T dxy = F::sqrt_(dx * dx + dy * dy);
-              if (dz > T(0) && dxy < T(10)) {
-                T ratio = T(cf2x::PROP_R) / (T(4) * dz);
-                T alpha = T(cf2x::DW1) * (ratio * ratio);
-                T beta = T(cf2x::DW2) * dz + T(cf2x::DW3);
-                T qq = dxy / beta;
-                zb += -alpha * F::exp_(T(-.5) * (qq * qq));
-              }
-            }
-          }
-        }
-      }
-      if constexpr (PHYS == QS_PHYS_PYB) {
-        // Bullet's step of the _physics forces (BA:679-711, 369-370), restated
-        // as the oracle's pyb_dynamics.  No contraction: the
-        // prop-torque sums cancel exactly for equal rotors only without FMA.
-#pragma clang fp contract(off)
-        T R[9];
-        quat_to_rot(q, R);
-        const T k = T(kPybDamping);
-        T fw0 = R[2] * zb + fwx, fw1 = R[5] * zb + fwy, fw2 = (R[8] * zb - T(cf2x::GRAVITY)) + fwz;
-        const T vd = k + k * F::sqrt_(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
-        const T a0 = fw0 / T(cf2x::M) - vd * vel[0], a1 = fw1 / T(cf2x::M) - vd * vel[1];
-        const T a2 = fw2 / T(cf2x::M) - vd * vel[2];
-        T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
-        T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
-        const T wdm = k + k * F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        T wd0 = T(1.0 / cf2x::IXX) * (((pbx + txe) - c0) - wdm * Jw0);
-        T wd1 = T(1.0 / cf2x::IYY) * (((pby + tye) - c1) - wdm * Jw1);
-        T wd2 = T(1.0 / cf2x::IZZ) * ((tz - c2) - wdm * Jw2);
-        vel[0] = vel[0] + dt * a0;
-        vel[1] = vel[1] + dt * a1;
-        vel[2] = vel[2] + dt * a2;
-        w[0] = w[0] + dt * wd0;
-        w[1] = w[1] + dt * wd1;
-        w[2] = w[2] + dt * wd2;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
-        // exp map of the world angular velocity (|ω|dt clamped to π/4), renormalised
-        const T ww0 = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
-        const T ww1 = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
-        const T ww2 = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
-        T ang2 = ww0 * ww0 + ww1 * ww1 + ww2 * ww2;
-        const T amax = T(0.25 * M_PI) / dt;
-        if (ang2 > amax * amax) ang2 = amax * amax;
-        T c, kk;
-        expmap_coeffs(ang2, P.hdt, P.hdt2, c, kk);   // cos(|ω|dt/2), sin(|ω|dt/2)/|ω|
-        const T e0 = ww0 * kk, e1 = ww1 * kk, e2 = ww2 * kk;
-        const T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
-        T n0 = ((c * x0 + e0 * x3) + e1 * x2) - e2 * x1;
-        T n1 = ((c * x1 - e0 * x2) + e1 * x3) + e2 * x0;
-        T n2 = ((c * x2 + e0 * x1) - e1 * x0) + e2 * x3;
-        T n3 = ((c * x3 - e0 * x0) - e1 * x1) - e2 * x2;
-        const T qn = F::sqrt_(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
-        q[0] = n0 / qn; q[1] = n1 / qn; q[2] = n2 / qn; q[3] = n3 / qn;
-        // ground plane vs the collision cylinder (cf2x.urdf:32-35)
-        T Rn[9];
-        quat_to_rot(q, Rn);
-        const T cz = F::abs_(Rn[8]);
-        const T sz = F::sqrt_(T(1) - Rn[8] * Rn[8] > T(0) ? T(1) - Rn[8] * Rn[8] : T(0));
-        const T zmin = pos[2] - (T(kCylHalfLen) * cz + T(kCylR) * sz);
-        if (zmin < T(0)) {
-          pos[2] = pos[2] - zmin;
-          if (vel[2] < T(0)) vel[2] = T(0);
-        }
-        if (sub == S - 1) {   // getBaseVelocity: world angular velocity at the new pose
-          angv[0] = Rn[0] * w[0] + Rn[1] * w[1] + Rn[2] * w[2];
-          angv[1] = Rn[3] * w[0] + Rn[4] * w[1] + Rn[5] * w[2];
-          angv[2] = Rn[6] * w[0] + Rn[7] * w[1] + Rn[8] * w[2];
-        }
-      } else {
-        // _dynamics (BaseAviary.py:836-877)
-        T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
-        T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
-        T c0 = F::sub_rn(F::mul_rn(w[1], Jw2), F::mul_rn(w[2], Jw1));
-        T c1 = F::sub_rn(F::mul_rn(w[2], Jw0), F::mul_rn(w[0], Jw2));
-        T c2 = F::sub_rn(F::mul_rn(w[0], Jw1), F::mul_rn(w[1], Jw0));
-        T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
-        T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
-        vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
-        vel[1] = vel[1] + dt * F::divc(fw1, cf2x::M);
-        vel[2] = vel[2] + dt * F::divc(fw2, cf2x::M);
-        w[0] = w[0] + dt * wd0;
-        w[1] = w[1] + dt * wd1;
-        w[2] = w[2] + dt * wd2;
-  #pragma unroll
-        for (int i = 0; i < 3; ++i) pos[i] = pos[i] + dt * vel[i];
-        if (sub == S - 1) {
-          // world angular velocity R_old·ω written to Bullet (BaseAviary.py:871-875);
-          // only the last substep's value reaches the obs.
-          T R[9];
-          quat_to_rot(q, R);
-          angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
-          angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
-          angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
-        }
-        // _integrateQ (BaseAviary.py:879-892); np.isclose(|ω|, 0) ⇔ |ω| <= 1e-8
-        const T wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-        if (wn2 > T(1e-16)) {
-          T c, k;
-          expmap_coeffs(wn2, P.hdt, P.hdt2, c, k);
-          const T p_ = w[0], q_ = w[1], r_ = w[2];
-          const T x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
-          q[0] = c * x0 + k * (r_ * x1 - q_ * x2 + p_ * x3);
-          q[1] = c * x1 + k * (-r_ * x0 + p_ * x2 + q_ * x3);
-          q[2] = c * x2 + k * (q_ * x0 - p_ * x1 + r_ * x3);
-          q[3] = c * x3 + k * (-p_ * x0 - q_ * x1 - r_ * x2);
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
-    }
-    quat_to_rpy(q, rpy);   // readback (BaseAviary.py:374, 518)
-    total += 1;
-    // Kinematic state is final unless this env auto-resets (rewritten below):
-    // store now so the writes drain under the reward / obs phases.
-    if (valid) store_kin();
-    QS_STAMP(3);
-
-    // ---------------- reward / termination per drone
-    T rterm = 0;
-    uint8_t bits = 0;
-    if (valid) {
-      if constexpr (kHover) {  // MultiHoverAviary.py:128-186, 216-241
-        T ex = pos[0] - tgt[0], ey = pos[1] - tgt[1];
-        T err_xy = F::sqrt_(ex * ex + ey * ey);
-        T err_z = pos[2] - tgt[2];
-        T vz = vel[2];
-        T r_xy = F::rcp(T(1) + err_xy);
-        T r_z = F::exp_(T(-7.5) * F::abs_(err_z));
-        T r_vel = F::abs_(err_z) < T(0.2) ? T(-1.5) * (vz * vz) : T(0);
-        T hover = (err_xy < T(0.03) && F::abs_(err_z) < T(0.03) && F::abs_(vz) < T(0.03)) ? T(0.5) : T(0);
-        rterm = ((r_xy + r_z) + r_vel) + hover;
-        if (pos[2] < T(0.03)) bits |= QS_REASON_CRASH;
-        if (F::abs_(rpy[0]) > T(1.2) || F::abs_(rpy[1]) > T(1.2)) bits |= QS_REASON_FLIP;
-        if (F::abs_(pos[0]) > T(3.0) || F::abs_(pos[1]) > T(3.0)) bits |= QS_REASON_OOB;
-      } else {  // SpiralAviary.py:82-99, 150-191
-        T t = T((double)step_counter / (double)P.pyb_freq);
-        T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
-        T prx = P.sp_cx + P.sp_R * F::cos_(ph), pry = P.sp_cy + P.sp_R * F::sin_(ph), prz = T(0.3) + P.sp_VZ * t;
-        T vrx = -P.sp_R * P.sp_OMEGA * F::sin_(ph), vry = P.sp_R * P.sp_OMEGA * F::cos_(ph), vrz = P.sp_VZ;
-        T dp0 = pos[0] - prx, dp1 = pos[1] - pry, dp2 = pos[2] - prz;
-        T dv0 = q[0] - vrx, dv1 = q[1] - vry, dv2 = q[2] - vrz;   // "vel" = quat xyz (SP:156)
-        T np_ = F::sqrt_(dp0 * dp0 + dp1 * dp1 + dp2 * dp2), nv = F::sqrt_(dv0 * dv0 + dv1 * dv1 + dv2 * dv2);
-        T r_pos = F::exp_(T(-4.0) * (np_ * np_));
-        T r_vel = F::exp_(T(-2.0) * (nv * nv));
-        T rx = pos[0] - P.sp_cx, ry = pos[1] - P.sp_cy;
-        T rn = F::sqrt_(rx * rx + ry * ry);
-        T r_tan = 0;
-        if (rn > T(1e-3)) {
-          T tnx = -(ry / rn), tny = rx / rn;
-          T vx = q[0], vy = q[1];
-          T vn = F::sqrt_(vx * vx + vy * vy);
-          if (vn > T(1e-3)) {
-            T dot = (vx / vn) * tnx + (vy / vn) * tny;
-            r_tan = dot > T(0) ? dot : T(0);
-          }
-        }
-        rterm = (T(1.0) * r_pos + T(2.0) * r_vel) + T(1.0) * r_tan;
-        if (pos[2] < T(0.05) || pos[2] > T(3.0)) bits |= QS_REASON_ZRANGE;
-      }
-    }
-    s.rew[tid] = rterm;
-    s.bits[tid] = bits;
-    __syncthreads();
-    // per-env reduction in drone order (reference: reward += ... for i in range(D))
-    bool dn = false;
-    double ret = 0;
-    int len = 0;
-    if (valid && d == 0) {
-      T rsum = 0;
-      uint8_t any = 0;
-      for (int j = 0; j < D; ++j) { rsum += s.rew[tid + j]; any |= s.bits[tid + j]; }
-      T r = rsum / T(D);
-      bool te = any != 0;
-      bool tr = ((double)step_counter / (double)P.pyb_freq) > P.ep_len_sec;   // MultiHoverAviary.py:267-268
-      if (P.rew) P.rew[e] = r;
-      if (P.term) P.term[e] = te;
-      if (P.trunc) P.trunc[e] = tr;
-      ret = ep_ret0 + (double)r;
-      len = ep_len + 1;
-      dn = te || tr;
-      P.ep_return[e] = dn ? 0.0 : ret;
-      P.env[QS_E_EP_LEN * P.E + e] = dn ? 0 : len;
-      s.done[lenv] = dn;
-    }
-    // Episode log (VecRecordEpisodeStatistics, record_episode_statistics.py:155-166).
-    // The atomic's returned slot makes a wave wait for all its outstanding
-    // stores, so only waves holding a finished episode take this branch.
-    if (__ballot(dn) != 0ull) {
-      if (dn) {
-        unsigned long long slot = atomicAdd(P.log_count, 1ull);
-        qs_episode_rec rec;
-        rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
-        P.log[slot % (unsigned long long)P.log_cap] = rec;
-      }
-    }
-    if (P.reasons && valid) P.reasons[a] = bits;
-    step_counter += S;   // BaseAviary.py:382
-    __syncthreads();
-    done_env = valid && s.done[lenv];
-  } else if (P.mode == MODE_RESET_ALL) {
-    wait_vm0();
-    // qs_reset: every env starts episode 0 (history is zero after qs_reset)
-    done_env = valid;
-  } else {
-    wait_vm0();
-    // qs_reset_envs: env.reset() on the masked envs; the obs lists the latest
-    // action (ring slot wslot-1) last
-    if (total > 0) {   // (no global read here: it would blur the step path's wait counts)
-      const int sl = wslot == 0 ? H - 1 : wslot - 1;
-      if constexpr (CF != 0) {
-#pragma unroll
-        for (int r = 0; r < HR; ++r)
-#pragma unroll
-          for (int k = 0; k < A; ++k) cur_act[k] = r == sl ? hreg[r][k] : cur_act[k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < A; ++k) cur_act[k] = hist_at(sl, k);
-      }
-    }
-    done_env = valid && masked;
-  }
-  // worker.step_env resets on done unless this is a single-env facade
-  const bool do_reset = done_env && !(P.mode == MODE_STEP && (P.flags & QS_FLAG_NO_AUTORESET));
-
-  // ---------------- obs writer (BaseRLAviary._computeObs + Spiral extras)
-  auto write_obs_row = [&](float* o, int sc) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      o[i] = (float)pos[i]; o[3 + i] = (float)rpy[i]; o[6 + i] = (float)vel[i]; o[9 + i] = (float)angv[i];
-    }
-    // history, oldest first: ring slots base .. base+H-2 (mod H), then this
-    // step's action (BaseRLAviary.py:317-318)
-    const int base = P.mode == MODE_STEP ? wslot + 1 : wslot;
-    if constexpr (CF != 0) {   // register ring: slot sl goes to column (sl - base) mod H
-#pragma unroll
-      for (int sl = 0; sl < HR; ++sl) {
-        int col = sl - base;
-        col += col < 0 ? HR : 0;
-        if (col != HR - 1) {
-#pragma unroll
-          for (int k = 0; k < A; ++k) o[12 + col * A + k] = hreg[sl][k];
-        }
-      }
-    } else {
-      int sl = base >= H ? base - H : base;
-      for (int i = 0; i < H - 1; ++i) {
-#pragma unroll
-        for (int k = 0; k < A; ++k) o[12 + i * A + k] = hist_at(sl, k);
-        if (++sl == H) sl = 0;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < A; ++k) o[12 + (H - 1) * A + k] = cur_act[k];   // newest = this step's action
-    if constexpr (!kHover) {
-      T t = T((double)sc / (double)P.pyb_freq);
-      T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
-      T sn = F::sin_(ph), cs = F::cos_(ph);
-      T prx = P.sp_cx + P.sp_R * cs, pry = P.sp_cy + P.sp_R * sn, prz = T(0.3) + P.sp_VZ * t;
-      T vrx = -P.sp_R * P.sp_OMEGA * sn, vry = P.sp_R * P.sp_OMEGA * cs, vrz = P.sp_VZ;
-      float* x = o + 12 + H * A;
-      x[0] = (float)(prx - pos[0]); x[1] = (float)(pry - pos[1]); x[2] = (float)(prz - pos[2]);
-      x[3] = (float)(vrx - q[0]); x[4] = (float)(vry - q[1]); x[5] = (float)(vrz - q[2]);
-      x[6] = (float)sn; x[7] = (float)cs;
-      x[8] = (float)vrx; x[9] = (float)vry; x[10] = (float)vrz;
-    }
-  };
-
-  QS_STAMP(4);
-  if (valid && done_env && P.mode == MODE_STEP && P.tobs) write_obs_row(P.tobs + (size_t)a * O, obs_sc);
-
-  // ---------------- auto-reset (worker.step_env → env.reset)
-  s.any = 0;
-  __syncthreads();
-  if (do_reset && d == 0) s.any = 1;
-  __syncthreads();
-  if (s.any) {
-    if (d == 0 && lenv < P.EPB) s.need[lenv] = do_reset ? 1 : 0;
-    if (P.mode != MODE_RESET_ALL && do_reset) episode += 1;
-    T init[3];
-    if constexpr (kHover) {
-      // Phase 1: every group tries index 0 for its own env.
-      if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
-      __syncthreads();
-      eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset);
-      if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
-      __syncthreads();
-      // Phase 2: for each still-rejected env, all groups search in parallel,
-      // tries base+g; the smallest accepted index wins (= sequential order).
-      for (int k = 0; k < P.EPB; ++k) {
-        if (!s.need[k]) continue;   // block-uniform (LDS)
-        const int ek = blockIdx.x * P.EPB + k;
-        const uint32_t genv_k = (uint32_t)(P.env_offset + ek);
-        // episode number of env k lives in its drone-0 thread; broadcast via LDS
-        __syncthreads();
-        if (tid == k * D) s.ep_bcast = (uint32_t)episode;
-        __syncthreads();
-        const uint32_t epk = s.ep_bcast;
-        uint32_t base = 1;
-        for (;;) {
-          if (tid < P.EPB) s.reject[tid] = 0;
-          if (tid == 0) s.win_group = 1 << 30;
-          __syncthreads();
-          const bool act_ = lenv < P.EPB;
-          eval_candidate(P, s, orig, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
-          if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
-          __syncthreads();
-          if (s.win_group < (1 << 30) || base + P.EPB >= kMaxResetTries) {
-            if (tid == 0) {
-              if (s.win_group < (1 << 30)) s.win_try[k] = base + (uint32_t)s.win_group;
-              else { s.win_try[k] = 0; atomicExch(P.err, 1); }
-            }
-            __syncthreads();
-            break;
-          }
-          base += (uint32_t)P.EPB;
-        }
-        if (tid == 0) s.need[k] = 2;   // resolved by phase 2 (win_try holds the index)
-        __syncthreads();
-      }
-      if (do_reset) {
-        uint32_t wt = (s.need[lenv] == 2) ? s.win_try[lenv] : 0u;
-        U4 r = philox(U4{wt, genv, (uint32_t)episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
-        init[0] = F::add_rn(orig[0], T(0.5) * u01<T>(r.x) - T(0.25));
-        init[1] = F::add_rn(orig[1], T(0.5) * u01<T>(r.y) - T(0.25));
-        init[2] = clampv(F::add_rn(orig[2], T(0.5) * u01<T>(r.z) - T(0.25)), T(0.1), T(1.0));
-      }
-    } else {
-      if (do_reset) { init[0] = orig[0]; init[1] = orig[1]; init[2] = orig[2]; }
-    }
-    if (do_reset) {
-      // BaseAviary._housekeeping (BaseAviary.py:458-477): PID state and the
-      // action history are NOT reset (reference quirk).
-#pragma unroll
-      for (int i = 0; i < 3; ++i) { pos[i] = init[i]; vel[i] = 0; w[i] = 0; rpy[i] = 0; angv[i] = 0; }
-      q[0] = q[1] = q[2] = 0; q[3] = 1;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) lrpm[m] = 0;
-      tgt[0] = init[0]; tgt[1] = init[1]; tgt[2] = init[2] + T(1.0 / (double)(d + 1));   // MH:106
-      step_counter = 0;
-      obs_sc = 0;
-    }
-  }
-
-  QS_STAMP(5);
-  // ---------------- obs output
-  if (P.obs) {
-    if (P.mode == MODE_RESET_MASK) {
-      if (valid && do_reset) write_obs_row(P.obs + (size_t)a * O, obs_sc);
-    } else {
-      // The block's obs rows are one contiguous span of HBM: build them in LDS
-      // and store the span with 16-byte coalesced stores (a per-lane row store
-      // touches 64 lines per wave instruction and doubled the write traffic).
-      const int nvalid = [&] { const int e0 = blockIdx.x * P.EPB; return min(P.EPB, P.E - e0) * D; }();
-      float* const blk = P.obs + (size_t)blockIdx.x * P.EPB * D * O;
-      for (int p0 = 0; p0 < nvalid; p0 += P.stage_rows) {   // block-uniform
-        const int p1 = min(nvalid, p0 + P.stage_rows);
-        if (tid >= p0 && tid < p1) write_obs_row(stage + (tid - p0) * O, obs_sc);
-        __syncthreads();
-        float* const g = blk + (size_t)p0 * O;                 // span start
-        const int n = (p1 - p0) * O;                          // floats in the span
-        const int head = min(n, (int)((4 - (((uintptr_t)g >> 2) & 3)) & 3));   // floats to 16-B alignment
-        if (tid < head) nt_store(g + tid, stage[tid]);
-        const int nv = (n - head) >> 2;
-        if ((head & 3) == 0) {
-          for (int i = tid; i < nv; i += kBlock)
-            obs_store4(reinterpret_cast<float4*>(g + 4 * i), *reinterpret_cast<const float4*>(stage + 4 * i));
-        } else {
-          for (int i = tid; i < nv; i += kBlock) {
-            const float* src = stage + head + 4 * i;
-            obs_store4(reinterpret_cast<float4*>(g + head + 4 * i), make_float4(src[0], src[1], src[2], src[3]));
-          }
-        }
-        for (int i = head + 4 * nv + tid; i < n; i += kBlock) nt_store(g + i, stage[i]);
-        __syncthreads();
-      }
-    }
-  }
-  QS_STAMP(6);
-  if (!valid) return;
-
-  // ---------------- store state of the envs that (auto-)reset
-  if (do_reset) {
-    store_kin();
-    if constexpr (kHover) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) SA.st(QS_F_TARGET + i, tgt[i]);
-    }
-  }
-  if (d == 0) {
-    P.env[QS_E_STEP_COUNTER * P.E + e] = step_counter;
-    P.env[QS_E_EPISODE * P.E + e] = episode;
-    P.env[QS_E_TOTAL_STEPS * P.E + e] = total;
-  }
-}
-
 // Calibration kernel: dword per lane, grid-stride (MI355X_MICROARCH §HBM).
 __global__ void calib_copy_kernel(float* __restrict__ dst, const float* __restrict__ src, long long n) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1218,43 +97,16 @@ static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
   return QS_OK;
 }
 
-template <class T, int TASK, int ACT> static void launch_one(int grid, size_t lds, hipStream_t st, const qs::Params<T>& P,
-                                                             int ctrl_freq, int pyb_freq, int phys) {
-  constexpr int kCF = TASK == QS_TASK_MULTIHOVER ? 30 : 48;   // MultiHoverAviary.py:20, SpiralAviary.py:28
-  const bool cf = ctrl_freq == kCF && pyb_freq == 240;
-  if (phys == QS_PHYS_DYN) {
-    if (cf) hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN>), dim3(grid), dim3(qs::kBlock), lds, st, P);
-    else hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN>), dim3(grid), dim3(qs::kBlock), lds, st, P);
-  } else {
-    if (cf) hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB>), dim3(grid), dim3(qs::kBlock), lds, st, P);
-    else hipLaunchKernelGGL((qs::step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB>), dim3(grid), dim3(qs::kBlock), lds, st, P);
-  }
-}
-
-template <class T, int TASK> static int launch_act(int act, int grid, size_t lds, hipStream_t st, const qs::Params<T>& P,
-                                                   int cf, int pf, int ph) {
-  switch (act) {
-    case QS_ACT_RPM: launch_one<T, TASK, QS_ACT_RPM>(grid, lds, st, P, cf, pf, ph); break;
-    case QS_ACT_PID: launch_one<T, TASK, QS_ACT_PID>(grid, lds, st, P, cf, pf, ph); break;
-    case QS_ACT_VEL: launch_one<T, TASK, QS_ACT_VEL>(grid, lds, st, P, cf, pf, ph); break;
-    case QS_ACT_ONE_D_RPM: launch_one<T, TASK, QS_ACT_ONE_D_RPM>(grid, lds, st, P, cf, pf, ph); break;
-    case QS_ACT_ONE_D_PID: launch_one<T, TASK, QS_ACT_ONE_D_PID>(grid, lds, st, P, cf, pf, ph); break;
-    default: return fail(QS_E_INVALID, "launch: bad act_type");
-  }
-  return QS_OK;
-}
-
 template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t st) {
   const int grid = (P.E + P.EPB - 1) / P.EPB;
   size_t lds = 0;
   if (lds_plan(h->dims, &P.stage_rows, &lds) != QS_OK)
     return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
-  const int rc = h->spec.task == QS_TASK_MULTIHOVER
-                     ? launch_act<T, QS_TASK_MULTIHOVER>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq,
-                                                         h->spec.pyb_freq, h->spec.physics)
-                     : launch_act<T, QS_TASK_SPIRAL>(h->spec.act_type, grid, lds, st, P, h->spec.ctrl_freq,
-                                                     h->spec.pyb_freq, h->spec.physics);
-  if (rc != QS_OK) return rc;
+  const qs_spec& s = h->spec;
+  const bool ok = s.task == QS_TASK_MULTIHOVER
+                      ? qs::launch_task<T, QS_TASK_MULTIHOVER>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics)
+                      : qs::launch_task<T, QS_TASK_SPIRAL>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
+  if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
   return QS_OK;
 }
@@ -1386,9 +238,9 @@ extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n
 
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
-  hipSetDevice(h->device);
+  (void)hipSetDevice(h->device);   // teardown: best effort, nothing to report to
   void* ptrs[] = {h->st, h->env, h->hist, h->ep_return, h->orig, h->log, h->log_count, h->err, h->stamps};
-  for (void* p : ptrs) if (p) hipFree(p);
+  for (void* p : ptrs) if (p) (void)hipFree(p);
   delete h;
   return QS_OK;
 }

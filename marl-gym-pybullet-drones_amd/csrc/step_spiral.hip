@@ -1,0 +1,4 @@
+// step_spiral.hip — step-kernel instantiations for QS_TASK_SPIRAL (see step_launch_impl.h).
+#include "step_launch_impl.h"
+
+QS_INSTANTIATE_LAUNCH(QS_TASK_SPIRAL)
