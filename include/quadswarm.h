@@ -61,7 +61,10 @@ extern "C" {
 /* ---- enums mirroring gym_pybullet_drones/utils/enums.py:3-48 ------------ */
 typedef enum {
   QS_TASK_MULTIHOVER = 0, /* MultiHoverAviary.py                          */
-  QS_TASK_SPIRAL = 1      /* SpiralAviary.py (SpiralFormationAviary)      */
+  QS_TASK_SPIRAL = 1,     /* SpiralAviary.py (SpiralFormationAviary)      */
+  QS_TASK_FLOCK = 2,      /* FlockAviary.py                               */
+  QS_TASK_MEETUP = 3,     /* MeetupAviary.py                              */
+  QS_TASK_LEADERFOLLOWER = 4 /* LeaderFollowerAviary.py                   */
 } qs_task;
 
 typedef enum {            /* ActionType (enums.py:35-41)                   */

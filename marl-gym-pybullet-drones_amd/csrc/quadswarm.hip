@@ -71,7 +71,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.E = s.num_envs; P.D = s.num_drones; P.N = h->dims.num_agents; P.O = h->dims.obs_dim;
   P.H = h->dims.hist_len; P.S = h->dims.substeps;
   P.EPB = qs::kBlock / s.num_drones;
-  P.aux = s.aux_forces; P.flags = s.flags; P.pyb_freq = s.pyb_freq;
+  P.aux = s.aux_forces; P.flags = s.flags; P.pyb_freq = s.pyb_freq; P.task = s.task;
   P.ep_len_sec = s.episode_len_sec;
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
   P.env_offset = s.env_offset;
@@ -103,9 +103,13 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (lds_plan(h->dims, &P.stage_rows, &lds) != QS_OK)
     return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
   const qs_spec& s = h->spec;
-  const bool ok = s.task == QS_TASK_MULTIHOVER
-                      ? qs::launch_task<T, QS_TASK_MULTIHOVER>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics)
-                      : qs::launch_task<T, QS_TASK_SPIRAL>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
+  bool ok;
+  if (s.task == QS_TASK_MULTIHOVER)
+    ok = qs::launch_task<T, QS_TASK_MULTIHOVER>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
+  else if (s.task == QS_TASK_SPIRAL)
+    ok = qs::launch_task<T, QS_TASK_SPIRAL>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
+  else
+    ok = qs::launch_task<T, qs::kTaskMarl>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
   if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
   return QS_OK;
@@ -139,7 +143,7 @@ int qs_abi_version(void) { return QS_ABI_VERSION; }
 int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   if (!spec || !out) return fail(QS_E_INVALID, "qs_create: null argument");
   const qs_spec& s = *spec;
-  if (s.task != QS_TASK_MULTIHOVER && s.task != QS_TASK_SPIRAL) return fail(QS_E_INVALID, "qs_create: bad task");
+  if (s.task < QS_TASK_MULTIHOVER || s.task > QS_TASK_LEADERFOLLOWER) return fail(QS_E_INVALID, "qs_create: bad task");
   if (s.num_drones < 1 || s.num_drones > 64) return fail(QS_E_INVALID, "qs_create: num_drones must be in 1..64");
   if (s.num_envs < 1) return fail(QS_E_INVALID, "qs_create: num_envs must be >= 1");
   if (s.physics != QS_PHYS_DYN && s.physics != QS_PHYS_PYB) return fail(QS_E_INVALID, "qs_create: bad physics");

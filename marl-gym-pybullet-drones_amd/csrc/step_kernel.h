@@ -182,6 +182,7 @@ template <class T> struct Params {
   // sizes
   int E, D, N, O, H, S, EPB;
   int mode;
+  int task;               // qs_task (the MARL family kernel switches on it at run time)
   uint32_t aux, flags;
   int pyb_freq;
   double ep_len_sec;
@@ -323,7 +324,8 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T 
 
 // --------------------------------------------------- LDS workspace layout
 template <class T> struct Shared {
-  T cand[kBlock][3];        // reset candidates / downwash snapshot positions
+  T cand[kBlock][3];        // reset candidates / downwash snapshot / MARL-task positions
+  T velw[kBlock][3];        // MARL-task velocities (Flock alignment and speed)
   T rew[kBlock];            // per-drone reward terms
   uint8_t bits[kBlock];     // per-drone termination reason bits
   int reject[kBlock];       // per-group rejection flag (reset search)
@@ -434,6 +436,82 @@ __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70);
 // interleave them), so operands needed first are issued first.
 __device__ __forceinline__ void issue_fence() { __asm__ volatile("" ::: "memory"); }
 
+// ------------------------------------------------------- MARL task rewards
+// Per-env rewards of FlockAviary.py:74-149, MeetupAviary.py:71-93 and
+// LeaderFollowerAviary.py:71-98 from the env's drones' positions p[D][3] and
+// velocities v[D][3] (LDS), in the reference's summation order.
+constexpr int kTaskMarl = QS_TASK_FLOCK;   // kernel family of the three run-time MARL tasks
+// Nearest-neighbour distance of drone i (FlockAviary.py:120-128).
+template <class T> __device__ __forceinline__ T flock_spacing(const T (*p)[3], int D, int i) {
+  T m = T(INFINITY);
+  for (int j = 0; j < D; ++j)
+    if (j != i) {
+      const T dx = p[j][0] - p[i][0], dy = p[j][1] - p[i][1], dz = p[j][2] - p[i][2];
+      const T dist = M<T>::sqrt_(dx * dx + dy * dy + dz * dz);
+      m = dist < m ? dist : m;
+    }
+  return m;
+}
+// MeetupAviary._computeTerminated (MeetupAviary.py:97-117): every pair within 0.1 m.
+template <class T> __device__ bool meetup_met(const T (*p)[3], int D) {
+  for (int i = 0; i < D / 2; ++i) {
+    const T dx = p[i][0] - p[D - 1 - i][0], dy = p[i][1] - p[D - 1 - i][1], dz = p[i][2] - p[D - 1 - i][2];
+    if (M<T>::sqrt_(dx * dx + dy * dy + dz * dz) > T(0.1)) return false;
+  }
+  return true;
+}
+
+template <class T> __device__ T marl_reward(int task, const T (*p)[3], const T (*v)[3], int D) {
+  using F = M<T>;
+  auto n3 = [](T a, T b, T c) { return M<T>::sqrt_(a * a + b * b + c * c); };
+  if (task == QS_TASK_FLOCK) {
+    const T EPS = T(1e-3);
+    T ali = 0;
+    for (int i = 0; i < D; ++i) {
+      const T ni = n3(v[i][0], v[i][1], v[i][2]);
+      for (int j = 0; j < D; ++j)
+        if (j != i) {
+          const T nj = n3(v[j][0], v[j][1], v[j][2]);
+          const T dd = (v[i][0] * v[j][0] + v[i][1] * v[j][1]) + v[i][2] * v[j][2];
+          ali += (dd / (ni + EPS)) / (nj + EPS);
+        }
+    }
+    ali = D > 1 ? ali / T(D * (D - 1)) : T(0);
+    T c0 = 0, c1 = 0, c2 = 0;
+    for (int i = 0; i < D; ++i) { c0 += v[i][0]; c1 += v[i][1]; c2 += v[i][2]; }
+    const T speed = n3(c0 / T(D), c1 / T(D), c2 / T(D));
+    T pen = 0, var = 0;
+    if (D > 1) {
+      T mean = 0;
+      for (int i = 0; i < D; ++i) mean += flock_spacing(p, D, i);
+      mean /= T(D);
+      for (int i = 0; i < D; ++i) { const T dv = flock_spacing(p, D, i) - mean; var += dv * dv; }
+      var /= T(D);
+      if (!(T(1.0) < mean && mean < T(3.0))) {
+        const T a = F::abs_(mean - T(1.0)), b = F::abs_(mean - T(3.0));
+        pen = a < b ? a : b;
+      }
+    }
+    return ((ali + speed) - pen) - var;
+  }
+  if (task == QS_TASK_MEETUP) {
+    T total = 0;
+    for (int i = 0; i < D / 2; ++i) {
+      const T n = n3(p[i][0] - p[D - 1 - i][0], p[i][1] - p[D - 1 - i][1], p[i][2] - p[D - 1 - i][2]);
+      total += (T(-1) * (n * n)) * T(2);
+    }
+    return total;
+  }
+  // LeaderFollower
+  const T n0 = n3(T(0) - p[0][0], T(0) - p[0][1], T(0.5) - p[0][2]);
+  T total = T(-1) * (n0 * n0);
+  for (int i = 1; i < D; ++i) {
+    const T dz = p[0][2] - p[i][2];
+    const T n = F::sqrt_(dz * dz);
+    total += (-(T(1) / T(D))) * (n * n);
+  }
+  return total;
+}
 #ifdef QS_STAMPS_BUILD
 #define QS_STAMP(k)                                                                         \
   do {                                                                                      \
@@ -457,12 +535,14 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   constexpr int A = Act<ACT>::A;
   constexpr bool kPid = Act<ACT>::pid;
   constexpr bool kHover = TASK == QS_TASK_MULTIHOVER;
+  constexpr bool kSpiral = TASK == QS_TASK_SPIRAL;
+  constexpr bool kMarl = TASK == kTaskMarl;   // Flock / Meetup / LeaderFollower (P.task)
   __shared__ Shared<T> s;
   const int tid = threadIdx.x;
   const int D = P.D, N = P.N;
   const int H = CF ? CF / 2 : P.H;
   const int S = CF ? 240 / CF : P.S;
-  const int O = CF ? 12 + (CF / 2) * A + (kHover ? 0 : 11) : P.O;
+  const int O = CF ? 12 + (CF / 2) * A + (kSpiral ? 11 : 0) : P.O;
   const int lenv = tid / D, d = tid - lenv * D;
   const int e = blockIdx.x * P.EPB + lenv;
   const bool valid = (lenv < P.EPB) && (e < P.E);
@@ -878,6 +958,18 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         if (pos[2] < T(0.03)) bits |= QS_REASON_CRASH;
         if (F::abs_(rpy[0]) > T(1.2) || F::abs_(rpy[1]) > T(1.2)) bits |= QS_REASON_FLIP;
         if (F::abs_(pos[0]) > T(3.0) || F::abs_(pos[1]) > T(3.0)) bits |= QS_REASON_OOB;
+      } else if constexpr (kMarl) {
+        // Flock/Meetup/LeaderFollower._computeTruncated: out of the task's box or
+        // |roll|, |pitch| > 0.4 (FlockAviary.py:169-186, MeetupAviary.py:121-151,
+        // LeaderFollowerAviary.py:118-144); the env reward is formed below
+        bool out;
+        if (P.task == QS_TASK_FLOCK)
+          out = F::abs_(pos[0]) > T(10.0) || F::abs_(pos[1]) > T(10.0) || pos[2] > T(10.0);
+        else if (P.task == QS_TASK_MEETUP)
+          out = F::abs_(pos[0]) > T(5.0) || F::abs_(pos[1]) > T(5.0) || pos[2] > T(3.0) || pos[2] < T(0.1);
+        else
+          out = F::abs_(pos[0]) > T(2.0) || F::abs_(pos[1]) > T(2.0) || pos[2] > T(2.0);
+        if (out || F::abs_(rpy[0]) > T(.4) || F::abs_(rpy[1]) > T(.4)) bits = 1;
       } else {  // SpiralAviary.py:82-99, 150-191
         T t = T((double)step_counter / (double)P.pyb_freq);
         T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
@@ -906,6 +998,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
     s.rew[tid] = rterm;
     s.bits[tid] = bits;
+    if constexpr (kMarl) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { s.cand[tid][i] = pos[i]; s.velw[tid][i] = vel[i]; }
+    }
     __syncthreads();
     // per-env reduction in drone order (reference: reward += ... for i in range(D))
     bool dn = false;
@@ -918,6 +1014,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       T r = rsum / T(D);
       bool te = any != 0;
       bool tr = ((double)step_counter / (double)P.pyb_freq) > P.ep_len_sec;   // MultiHoverAviary.py:267-268
+      if constexpr (kMarl) {
+        r = marl_reward<T>(P.task, &s.cand[tid], &s.velw[tid], D);
+        te = P.task == QS_TASK_MEETUP && meetup_met<T>(&s.cand[tid], D);
+        tr = any != 0 || tr;   // (no termination-reason strings for these tasks)
+      }
       if (P.rew) P.rew[e] = r;
       if (P.term) P.term[e] = te;
       if (P.trunc) P.trunc[e] = tr;
@@ -939,7 +1040,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         P.log[slot % (unsigned long long)P.log_cap] = rec;
       }
     }
-    if (P.reasons && valid) P.reasons[a] = bits;
+    if (P.reasons && valid) P.reasons[a] = kMarl ? 0 : bits;
     step_counter += S;   // BaseAviary.py:382
     __syncthreads();
     done_env = valid && s.done[lenv];
@@ -997,7 +1098,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
 #pragma unroll
     for (int k = 0; k < A; ++k) o[12 + (H - 1) * A + k] = cur_act[k];   // newest = this step's action
-    if constexpr (!kHover) {
+    if constexpr (kSpiral) {
       T t = T((double)sc / (double)P.pyb_freq);
       T ph = P.sp_OMEGA * t + T(2 * M_PI) * T(d) / T(D);
       T sn = F::sin_(ph), cs = F::cos_(ph);

@@ -8,7 +8,7 @@ namespace qs {
 
 template <class T, int TASK, int ACT> static void launch_one(int grid, size_t lds, hipStream_t st, const Params<T>& P,
                                                              int ctrl_freq, int pyb_freq, int phys) {
-  constexpr int kCF = TASK == QS_TASK_MULTIHOVER ? 30 : 48;   // MultiHoverAviary.py:20, SpiralAviary.py:28
+  constexpr int kCF = TASK == QS_TASK_SPIRAL ? 48 : 30;   // SpiralAviary.py:28; MH:20 and the MARL tasks
   const bool cf = ctrl_freq == kCF && pyb_freq == 240;
   if (phys == QS_PHYS_DYN) {
     if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN>), dim3(grid), dim3(kBlock), lds, st, P);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libquadswarm.so")
 
 QS_OK = 0
-TASK_MULTIHOVER, TASK_SPIRAL = 0, 1
+TASK_MULTIHOVER, TASK_SPIRAL, TASK_FLOCK, TASK_MEETUP, TASK_LEADERFOLLOWER = 0, 1, 2, 3, 4
 ACT_RPM, ACT_PID, ACT_VEL, ACT_ONE_D_RPM, ACT_ONE_D_PID = 0, 1, 2, 3, 4
 PHYS_PYB, PHYS_DYN = 0, 1
 AUX_GND, AUX_DRAG, AUX_DW = 1, 2, 4

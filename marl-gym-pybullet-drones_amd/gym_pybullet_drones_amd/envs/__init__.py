@@ -1,4 +1,6 @@
 from .swarm import QuadSwarm, StepResult, grid_layout
-from .aviaries import MultiHoverAviary, SpiralFormationAviary
+from .aviaries import (FlockAviary, LeaderFollowerAviary, MeetupAviary, MultiHoverAviary,
+                       SpiralFormationAviary)
 
-__all__ = ["QuadSwarm", "StepResult", "grid_layout", "MultiHoverAviary", "SpiralFormationAviary"]
+__all__ = ["QuadSwarm", "StepResult", "grid_layout", "MultiHoverAviary", "SpiralFormationAviary", "FlockAviary",
+           "MeetupAviary", "LeaderFollowerAviary"]

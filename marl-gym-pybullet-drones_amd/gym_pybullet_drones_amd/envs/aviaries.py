@@ -147,3 +147,33 @@ class SpiralFormationAviary(_SingleEnvAviary):
 
     def _info(self, sc, reasons=()):
         return {"time": sc / self.PYB_FREQ, "omega": self.OMEGA, "radius": self.R}
+
+
+class _MarlAviary(_SingleEnvAviary):
+    """Base of the three BaseRLAviary MARL tasks without a custom reset: KIN obs,
+    EPISODE_LEN_SEC 8, ctrl_freq 30, ActionType.RPM, info {"answer": 42}."""
+
+    def __init__(self, drone_model=DroneModel.CF2X, num_drones=2, neighbourhood_radius=np.inf, initial_xyzs=None,
+                 initial_rpys=None, physics=Physics.PYB, pyb_freq=240, ctrl_freq=30, gui=False, record=False,
+                 obs=ObservationType.KIN, act=ActionType.RPM, **kw):
+        super().__init__(drone_model, num_drones, neighbourhood_radius, initial_xyzs, initial_rpys, physics,
+                         pyb_freq, ctrl_freq, gui, record, obs, act, **kw)
+
+    def _info(self, sc, reasons=()):
+        return {"answer": 42}
+
+
+class FlockAviary(_MarlAviary):
+    """FlockAviary.py:7-199: alignment + flock speed - spacing penalty - spacing variance;
+    never terminates; truncated out of a 10 m box or tilted."""
+    TASK = "flock"
+
+
+class MeetupAviary(_MarlAviary):
+    """MeetupAviary.py:6-164: pairs (i, D-1-i) meet; terminates when all pairs are within 0.1 m."""
+    TASK = "meetup"
+
+
+class LeaderFollowerAviary(_MarlAviary):
+    """LeaderFollowerAviary.py:6-157: drone 0 hovers at (0, 0, 0.5), the others match its height."""
+    TASK = "leaderfollower"

@@ -31,7 +31,8 @@ _PHYS = {Physics.DYN: (L.PHYS_DYN, 0), Physics.PYB: (L.PHYS_PYB, 0),
          Physics.PYB_DW: (L.PHYS_PYB, L.AUX_DW),
          Physics.PYB_GND_DRAG_DW: (L.PHYS_PYB, L.AUX_GND | L.AUX_DRAG | L.AUX_DW)}
 _AUX_NAMES = {"gnd": L.AUX_GND, "drag": L.AUX_DRAG, "dw": L.AUX_DW}
-TASKS = {"multihover": L.TASK_MULTIHOVER, "spiral": L.TASK_SPIRAL}
+TASKS = {"multihover": L.TASK_MULTIHOVER, "spiral": L.TASK_SPIRAL, "flock": L.TASK_FLOCK, "meetup": L.TASK_MEETUP,
+         "leaderfollower": L.TASK_LEADERFOLLOWER}
 
 
 @dataclass
@@ -91,9 +92,9 @@ class QuadSwarm:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         if ctrl_freq is None:
-            ctrl_freq = 30 if task == "multihover" else 48       # MH:20, SP:28
+            ctrl_freq = 48 if task == "spiral" else 30           # SP:28; MH:20 and the other MARL tasks
         if episode_len_sec is None:
-            episode_len_sec = 8.0 if task == "multihover" else 12.0   # MH:58, SP:39
+            episode_len_sec = 12.0 if task == "spiral" else 8.0       # SP:39; MH:58 and the other MARL tasks
         spec = L.QsSpec()
         spec.task = TASKS[task]
         spec.num_envs = int(num_envs)

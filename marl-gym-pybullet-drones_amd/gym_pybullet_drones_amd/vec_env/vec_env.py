@@ -121,6 +121,8 @@ class SwarmVecEnv(VecEnv):
             sp = self.swarm.spec
             return {"time": step_counter / self.PYB_FREQ, "omega": 2 * np.pi / sp.spiral_period,
                     "radius": sp.spiral_radius}
+        if self.swarm.task != "multihover":   # Flock/Meetup/LeaderFollower._computeInfo
+            return {"answer": 42}
         return {"answer": 42, "termination_reasons": list(reasons)}   # MH:274-285
 
     # ----------------------------------------------------------- numpy API

@@ -512,7 +512,7 @@ template <class R> struct Sim {
   void draw_init(int e, R out[][3]) {
     const int D = P.D;
     const uint32_t genv = (uint32_t)(env_offset + e);
-    if (P.task == QS_TASK_SPIRAL) {
+    if (P.task != QS_TASK_MULTIHOVER) {   // BaseAviary.reset: INIT_XYZS as given (BA:245-255)
       for (int d = 0; d < D; ++d) for (int i = 0; i < 3; ++i) out[d][i] = P.orig_xyz[d * 3 + i];
       return;
     }
@@ -609,9 +609,86 @@ template <class R> struct Sim {
     }
   }
 
+  // FlockAviary._computeReward (FlockAviary.py:74-149): velocity alignment +
+  // flock speed - spacing penalty - spacing variance, per env.
+  R flock_reward(int e) const {
+    const int D = P.D;
+    const Drone<R>* dr = &drones[e * D];
+    const R EPS = R(1e-3);
+    R ali = 0;
+    std::vector<R> vn(D);
+    for (int i = 0; i < D; ++i) vn[i] = norm3(dr[i].vel);
+    for (int i = 0; i < D; ++i)
+      for (int j = 0; j < D; ++j)
+        if (j != i) {
+          R dd = (dr[i].vel[0] * dr[j].vel[0] + dr[i].vel[1] * dr[j].vel[1]) + dr[i].vel[2] * dr[j].vel[2];
+          ali += (dd / (vn[i] + EPS)) / (vn[j] + EPS);
+        }
+    ali = D > 1 ? ali / R(D * (D - 1)) : R(0);
+    R cv[3] = {0, 0, 0};
+    for (int i = 0; i < D; ++i) for (int k = 0; k < 3; ++k) cv[k] += dr[i].vel[k];
+    for (int k = 0; k < 3; ++k) cv[k] /= R(D);
+    R speed = norm3(cv);
+    R spac_rew = 0, var = 0;
+    if (D > 1) {
+      std::vector<R> sp(D);
+      for (int i = 0; i < D; ++i) {
+        R m = R(INFINITY);
+        for (int j = 0; j < D; ++j)
+          if (j != i) {
+            R dp[3] = {dr[j].pos[0] - dr[i].pos[0], dr[j].pos[1] - dr[i].pos[1], dr[j].pos[2] - dr[i].pos[2]};
+            R dist = norm3(dp);
+            m = dist < m ? dist : m;
+          }
+        sp[i] = m;
+      }
+      R mean = 0;
+      for (int i = 0; i < D; ++i) mean += sp[i];
+      mean /= R(D);
+      for (int i = 0; i < D; ++i) var += (sp[i] - mean) * (sp[i] - mean);
+      var /= R(D);
+      if (!(R(1.0) < mean && mean < R(3.0)))
+        spac_rew = std::min(std::fabs(mean - R(1.0)), std::fabs(mean - R(3.0)));
+    }
+    return ((ali + speed) - spac_rew) - var;
+  }
+
+  // MeetupAviary._computeReward (MeetupAviary.py:71-93): -2·|p_i - p_{D-1-i}|² per pair.
+  R meetup_reward(int e) const {
+    const int D = P.D;
+    const Drone<R>* dr = &drones[e * D];
+    R total = 0;
+    for (int i = 0; i < D / 2; ++i) {
+      R dp[3] = {dr[i].pos[0] - dr[D - 1 - i].pos[0], dr[i].pos[1] - dr[D - 1 - i].pos[1],
+                 dr[i].pos[2] - dr[D - 1 - i].pos[2]};
+      R n = norm3(dp);
+      total += (R(-1) * (n * n)) * R(2);
+    }
+    return total;
+  }
+
+  // LeaderFollowerAviary._computeReward (LeaderFollowerAviary.py:71-98): the leader
+  // hovers at (0,0,0.5); follower i matches the leader's height at its own x, y.
+  R leader_reward(int e) const {
+    const int D = P.D;
+    const Drone<R>* dr = &drones[e * D];
+    R dp[3] = {R(0) - dr[0].pos[0], R(0) - dr[0].pos[1], R(0.5) - dr[0].pos[2]};
+    R n0 = norm3(dp);
+    R total = R(-1) * (n0 * n0);
+    for (int i = 1; i < D; ++i) {
+      R dz = dr[0].pos[2] - dr[i].pos[2];
+      R n = std::sqrt(dz * dz);   // |(x_i, y_i, z_0) - p_i|: only z differs
+      total += (-(R(1) / R(D))) * (n * n);
+    }
+    return total;
+  }
+
   // MultiHoverAviary._computeReward (MH:128-186) / SpiralAviary (SP:150-181).
   R compute_reward(int e) const {
     const int D = P.D;
+    if (P.task == QS_TASK_FLOCK) return flock_reward(e);
+    if (P.task == QS_TASK_MEETUP) return meetup_reward(e);
+    if (P.task == QS_TASK_LEADERFOLLOWER) return leader_reward(e);
     R reward = 0;
     for (int d = 0; d < D; ++d) {
       const Drone<R>& dr = drones[e * D + d];
@@ -652,8 +729,45 @@ template <class R> struct Sim {
     return reward / R(D);
   }
 
+  // Flock / LeaderFollower never terminate (FlockAviary.py:153-165,
+  // LeaderFollowerAviary.py:102-114); Meetup does when every pair is within
+  // 0.1 m (MeetupAviary.py:97-117; vacuously true for one drone).
+  // _computeTruncated of the three (FlockAviary.py:169-186, MeetupAviary.py:
+  // 121-151, LeaderFollowerAviary.py:118-144): any drone out of the box or
+  // tilted (|roll| or |pitch| > 0.4), or the time limit.
+  bool marl_terminated(int e) const {
+    if (P.task != QS_TASK_MEETUP) return false;
+    const int D = P.D;
+    const Drone<R>* dr = &drones[e * D];
+    for (int i = 0; i < D / 2; ++i) {
+      R dp[3] = {dr[i].pos[0] - dr[D - 1 - i].pos[0], dr[i].pos[1] - dr[D - 1 - i].pos[1],
+                 dr[i].pos[2] - dr[D - 1 - i].pos[2]};
+      if (norm3(dp) > R(0.1)) return false;
+    }
+    return true;
+  }
+  bool marl_out_of_bounds(int e) const {
+    for (int d = 0; d < P.D; ++d) {
+      const Drone<R>& x = drones[e * P.D + d];
+      bool tilt = std::fabs(x.rpy[0]) > R(.4) || std::fabs(x.rpy[1]) > R(.4);
+      bool out;
+      if (P.task == QS_TASK_FLOCK)
+        out = std::fabs(x.pos[0]) > R(10.0) || std::fabs(x.pos[1]) > R(10.0) || x.pos[2] > R(10.0);
+      else if (P.task == QS_TASK_MEETUP)
+        out = std::fabs(x.pos[0]) > R(5.0) || std::fabs(x.pos[1]) > R(5.0) || x.pos[2] > R(3.0) || x.pos[2] < R(0.1);
+      else
+        out = std::fabs(x.pos[0]) > R(2.0) || std::fabs(x.pos[1]) > R(2.0) || x.pos[2] > R(2.0);
+      if (out || tilt) return true;
+    }
+    return false;
+  }
+
   // _computeTerminated (MH:216-241 / SP:185-191); reasons bits per drone.
   bool compute_terminated(int e, uint8_t* reasons) const {
+    if (P.task >= QS_TASK_FLOCK) {
+      if (reasons) std::memset(reasons, 0, P.D);
+      return marl_terminated(e);
+    }
     bool term = false;
     for (int d = 0; d < P.D; ++d) {
       const Drone<R>& dr = drones[e * P.D + d];
@@ -720,6 +834,7 @@ template <class R> struct Sim {
     uint8_t rs[64];
     bool te = compute_terminated(e, rs);
     bool tr = ((double)step_counter[e] / (double)P.pyb_freq) > (double)P.ep_len_sec;  // MH:267-268
+    if (P.task >= QS_TASK_FLOCK) tr = marl_out_of_bounds(e) || tr;
     step_counter[e] += P.S;                                                          // BA:382
     if (rew) rew[e] = r;
     if (term) term[e] = te;
@@ -754,7 +869,7 @@ struct OracleHandle {
 };
 
 template <class R> int make_params(const qs_spec* s, Params<R>& P) {
-  if (s->task != QS_TASK_MULTIHOVER && s->task != QS_TASK_SPIRAL) return fail(QS_E_INVALID, "bad task");
+  if (s->task < QS_TASK_MULTIHOVER || s->task > QS_TASK_LEADERFOLLOWER) return fail(QS_E_INVALID, "bad task");
   if (s->num_drones < 1 || s->num_drones > 64) return fail(QS_E_INVALID, "num_drones must be 1..64");
   if (s->num_envs < 1) return fail(QS_E_INVALID, "num_envs must be >= 1");
   if (s->physics != QS_PHYS_DYN && s->physics != QS_PHYS_PYB) return fail(QS_E_INVALID, "bad physics");

@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libqs_oracle.so")
 
-TASK = {"multihover": 0, "spiral": 1}
+TASK = {"multihover": 0, "spiral": 1, "flock": 2, "meetup": 3, "leaderfollower": 4}
 ACT = {"rpm": 0, "pid": 1, "vel": 2, "one_d_rpm": 3, "one_d_pid": 4}
 AUX = {"gnd": 1, "drag": 2, "dw": 4}
 AGENT_FIELDS = 29
@@ -103,11 +103,11 @@ def make_spec(task="multihover", num_envs=1, num_drones=2, act="rpm", aux=(), ph
     s.physics = {"pyb": 0, "dyn": 1}[physics]
     s.aux_forces = sum(AUX[a] for a in aux)
     s.pyb_freq = pyb_freq
-    s.ctrl_freq = ctrl_freq if ctrl_freq is not None else (30 if task == "multihover" else 48)
+    s.ctrl_freq = ctrl_freq if ctrl_freq is not None else (48 if task == "spiral" else 30)
     s.precision = precision
     s.flags = 0 if autoreset else 1
     s.env_offset = env_offset
-    s.episode_len_sec = episode_len_sec if episode_len_sec is not None else (8.0 if task == "multihover" else 12.0)
+    s.episode_len_sec = episode_len_sec if episode_len_sec is not None else (12.0 if task == "spiral" else 8.0)
     keep = None
     if initial_xyzs is not None:
         keep = np.ascontiguousarray(np.asarray(initial_xyzs, dtype=np.float64).reshape(num_drones, 3))

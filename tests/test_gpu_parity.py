@@ -46,6 +46,10 @@ CONFIGS = {
     "C4p_spiral_vel_d5_pyb": dict(task="spiral", num_drones=5, act="vel", physics="pyb"),
     "pyb_gnd_drag_dw_d4": dict(task="multihover", num_drones=4, act="one_d_pid", physics="pyb",
                                aux=("gnd", "drag", "dw")),
+    # the other MARL tasks (FlockAviary, MeetupAviary, LeaderFollowerAviary), SURVEY §8(f) next-4
+    "flock_rpm_d3_pyb": dict(task="flock", num_drones=3, act="rpm", physics="pyb"),
+    "meetup_vel_d4": dict(task="meetup", num_drones=4, act="vel"),
+    "leader_onedpid_d3_pyb": dict(task="leaderfollower", num_drones=3, act="one_d_pid", physics="pyb"),
 }
 
 
@@ -137,9 +141,10 @@ def free_running(cfg, E, precision, steps=30, seed=11):
         c = orc.step(None)
         tr = truth.step(None)
         torch.cuda.synchronize()
-        # an env that terminates in any of the three runs is dropped from then on
+        # an env that ends its episode in any of the three runs is dropped from then on
         alive &= ~(r.terminated.cpu().numpy().astype(bool) | c["terminated"].astype(bool)
-                   | tr["terminated"].astype(bool))
+                   | tr["terminated"].astype(bool) | r.truncated.cpu().numpy().astype(bool)
+                   | c["truncated"].astype(bool) | tr["truncated"].astype(bool))
         cols = np.repeat(alive, sw.num_drones)
         g, o, T = sw.get_state(0).cpu().numpy()[:, cols], orc.get_state(0)[:, cols], truth.get_state(0)[:, cols]
         for name, sl in (("pos", slice(0, 3)), ("quat", slice(3, 7)), ("vel", slice(7, 10))):
