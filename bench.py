@@ -13,6 +13,9 @@ rank) with no data-path collective; value = all ranks' agent-steps ÷ max-over-
 ranks wall time.
 
 Extra JSON fields:
+  pyb           the same rollout under Physics.PYB (the kernel's restatement of
+                Bullet's step, the reference's training default): agent-steps/s,
+                kernel ms and roofline fraction (same algorithmic bytes).
   mappo         full MAPPO on the same C3 envs (BASELINE config 3): agent-steps/s of
                 MAPPO.train_step = T-step rollout with the shared actor + simulator,
                 last value, GAE, advantage normalisation and the PPO update
@@ -56,6 +59,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--mappo", type=int, default=1, help="also time full MAPPO train steps (0 = skip)")
+    p.add_argument("--pyb", type=int, default=1, help="also time the rollout under Physics.PYB (0 = skip)")
     p.add_argument("--mappo-steps", type=int, default=32, help="rollout_steps T of the MAPPO leg")
     p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO leg")
     p.add_argument("--mappo-iters", type=int, default=3, help="timed train steps (after one warm-up)")
@@ -104,61 +108,15 @@ def pmc_traffic(E, D, act):
     return best[1]["step_traffic_bytes"], os.path.relpath(best[0], ROOT)
 
 
-def mappo_leg(args, rank, world, dist):
-    """Full MAPPO train steps on the bench's C3 envs (learn_mappo.py:196-203 hyper-parameters,
-    hidden 256, opt_epochs 10; minibatch scaled to the 128x larger env batch)."""
-    from gym_pybullet_drones_amd.envs import MultiHoverAviary
-    from gym_pybullet_drones_amd.mappo import MAPPO
-    from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
-    D, E = args.drones, args.envs
-    act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[args.act]
-    env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act, physics=Physics.DYN,
-                                               initial_xyzs=grid_layout(D) if D >= 6 else None)
-    m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
-              rollout_steps=args.mappo_steps, rollout_batch_size=E, opt_epochs=10,
-              mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
-    m.reset()
-    m.train_step()   # warm-up: graph capture, lazy kernel loads
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.mappo_iters):
-        m.train_step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.mappo_iters
-    if dist:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    m.close()
-    T = args.mappo_steps
-    return {"value": T * E * D * world / dt, "unit": "agent-steps/s", "ms_per_train_step": dt * 1e3,
-            "train_steps": args.mappo_iters,
-            "config": {"rollout_steps": T, "envs_per_gpu": E, "drones": D, "hidden": 256, "opt_epochs": 10,
-                       "mini_batch_size": args.mappo_mb,
-                       "minibatches_per_epoch": T * E // args.mappo_mb,
-                       "graphs": world == 1, "grad_allreduce": "one fused all-reduce per minibatch" if world > 1
-                       else None}}
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+def sim_leg(args, rank, world, dist, physics="dyn"):
+    """The timed random-policy rollout: `steps` control steps of E envs per rank, as
+    replays of a HIP graph of `slots` step launches.  Returns (agent-steps/s over all
+    ranks, max-over-ranks seconds, mean step-kernel ms on the launch stream, steps)."""
     from gym_pybullet_drones_amd.envs import QuadSwarm
+    from gym_pybullet_drones_amd.utils.enums import Physics
     E, D = args.envs, args.drones
     sw = QuadSwarm("multihover", num_envs=E, num_drones=D, act=args.act, precision=4,
+                   physics=Physics.PYB if physics == "pyb" else Physics.DYN,
                    initial_xyzs=grid_layout(D) if D >= 6 else None, env_offset=rank * E)
     O, A = sw.obs_dim, sw.act_dim
     obs_buf = torch.empty((args.slots, E, D, O), dtype=torch.float32, device=sw.device)
@@ -204,19 +162,78 @@ def main():
     elapsed = time.perf_counter() - t0
     # mean step-kernel duration on the launch stream: graph time / launches per graph
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) / args.slots
-    args.steps = steps
     if dist:
         t = torch.tensor([elapsed], device=sw.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    agents_total = E * D * world
-    value = agents_total * args.steps / elapsed
-    nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
-    achieved = nbytes / (kern_ms * 1e-3) / 1e9
     assert sw.reset_error() == 0
-    assert torch.isfinite(obs_buf[:min(args.slots, args.steps)]).all()
+    assert torch.isfinite(obs_buf[:min(args.slots, steps)]).all()
     del graph
     sw.close()
+    return E * D * world * steps / elapsed, elapsed, kern_ms, steps
+
+
+def mappo_leg(args, rank, world, dist):
+    """Full MAPPO train steps on the bench's C3 envs (learn_mappo.py:196-203 hyper-parameters,
+    hidden 256, opt_epochs 10; minibatch scaled to the 128x larger env batch)."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
+    D, E = args.drones, args.envs
+    act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[args.act]
+    env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act, physics=Physics.DYN,
+                                               initial_xyzs=grid_layout(D) if D >= 6 else None)
+    m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
+              rollout_steps=args.mappo_steps, rollout_batch_size=E, opt_epochs=10,
+              mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
+    m.reset()
+    m.train_step()   # warm-up: graph capture, lazy kernel loads
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.mappo_iters):
+        m.train_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.mappo_iters
+    if dist:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    m.close()
+    T = args.mappo_steps
+    return {"value": T * E * D * world / dt, "unit": "agent-steps/s", "ms_per_train_step": dt * 1e3,
+            "train_steps": args.mappo_iters,
+            "config": {"rollout_steps": T, "envs_per_gpu": E, "drones": D, "hidden": 256, "opt_epochs": 10,
+                       "mini_batch_size": args.mappo_mb,
+                       "minibatches_per_epoch": T * E // args.mappo_mb,
+                       "graphs": "rollout + update" if world == 1 else "rollout", "grad_allreduce": "one fused all-reduce per minibatch" if world > 1
+                       else None}}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    E, D = args.envs, args.drones
+    value, elapsed, kern_ms, args.steps = sim_leg(args, rank, world, dist, "dyn")
+    nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    pyb = None
+    if args.pyb:   # the same rollout under Physics.PYB (the reference's training default)
+        pv, _, pk, _ = sim_leg(args, rank, world, dist, "pyb")
+        pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
+               "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
     mappo = mappo_leg(args, rank, world, dist) if args.mappo else None
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
@@ -236,6 +253,7 @@ def main():
                          "algorithmic_bytes_per_launch": nbytes,
                          "kernel_ms": kern_ms, "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act)},
             "cpu_baseline": cpu,
+            "pyb": pyb,
             "mappo": mappo,
         }
         print(json.dumps(line), flush=True)

@@ -337,7 +337,7 @@ class MAPPO:
         start = time.time()
         rollouts.next_obs_slots[0].copy_(self.obs)
         # the quirk path (norm_obs + double normalisation on done) needs a host branch per step
-        graph_ok = self.use_graphs and self.world == 1 and not self.norm_obs and not self.norm_reward
+        graph_ok = self.use_graphs and not self.norm_obs and not self.norm_reward   # no collective in a step
         if graph_ok:
             if self._rollout_graph is None:
                 # the capture records the T steps; the stream runs them only at replay
