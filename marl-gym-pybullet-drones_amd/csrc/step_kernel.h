@@ -765,6 +765,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // s = 2/|q|² (getMatrixFromQuaternion) is formed once per control step; it
     // moves by rounding only between substeps.
     const T s2 = T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    T R[9];   // PYB: rotation of the current pose, carried across substeps
+    if constexpr (PHYS == QS_PHYS_PYB) quat_to_rot(q, R);
     // One substep (BaseAviary.py:343-372).  kAux: ground effect / drag /
     // downwash enabled; the common force-free path is compiled separately.
 #ifdef QS_SUB_NOUNROLL
@@ -837,15 +839,16 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       if constexpr (PHYS == QS_PHYS_PYB) {
         // Bullet's step of the _physics forces (BA:679-711, 369-370), restated
         // as the oracle's pyb_dynamics.  No contraction: the
-        // prop-torque sums cancel exactly for equal rotors only without FMA.
+        // torque sums cancel exactly for equal rotors only without FMA, and the
+        // fp64 build tracks the oracle over long free-running rollouts.
+        // R is the rotation of the (normalised) q, carried from the previous
+        // substep's ground check.
 #pragma clang fp contract(off)
-        T R[9];
-        quat_to_rot(q, R);
         const T k = T(kPybDamping);
         T fw0 = R[2] * zb + fwx, fw1 = R[5] * zb + fwy, fw2 = (R[8] * zb - T(cf2x::GRAVITY)) + fwz;
         const T vd = k + k * F::sqrt_(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
-        const T a0 = fw0 / T(cf2x::M) - vd * vel[0], a1 = fw1 / T(cf2x::M) - vd * vel[1];
-        const T a2 = fw2 / T(cf2x::M) - vd * vel[2];
+        const T a0 = F::divc(fw0, cf2x::M) - vd * vel[0], a1 = F::divc(fw1, cf2x::M) - vd * vel[1];
+        const T a2 = F::divc(fw2, cf2x::M) - vd * vel[2];
         T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
         T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
         const T wdm = k + k * F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
@@ -875,30 +878,35 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         T n1 = ((c * x1 - e0 * x2) + e1 * x3) + e2 * x0;
         T n2 = ((c * x2 + e0 * x1) - e1 * x0) + e2 * x3;
         T n3 = ((c * x3 - e0 * x0) - e1 * x1) - e2 * x2;
-        const T qn = F::sqrt_(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
-        q[0] = n0 / qn; q[1] = n1 / qn; q[2] = n2 / qn; q[3] = n3 / qn;
-        // ground plane vs the collision cylinder (cf2x.urdf:32-35)
-        T Rn[9];
-        quat_to_rot(q, Rn);
-        const T cz = F::abs_(Rn[8]);
-        const T sz = F::sqrt_(T(1) - Rn[8] * Rn[8] > T(0) ? T(1) - Rn[8] * Rn[8] : T(0));
-        const T zmin = pos[2] - (T(kCylHalfLen) * cz + T(kCylR) * sz);
-        if (zmin < T(0)) {
-          pos[2] = pos[2] - zmin;
-          if (vel[2] < T(0)) vel[2] = T(0);
+        if constexpr (sizeof(T) == 4) {
+          const T rn = F::rsqrt(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
+          q[0] = n0 * rn; q[1] = n1 * rn; q[2] = n2 * rn; q[3] = n3 * rn;
+        } else {
+          const T qn = F::sqrt_(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
+          q[0] = n0 / qn; q[1] = n1 / qn; q[2] = n2 / qn; q[3] = n3 / qn;
+        }
+        quat_to_rot(q, R);   // the new pose: ground check, readback, next substep
+        // ground plane vs the collision cylinder (cf2x.urdf:32-35); the cylinder
+        // reaches at most kCylHalfLen + kCylR below its centre
+        if (pos[2] < T(kCylHalfLen + kCylR)) {
+          const T cz = F::abs_(R[8]);
+          const T sz = F::sqrt_(T(1) - R[8] * R[8] > T(0) ? T(1) - R[8] * R[8] : T(0));
+          const T zmin = pos[2] - (T(kCylHalfLen) * cz + T(kCylR) * sz);
+          if (zmin < T(0)) {
+            pos[2] = pos[2] - zmin;
+            if (vel[2] < T(0)) vel[2] = T(0);
+          }
         }
         if (sub == S - 1) {   // getBaseVelocity: world angular velocity at the new pose
-          angv[0] = Rn[0] * w[0] + Rn[1] * w[1] + Rn[2] * w[2];
-          angv[1] = Rn[3] * w[0] + Rn[4] * w[1] + Rn[5] * w[2];
-          angv[2] = Rn[6] * w[0] + Rn[7] * w[1] + Rn[8] * w[2];
+          angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
+          angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];
+          angv[2] = R[6] * w[0] + R[7] * w[1] + R[8] * w[2];
         }
       } else {
         // _dynamics (BaseAviary.py:836-877)
         T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
         T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
-        T c0 = F::sub_rn(F::mul_rn(w[1], Jw2), F::mul_rn(w[2], Jw1));
-        T c1 = F::sub_rn(F::mul_rn(w[2], Jw0), F::mul_rn(w[0], Jw2));
-        T c2 = F::sub_rn(F::mul_rn(w[0], Jw1), F::mul_rn(w[1], Jw0));
+        T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
         T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
         T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
         vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
