@@ -51,9 +51,8 @@ struct qs_handle {
   qs_dims dims;
   int device = 0;
   void* st = nullptr;          // agent SoA (real)
-  int32_t* env = nullptr;      // env int32 SoA
+  int32_t* env = nullptr;      // per-env records [E][qs::kEnvRec] (counters + episode return)
   float* hist = nullptr;
-  double* ep_return = nullptr;
   void* orig = nullptr;        // [D][3] real
   qs_episode_rec* log = nullptr;
   unsigned long long* log_count = nullptr;
@@ -79,13 +78,13 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq); P.ctrl_hz = T(s.ctrl_freq);
   P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
   P.sp_cx = T(s.target_center[0]); P.sp_cy = T(s.target_center[1]); P.sp_cz = T(s.target_center[2]);
-  P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.ep_return = h->ep_return; P.orig_xyz = (const T*)h->orig;
+  P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.orig_xyz = (const T*)h->orig;
   P.log = h->log; P.log_count = h->log_count; P.log_cap = h->log_cap; P.err = h->err;
   P.stamps = h->stamps;
 }
 
 // LDS per workgroup: the history prefetch image plus as many obs rows as fit.
-static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 4096, kStageBudget = 48 * 1024;
+static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 8192, kStageBudget = 48 * 1024;
 static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
   const size_t hist = (size_t)d.hist_len * qs::kBlock * d.act_dim * sizeof(float);
   const size_t row = (size_t)d.obs_dim * sizeof(float);
@@ -202,22 +201,21 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   h->log_cap = std::max<long long>(1 << 16, 4LL * s.num_envs);
   auto cleanup = [&]() { qs_destroy(h); };
   hipError_t e1 = hipMalloc(&h->st, rs * QS_AGENT_FIELDS * N);
-  hipError_t e2 = hipMalloc((void**)&h->env, sizeof(int32_t) * QS_ENV_FIELDS * s.num_envs);
+  hipError_t e2 = hipMalloc((void**)&h->env, sizeof(int32_t) * qs::kEnvRec * s.num_envs);
   hipError_t e3 = hipMalloc((void**)&h->hist, sizeof(float) * d.hist_len * N * A);
-  hipError_t e4 = hipMalloc((void**)&h->ep_return, sizeof(double) * s.num_envs);
   hipError_t e5 = hipMalloc(&h->orig, rs * 3 * s.num_drones);
   hipError_t e6 = hipMalloc((void**)&h->log, sizeof(qs_episode_rec) * h->log_cap);
   hipError_t e7 = hipMalloc((void**)&h->log_count, sizeof(unsigned long long));
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
-  if (e1 || e2 || e3 || e4 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
+  if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
   if (s.precision == 8) {
     if (hipMemcpy(h->orig, h->orig_host.data(), 8 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }
   } else {
     std::vector<float> of(h->orig_host.begin(), h->orig_host.end());
     if (hipMemcpy(h->orig, of.data(), 4 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }
   }
-  if (hipMemset(h->st, 0, rs * QS_AGENT_FIELDS * N) || hipMemset(h->env, 0, sizeof(int32_t) * QS_ENV_FIELDS * s.num_envs) ||
-      hipMemset(h->hist, 0, sizeof(float) * d.hist_len * N * A) || hipMemset(h->ep_return, 0, sizeof(double) * s.num_envs) ||
+  if (hipMemset(h->st, 0, rs * QS_AGENT_FIELDS * N) || hipMemset(h->env, 0, sizeof(int32_t) * qs::kEnvRec * s.num_envs) ||
+      hipMemset(h->hist, 0, sizeof(float) * d.hist_len * N * A) ||
       hipMemset(h->log_count, 0, sizeof(unsigned long long)) || hipMemset(h->err, 0, sizeof(int))) {
     cleanup(); return fail(QS_E_HIP, "qs_create: memset");
   }
@@ -243,7 +241,7 @@ extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
   (void)hipSetDevice(h->device);   // teardown: best effort, nothing to report to
-  void* ptrs[] = {h->st, h->env, h->hist, h->ep_return, h->orig, h->log, h->log_count, h->err, h->stamps};
+  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->log_count, h->err, h->stamps};
   for (void* p : ptrs) if (p) (void)hipFree(p);
   delete h;
   return QS_OK;
@@ -262,9 +260,8 @@ int qs_reset(qs_handle* h, uint64_t seed, float* obs, void* stream) {
   const size_t N = d.num_agents, rs = d.precision;
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipMemsetAsync(h->st, 0, rs * QS_AGENT_FIELDS * N, st));
-  HIP_TRY(hipMemsetAsync(h->env, 0, sizeof(int32_t) * QS_ENV_FIELDS * d.num_envs, st));
+  HIP_TRY(hipMemsetAsync(h->env, 0, sizeof(int32_t) * qs::kEnvRec * d.num_envs, st));
   HIP_TRY(hipMemsetAsync(h->hist, 0, sizeof(float) * d.hist_len * N * d.act_dim, st));
-  HIP_TRY(hipMemsetAsync(h->ep_return, 0, sizeof(double) * d.num_envs, st));
   HIP_TRY(hipMemsetAsync(h->log_count, 0, sizeof(unsigned long long), st));
   HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(int), st));
   h->seed = seed;
@@ -310,6 +307,26 @@ int qs_step(qs_handle* h, const float* actions, const qs_step_out* out, void* st
   return launch(h, P, st);
 }
 
+// qs_state_io's view of the per-env records: counters as [QS_ENV_FIELDS][E]
+// int32 (counters = true) or the episode returns as [E] f64.
+__global__ void env_io_kernel(int32_t* rec, void* ext, int E, bool counters, bool to_rec) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  int32_t* r = rec + (size_t)e * qs::kEnvRec;
+  if (counters) {
+    int32_t* x = (int32_t*)ext;
+    for (int f = 0; f < QS_ENV_FIELDS; ++f) {
+      if (to_rec) r[f] = x[(size_t)f * E + e];
+      else x[(size_t)f * E + e] = r[f];
+    }
+  } else {
+    double* x = (double*)ext;
+    double* rr = reinterpret_cast<double*>(r + qs::kEnvRetWord);
+    if (to_rec) *rr = x[e];
+    else x[e] = *rr;
+  }
+}
+
 int qs_state_io(qs_handle* h, int block, void* buf, int dir, void* stream) {
   if (!h || !buf) return fail(QS_E_INVALID, "qs_state_io: null argument");
   hipStream_t st = (hipStream_t)stream;
@@ -318,9 +335,16 @@ int qs_state_io(qs_handle* h, int block, void* buf, int dir, void* stream) {
   size_t bytes = 0;
   switch (block) {
     case QS_STATE_AGENT: src = h->st; bytes = (size_t)d.precision * QS_AGENT_FIELDS * d.num_agents; break;
-    case QS_STATE_ENV: src = h->env; bytes = sizeof(int32_t) * QS_ENV_FIELDS * d.num_envs; break;
+    case QS_STATE_ENV:
+    case QS_STATE_EP_RETURN: {   // the external layouts [4][E] int32 / [E] f64, from the records
+      HIP_TRY(hipSetDevice(h->device));
+      const int E = d.num_envs;
+      env_io_kernel<<<(E + 255) / 256, 256, 0, st>>>(h->env, buf, E, block == QS_STATE_ENV, dir != 0);
+      HIP_TRY(hipGetLastError());
+      if (dir) h->reset_done = true;
+      return QS_OK;
+    }
     case QS_STATE_HISTORY: src = h->hist; bytes = sizeof(float) * d.hist_len * d.num_agents * d.act_dim; break;
-    case QS_STATE_EP_RETURN: src = h->ep_return; bytes = sizeof(double) * d.num_envs; break;
     default: return fail(QS_E_INVALID, "qs_state_io: bad block");
   }
   HIP_TRY(hipSetDevice(h->device));

@@ -37,6 +37,12 @@ namespace qs {
 // per-env reduction, neighbour scan and reset search stays inside one wave and
 // the workgroup barriers below cost nothing (no inter-wave coupling).
 constexpr int kBlock = 64;
+// Per-env record, kEnvRec int32 words: the QS_ENV_FIELDS counters (words 0-3,
+// QS_E_* order), the episode return as f64 (words 4-5), padding.  32 B per env
+// make a wave's envs (D = 8) one 256-B span, loaded and stored whole: written
+// field by field, [field][E] arrays took partial-line writes.
+constexpr int kEnvRec = 8;
+constexpr int kEnvRetWord = 4;
 constexpr uint32_t kMaxResetTries = 1u << 24;
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
 enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
@@ -192,9 +198,8 @@ template <class T> struct Params {
   T sp_R, sp_OMEGA, sp_VZ, sp_cx, sp_cy, sp_cz;
   // device buffers
   T* st;                  // [QS_AGENT_FIELDS][N]
-  int32_t* env;           // [QS_ENV_FIELDS][E]
+  int32_t* env;           // [E][kEnvRec] per-env records (see kEnvRec)
   float* hist;            // [H][N][A]
-  double* ep_return;      // [E]
   const T* orig_xyz;      // [D][3]
   qs_episode_rec* log;    // [log_cap]
   unsigned long long* log_count;
@@ -335,6 +340,7 @@ template <class T> struct Shared {
   int win_group;
   int any;
   uint32_t ep_bcast;
+  int32_t rec[kBlock * kEnvRec];   // per-env records on their way out
 };
 
 // Reset search (MultiHoverAviary.reset rejection loop, MH:83-102), group g
@@ -568,11 +574,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   SA.voff = valid ? SA.voff : kOOB;
   const unsigned E = (unsigned)P.E;
   // env counters first: the synthetic action draw needs only `total`
-  const __amdgpu_buffer_rsrc_t env_r = rsrc(P.env, (unsigned)QS_ENV_FIELDS * E * 4u);
-  const unsigned ev = valid ? (unsigned)e * 4u : kOOB;
-  auto ld_env = [&](int f) { return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(env_r, (int)ev, (int)(f * E * 4u), 0); };
-  int32_t step_counter = ld_env(QS_E_STEP_COUNTER), episode = ld_env(QS_E_EPISODE);
-  int32_t total = ld_env(QS_E_TOTAL_STEPS), ep_len = ld_env(QS_E_EP_LEN);
+  typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
+  static_assert(QS_E_STEP_COUNTER == 0 && QS_E_EPISODE == 1 && QS_E_TOTAL_STEPS == 2 && QS_E_EP_LEN == 3, "record");
+  const __amdgpu_buffer_rsrc_t env_r = rsrc(P.env, (unsigned)kEnvRec * E * 4u);
+  const unsigned ev = valid ? (unsigned)e * kEnvRec * 4u : kOOB;
+  const v2u_t c01 = __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, 0, 0);
+  const v2u_t c23 = __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, 8, 0);
+  int32_t step_counter = (int32_t)c01.x, episode = (int32_t)c01.y;
+  int32_t total = (int32_t)c23.x, ep_len = (int32_t)c23.y;
+  const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvRetWord * 4, 0));
   issue_fence();
   T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
 #pragma unroll
@@ -605,8 +615,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
     for (int k = 0; k < A; ++k) act_in[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)v, k * 4, 0));
   }
-  const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-      rsrc(P.ep_return, E * 8u), valid ? (int)((unsigned)e * 8u) : (int)kOOB, 0, 0));
   const uint8_t mask_v = __builtin_amdgcn_raw_buffer_load_b8(
       rsrc(P.reset_mask, P.reset_mask ? E : 0u), valid ? e : (int)kOOB, 0, 0);
   const bool masked = P.reset_mask == nullptr || mask_v != 0;
@@ -673,6 +681,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     for (int i = 0; i < 4; ++i) SA.st(QS_F_LAST_RPM + i, lrpm[i]);
   };
   T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
+  double ep_ret_out = ep_ret0;   // VecRecordEpisodeStatistics accumulators after this call
+  int32_t ep_len_out = ep_len;
   bool done_env = false;
   int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
 
@@ -1033,8 +1043,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       ret = ep_ret0 + (double)r;
       len = ep_len + 1;
       dn = te || tr;
-      P.ep_return[e] = dn ? 0.0 : ret;
-      P.env[QS_E_EP_LEN * P.E + e] = dn ? 0 : len;
+      ep_ret_out = dn ? 0.0 : ret;
+      ep_len_out = dn ? 0 : len;
       s.done[lenv] = dn;
     }
     // Episode log (VecRecordEpisodeStatistics, record_episode_statistics.py:155-166).
@@ -1231,6 +1241,21 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     }
   }
   QS_STAMP(6);
+  // ---------------- per-env records: staged in LDS, stored as one span
+  if (valid && d == 0) {
+    int32_t* r = &s.rec[lenv * kEnvRec];
+    const unsigned long long rb = __builtin_bit_cast(unsigned long long, ep_ret_out);
+    r[QS_E_STEP_COUNTER] = step_counter; r[QS_E_EPISODE] = episode; r[QS_E_TOTAL_STEPS] = total;
+    r[QS_E_EP_LEN] = ep_len_out;
+    r[kEnvRetWord] = (int32_t)(unsigned)rb; r[kEnvRetWord + 1] = (int32_t)(unsigned)(rb >> 32);
+    r[6] = 0; r[7] = 0;
+  }
+  __syncthreads();
+  {
+    const int nrec = min(P.EPB, P.E - (int)blockIdx.x * P.EPB) * kEnvRec;
+    int32_t* const g = P.env + (size_t)blockIdx.x * P.EPB * kEnvRec;
+    for (int i = tid; i < nrec; i += kBlock) __builtin_nontemporal_store(s.rec[i], g + i);
+  }
   if (!valid) return;
 
   // ---------------- store state of the envs that (auto-)reset
@@ -1240,11 +1265,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) SA.st(QS_F_TARGET + i, tgt[i]);
     }
-  }
-  if (d == 0) {
-    P.env[QS_E_STEP_COUNTER * P.E + e] = step_counter;
-    P.env[QS_E_EPISODE * P.E + e] = episode;
-    P.env[QS_E_TOTAL_STEPS * P.E + e] = total;
   }
 }
 
