@@ -9,6 +9,9 @@
  *   MAPPOAgent.update optimizer steps (mappo/agent.py:731-734,  qs_adam_gated +
  *     757-760): torch.optim.Adam.step, actor step skipped         qs_adam_commit
  *     unless approx_kl <= 1.5*target_kl (host .item() sync)
+ *   compute_policy_loss / compute_value_loss forward and their   qs_ppo_heads
+ *     autograd backward down to the actor mean and critic value
+ *     (mappo/agent.py:602-683): ~60 small torch kernels
  *
  * All pointers are device pointers; every call is asynchronous on `stream`
  * (hipStream_t as void*) and contains no host synchronisation, so it can be
@@ -45,6 +48,24 @@ int qs_adam_gated(int64_t n, float* params, const float* grads, float* exp_avg, 
                   const float* step, float lr, float beta1, float beta2, float eps, const float* gate_val,
                   float gate_thr, void* stream);
 int qs_adam_commit(float* step, const float* gate_val, float gate_thr, void* stream);
+
+/* The PPO loss heads of one minibatch (agent.py:602-683), forward and backward.
+ * The minibatch is mb env-timesteps idx[mb] (int64) of the rollout buffer, all
+ * D agents each: row r = i·D + d.
+ *   mean[mb·D][A]   actor MLP output (before action_scale)
+ *   logstd[A]       actor log standard deviation
+ *   act[·][D][A], logp_old[·][D]  rollout actions and their log-probs (float)
+ *   adv[·], ret[·]  per env-timestep advantages / returns (double)
+ *   v[mb]           critic output on the gathered global obs
+ * Losses: policy = -mean_r min(ratio·adv, clamp(ratio, 1±clip)·adv),
+ * entropy = -mean_r Σ_a H(Normal), value = 0.5·mean_i (v - mean_d ret)².
+ * Writes dmean = ∂L/∂mean, dlogstd = ∂L/∂logstd, dv = ∂L/∂v for
+ * L = policy + ent_coef·entropy + value; kl_out[0] = approx_kl (float);
+ * acc[4] (double) += {policy, value, entropy, approx_kl}.  A <= 4. */
+int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const float* mean, const float* logstd,
+                 float action_scale, const float* act, const float* logp_old, const double* adv, const double* ret,
+                 const float* v, float clip, float ent_coef, float* dmean, float* dlogstd, float* dv, float* kl_out,
+                 double* acc, void* stream);
 
 const char* qs_learner_last_error(void);
 

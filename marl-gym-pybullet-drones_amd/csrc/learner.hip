@@ -10,6 +10,10 @@
 // reference's KL gate (mappo/agent.py:731-734): the gate is evaluated on the
 // device from approx_kl, so an update iteration needs no host sync and can be
 // replayed from a HIP graph.
+//
+// qs_ppo_heads forms both PPO losses and their gradients with respect to the
+// actor mean, logstd and the critic value in one launch, replacing some sixty
+// small torch kernels per minibatch; the MLP backward stays with autograd.
 
 #include <hip/hip_runtime.h>
 #include <cmath>
@@ -85,6 +89,110 @@ __global__ void adam_kernel(long long n, float* __restrict__ p, const float* __r
 __global__ void adam_commit_kernel(float* step, const float* gate_val, float gate_thr) {
   if (threadIdx.x == 0 && gate_ok(gate_val, gate_thr)) *step = *step + 1.0f;
 }
+
+// ------------------------------------------------------------- PPO loss heads
+// compute_policy_loss (mappo/agent.py:602-640) and compute_value_loss
+// (agent.py:642-683) of one minibatch, forward and backward, in one launch.
+// Row r = i·D + d is agent d of env-timestep idx[i].  The arithmetic follows
+// the autograd graph of the torch expressions: log_prob of Normal in fp32,
+// ratio·adv and clamp(ratio)·adv promoted to f64 (adv is f64), torch.minimum's
+// gradient split in half on ties, clamp's gradient inside [lo, hi] inclusive,
+// f32 divisions formed in f64 and rounded (correctly rounded, like torch's).
+// One workgroup: the batch reductions (losses, approx_kl, d logstd) stay in a
+// fixed order, so a replay gives bit-identical results.
+constexpr int kHeadsBlock = 1024;
+constexpr int kMaxA = 4;
+
+__device__ __forceinline__ double block_sum(double x, double* lds) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) lds[w] = x;
+  __syncthreads();
+  double t = 0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += lds[k];
+  return t;   // valid in thread 0
+}
+
+__global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
+    int mb, int D, int A, const long long* __restrict__ idx, const float* __restrict__ mean,
+    const float* __restrict__ logstd, float scale, const float* __restrict__ act, const float* __restrict__ logp_old,
+    const double* __restrict__ adv, const double* __restrict__ ret, const float* __restrict__ v, float clip,
+    float ent_coef, float* __restrict__ dmean, float* __restrict__ dlogstd, float* __restrict__ dv,
+    float* __restrict__ kl_out, double* __restrict__ acc) {
+  __shared__ double lds[kHeadsBlock / 64];
+  const int R = mb * D;
+  float sd[kMaxA], lsd[kMaxA], var2[kMaxA];
+  for (int a = 0; a < A; ++a) {
+    sd[a] = expf(logstd[a]);          // scale = logstd.exp()
+    lsd[a] = logf(sd[a]);             // Normal.log_prob: scale.log()
+    var2[a] = 2.0f * (sd[a] * sd[a]); // 2 * scale ** 2
+  }
+  const float lc = (float)log(sqrt(2.0 * M_PI));
+  const float lo = 1.0f - clip, hi = 1.0f + clip;
+  const double G = -1.0 / (double)R;  // d(-mean(min(...)))/d min_r
+  double s_pl = 0, s_kl = 0, s_dls[kMaxA] = {0, 0, 0, 0};
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    const int i = r / D, d = r - i * D;
+    const long long g = idx[i];
+    const float* x = act + ((size_t)g * D + d) * A;
+    float t1[kMaxA], logp = 0.0f;
+    for (int a = 0; a < A; ++a) {
+      const float mu = mean[(size_t)r * A + a] * scale;
+      t1[a] = x[a] - mu;
+      const float t4 = (float)((double)(-(t1[a] * t1[a])) / (double)var2[a]);
+      const float lp = (t4 - lsd[a]) - lc;
+      logp = a == 0 ? lp : logp + lp;
+    }
+    const float lpo = logp_old[(size_t)g * D + d];
+    const float ratio = expf(logp - lpo);
+    const double ad = adv[g];
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
+    s_pl += -(s1 < s2 ? s1 : s2);
+    s_kl += (double)(lpo - logp);
+    const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
+    const double g2 = s2 < s1 ? G : (s1 == s2 ? G / 2 : 0.0);
+    float gr = (float)(g1 * ad);
+    if (ratio >= lo && ratio <= hi) gr = gr + (float)(g2 * ad);
+    const float gl = gr * ratio;                    // d/d logp
+    for (int a = 0; a < A; ++a) {
+      const float gt3 = (float)((double)gl / (double)var2[a]);
+      const float gt1 = -gt3 * 2.0f * t1[a];
+      dmean[(size_t)r * A + a] = -gt1 * scale;
+      // d/d logstd_a of log_prob: ((x-mu)²/scale² - 1)·gl
+      s_dls[a] += (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
+    }
+  }
+  // value head: 0.5·mean((v - mean_d ret)²) over the mb env-timesteps
+  double s_vl = 0;
+  for (int i = threadIdx.x; i < mb; i += blockDim.x) {
+    const double rt = ret[idx[i]];
+    double rs = 0;
+    for (int d = 0; d < D; ++d) rs += rt;
+    const double diff = (double)v[i] - rs / (double)D;
+    s_vl += diff * diff;
+    dv[i] = (float)(diff / (double)mb);
+  }
+  const double pl = block_sum(s_pl, lds);
+  const double kl = block_sum(s_kl, lds);
+  const double vl = block_sum(s_vl, lds);
+  double dls[kMaxA];
+  for (int a = 0; a < A; ++a) dls[a] = block_sum(s_dls[a], lds);
+  if (threadIdx.x == 0) {
+    float ent = 0.0f;   // Normal.entropy summed over A: 0.5 + 0.5·log(2π) + log(scale)
+    for (int a = 0; a < A; ++a) ent = a == 0 ? (0.5f + lc) + lsd[a] : ent + ((0.5f + lc) + lsd[a]);
+    // d(ent_coef · -mean(entropy))/d logstd_a = -ent_coef
+    for (int a = 0; a < A; ++a) dlogstd[a] = (float)dls[a] - ent_coef;
+    const float akl = (float)(kl / (double)R);
+    *kl_out = akl;
+    acc[0] += pl / (double)R;
+    acc[1] += 0.5 * (vl / (double)mb);
+    acc[2] += (double)(-ent);
+    acc[3] += (double)akl;
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -121,6 +229,20 @@ int qs_adam_commit(float* step, const float* gate_val, float gate_thr, void* str
   hipLaunchKernelGGL(adam_commit_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, gate_val, gate_thr);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_commit: ") + hipGetErrorString(e));
+}
+
+int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const float* mean, const float* logstd,
+                 float action_scale, const float* act, const float* logp_old, const double* adv, const double* ret,
+                 const float* v, float clip, float ent_coef, float* dmean, float* dlogstd, float* dv, float* kl_out,
+                 double* acc, void* stream) {
+  if (mb <= 0 || D <= 0 || A <= 0 || A > kMaxA || !idx || !mean || !logstd || !act || !logp_old || !adv || !ret || !v ||
+      !dmean || !dlogstd || !dv || !kl_out || !acc)
+    return fail(QS_E_INVALID, "qs_ppo_heads: bad argument");
+  hipLaunchKernelGGL(ppo_heads_kernel, dim3(1), dim3(kHeadsBlock), 0, (hipStream_t)stream, (int)mb, (int)D, (int)A,
+                     (const long long*)idx, mean, logstd, action_scale, act, logp_old, adv, ret, v, clip, ent_coef,
+                     dmean, dlogstd, dv, kl_out, acc);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_ppo_heads: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -796,7 +796,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       const T sq = sizeof(T) == 8 ? T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) : s2;
       quat_to_zaxis_s(q, sq, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
+#ifdef QS_X_NOAUX
+      if (false) {
+#else
       if (P.aux) {
+#endif
         // no contraction here: the four ground-effect torque arms cancel exactly
         // for a level drone only in plain multiply-then-add arithmetic
 #pragma clang fp contract(off)

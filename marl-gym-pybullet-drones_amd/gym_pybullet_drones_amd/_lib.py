@@ -59,7 +59,7 @@ EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq"
 EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
            "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
            # include/qs_learner.h
-           "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_learner_last_error")
+           "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_learner_last_error")
 
 _lib = None
 
@@ -100,6 +100,8 @@ def load():
     f32 = ctypes.c_float
     L.qs_adam_gated.argtypes = [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, f32, vp]
     L.qs_adam_commit.argtypes = [vp, vp, f32, vp]
+    L.qs_ppo_heads.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, f32, vp, vp, vp, vp, vp,
+                               f32, f32, vp, vp, vp, vp, vp, vp]
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):
@@ -111,7 +113,7 @@ def load():
 def check(rc, what=""):
     if rc != QS_OK:
         lib = load()
-        msg = lib.qs_learner_last_error() if what.startswith(("qs_gae", "qs_adam")) else lib.qs_last_error()
+        msg = lib.qs_learner_last_error() if what.startswith(("qs_gae", "qs_adam", "qs_ppo")) else lib.qs_last_error()
         raise QuadSwarmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
 
 

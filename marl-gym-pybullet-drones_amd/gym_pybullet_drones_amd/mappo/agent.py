@@ -240,7 +240,7 @@ class MAPPOAgent:
     def __init__(self, obs_space, act_space, hidden_dim=256, use_clipped_value=False, clip_param=0.2, target_kl=0.01,
                  entropy_coef=0.01, actor_lr=0.0003, critic_lr=0.001, opt_epochs=10, mini_batch_size=64,
                  activation='tanh', share_actor_weights=True, centralized_critic=True, include_actions_in_critic=False,
-                 global_state_dim=None, action_scale=1.0, use_graphs=True, device='cuda', **kwargs):
+                 global_state_dim=None, action_scale=1.0, use_graphs=True, fused_heads=True, device='cuda', **kwargs):
         self.obs_space, self.act_space = obs_space, act_space
         self.use_clipped_value, self.clip_param, self.target_kl = use_clipped_value, clip_param, target_kl
         self.entropy_coef, self.opt_epochs, self.mini_batch_size = entropy_coef, opt_epochs, mini_batch_size
@@ -249,6 +249,7 @@ class MAPPOAgent:
         self.include_actions_in_critic = include_actions_in_critic
         self.action_scale = action_scale
         self.use_graphs = use_graphs
+        self.fused_heads = fused_heads   # qs_ppo_heads (False: the loss heads as plain torch ops)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
                                    share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
@@ -321,6 +322,42 @@ class MAPPOAgent:
         return 0.5 * (v_cur - ret).pow(2).mean()
 
     # ------------------------------------------------------------- update
+    def _fused_heads_ok(self, rollouts):
+        """The fused loss heads cover the configuration of both reference MAPPO
+        scripts: unclipped value loss, critic on the concatenated obs only."""
+        return (self.device.type == 'cuda' and not self.use_clipped_value and not self.include_actions_in_critic
+                and getattr(rollouts, 'include_global_state', False) and self.ac.act_dim <= 4)
+
+    def _iteration_fused(self, rollouts, idx, acc):
+        """One minibatch with the loss heads in one HIP launch (qs_ppo_heads): the
+        same losses and gradients as _iteration; autograd only runs the MLPs."""
+        world = _dist_world()
+        D, O, A = rollouts.num_agents, rollouts.obs_dim, self.ac.act_dim
+        mb = idx.shape[0]
+        obs = rollouts.sample_obs(idx)
+        mean = self.ac.actor.pi_net(obs.reshape(mb * D, O))
+        v = self.ac.critic(obs.reshape(mb, D * O))
+        if getattr(self, '_heads_mb', None) != (mb, D, A):
+            self._dmean = torch.empty(mb * D, A, device=self.device)
+            self._dv = torch.empty(mb, 1, device=self.device)
+            self._heads_mb = (mb, D, A)
+        self._reduce_buf.zero_()
+        logstd = self.ac.actor.logstd
+        lib = L.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.check(lib.qs_ppo_heads(mb, D, A, L.ptr(idx), L.ptr(mean), L.ptr(logstd), float(self.action_scale),
+                                 L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
+                                 L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
+                                 L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
+                                 st), "qs_ppo_heads")
+        torch.autograd.backward([mean, v], [self._dmean, self._dv])
+        if world > 1:
+            tdist.all_reduce(self._reduce_buf)
+            self._reduce_buf.div_(world)
+        gate = self._kl if self.target_kl > 0 else None
+        self.actor_opt.adam(gate, 1.5 * self.target_kl)
+        self.critic_opt.adam(None, 0.0)
+
     def _iteration(self, batch, acc):
         """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.
 
@@ -345,6 +382,12 @@ class MAPPOAgent:
         acc += torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
                             entropy_loss.detach().double(), approx_kl.detach().double()])
 
+    def _step_minibatch(self, rollouts, idx, acc):
+        if self.fused_heads and self._fused_heads_ok(rollouts):
+            self._iteration_fused(rollouts, idx, acc)
+        else:
+            self._iteration(rollouts.sample(idx), acc)
+
     def _capture(self, rollouts):
         """Capture one update iteration as a HIP graph over static index/accumulator tensors."""
         mb = self.mini_batch_size
@@ -360,11 +403,11 @@ class MAPPOAgent:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._iteration(rollouts.sample(self._g_idx), self._g_acc)
+                self._step_minibatch(rollouts, self._g_idx, self._g_acc)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._iteration(rollouts.sample(self._g_idx), self._g_acc)
+            self._step_minibatch(rollouts, self._g_idx, self._g_acc)
         for t, v in zip((self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq, self.actor_opt.step,
                          self.critic_opt.flat, self.critic_opt.exp_avg, self.critic_opt.exp_avg_sq,
                          self.critic_opt.step), snap):
@@ -392,8 +435,7 @@ class MAPPOAgent:
             else:
                 acc = torch.zeros(4, dtype=torch.float64, device=self.device)
                 for i in range(num_mini_batch):
-                    self._iteration(rollouts.sample(perm[i * self.mini_batch_size:(i + 1) * self.mini_batch_size]),
-                                    acc)
+                    self._step_minibatch(rollouts, perm[i * self.mini_batch_size:(i + 1) * self.mini_batch_size], acc)
                 per_epoch.append(acc)
         stats = (torch.stack(per_epoch) / num_mini_batch).cpu()   # one host sync per update
         for j, k in enumerate(['policy_loss', 'value_loss', 'entropy_loss', 'approx_kl']):

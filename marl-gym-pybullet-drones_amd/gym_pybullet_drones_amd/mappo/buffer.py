@@ -185,6 +185,12 @@ class MAPPOBuffer:
             batch['global_obs'] = batch['obs'].reshape(-1, D * self.obs_dim)
         return batch
 
+    def sample_obs(self, indices):
+        """The obs rows of env-timesteps `indices` only, (mb, D, O): what the fused
+        loss heads (qs_ppo_heads) need gathered; they read act/logp/adv/ret by index."""
+        T, E, D = self.max_length, self.batch_size, self.num_agents
+        return self.obs.reshape(T * E, D, self.obs_dim).index_select(0, indices)
+
     def sampler(self, mini_batch_size, device=None, drop_last=True, generator=None):
         """random_sample (BUF:399-425): a permutation of the env-timesteps, in
         mini-batches of whole env-timesteps (all D agents together)."""
