@@ -61,11 +61,15 @@ int qs_adam_commit(float* step, const float* gate_val, float gate_thr, void* str
  * entropy = -mean_r Σ_a H(Normal), value = 0.5·mean_i (v - mean_d ret)².
  * Writes dmean = ∂L/∂mean, dlogstd = ∂L/∂logstd, dv = ∂L/∂v for
  * L = policy + ent_coef·entropy + value; kl_out[0] = approx_kl (float);
- * acc[4] (double) += {policy, value, entropy, approx_kl}.  A <= 4. */
+ * acc[4] (double) += {policy, value, entropy, approx_kl}.  A <= 4.
+ * work: device scratch of qs_ppo_heads_work_bytes(mb, D) bytes, zeroed once
+ * before the first call (the kernel leaves it ready for the next one); one
+ * call at a time per workspace. */
 int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const float* mean, const float* logstd,
                  float action_scale, const float* act, const float* logp_old, const double* adv, const double* ret,
                  const float* v, float clip, float ent_coef, float* dmean, float* dlogstd, float* dv, float* kl_out,
-                 double* acc, void* stream);
+                 double* acc, void* work, void* stream);
+int64_t qs_ppo_heads_work_bytes(int32_t mb, int32_t D);
 
 const char* qs_learner_last_error(void);
 

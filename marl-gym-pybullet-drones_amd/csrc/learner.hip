@@ -12,10 +12,12 @@
 // replayed from a HIP graph.
 //
 // qs_ppo_heads forms both PPO losses and their gradients with respect to the
-// actor mean, logstd and the critic value in one launch, replacing some sixty
-// small torch kernels per minibatch; the MLP backward stays with autograd.
+// actor mean, logstd and the critic value in one launch (one thread per agent
+// row), replacing some sixty small torch kernels per minibatch; the MLP
+// backward stays with autograd.
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -98,10 +100,12 @@ __global__ void adam_commit_kernel(float* step, const float* gate_val, float gat
 // ratio·adv and clamp(ratio)·adv promoted to f64 (adv is f64), torch.minimum's
 // gradient split in half on ties, clamp's gradient inside [lo, hi] inclusive,
 // f32 divisions formed in f64 and rounded (correctly rounded, like torch's).
-// One workgroup: the batch reductions (losses, approx_kl, d logstd) stay in a
-// fixed order, so a replay gives bit-identical results.
-constexpr int kHeadsBlock = 1024;
+// One thread per row; each workgroup reduces its rows, writes its partial
+// sums to the workspace, and the last workgroup to finish adds the partials in
+// workgroup order — a fixed order, so a replay gives bit-identical results.
+constexpr int kHeadsBlock = 256;
 constexpr int kMaxA = 4;
+constexpr int kHeadsSums = 3 + kMaxA;   // policy, approx_kl, value, d logstd[A]
 
 __device__ __forceinline__ double block_sum(double x, double* lds) {
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
@@ -120,8 +124,9 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     const float* __restrict__ logstd, float scale, const float* __restrict__ act, const float* __restrict__ logp_old,
     const double* __restrict__ adv, const double* __restrict__ ret, const float* __restrict__ v, float clip,
     float ent_coef, float* __restrict__ dmean, float* __restrict__ dlogstd, float* __restrict__ dv,
-    float* __restrict__ kl_out, double* __restrict__ acc) {
+    float* __restrict__ kl_out, double* __restrict__ acc, double* __restrict__ partial, unsigned* __restrict__ count) {
   __shared__ double lds[kHeadsBlock / 64];
+  __shared__ bool last;
   const int R = mb * D;
   float sd[kMaxA], lsd[kMaxA], var2[kMaxA];
   for (int a = 0; a < A; ++a) {
@@ -132,8 +137,9 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
   const float lc = (float)log(sqrt(2.0 * M_PI));
   const float lo = 1.0f - clip, hi = 1.0f + clip;
   const double G = -1.0 / (double)R;  // d(-mean(min(...)))/d min_r
-  double s_pl = 0, s_kl = 0, s_dls[kMaxA] = {0, 0, 0, 0};
-  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+  double sums[kHeadsSums] = {0, 0, 0, 0, 0, 0, 0};
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) {
     const int i = r / D, d = r - i * D;
     const long long g = idx[i];
     const float* x = act + ((size_t)g * D + d) * A;
@@ -150,8 +156,8 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     const double ad = adv[g];
     const float rc = fminf(fmaxf(ratio, lo), hi);
     const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
-    s_pl += -(s1 < s2 ? s1 : s2);
-    s_kl += (double)(lpo - logp);
+    sums[0] = -(s1 < s2 ? s1 : s2);
+    sums[1] = (double)(lpo - logp);
     const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
     const double g2 = s2 < s1 ? G : (s1 == s2 ? G / 2 : 0.0);
     float gr = (float)(g1 * ad);
@@ -162,36 +168,44 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
       const float gt1 = -gt3 * 2.0f * t1[a];
       dmean[(size_t)r * A + a] = -gt1 * scale;
       // d/d logstd_a of log_prob: ((x-mu)²/scale² - 1)·gl
-      s_dls[a] += (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
+      sums[3 + a] = (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
     }
   }
   // value head: 0.5·mean((v - mean_d ret)²) over the mb env-timesteps
-  double s_vl = 0;
-  for (int i = threadIdx.x; i < mb; i += blockDim.x) {
-    const double rt = ret[idx[i]];
+  if (r < mb) {
+    const double rt = ret[idx[r]];
     double rs = 0;
     for (int d = 0; d < D; ++d) rs += rt;
-    const double diff = (double)v[i] - rs / (double)D;
-    s_vl += diff * diff;
-    dv[i] = (float)(diff / (double)mb);
+    const double diff = (double)v[r] - rs / (double)D;
+    sums[2] = diff * diff;
+    dv[r] = (float)(diff / (double)mb);
   }
-  const double pl = block_sum(s_pl, lds);
-  const double kl = block_sum(s_kl, lds);
-  const double vl = block_sum(s_vl, lds);
-  double dls[kMaxA];
-  for (int a = 0; a < A; ++a) dls[a] = block_sum(s_dls[a], lds);
+  for (int k = 0; k < 3 + A; ++k) {
+    const double t = block_sum(sums[k], lds);
+    if (threadIdx.x == 0) partial[(size_t)blockIdx.x * kHeadsSums + k] = t;
+  }
   if (threadIdx.x == 0) {
-    float ent = 0.0f;   // Normal.entropy summed over A: 0.5 + 0.5·log(2π) + log(scale)
-    for (int a = 0; a < A; ++a) ent = a == 0 ? (0.5f + lc) + lsd[a] : ent + ((0.5f + lc) + lsd[a]);
-    // d(ent_coef · -mean(entropy))/d logstd_a = -ent_coef
-    for (int a = 0; a < A; ++a) dlogstd[a] = (float)dls[a] - ent_coef;
-    const float akl = (float)(kl / (double)R);
-    *kl_out = akl;
-    acc[0] += pl / (double)R;
-    acc[1] += 0.5 * (vl / (double)mb);
-    acc[2] += (double)(-ent);
-    acc[3] += (double)akl;
+    __threadfence();
+    last = atomicAdd(count, 1u) == gridDim.x - 1;
   }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  double tot[kHeadsSums] = {0, 0, 0, 0, 0, 0, 0};
+  for (unsigned b = 0; b < gridDim.x; ++b)
+    for (int k = 0; k < 3 + A; ++k) tot[k] += __hip_atomic_load(&partial[(size_t)b * kHeadsSums + k], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+  *count = 0;   // ready for the next launch (graph replay)
+  float ent = 0.0f;   // Normal.entropy summed over A: 0.5 + 0.5·log(2π) + log(scale)
+  for (int a = 0; a < A; ++a) ent = a == 0 ? (0.5f + lc) + lsd[a] : ent + ((0.5f + lc) + lsd[a]);
+  // d(ent_coef · -mean(entropy))/d logstd_a = -ent_coef
+  for (int a = 0; a < A; ++a) dlogstd[a] = (float)tot[3 + a] - ent_coef;
+  const float akl = (float)(tot[1] / (double)R);
+  *kl_out = akl;
+  acc[0] += tot[0] / (double)R;
+  acc[1] += 0.5 * (tot[2] / (double)mb);
+  acc[2] += (double)(-ent);
+  acc[3] += (double)akl;
 }
 }  // namespace
 
@@ -231,16 +245,26 @@ int qs_adam_commit(float* step, const float* gate_val, float gate_thr, void* str
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_commit: ") + hipGetErrorString(e));
 }
 
+int64_t qs_ppo_heads_work_bytes(int32_t mb, int32_t D) {
+  const int64_t rows = (int64_t)mb * D;
+  const int64_t blocks = (std::max<int64_t>(rows, mb) + kHeadsBlock - 1) / kHeadsBlock;
+  return 64 + blocks * kHeadsSums * (int64_t)sizeof(double);
+}
+
 int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const float* mean, const float* logstd,
                  float action_scale, const float* act, const float* logp_old, const double* adv, const double* ret,
                  const float* v, float clip, float ent_coef, float* dmean, float* dlogstd, float* dv, float* kl_out,
-                 double* acc, void* stream) {
+                 double* acc, void* work, void* stream) {
   if (mb <= 0 || D <= 0 || A <= 0 || A > kMaxA || !idx || !mean || !logstd || !act || !logp_old || !adv || !ret || !v ||
-      !dmean || !dlogstd || !dv || !kl_out || !acc)
+      !dmean || !dlogstd || !dv || !kl_out || !acc || !work)
     return fail(QS_E_INVALID, "qs_ppo_heads: bad argument");
-  hipLaunchKernelGGL(ppo_heads_kernel, dim3(1), dim3(kHeadsBlock), 0, (hipStream_t)stream, (int)mb, (int)D, (int)A,
+  const long long rows = (long long)mb * D;
+  const unsigned blocks = (unsigned)((std::max<long long>(rows, mb) + kHeadsBlock - 1) / kHeadsBlock);
+  unsigned* count = (unsigned*)work;
+  double* partial = (double*)((char*)work + 64);
+  hipLaunchKernelGGL(ppo_heads_kernel, dim3(blocks), dim3(kHeadsBlock), 0, (hipStream_t)stream, (int)mb, (int)D, (int)A,
                      (const long long*)idx, mean, logstd, action_scale, act, logp_old, adv, ret, v, clip, ent_coef,
-                     dmean, dlogstd, dv, kl_out, acc);
+                     dmean, dlogstd, dv, kl_out, acc, partial, count);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_ppo_heads: ") + hipGetErrorString(e));
 }

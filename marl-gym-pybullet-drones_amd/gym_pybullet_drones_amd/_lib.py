@@ -59,7 +59,8 @@ EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq"
 EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
            "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
            # include/qs_learner.h
-           "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_learner_last_error")
+           "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_ppo_heads_work_bytes",
+           "qs_learner_last_error")
 
 _lib = None
 
@@ -101,11 +102,13 @@ def load():
     L.qs_adam_gated.argtypes = [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, f32, vp]
     L.qs_adam_commit.argtypes = [vp, vp, f32, vp]
     L.qs_ppo_heads.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, f32, vp, vp, vp, vp, vp,
-                               f32, f32, vp, vp, vp, vp, vp, vp]
+                               f32, f32, vp, vp, vp, vp, vp, vp, vp]
+    L.qs_ppo_heads_work_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):
             getattr(L, name).restype = i32
+    L.qs_ppo_heads_work_bytes.restype = i64
     _lib = L
     return L
 

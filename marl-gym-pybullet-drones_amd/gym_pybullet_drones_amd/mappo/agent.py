@@ -337,19 +337,21 @@ class MAPPOAgent:
         obs = rollouts.sample_obs(idx)
         mean = self.ac.actor.pi_net(obs.reshape(mb * D, O))
         v = self.ac.critic(obs.reshape(mb, D * O))
+        lib = L.load()
         if getattr(self, '_heads_mb', None) != (mb, D, A):
             self._dmean = torch.empty(mb * D, A, device=self.device)
             self._dv = torch.empty(mb, 1, device=self.device)
+            self._heads_work = torch.zeros(int(lib.qs_ppo_heads_work_bytes(mb, D)), dtype=torch.uint8,
+                                           device=self.device)
             self._heads_mb = (mb, D, A)
         self._reduce_buf.zero_()
         logstd = self.ac.actor.logstd
-        lib = L.load()
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         L.check(lib.qs_ppo_heads(mb, D, A, L.ptr(idx), L.ptr(mean), L.ptr(logstd), float(self.action_scale),
                                  L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
                                  L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
-                                 st), "qs_ppo_heads")
+                                 L.ptr(self._heads_work), st), "qs_ppo_heads")
         torch.autograd.backward([mean, v], [self._dmean, self._dv])
         if world > 1:
             tdist.all_reduce(self._reduce_buf)
