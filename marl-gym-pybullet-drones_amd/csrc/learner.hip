@@ -119,8 +119,11 @@ __device__ __forceinline__ double block_sum(double x, double* lds) {
   return t;   // valid in thread 0
 }
 
+// A (actions per agent) is a template value: the per-action arrays stay in
+// registers (a run-time A put them in scratch memory and cost ~70 µs a launch).
+template <int A>
 __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
-    int mb, int D, int A, const long long* __restrict__ idx, const float* __restrict__ mean,
+    int mb, int D, const long long* __restrict__ idx, const float* __restrict__ mean,
     const float* __restrict__ logstd, float scale, const float* __restrict__ act, const float* __restrict__ logp_old,
     const double* __restrict__ adv, const double* __restrict__ ret, const float* __restrict__ v, float clip,
     float ent_coef, float* __restrict__ dmean, float* __restrict__ dlogstd, float* __restrict__ dv,
@@ -128,7 +131,8 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
   __shared__ double lds[kHeadsBlock / 64];
   __shared__ bool last;
   const int R = mb * D;
-  float sd[kMaxA], lsd[kMaxA], var2[kMaxA];
+  float sd[A], lsd[A], var2[A];
+#pragma unroll
   for (int a = 0; a < A; ++a) {
     sd[a] = expf(logstd[a]);          // scale = logstd.exp()
     lsd[a] = logf(sd[a]);             // Normal.log_prob: scale.log()
@@ -143,7 +147,8 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     const int i = r / D, d = r - i * D;
     const long long g = idx[i];
     const float* x = act + ((size_t)g * D + d) * A;
-    float t1[kMaxA], logp = 0.0f;
+    float t1[A], logp = 0.0f;
+#pragma unroll
     for (int a = 0; a < A; ++a) {
       const float mu = mean[(size_t)r * A + a] * scale;
       t1[a] = x[a] - mu;
@@ -163,6 +168,7 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     float gr = (float)(g1 * ad);
     if (ratio >= lo && ratio <= hi) gr = gr + (float)(g2 * ad);
     const float gl = gr * ratio;                    // d/d logp
+#pragma unroll
     for (int a = 0; a < A; ++a) {
       const float gt3 = (float)((double)gl / (double)var2[a]);
       const float gt1 = -gt3 * 2.0f * t1[a];
@@ -180,6 +186,7 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     sums[2] = diff * diff;
     dv[r] = (float)(diff / (double)mb);
   }
+#pragma unroll
   for (int k = 0; k < 3 + A; ++k) {
     const double t = block_sum(sums[k], lds);
     if (threadIdx.x == 0) partial[(size_t)blockIdx.x * kHeadsSums + k] = t;
@@ -189,16 +196,24 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     last = atomicAdd(count, 1u) == gridDim.x - 1;
   }
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __threadfence();
-  double tot[kHeadsSums] = {0, 0, 0, 0, 0, 0, 0};
-  for (unsigned b = 0; b < gridDim.x; ++b)
-    for (int k = 0; k < 3 + A; ++k) tot[k] += __hip_atomic_load(&partial[(size_t)b * kHeadsSums + k], __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT);
+  if (!last) return;
+  // the last workgroup: every thread sums a fixed strided subset of the
+  // partials in workgroup order, then the same fixed-order block reduction
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double tot[kHeadsSums];
+#pragma unroll
+  for (int k = 0; k < 3 + A; ++k) {
+    double t = 0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) t += partial[(size_t)b * kHeadsSums + k];
+    tot[k] = block_sum(t, lds);
+  }
+  if (threadIdx.x != 0) return;
   *count = 0;   // ready for the next launch (graph replay)
   float ent = 0.0f;   // Normal.entropy summed over A: 0.5 + 0.5·log(2π) + log(scale)
+#pragma unroll
   for (int a = 0; a < A; ++a) ent = a == 0 ? (0.5f + lc) + lsd[a] : ent + ((0.5f + lc) + lsd[a]);
   // d(ent_coef · -mean(entropy))/d logstd_a = -ent_coef
+#pragma unroll
   for (int a = 0; a < A; ++a) dlogstd[a] = (float)tot[3 + a] - ent_coef;
   const float akl = (float)(tot[1] / (double)R);
   *kl_out = akl;
@@ -262,9 +277,17 @@ int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const flo
   const unsigned blocks = (unsigned)((std::max<long long>(rows, mb) + kHeadsBlock - 1) / kHeadsBlock);
   unsigned* count = (unsigned*)work;
   double* partial = (double*)((char*)work + 64);
-  hipLaunchKernelGGL(ppo_heads_kernel, dim3(blocks), dim3(kHeadsBlock), 0, (hipStream_t)stream, (int)mb, (int)D, (int)A,
-                     (const long long*)idx, mean, logstd, action_scale, act, logp_old, adv, ret, v, clip, ent_coef,
-                     dmean, dlogstd, dv, kl_out, acc, partial, count);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(kHeadsBlock), 0, (hipStream_t)stream, (int)mb, (int)D,
+                       (const long long*)idx, mean, logstd, action_scale, act, logp_old, adv, ret, v, clip, ent_coef,
+                       dmean, dlogstd, dv, kl_out, acc, partial, count);
+  };
+  switch (A) {
+    case 1: go(ppo_heads_kernel<1>); break;
+    case 2: go(ppo_heads_kernel<2>); break;
+    case 3: go(ppo_heads_kernel<3>); break;
+    default: go(ppo_heads_kernel<4>); break;
+  }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_ppo_heads: ") + hipGetErrorString(e));
 }
