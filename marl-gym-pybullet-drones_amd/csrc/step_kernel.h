@@ -559,6 +559,13 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   SA.fstride = (unsigned)N * (unsigned)sizeof(T);
   SA.voff = (unsigned)a * (unsigned)sizeof(T);
   QS_STAMP(0);
+#ifdef QS_STAGGER
+  // dev experiment: the second half of the grid (the second wave on each SIMD)
+  // starts its loads later, so its memory phase overlaps the first half's VALU phase
+  if (blockIdx.x >= gridDim.x / 2) {
+    for (int i = 0; i < QS_STAGGER; i += 8) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
 
   // ---------------- loads
   // Every global read of the launch is issued here, unconditionally and
