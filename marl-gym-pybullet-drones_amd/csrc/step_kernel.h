@@ -265,6 +265,9 @@ template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T r
 template <class T>
 __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T pos[3], const T q[4], const T vel[3],
                                         const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
+#if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOPID)
+  return;
+#endif
   using F = M<T>;
   const T dt = ctrl_dt;
   T R[9];
@@ -535,7 +538,10 @@ template <class T> __device__ T marl_reward(int task, const T (*p)[3], const T (
 // 30 Hz, Spiral 48 Hz): the substep count, history length and obs width are
 // then constants (fully unrolled substeps, constant obs offsets); CF = 0 reads
 // them from P.
-template <class T, int TASK, int ACT, int CF, int PHYS>
+// AUX = false compiles out the ground-effect / drag / downwash forces (the
+// common P.aux == 0 case): a run-time force branch inside the unrolled substeps
+// cost 0.65 µs of the 10.5 µs C3 launch.
+template <class T, int TASK, int ACT, int CF, int PHYS, bool AUX>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   using F = M<T>;
   constexpr int A = Act<ACT>::A;
@@ -547,7 +553,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const int tid = threadIdx.x;
   const int D = P.D, N = P.N;
   const int H = CF ? CF / 2 : P.H;
+#if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOSUB)
+  const int S = 0;   // dev probe: memory traffic of the launch without the substeps and PID
+#else
   const int S = CF ? 240 / CF : P.S;
+#endif
   const int O = CF ? 12 + (CF / 2) * A + (kSpiral ? 11 : 0) : P.O;
   const int lenv = tid / D, d = tid - lenv * D;
   const int e = blockIdx.x * P.EPB + lenv;
@@ -562,7 +572,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #ifdef QS_STAGGER
   // dev experiment: the second half of the grid (the second wave on each SIMD)
   // starts its loads later, so its memory phase overlaps the first half's VALU phase
-  if (blockIdx.x >= gridDim.x / 2) {
+#ifndef QS_STAGGER_MODE
+#define QS_STAGGER_MODE 0
+#endif
+  bool late;
+  if constexpr (QS_STAGGER_MODE == 0) late = blockIdx.x >= gridDim.x / 2;
+  else if constexpr (QS_STAGGER_MODE == 1) late = __builtin_amdgcn_s_getreg((3 << 11) | 4) & 1;   // HW_ID wave slot
+  else if constexpr (QS_STAGGER_MODE == 2) late = (blockIdx.x >> 5) & 1;
+  else late = blockIdx.x & 1;
+  if (late) {
     for (int i = 0; i < QS_STAGGER; i += 8) __builtin_amdgcn_s_sleep(8);
   }
 #endif
@@ -602,7 +620,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   for (int i = 0; i < 4; ++i) q[i] = SA.ld(QS_F_QUAT + i);
   {   // last rpm: read only by the drag model (zero offset range otherwise: no traffic)
     SoA<T> LR = SA;
-    LR.voff = (P.aux & QS_AUX_DRAG) ? SA.voff : kOOB;
+    LR.voff = (AUX && (P.aux & QS_AUX_DRAG)) ? SA.voff : kOOB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) lrpm[i] = LR.ld(QS_F_LAST_RPM + i);
   }
@@ -725,6 +743,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         T r = T(cf2x::HOVER_RPM) * (T(1) + T(0.05) * T(act[0]));
         rpm[0] = rpm[1] = rpm[2] = rpm[3] = r;
       } else {
+#if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOPID)
+        if (false)
+#endif
         quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
         if constexpr (ACT == QS_ACT_ONE_D_PID) {
           T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
@@ -784,6 +805,118 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const T s2 = T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     T R[9];   // PYB: rotation of the current pose, carried across substeps
     if constexpr (PHYS == QS_PHYS_PYB) quat_to_rot(q, R);
+    // fp32 without extra forces at pyb_freq 240 (the hot configurations): the
+    // substep is restated algebraically with every per-control-step constant
+    // hoisted — the thrust, gravity and torque terms premultiplied by dt/M and
+    // dt/J, the body z axis from q directly (s = 2/|q|² once per step), the
+    // gyroscopic term reduced with IXX == IYY, and the PYB world-frame exp map
+    // applied as the equivalent right product q ⊗ exp(ω_body dt/2) (R(q)ω = q ω q*).
+    // Same mathematics as the general path below; fp32 rounding only.
+    constexpr bool kFastSub = sizeof(T) == 4 && !AUX && CF != 0;
+    if constexpr (kFastSub) {
+#pragma clang fp contract(fast)
+      constexpr double kDt = 1.0 / 240.0;   // CF != 0 ⇒ pyb_freq == 240 (step_launch_impl.h)
+      constexpr double IXX = cf2x::IXX, IYY = cf2x::IYY, IZZ = cf2x::IZZ;
+      static_assert(cf2x::IXX == cf2x::IYY, "gyroscopic reduction assumes IXX == IYY (cf2x.urdf:11-12)");
+      constexpr float kx = float(kDt * (IZZ - IYY) / IXX), ky = float(kDt * (IXX - IZZ) / IYY);
+      constexpr float kHdt = float(kDt / 2), kHdt2 = float(kDt / 2 * (kDt / 2));
+      const float dtm = float(kDt / cf2x::M);
+      // exp-map coefficients: c = cos θ, k = sin θ / |ω|, θ = |ω| dt / 2
+      auto expmap = [&](float wn2, float& c, float& k) {
+        const float u = wn2 * kHdt2;
+        if (u < 0.0625f) {
+          k = __builtin_fmaf(u, __builtin_fmaf(u, __builtin_fmaf(u, float(kDt / 2 * (-1.0 / 5040)), float(kDt / 2 / 120)),
+                                               float(kDt / 2 * (-1.0 / 6))), kHdt);
+          c = __builtin_fmaf(u, __builtin_fmaf(u, __builtin_fmaf(u, __builtin_fmaf(u, float(1.0 / 40320), float(-1.0 / 720)),
+                                                                 float(1.0 / 24)), -0.5f), 1.0f);
+        } else {
+          const float wn = sqrtf(wn2), th = wn * kHdt;
+          c = cosf(th);
+          k = sinf(th) / wn;
+        }
+      };
+      if constexpr (PHYS == QS_PHYS_PYB) {
+        const float kd = float(kDt * kPybDamping);
+        const float g1 = thrust_z * dtm, g2 = 2.0f * g1, c8 = g1 - float(cf2x::GRAVITY * kDt / cf2x::M);
+        const float bx = float(kDt / IXX) * pbx, by = float(kDt / IYY) * pby, bz = float(kDt / IZZ) * tz;
+        constexpr float amax2 = float((0.25 * M_PI / kDt) * (0.25 * M_PI / kDt));
+#pragma unroll
+        for (int sub = 0; sub < S; ++sub) {
+          const float x = q[0], y = q[1], z = q[2], qw = q[3];
+          const float m = __builtin_fmaf(-kd, sqrtf(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]), 1.0f - kd);
+          const float mw = __builtin_fmaf(-kd, sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]), 1.0f - kd);
+          vel[0] = vel[0] * m + g2 * (x * z + qw * y);
+          vel[1] = vel[1] * m + g2 * (y * z - qw * x);
+          vel[2] = vel[2] * m + (c8 - g2 * (x * x + y * y));
+          const float w0 = w[0], w1 = w[1], w2 = w[2];
+          w[0] = w0 * mw + (bx - kx * (w1 * w2));
+          w[1] = w1 * mw + (by - ky * (w2 * w0));
+          w[2] = w2 * mw + bz;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) pos[i] = pos[i] + float(kDt) * vel[i];
+          float ang2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+          ang2 = ang2 > amax2 ? amax2 : ang2;
+          float c, kk;
+          expmap(ang2, c, kk);
+          const float e0 = w[0] * kk, e1 = w[1] * kk, e2 = w[2] * kk;
+          const float n0 = c * x + qw * e0 + (y * e2 - z * e1);
+          const float n1 = c * y + qw * e1 + (z * e0 - x * e2);
+          const float n2 = c * z + qw * e2 + (x * e1 - y * e0);
+          const float n3 = c * qw - (x * e0 + y * e1 + z * e2);
+          const float rn = __builtin_amdgcn_rsqf(n0 * n0 + n1 * n1 + n2 * n2 + n3 * n3);
+          q[0] = n0 * rn; q[1] = n1 * rn; q[2] = n2 * rn; q[3] = n3 * rn;
+          if (pos[2] < float(kCylHalfLen + kCylR)) {   // ground plane vs the collision cylinder
+            const float r8 = 1.0f - 2.0f * (q[0] * q[0] + q[1] * q[1]);
+            const float sz2 = 1.0f - r8 * r8;
+            const float zmin = pos[2] - (float(kCylHalfLen) * fabsf(r8) + float(kCylR) * sqrtf(sz2 > 0.f ? sz2 : 0.f));
+            if (zmin < 0.f) {
+              pos[2] = pos[2] - zmin;
+              if (vel[2] < 0.f) vel[2] = 0.f;
+            }
+          }
+        }
+        T Rn[9];   // getBaseVelocity: world angular velocity at the new pose
+        quat_to_rot(q, Rn);
+        angv[0] = Rn[0] * w[0] + Rn[1] * w[1] + Rn[2] * w[2];
+        angv[1] = Rn[3] * w[0] + Rn[4] * w[1] + Rn[5] * w[2];
+        angv[2] = Rn[6] * w[0] + Rn[7] * w[1] + Rn[8] * w[2];
+      } else {
+        const float gk = thrust_z * s2 * dtm, c8 = (thrust_z - float(cf2x::GRAVITY)) * dtm;
+        const float ax = float(kDt / IXX) * tx, ay = float(kDt / IYY) * ty, az = float(kDt / IZZ) * tz;
+#pragma unroll
+        for (int sub = 0; sub < S; ++sub) {
+          const float x = q[0], y = q[1], z = q[2], qw = q[3];
+          vel[0] = vel[0] + gk * (x * z + qw * y);
+          vel[1] = vel[1] + gk * (y * z - qw * x);
+          vel[2] = (vel[2] + c8) - gk * (x * x + y * y);
+          const float w0 = w[0], w1 = w[1], w2 = w[2];
+          w[0] = (w0 + ax) - kx * (w1 * w2);
+          w[1] = (w1 + ay) - ky * (w2 * w0);
+          w[2] = w2 + az;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) pos[i] = pos[i] + float(kDt) * vel[i];
+          if (sub == S - 1) {   // world angular velocity R_old·ω (BaseAviary.py:871-875)
+            T Ro[9];
+            quat_to_rot(q, Ro);
+            angv[0] = Ro[0] * w[0] + Ro[1] * w[1] + Ro[2] * w[2];
+            angv[1] = Ro[3] * w[0] + Ro[4] * w[1] + Ro[5] * w[2];
+            angv[2] = Ro[6] * w[0] + Ro[7] * w[1] + Ro[8] * w[2];
+          }
+          const float wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+          if (wn2 > 1e-16f) {   // _integrateQ (BaseAviary.py:879-892)
+            float c, k;
+            expmap(wn2, c, k);
+            const float kp = k * w[0], kq = k * w[1], kr = k * w[2];
+            q[0] = c * x + (kr * y - kq * z + kp * qw);
+            q[1] = c * y + (-kr * x + kp * z + kq * qw);
+            q[2] = c * z + (kq * x - kp * y + kr * qw);
+            q[3] = c * qw + (-kp * x - kq * y - kr * z);
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
+    } else {
     // One substep (BaseAviary.py:343-372).  kAux: ground effect / drag /
     // downwash enabled; the common force-free path is compiled separately.
 #ifdef QS_SUB_NOUNROLL
@@ -803,11 +936,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       const T sq = sizeof(T) == 8 ? T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) : s2;
       quat_to_zaxis_s(q, sq, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
-#ifdef QS_X_NOAUX
-      if (false) {
-#else
-      if (P.aux) {
-#endif
+      if (AUX && P.aux) {
         // no contraction here: the four ground-effect torque arms cancel exactly
         // for a level drone only in plain multiply-then-add arithmetic
 #pragma clang fp contract(off)
@@ -963,7 +1092,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
     }
+    }   // general substep path
+#ifndef QS_X_NORB
     quat_to_rpy(q, rpy);   // readback (BaseAviary.py:374, 518)
+#endif
     total += 1;
     // Kinematic state is final unless this env auto-resets (rewritten below):
     // store now so the writes drain under the reward / obs phases.

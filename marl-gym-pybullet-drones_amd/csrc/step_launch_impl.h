@@ -10,12 +10,17 @@ template <class T, int TASK, int ACT> static void launch_one(int grid, size_t ld
                                                              int ctrl_freq, int pyb_freq, int phys) {
   constexpr int kCF = TASK == QS_TASK_SPIRAL ? 48 : 30;   // SpiralAviary.py:28; MH:20 and the MARL tasks
   const bool cf = ctrl_freq == kCF && pyb_freq == 240;
+  // the default control frequency without extra forces is the hot configuration:
+  // fully compile-time (constant substeps/history, no force branch)
+  const bool aux = P.aux != 0;
   if (phys == QS_PHYS_DYN) {
-    if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN>), dim3(grid), dim3(kBlock), lds, st, P);
-    else hipLaunchKernelGGL((step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN>), dim3(grid), dim3(kBlock), lds, st, P);
+    if (cf && !aux) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, false>), dim3(grid), dim3(kBlock), lds, st, P);
+    else if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, true>), dim3(grid), dim3(kBlock), lds, st, P);
+    else hipLaunchKernelGGL((step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN, true>), dim3(grid), dim3(kBlock), lds, st, P);
   } else {
-    if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB>), dim3(grid), dim3(kBlock), lds, st, P);
-    else hipLaunchKernelGGL((step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB>), dim3(grid), dim3(kBlock), lds, st, P);
+    if (cf && !aux) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, false>), dim3(grid), dim3(kBlock), lds, st, P);
+    else if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, true>), dim3(grid), dim3(kBlock), lds, st, P);
+    else hipLaunchKernelGGL((step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB, true>), dim3(grid), dim3(kBlock), lds, st, P);
   }
 }
 

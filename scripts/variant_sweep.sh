@@ -11,6 +11,6 @@ for v in "${VS[@]}"; do
   make -s -C marl-gym-pybullet-drones_amd clean && make -s -j16 -C marl-gym-pybullet-drones_amd EXTRA="$ex" > /dev/null 2>&1 || { echo "build failed: $v"; exit 1; }
   timeout -k 10 120 python bench.py --no-cpu-baseline --mappo 0 --pyb ${PYB:-0} --steps ${STEPS:-640} > gpurun_out/var_$i.json 2>/dev/null
   rc=$?; if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; exit $rc; fi
-  python3 -c "import json;d=json.load(open('gpurun_out/var_$i.json'));print('variant [$v] kernel_us %.2f value %.3e'%(d['roofline']['kernel_ms']*1e3, d['value']))"
+  python3 -c "import json;d=json.load(open('gpurun_out/var_$i.json'));print('variant [$v] kernel_us %.2f value %.3e'%(d['roofline']['kernel_ms']*1e3, d['value']), ('pyb_us %.2f'%(d['pyb']['kernel_ms']*1e3)) if d.get('pyb') else '')"
   i=$((i+1))
 done
