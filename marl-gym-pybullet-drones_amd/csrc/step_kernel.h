@@ -135,6 +135,8 @@ template <> struct M<double> {
 };
 
 template <class T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
+// fp32: one v_med3_f32 (same result as the compare/select form for every non-NaN x, lo <= hi)
+template <> __device__ __forceinline__ float clampv<float>(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 
 // cos θ and sin θ / |ω| for the exp-map update (BaseAviary.py:889-891), with
 // θ = |ω|·dt/2, from u = θ² = |ω|²·(dt/2)² — no square root and no division
@@ -174,8 +176,15 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    // one 32x32->64 product per multiplier (a single v_mad_u64_u32, where separate
+    // lo/hi halves are two quarter-rate v_mul_lo/v_mul_hi)
+#ifndef QS_PHILOX_MAD64
     uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
     uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+#else
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32), lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+#endif
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
   }
   return c;
@@ -266,6 +275,7 @@ template <class T>
 __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T pos[3], const T q[4], const T vel[3],
                                         const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
 #if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOPID)
+  rpm[0] = rpm[1] = rpm[2] = rpm[3] = T(cf2x::HOVER_RPM) + T(1e-3) * pos[2];
   return;
 #endif
   using F = M<T>;
@@ -723,7 +733,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
       for (int k = 0; k < A; ++k) cur_act[k] = act_in[k];
     } else {
+#ifdef QS_X_NOPHILOX
+      U4 r = U4{(uint32_t)total * 2654435761u, genv, 0u, 0u};
+#else
       U4 r = philox(U4{(uint32_t)total, genv, 0u, (uint32_t)((STREAM_ACT << 24) | d)}, P.k0, P.k1);
+#endif
       const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
       for (int k = 0; k < A; ++k) cur_act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
@@ -830,9 +844,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           c = __builtin_fmaf(u, __builtin_fmaf(u, __builtin_fmaf(u, __builtin_fmaf(u, float(1.0 / 40320), float(-1.0 / 720)),
                                                                  float(1.0 / 24)), -0.5f), 1.0f);
         } else {
+          // rare (|ω| > 120 rad/s): hardware sin/cos, no library range reduction
+          // unrolled into every substep
           const float wn = sqrtf(wn2), th = wn * kHdt;
-          c = cosf(th);
-          k = sinf(th) / wn;
+          c = __cosf(th);
+          k = __sinf(th) * __builtin_amdgcn_rcpf(wn);
         }
       };
       if constexpr (PHYS == QS_PHYS_PYB) {

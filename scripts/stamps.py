@@ -26,3 +26,10 @@ for k in range(7):
     print(f"{names[k]:20s} {np.percentile(v,10):7.2f} {np.median(v):7.2f} {np.percentile(v,90):7.2f}")
 d = np.diff(st[:, :7], axis=1)
 print("per-wave phase durations median:", np.round(np.median(d, axis=0), 2))
+print("last wave obs stored at %.2f us; waves started by: p50 %.2f, max %.2f" % (
+    (st[:, 6] - t0).max(), np.median(st[:, 0] - t0), (st[:, 0] - t0).max()))
+# how many waves are in each phase over time (0.5 us bins)
+bins = np.arange(0, (st[:, 6] - t0).max() + 0.5, 0.5)
+for b in bins:
+    ph = [(((st[:, k] - t0) <= b) & ((st[:, k + 1] - t0) > b)).sum() for k in range(6)]
+    print(f"t={b:5.1f}  " + " ".join(f"{n:5d}" for n in ph))
