@@ -35,8 +35,44 @@ def get_activation(name):
     return getattr(torch, name) if name in ("tanh", "relu", "sigmoid") else (getattr(F, name) if name else (lambda x: x))
 
 
+def _splitk_chunks(rows):
+    """Row chunks of the split-K weight gradient: the largest power of two S with
+    rows / S >= 1024 that divides rows (1 = plain GEMM)."""
+    s = 1
+    while rows % (2 * s) == 0 and rows // (2 * s) >= 1024 and s < 64:
+        s *= 2
+    return s
+
+
+class _LinearSplitK(torch.autograd.Function):
+    """nn.Linear with a split-K weight gradient.  A PPO minibatch's dW = dYᵀ X
+    reduces over 32 768 rows into a 256×256 result: as one GEMM that is a few dozen
+    output tiles on a 256-CU chip (hipBLASLt ran it at ~30 TFLOP/s); as S batched
+    GEMMs over row chunks plus a sum over S it fills the chip (actor fwd+bwd
+    587 → 339 µs per minibatch, scripts/mlp_bench.py).  Same math; fp32 rounding
+    of the reduction order only."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, splits):
+        ctx.save_for_backward(x, w)
+        ctx.splits = splits
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        S, K = ctx.splits, x.shape[0]
+        if S > 1:
+            dw = torch.bmm(dy.reshape(S, K // S, -1).transpose(1, 2), x.reshape(S, K // S, -1)).sum(0)
+        else:
+            dw = dy.t() @ x
+        return dx, dw, dy.sum(0), None
+
+
 class MLP(nn.Module):
-    """neural_networks.py:18-54 (nn.Linear default init; init_weights=False there)."""
+    """neural_networks.py:18-54 (nn.Linear default init; init_weights=False there).
+    Under autograd with >= 2048 rows the layers take the split-K weight gradient."""
 
     def __init__(self, input_dim, output_dim, hidden_dims=(), act='relu', output_act=None, **kwargs):
         super().__init__()
@@ -47,9 +83,11 @@ class MLP(nn.Module):
 
     def forward(self, x):
         out = x
-        for fc in self.fcs[:-1]:
-            out = self.act(fc(out))
-        return self.output_act(self.fcs[-1](out))
+        splits = _splitk_chunks(x.shape[0]) if (torch.is_grad_enabled() and x.dim() == 2) else 1
+        for i, fc in enumerate(self.fcs):
+            out = _LinearSplitK.apply(out, fc.weight, fc.bias, splits) if splits > 1 else fc(out)
+            out = self.act(out) if i < len(self.fcs) - 1 else self.output_act(out)
+        return out
 
 
 class Normal(torch.distributions.Normal):
@@ -335,8 +373,17 @@ class MAPPOAgent:
         D, O, A = rollouts.num_agents, rollouts.obs_dim, self.ac.act_dim
         mb = idx.shape[0]
         obs = rollouts.sample_obs(idx)
+        # The critic (4 096-row GEMMs that fill a fraction of the chip) runs on a side
+        # stream beside the actor; autograd runs each backward op on its forward op's
+        # stream, so the two backward passes overlap too.
+        main = torch.cuda.current_stream()
+        if getattr(self, '_side', None) is None:
+            self._side = torch.cuda.Stream()
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            v = self.ac.critic(obs.reshape(mb, D * O))
         mean = self.ac.actor.pi_net(obs.reshape(mb * D, O))
-        v = self.ac.critic(obs.reshape(mb, D * O))
+        main.wait_stream(self._side)
         lib = L.load()
         if getattr(self, '_heads_mb', None) != (mb, D, A):
             self._dmean = torch.empty(mb * D, A, device=self.device)
@@ -353,6 +400,7 @@ class MAPPOAgent:
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), st), "qs_ppo_heads")
         torch.autograd.backward([mean, v], [self._dmean, self._dv])
+        main.wait_stream(self._side)
         if world > 1:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)

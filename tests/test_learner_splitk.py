@@ -1,0 +1,55 @@
+"""Split-K weight gradient of the learner MLPs (agent._LinearSplitK) against plain
+nn.Linear autograd: same forward, gradients equal up to fp32 reduction order.
+Runs on the CPU (the split path is device-independent) and, marked gpu, on cuda:0."""
+import copy
+
+import pytest
+import torch
+
+from gym_pybullet_drones_amd.mappo.agent import MLP, _splitk_chunks
+
+
+def _grads(net, x, g):
+    for p in net.parameters():
+        p.grad = None
+    net(x).backward(g)
+    return [p.grad.clone() for p in net.parameters()]
+
+
+def _check(device, rows, din):
+    torch.manual_seed(0)
+    net = MLP(din, 1, [256, 256], act='tanh').to(device)
+    x = torch.randn(rows, din, device=device)
+    g = torch.randn(rows, 1, device=device)
+    assert _splitk_chunks(rows) > 1
+    got = _grads(net, x, g)
+    ref_net = copy.deepcopy(net)
+    want = []
+    for p in ref_net.parameters():
+        p.grad = None
+    out = x
+    for i, fc in enumerate(ref_net.fcs):   # plain nn.Linear path
+        out = fc(out)
+        out = torch.tanh(out) if i < len(ref_net.fcs) - 1 else out
+    out.backward(g)
+    want = [p.grad for p in ref_net.parameters()]
+    with torch.no_grad():
+        torch.testing.assert_close(net(x), ref_net(x), rtol=0, atol=0)
+    for a, b in zip(got, want):
+        scale = float(b.abs().max())
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * scale)
+
+
+def test_splitk_chunks():
+    assert [_splitk_chunks(r) for r in (96, 2048, 4096, 32768, 131072, 3000)] == [1, 2, 4, 32, 64, 2]
+
+
+@pytest.mark.parametrize("rows,din", [(4096, 27), (8192, 216)])
+def test_splitk_matches_linear_cpu(rows, din):
+    _check("cpu", rows, din)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,din", [(32768, 27), (4096, 216)])
+def test_splitk_matches_linear_gpu(rows, din):
+    _check("cuda", rows, din)
