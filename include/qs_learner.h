@@ -12,6 +12,9 @@
  *   compute_policy_loss / compute_value_loss forward and their   qs_ppo_heads
  *     autograd backward down to the actor mean and critic value
  *     (mappo/agent.py:602-683): ~60 small torch kernels
+ *   MLP forward/backward (neural_networks.py:18-54) outside the   qs_mlp_bias_tanh,
+ *     GEMMs: bias + tanh, the linear head, tanh backward and the   qs_mlp_tanh_bwd,
+ *     bias / weight-gradient reductions (torch autograd kernels)   qs_mlp_sum_partials
  *
  * All pointers are device pointers; every call is asynchronous on `stream`
  * (hipStream_t as void*) and contains no host synchronisation, so it can be
@@ -70,6 +73,28 @@ int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const flo
                  const float* v, float clip, float ent_coef, float* dmean, float* dlogstd, float* dv, float* kl_out,
                  double* acc, void* work, void* stream);
 int64_t qs_ppo_heads_work_bytes(int32_t mb, int32_t D);
+
+/* The elementwise / reduction side of the tanh MLP layers (actor and critic,
+ * safe_control_gym neural_networks.py:18-54; autograd of nn.Linear + torch.tanh
+ * in the reference) around the GEMMs.  Row-major [K][N] fp32, N = hidden size
+ * in {64, 128, 256, 512}; A = head outputs (<= 4).
+ *
+ * qs_mlp_bias_tanh: h = tanh(z + b) (h may alias z); if A > 0 also the linear
+ *   head out[K][A] = h·w3ᵀ + b3 (w3 [A][N]).
+ * qs_mlp_tanh_bwd: dz = dH ⊙ (1 − h²) with dH = dh (A = 0) or dH = dout·w3
+ *   (A > 0, dout [K][A]); writes dz (may alias dh) and, per block g of
+ *   qs_mlp_bwd_blocks(K), the partial sums partial[g][P], P = N·(1+A) + A:
+ *   [Σ dz | Σ dout_a·h (A rows of N) | Σ dout_a] over the block's rows.
+ * qs_mlp_sum_partials: d += Σ_g partial[g][j] in block order (deterministic),
+ *   j in [0, n0) → d0, [n0, n0+n1) → d1, the rest → d2.  Also reduces split-K
+ *   weight-gradient partials [S][M] (G = S, P = M, n0 = M). */
+int qs_mlp_bias_tanh(int64_t K, int32_t N, const float* z, const float* b, float* h, int32_t A, const float* w3,
+                     const float* b3, float* out, void* stream);
+int32_t qs_mlp_bwd_blocks(int64_t K);
+int qs_mlp_tanh_bwd(int64_t K, int32_t N, const float* dh, const float* dout, int32_t A, const float* w3, const float* h,
+                    float* dz, float* partial, void* stream);
+int qs_mlp_sum_partials(int32_t G, int64_t P, const float* partial, float* d0, int64_t n0, float* d1, int64_t n1,
+                        float* d2, void* stream);
 
 const char* qs_learner_last_error(void);
 

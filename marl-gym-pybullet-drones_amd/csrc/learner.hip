@@ -222,6 +222,159 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
   acc[2] += (double)(-ent);
   acc[3] += (double)akl;
 }
+
+// ------------------------------------------------------------- MLP tanh layers
+// The elementwise / reduction side of the actor and critic MLPs (MLP with tanh
+// hidden layers, safe_control_gym neural_networks.py:18-54) around the GEMMs:
+//   qs_mlp_bias_tanh: H = tanh(Z + b) in place of the GEMM output, and for the
+//     last hidden layer the linear head out = H·W3ᵀ + b3 in the same pass;
+//   qs_mlp_tanh_bwd: dZ = dH ⊙ (1 − H²) with dH given, or formed on the fly as
+//     dout·W3 (the head's backward), plus per-block partial sums of the bias
+//     gradient Σ_k dZ (and of dW3 = Σ_k dout_k H_k, db3 = Σ_k dout_k);
+//   qs_mlp_sum_partials: adds the [G][P] block partials (or the [S][M] split-K
+//     weight-gradient partials) in block order into up to three destinations —
+//     a fixed order, so a graph replay is bit-identical.
+// Rows are 64·C floats (N = hidden size): lane l of a wave owns columns
+// [l·C, l·C + C), so every row access is one coalesced wave instruction.
+constexpr int kMlpBlock = 256;
+constexpr int kMlpMaxA = 4;
+
+template <int C> struct VecC;
+template <> struct VecC<1> { typedef float T; };
+template <> struct VecC<2> { typedef float2 T; };
+template <> struct VecC<4> { typedef float4 T; };
+
+template <int C> __device__ __forceinline__ void ld_row(const float* p, float (&v)[C]) {
+  if constexpr (C == 8) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    const typename VecC<C>::T t = *reinterpret_cast<const typename VecC<C>::T*>(p);
+    __builtin_memcpy(v, &t, sizeof(t));
+  }
+}
+template <int C> __device__ __forceinline__ void st_row(float* p, const float (&v)[C]) {
+  if constexpr (C == 8) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    typename VecC<C>::T t;
+    __builtin_memcpy(&t, v, sizeof(t));
+    *reinterpret_cast<typename VecC<C>::T*>(p) = t;
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(kMlpBlock) mlp_bias_tanh_kernel(long long K, const float* __restrict__ z,
+                                                                  const float* __restrict__ b, float* __restrict__ h,
+                                                                  int A, const float* __restrict__ w3,
+                                                                  const float* __restrict__ b3, float* __restrict__ out) {
+  constexpr int N = 64 * C;
+  const int lane = threadIdx.x & 63;
+  const long long nw = (long long)gridDim.x * (kMlpBlock / 64);
+  float bias[C], w[kMlpMaxA][C];
+  ld_row<C>(b + lane * C, bias);
+  for (int a = 0; a < A; ++a) ld_row<C>(w3 + (size_t)a * N + lane * C, w[a]);
+  for (long long r = (long long)blockIdx.x * (kMlpBlock / 64) + (threadIdx.x >> 6); r < K; r += nw) {
+    float v[C];
+    ld_row<C>(z + r * N + lane * C, v);
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = tanhf(v[c] + bias[c]);
+    st_row<C>(h + r * N + lane * C, v);
+    for (int a = 0; a < A; ++a) {
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) t += v[c] * w[a][c];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) out[r * A + a] = t + b3[a];
+    }
+  }
+}
+
+// Partial layout per block: [db N | dw3 A·N | db3 A].
+template <int C, int A>
+__global__ void __launch_bounds__(kMlpBlock) mlp_tanh_bwd_kernel(long long K, long long rows_per_block,
+                                                                 const float* __restrict__ dh,
+                                                                 const float* __restrict__ dout,
+                                                                 const float* __restrict__ w3,
+                                                                 const float* __restrict__ h, float* __restrict__ dz,
+                                                                 float* __restrict__ partial) {
+  constexpr int N = 64 * C, P = N * (1 + A) + A, W = kMlpBlock / 64;
+  __shared__ float lds[W][P];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float w[A > 0 ? A : 1][C];
+  for (int a = 0; a < A; ++a) ld_row<C>(w3 + (size_t)a * N + lane * C, w[a]);
+  float sdb[C] = {}, sdw[A > 0 ? A : 1][C] = {}, sdb3[A > 0 ? A : 1] = {};
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < K ? r0 + rows_per_block : K;
+  for (long long r = r0 + wv; r < r1; r += W) {
+    float hv[C], g[C];
+    ld_row<C>(h + r * N + lane * C, hv);
+    float dv[A > 0 ? A : 1];
+    if constexpr (A > 0) {
+#pragma unroll
+      for (int a = 0; a < A; ++a) dv[a] = dout[r * A + a];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float t = 0.f;
+#pragma unroll
+        for (int a = 0; a < A; ++a) t += dv[a] * w[a][c];
+        g[c] = t;
+      }
+    } else {
+      ld_row<C>(dh + r * N + lane * C, g);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      g[c] = g[c] * (1.0f - hv[c] * hv[c]);   // tanh_backward: grad·(1 − y²)
+      sdb[c] += g[c];
+    }
+    st_row<C>(dz + r * N + lane * C, g);
+    if constexpr (A > 0) {
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) sdw[a][c] += dv[a] * hv[c];
+        sdb3[a] += dv[a];
+      }
+    }
+  }
+  // waves → block partial, in wave order
+#pragma unroll
+  for (int c = 0; c < C; ++c) lds[wv][lane * C + c] = sdb[c];
+  if constexpr (A > 0) {
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) lds[wv][N + a * N + lane * C + c] = sdw[a][c];
+      if (lane == 0) lds[wv][N * (1 + A) + a] = sdb3[a];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < P; j += kMlpBlock) {
+    float t = lds[0][j];
+    for (int k = 1; k < W; ++k) t += lds[k][j];
+    partial[(size_t)blockIdx.x * P + j] = t;
+  }
+}
+
+// dst segments: [0, n0) → d0, [n0, n0+n1) → d1, [n0+n1, P) → d2; d += Σ_g partial[g][j].
+__global__ void __launch_bounds__(kMlpBlock) mlp_sum_partials_kernel(int G, long long P, const float* __restrict__ partial,
+                                                                     float* d0, long long n0, float* d1, long long n1,
+                                                                     float* d2) {
+  const long long j = (long long)blockIdx.x * kMlpBlock + threadIdx.x;
+  if (j >= P) return;
+  float t = 0.f;
+  int g = 0;
+  for (; g + 4 <= G; g += 4) {   // independent loads in flight, added in block order
+    const float a = partial[(size_t)g * P + j], b = partial[(size_t)(g + 1) * P + j];
+    const float c = partial[(size_t)(g + 2) * P + j], d = partial[(size_t)(g + 3) * P + j];
+    t = (((t + a) + b) + c) + d;
+  }
+  for (; g < G; ++g) t += partial[(size_t)g * P + j];
+  float* dst = j < n0 ? d0 + j : (j < n0 + n1 ? d1 + (j - n0) : d2 + (j - n0 - n1));
+  *dst += t;
+}
 }  // namespace
 
 extern "C" {
@@ -290,6 +443,77 @@ int qs_ppo_heads(int32_t mb, int32_t D, int32_t A, const int64_t* idx, const flo
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_ppo_heads: ") + hipGetErrorString(e));
+}
+
+static int mlp_c(int32_t N) { return (N % 64 == 0 && (N / 64 == 1 || N / 64 == 2 || N / 64 == 4 || N / 64 == 8)) ? N / 64 : 0; }
+
+int qs_mlp_bias_tanh(int64_t K, int32_t N, const float* z, const float* b, float* h, int32_t A, const float* w3,
+                     const float* b3, float* out, void* stream) {
+  const int C = mlp_c(N);
+  if (K <= 0 || !C || !z || !b || !h || A < 0 || A > kMlpMaxA || (A > 0 && (!w3 || !b3 || !out)))
+    return fail(QS_E_INVALID, "qs_mlp_bias_tanh: bad argument (N must be 64, 128, 256 or 512; A <= 4)");
+  long long waves = K < 8192 ? K : 8192;
+  const unsigned grid = (unsigned)((waves + 3) / 4);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kMlpBlock), 0, (hipStream_t)stream, (long long)K, z, b, h, (int)A, w3, b3, out);
+  };
+  switch (C) {
+    case 1: go(mlp_bias_tanh_kernel<1>); break;
+    case 2: go(mlp_bias_tanh_kernel<2>); break;
+    case 4: go(mlp_bias_tanh_kernel<4>); break;
+    default: go(mlp_bias_tanh_kernel<8>); break;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_bias_tanh: ") + hipGetErrorString(e));
+}
+
+int32_t qs_mlp_bwd_blocks(int64_t K) {
+  const long long g = (K + 63) / 64;
+  return (int32_t)(g < 512 ? (g < 1 ? 1 : g) : 512);
+}
+
+int qs_mlp_tanh_bwd(int64_t K, int32_t N, const float* dh, const float* dout, int32_t A, const float* w3, const float* h,
+                    float* dz, float* partial, void* stream) {
+  const int C = mlp_c(N);
+  if (K <= 0 || !C || !h || !dz || !partial || A < 0 || A > kMlpMaxA || (A == 0 && !dh) || (A > 0 && (!dout || !w3)) ||
+      (C == 8 && A > 1))
+    return fail(QS_E_INVALID, "qs_mlp_tanh_bwd: bad argument (N in {64,128,256,512}; A <= 4, A <= 1 at N = 512)");
+  const int G = qs_mlp_bwd_blocks(K);
+  const long long rpb = (K + G - 1) / G;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(kMlpBlock), 0, (hipStream_t)stream, (long long)K, rpb, dh, dout, w3, h, dz, partial);
+  };
+#define QS_MLP_BWD_CASE(CC)                                   \
+  case CC:                                                    \
+    switch (A) {                                              \
+      case 0: go(mlp_tanh_bwd_kernel<CC, 0>); break;          \
+      case 1: go(mlp_tanh_bwd_kernel<CC, 1>); break;          \
+      case 2: if constexpr (CC < 8) go(mlp_tanh_bwd_kernel<CC, 2>); break; \
+      case 3: if constexpr (CC < 8) go(mlp_tanh_bwd_kernel<CC, 3>); break; \
+      default: if constexpr (CC < 8) go(mlp_tanh_bwd_kernel<CC, 4>); break; \
+    }                                                         \
+    break;
+  switch (C) {
+    QS_MLP_BWD_CASE(1)
+    QS_MLP_BWD_CASE(2)
+    QS_MLP_BWD_CASE(4)
+    QS_MLP_BWD_CASE(8)
+  }
+#undef QS_MLP_BWD_CASE
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_tanh_bwd: ") + hipGetErrorString(e));
+}
+
+int qs_mlp_sum_partials(int32_t G, int64_t P, const float* partial, float* d0, int64_t n0, float* d1, int64_t n1,
+                        float* d2, void* stream) {
+  if (G <= 0 || P <= 0 || !partial || !d0 || n0 <= 0 || n0 > P || (n0 < P && !d1) || (n0 + n1 < P && !d2) ||
+      n1 < 0 || n0 + n1 > P)
+    return fail(QS_E_INVALID, "qs_mlp_sum_partials: bad argument");
+  const unsigned grid = (unsigned)((P + kMlpBlock - 1) / kMlpBlock);
+  hipLaunchKernelGGL(mlp_sum_partials_kernel, dim3(grid), dim3(kMlpBlock), 0, (hipStream_t)stream, (int)G, (long long)P,
+                     partial, d0, (long long)n0, d1, (long long)n1, d2);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -60,6 +60,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
            # include/qs_learner.h
            "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_ppo_heads_work_bytes",
+           "qs_mlp_bias_tanh", "qs_mlp_bwd_blocks", "qs_mlp_tanh_bwd", "qs_mlp_sum_partials",
            "qs_learner_last_error")
 
 _lib = None
@@ -104,6 +105,10 @@ def load():
     L.qs_ppo_heads.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, f32, vp, vp, vp, vp, vp,
                                f32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.qs_ppo_heads_work_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    L.qs_mlp_bias_tanh.argtypes = [i64, ctypes.c_int32, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp]
+    L.qs_mlp_bwd_blocks.argtypes = [i64]
+    L.qs_mlp_tanh_bwd.argtypes = [i64, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp]
+    L.qs_mlp_sum_partials.argtypes = [ctypes.c_int32, i64, vp, vp, i64, vp, i64, vp, vp]
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):
@@ -116,7 +121,7 @@ def load():
 def check(rc, what=""):
     if rc != QS_OK:
         lib = load()
-        msg = lib.qs_learner_last_error() if what.startswith(("qs_gae", "qs_adam", "qs_ppo")) else lib.qs_last_error()
+        msg = lib.qs_learner_last_error() if what.startswith(("qs_gae", "qs_adam", "qs_ppo", "qs_mlp")) else lib.qs_last_error()
         raise QuadSwarmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
 
 

@@ -70,9 +70,78 @@ class _LinearSplitK(torch.autograd.Function):
         return dx, dw, dy.sum(0), None
 
 
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _splitk_into(dst, dy, x):
+    """dst += dyᵀ·x (a weight gradient) as S row-chunk GEMMs + a fixed-order sum."""
+    K = x.shape[0]
+    S = _splitk_chunks(K)
+    if S == 1:
+        dst.addmm_(dy.t(), x)
+        return
+    part = torch.bmm(dy.reshape(S, K // S, -1).transpose(1, 2), x.reshape(S, K // S, -1))
+    L.check(L.load().qs_mlp_sum_partials(S, part[0].numel(), L.ptr(part), L.ptr(dst), dst.numel(), None, 0, None,
+                                         _stream()), "qs_mlp_sum_partials")
+
+
+class _TanhMLP3(torch.autograd.Function):
+    """The reference MLP with two tanh hidden layers and a linear head
+    (neural_networks.py:18-54), forward and backward, on the MI355X path:
+    hipBLASLt GEMMs for the contractions, HIP kernels for everything between them
+    (qs_mlp_bias_tanh: bias + tanh, and the head's row dot products in the same
+    pass; qs_mlp_tanh_bwd: the head backward fused with tanh's, and the bias /
+    head-weight gradient partials; qs_mlp_sum_partials: fixed-order reductions,
+    accumulated straight into the parameters' .grad buffers).  Used by MLP when
+    every parameter already has a .grad buffer (the learner's flat buffers), so
+    the backward returns no tensors for autograd to add."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3):
+        lib, st = L.load(), _stream()
+        K, N1, N2, A = x.shape[0], w1.shape[0], w2.shape[0], w3.shape[0]
+        h1 = torch.mm(x, w1.t())
+        L.check(lib.qs_mlp_bias_tanh(K, N1, L.ptr(h1), L.ptr(b1), L.ptr(h1), 0, None, None, None, st), "qs_mlp_bias_tanh")
+        h2 = torch.mm(h1, w2.t())
+        out = torch.empty((K, A), device=x.device, dtype=x.dtype)
+        L.check(lib.qs_mlp_bias_tanh(K, N2, L.ptr(h2), L.ptr(b2), L.ptr(h2), A, L.ptr(w3), L.ptr(b3), L.ptr(out), st),
+                "qs_mlp_bias_tanh")
+        ctx.save_for_backward(x, w1, b1, w2, b2, w3, b3, h1, h2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w1, b1, w2, b2, w3, b3, h1, h2 = ctx.saved_tensors
+        lib, st = L.load(), _stream()
+        K, N1, N2, A = x.shape[0], w1.shape[0], w2.shape[0], w3.shape[0]
+        dout = dout.contiguous()
+        G = int(lib.qs_mlp_bwd_blocks(K))
+        # head + second tanh: dz2 = (dout·w3) ⊙ (1 − h2²); b2, w3, b3 gradients
+        dz2 = torch.empty_like(h2)
+        part = torch.empty((G, N2 * (1 + A) + A), device=x.device, dtype=torch.float32)
+        L.check(lib.qs_mlp_tanh_bwd(K, N2, None, L.ptr(dout), A, L.ptr(w3), L.ptr(h2), L.ptr(dz2), L.ptr(part), st),
+                "qs_mlp_tanh_bwd")
+        L.check(lib.qs_mlp_sum_partials(G, part.shape[1], L.ptr(part), L.ptr(b2.grad), N2, L.ptr(w3.grad), A * N2,
+                                        L.ptr(b3.grad), st), "qs_mlp_sum_partials")
+        dh1 = torch.mm(dz2, w2)
+        _splitk_into(w2.grad, dz2, h1)
+        # first tanh (in place on dh1): b1 gradient
+        part1 = torch.empty((G, N1), device=x.device, dtype=torch.float32)
+        L.check(lib.qs_mlp_tanh_bwd(K, N1, L.ptr(dh1), None, 0, None, L.ptr(h1), L.ptr(dh1), L.ptr(part1), st),
+                "qs_mlp_tanh_bwd")
+        L.check(lib.qs_mlp_sum_partials(G, N1, L.ptr(part1), L.ptr(b1.grad), N1, None, 0, None, st),
+                "qs_mlp_sum_partials")
+        _splitk_into(w1.grad, dh1, x)
+        dx = dh1 @ w1 if ctx.needs_input_grad[0] else None
+        return dx, None, None, None, None, None, None
+
+
 class MLP(nn.Module):
     """neural_networks.py:18-54 (nn.Linear default init; init_weights=False there).
-    Under autograd with >= 2048 rows the layers take the split-K weight gradient."""
+    Under autograd with >= 2048 rows the layers take the split-K weight gradient;
+    on the GPU with the learner's .grad buffers in place, the two-hidden-layer tanh
+    MLP runs as _TanhMLP3."""
 
     def __init__(self, input_dim, output_dim, hidden_dims=(), act='relu', output_act=None, **kwargs):
         super().__init__()
@@ -80,8 +149,21 @@ class MLP(nn.Module):
         self.fcs = nn.ModuleList([nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1)])
         self.act = get_activation(act)
         self.output_act = get_activation(output_act)
+        self._tanh3 = act == 'tanh' and output_act is None and len(dims) == 4
+
+    def _fused_ok(self, x):
+        if not (self._tanh3 and x.is_cuda and x.dim() == 2 and x.shape[0] >= 2048 and torch.is_grad_enabled()
+                and x.dtype == torch.float32):
+            return False
+        n1, n2, a = self.fcs[0].out_features, self.fcs[1].out_features, self.fcs[2].out_features
+        ok_n = (64, 128, 256, 512)
+        return (n1 in ok_n and n2 in ok_n and a <= (1 if n2 == 512 else 4)
+                and all(p.grad is not None and p.grad.is_contiguous() for p in self.parameters()))
 
     def forward(self, x):
+        if self._fused_ok(x):
+            f0, f1, f2 = self.fcs
+            return _TanhMLP3.apply(x.contiguous(), f0.weight, f0.bias, f1.weight, f1.bias, f2.weight, f2.bias)
         out = x
         splits = _splitk_chunks(x.shape[0]) if (torch.is_grad_enabled() and x.dim() == 2) else 1
         for i, fc in enumerate(self.fcs):
