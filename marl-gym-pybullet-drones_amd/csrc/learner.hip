@@ -292,14 +292,18 @@ __global__ void __launch_bounds__(kMlpBlock) mlp_bias_tanh_kernel(long long K, c
 }
 
 // Partial layout per block: [db N | dw3 A·N | db3 A].
+// 8 waves per block, one block per 64 rows up to one per CU: every CU streams,
+// and the final sum reads at most 256 partials per column.
+constexpr int kMlpBwdBlock = 512;
+constexpr int kMlpBwdMaxG = 256;
 template <int C, int A>
-__global__ void __launch_bounds__(kMlpBlock) mlp_tanh_bwd_kernel(long long K, long long rows_per_block,
+__global__ void __launch_bounds__(kMlpBwdBlock) mlp_tanh_bwd_kernel(long long K, long long rows_per_block,
                                                                  const float* __restrict__ dh,
                                                                  const float* __restrict__ dout,
                                                                  const float* __restrict__ w3,
                                                                  const float* __restrict__ h, float* __restrict__ dz,
                                                                  float* __restrict__ partial) {
-  constexpr int N = 64 * C, P = N * (1 + A) + A, W = kMlpBlock / 64;
+  constexpr int N = 64 * C, P = N * (1 + A) + A, W = kMlpBwdBlock / 64;
   __shared__ float lds[W][P];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float w[A > 0 ? A : 1][C];
@@ -351,7 +355,7 @@ __global__ void __launch_bounds__(kMlpBlock) mlp_tanh_bwd_kernel(long long K, lo
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < P; j += kMlpBlock) {
+  for (int j = threadIdx.x; j < P; j += kMlpBwdBlock) {
     float t = lds[0][j];
     for (int k = 1; k < W; ++k) t += lds[k][j];
     partial[(size_t)blockIdx.x * P + j] = t;
@@ -359,19 +363,32 @@ __global__ void __launch_bounds__(kMlpBlock) mlp_tanh_bwd_kernel(long long K, lo
 }
 
 // dst segments: [0, n0) → d0, [n0, n0+n1) → d1, [n0+n1, P) → d2; d += Σ_g partial[g][j].
-__global__ void __launch_bounds__(kMlpBlock) mlp_sum_partials_kernel(int G, long long P, const float* __restrict__ partial,
-                                                                     float* d0, long long n0, float* d1, long long n1,
-                                                                     float* d2) {
-  const long long j = (long long)blockIdx.x * kMlpBlock + threadIdx.x;
-  if (j >= P) return;
+// A block owns 64 columns; its 16 waves sum interleaved slices of g (g ≡ w mod 16),
+// combined in wave order — a fixed order for a given G.
+constexpr int kMlpSumBlock = 1024;
+__global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_partials_kernel(int G, long long P,
+                                                                        const float* __restrict__ partial, float* d0,
+                                                                        long long n0, float* d1, long long n1,
+                                                                        float* d2) {
+  constexpr int W = kMlpSumBlock / 64;
+  __shared__ float lds[W][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long j = (long long)blockIdx.x * 64 + lane;
   float t = 0.f;
-  int g = 0;
-  for (; g + 4 <= G; g += 4) {   // independent loads in flight, added in block order
-    const float a = partial[(size_t)g * P + j], b = partial[(size_t)(g + 1) * P + j];
-    const float c = partial[(size_t)(g + 2) * P + j], d = partial[(size_t)(g + 3) * P + j];
-    t = (((t + a) + b) + c) + d;
+  if (j < P) {
+    int g = wv;
+    for (; g + 3 * W < G; g += 4 * W) {   // four independent loads in flight
+      const float a = partial[(size_t)g * P + j], b = partial[(size_t)(g + W) * P + j];
+      const float c = partial[(size_t)(g + 2 * W) * P + j], d = partial[(size_t)(g + 3 * W) * P + j];
+      t = (((t + a) + b) + c) + d;
+    }
+    for (; g < G; g += W) t += partial[(size_t)g * P + j];
   }
-  for (; g < G; ++g) t += partial[(size_t)g * P + j];
+  lds[wv][lane] = t;
+  __syncthreads();
+  if (wv != 0 || j >= P) return;
+  t = lds[0][lane];
+  for (int k = 1; k < W; ++k) t += lds[k][lane];
   float* dst = j < n0 ? d0 + j : (j < n0 + n1 ? d1 + (j - n0) : d2 + (j - n0 - n1));
   *dst += t;
 }
@@ -469,7 +486,7 @@ int qs_mlp_bias_tanh(int64_t K, int32_t N, const float* z, const float* b, float
 
 int32_t qs_mlp_bwd_blocks(int64_t K) {
   const long long g = (K + 63) / 64;
-  return (int32_t)(g < 512 ? (g < 1 ? 1 : g) : 512);
+  return (int32_t)(g < kMlpBwdMaxG ? (g < 1 ? 1 : g) : kMlpBwdMaxG);
 }
 
 int qs_mlp_tanh_bwd(int64_t K, int32_t N, const float* dh, const float* dout, int32_t A, const float* w3, const float* h,
@@ -481,7 +498,7 @@ int qs_mlp_tanh_bwd(int64_t K, int32_t N, const float* dh, const float* dout, in
   const int G = qs_mlp_bwd_blocks(K);
   const long long rpb = (K + G - 1) / G;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(G), dim3(kMlpBlock), 0, (hipStream_t)stream, (long long)K, rpb, dh, dout, w3, h, dz, partial);
+    hipLaunchKernelGGL(kern, dim3(G), dim3(kMlpBwdBlock), 0, (hipStream_t)stream, (long long)K, rpb, dh, dout, w3, h, dz, partial);
   };
 #define QS_MLP_BWD_CASE(CC)                                   \
   case CC:                                                    \
@@ -509,8 +526,8 @@ int qs_mlp_sum_partials(int32_t G, int64_t P, const float* partial, float* d0, i
   if (G <= 0 || P <= 0 || !partial || !d0 || n0 <= 0 || n0 > P || (n0 < P && !d1) || (n0 + n1 < P && !d2) ||
       n1 < 0 || n0 + n1 > P)
     return fail(QS_E_INVALID, "qs_mlp_sum_partials: bad argument");
-  const unsigned grid = (unsigned)((P + kMlpBlock - 1) / kMlpBlock);
-  hipLaunchKernelGGL(mlp_sum_partials_kernel, dim3(grid), dim3(kMlpBlock), 0, (hipStream_t)stream, (int)G, (long long)P,
+  const unsigned grid = (unsigned)((P + 63) / 64);
+  hipLaunchKernelGGL(mlp_sum_partials_kernel, dim3(grid), dim3(kMlpSumBlock), 0, (hipStream_t)stream, (int)G, (long long)P,
                      partial, d0, (long long)n0, d1, (long long)n1, d2);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials: ") + hipGetErrorString(e));

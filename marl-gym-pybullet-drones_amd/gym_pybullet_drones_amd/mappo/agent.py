@@ -455,17 +455,8 @@ class MAPPOAgent:
         D, O, A = rollouts.num_agents, rollouts.obs_dim, self.ac.act_dim
         mb = idx.shape[0]
         obs = rollouts.sample_obs(idx)
-        # The critic (4 096-row GEMMs that fill a fraction of the chip) runs on a side
-        # stream beside the actor; autograd runs each backward op on its forward op's
-        # stream, so the two backward passes overlap too.
-        main = torch.cuda.current_stream()
-        if getattr(self, '_side', None) is None:
-            self._side = torch.cuda.Stream()
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            v = self.ac.critic(obs.reshape(mb, D * O))
         mean = self.ac.actor.pi_net(obs.reshape(mb * D, O))
-        main.wait_stream(self._side)
+        v = self.ac.critic(obs.reshape(mb, D * O))
         lib = L.load()
         if getattr(self, '_heads_mb', None) != (mb, D, A):
             self._dmean = torch.empty(mb * D, A, device=self.device)
@@ -482,7 +473,6 @@ class MAPPOAgent:
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), st), "qs_ppo_heads")
         torch.autograd.backward([mean, v], [self._dmean, self._dv])
-        main.wait_stream(self._side)
         if world > 1:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
