@@ -187,7 +187,15 @@ def mappo_leg(args, rank, world, dist):
               rollout_steps=args.mappo_steps, rollout_batch_size=E, opt_epochs=10,
               mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
     m.reset()
-    m.train_step()   # warm-up: graph capture, lazy kernel loads
+    try:
+        m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
+    except RuntimeError as e:   # every rank runs the same capture, so they fall back together
+        print(f"[bench] update-graph capture with collectives failed ({e}); eager update iterations",
+              file=sys.stderr, flush=True)
+        torch.cuda.synchronize()
+        m.agent.graph_collectives = False
+        m.agent._graph = None
+        m.train_step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -204,6 +212,7 @@ def mappo_leg(args, rank, world, dist):
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    graphed = world == 1 or m.agent.graph_collectives
     m.close()
     T = args.mappo_steps
     return {"value": T * E * D * world / dt, "unit": "agent-steps/s", "ms_per_train_step": dt * 1e3,
@@ -211,7 +220,7 @@ def mappo_leg(args, rank, world, dist):
             "config": {"rollout_steps": T, "envs_per_gpu": E, "drones": D, "hidden": 256, "opt_epochs": 10,
                        "mini_batch_size": args.mappo_mb,
                        "minibatches_per_epoch": T * E // args.mappo_mb,
-                       "graphs": "rollout + update" if world == 1 else "rollout", "grad_allreduce": "one fused all-reduce per minibatch" if world > 1
+                       "graphs": "rollout + update" if graphed else "rollout", "grad_allreduce": ("one fused all-reduce per minibatch" + (", captured in the update graph" if graphed else "")) if world > 1
                        else None}}
 
 

@@ -369,6 +369,10 @@ class MAPPOAgent:
         self.include_actions_in_critic = include_actions_in_critic
         self.action_scale = action_scale
         self.use_graphs = use_graphs
+        # with several ranks the per-minibatch all-reduce is captured into the update
+        # graph too (RCCL collectives are graph-capturable); False: eager iterations
+        self.graph_collectives = kwargs.get('graph_collectives', True)
+        self._force_allreduce = False   # tests: take the all-reduce path with one rank
         self.fused_heads = fused_heads   # qs_ppo_heads (False: the loss heads as plain torch ops)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
@@ -473,7 +477,7 @@ class MAPPOAgent:
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), st), "qs_ppo_heads")
         torch.autograd.backward([mean, v], [self._dmean, self._dv])
-        if world > 1:
+        if world > 1 or self._force_allreduce:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
         gate = self._kl if self.target_kl > 0 else None
@@ -495,7 +499,7 @@ class MAPPOAgent:
         self._reduce_buf.zero_()
         (policy_loss + self.entropy_coef * entropy_loss + value_loss).backward()
         self._kl.copy_(approx_kl.detach().float().reshape(1))
-        if world > 1:
+        if world > 1 or self._force_allreduce:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
         gate = self._kl if self.target_kl > 0 else None
@@ -542,7 +546,7 @@ class MAPPOAgent:
         total_steps = rollouts.max_length * rollouts.batch_size
         num_mini_batch = total_steps // self.mini_batch_size
         assert num_mini_batch != 0, 'num_mini_batch is 0'
-        graphs = self.use_graphs and self.device.type == 'cuda' and _dist_world() == 1
+        graphs = self.use_graphs and self.device.type == 'cuda' and (_dist_world() == 1 or self.graph_collectives)
         if graphs and (self._graph is None or self._g_rollouts is not rollouts):
             self._capture(rollouts)
         per_epoch = []

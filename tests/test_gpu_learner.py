@@ -239,3 +239,54 @@ def test_ppo_heads_kernel_matches_autograd(A):
     assert acc[1].item() == pytest.approx(vl.item(), rel=1e-12)
     assert acc[2].item() == pytest.approx(el.item(), rel=1e-6)
     assert klo.item() == pytest.approx(kl.item(), rel=1e-5, abs=1e-7)
+
+
+def test_update_graph_captures_the_allreduce():
+    """The multi-rank update: the gradient/approx_kl all-reduce (RCCL) captured into
+    the minibatch HIP graph.  One rank (world 1, nccl backend) forced through the
+    all-reduce path: graph replays must equal eager iterations exactly."""
+    import socket
+    import torch.distributed as dist
+    from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
+    from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
+    from gym_pybullet_drones_amd.utils.spaces import Box
+    own = not dist.is_initialized()
+    if own:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        E, D, O, A, T = 64, 3, 27, 1, 8
+        obs_space = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O)))
+        act_space = Box(-np.ones((D, A)), np.ones((D, A)))
+        agents = []
+        for graphs in (False, True):
+            torch.manual_seed(5)
+            ag = MAPPOAgent(obs_space, act_space, hidden_dim=64, opt_epochs=2, mini_batch_size=128,
+                            entropy_coef=0.005, use_graphs=graphs, device="cuda")
+            ag._force_allreduce = True
+            agents.append(ag)
+        torch.manual_seed(6)
+        buf = MAPPOBuffer(obs_space, act_space, T, E, include_global_state=True, device="cuda")
+        buf.next_obs_slots.normal_()
+        buf.act.normal_()
+        buf.logp.normal_()
+        buf.ret_env.normal_()
+        buf.adv_env.normal_()
+        buf.t, buf.full = 0, True
+        res = []
+        for ag in agents:
+            gen = torch.Generator(device="cuda")
+            gen.manual_seed(0)
+            res.append(ag.update(buf, generator=gen))
+        torch.cuda.synchronize()
+        assert agents[1]._graph is not None
+        assert torch.equal(agents[0].actor_opt.flat, agents[1].actor_opt.flat)
+        assert torch.equal(agents[0].critic_opt.flat, agents[1].critic_opt.flat)
+        for k in ('policy_loss', 'value_loss', 'approx_kl'):
+            assert res[0][k] == res[1][k]
+    finally:
+        if own:
+            dist.destroy_process_group()
