@@ -24,6 +24,10 @@ Extra JSON fields:
   roofline      the step kernel: §8(d) algorithmic bytes per agent-step (418 B,
                 C3 ONE_D_PID) × agents per launch ÷ mean launch time from HIP
                 events on the launch stream, vs 8 TB/s.
+  configs       the other BASELINE.json configs (C2, C3 with ActionType.VEL, C4
+                Spiral, C5 16-drone with the O(D²) downwash under Physics.PYB_DW),
+                each a random-policy rollout on one GPU: agent-steps/s, kernel ms
+                and roofline fraction with that config's §8(d) bytes per agent-step.
   cpu_baseline  the oracle (C++ CPU restatement of the reference semantics,
                 fp64 like the reference) on 176 envs (README's 22-worker
                 topology) timed on this host, rank 0 only.
@@ -60,6 +64,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--mappo", type=int, default=1, help="also time full MAPPO train steps (0 = skip)")
     p.add_argument("--pyb", type=int, default=1, help="also time the rollout under Physics.PYB (0 = skip)")
+    p.add_argument("--configs", type=int, default=1, help="also time BASELINE configs C2, C3-VEL, C4, C5 (N=1 only)")
     p.add_argument("--mappo-steps", type=int, default=32, help="rollout_steps T of the MAPPO leg")
     p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO leg")
     p.add_argument("--mappo-iters", type=int, default=3, help="timed train steps (after one warm-up)")
@@ -108,16 +113,33 @@ def pmc_traffic(E, D, act):
     return best[1]["step_traffic_bytes"], os.path.relpath(best[0], ROOT)
 
 
-def sim_leg(args, rank, world, dist, physics="dyn"):
+# BASELINE.json configs other than the headline one, each timed as its own
+# random-policy rollout on one rank (bytes per agent-step: SURVEY §8(d)).
+EXTRA_CONFIGS = {
+    "C2": dict(task="multihover", drones=4, envs=4096, act="rpm", physics="dyn", aux=(), bytes=720.0,
+               label="MultiHover 4-drone x 4096 envs, ActionType.RPM, Physics.DYN"),
+    "C3_vel": dict(task="multihover", drones=8, envs=16384, act="vel", physics="dyn", aux=(), bytes=790.0,
+                   label="MultiHover 8-drone x 16384 envs, ActionType.VEL, Physics.DYN"),
+    "C4": dict(task="spiral", drones=5, envs=8192, act="vel", physics="dyn", aux=(), bytes=1111.0,
+               label="Spiral 5-drone x 8192 envs, ActionType.VEL, Physics.DYN"),
+    "C5": dict(task="multihover", drones=16, envs=8192, act="one_d_pid", physics="pyb_dw", aux=(), bytes=418.0,
+               label="MultiHover 16-drone x 8192 envs, ActionType.ONE_D_PID, Physics.PYB_DW (O(D^2) downwash)"),
+}
+
+
+def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D=None, act=None, aux=()):
     """The timed random-policy rollout: `steps` control steps of E envs per rank, as
     replays of a HIP graph of `slots` step launches.  Returns (agent-steps/s over all
     ranks, max-over-ranks seconds, mean step-kernel ms on the launch stream, steps)."""
     from gym_pybullet_drones_amd.envs import QuadSwarm
     from gym_pybullet_drones_amd.utils.enums import Physics
-    E, D = args.envs, args.drones
-    sw = QuadSwarm("multihover", num_envs=E, num_drones=D, act=args.act, precision=4,
-                   physics=Physics.PYB if physics == "pyb" else Physics.DYN,
-                   initial_xyzs=grid_layout(D) if D >= 6 else None, env_offset=rank * E)
+    E = args.envs if E is None else E
+    D = args.drones if D is None else D
+    act = args.act if act is None else act
+    phys = {"dyn": Physics.DYN, "pyb": Physics.PYB, "pyb_dw": Physics.PYB_DW}[physics]
+    layout = grid_layout(D) if (D >= 6 and task == "multihover") else None
+    sw = QuadSwarm(task, num_envs=E, num_drones=D, act=act, precision=4, physics=phys, aux=aux,
+                   initial_xyzs=layout, env_offset=rank * E)
     O, A = sw.obs_dim, sw.act_dim
     obs_buf = torch.empty((args.slots, E, D, O), dtype=torch.float32, device=sw.device)
     act_buf = torch.empty((args.slots, E, D, A), dtype=torch.float32, device=sw.device)
@@ -244,6 +266,16 @@ def main():
         pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
                "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
     mappo = mappo_leg(args, rank, world, dist) if args.mappo else None
+    configs = None
+    if args.configs and world == 1:   # the other BASELINE configs, one GPU each
+        configs = {}
+        for name, c in EXTRA_CONFIGS.items():
+            v, el, km, st = sim_leg(args, rank, world, dist, c["physics"], c["task"], c["envs"], c["drones"], c["act"],
+                                    c["aux"])
+            nb = c["bytes"] * c["envs"] * c["drones"]
+            configs[name] = {"workload": c["label"], "value": v, "unit": "agent-steps/s", "kernel_ms": km,
+                             "bytes_per_agent_step": c["bytes"],
+                             "roofline_frac": nb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_src = pmc_traffic(E, D, args.act)
@@ -264,6 +296,7 @@ def main():
             "cpu_baseline": cpu,
             "pyb": pyb,
             "mappo": mappo,
+            "configs": configs,
         }
         print(json.dumps(line), flush=True)
     if dist:

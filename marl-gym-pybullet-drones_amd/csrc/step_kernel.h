@@ -81,8 +81,11 @@ template <int ACT> struct Act {
 template <class T> struct M;
 template <> struct M<float> {
   __device__ static float sqrt_(float x) { return sqrtf(x); }
-  __device__ static float sin_(float x) { return sinf(x); }
-  __device__ static float cos_(float x) { return cosf(x); }
+  // hardware v_sin/v_cos (argument in revolutions): ~1e-6 absolute over the
+  // angles used here (yaw in [-π, π], Spiral phases < 20 rad), no library range
+  // reduction in the instruction stream
+  __device__ static float sin_(float x) { return __sinf(x); }
+  __device__ static float cos_(float x) { return __cosf(x); }
   // atan2 on the fp32 hot path: reduction to [0,1] with one hardware reciprocal
   // and a degree-7 polynomial in a² (fitted here; |error| ≤ 2e-7 rad, ~3 ulp),
   // about a third of the instructions of the library atan2f.
@@ -648,7 +651,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const __amdgpu_buffer_rsrc_t r = rsrc(P.act_in, P.act_in ? (unsigned)N * A * 4u : 0u);
     const unsigned v = valid ? (unsigned)a * A * 4u : kOOB;
 #pragma unroll
-    for (int k = 0; k < A; ++k) act_in[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)v, k * 4, 0));
+    for (int k = 0; k < A; ++k) act_in[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(v + 4u * k), 0, 0));
   }
   const uint8_t mask_v = __builtin_amdgcn_raw_buffer_load_b8(
       rsrc(P.reset_mask, P.reset_mask ? E : 0u), valid ? e : (int)kOOB, 0, 0);
@@ -677,11 +680,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
     for (int sl = 0; sl < HR; ++sl) {
       const int so = (int)((unsigned)sl * (unsigned)N * A * 4u);
-      // (dword loads: ROCm 7.2's clang lowers __builtin_amdgcn_raw_buffer_load_b128
-      // to a single dword load; adjacent dwords are merged by the backend)
+      // (dword loads with the component in the immediate offset: the backend
+      // merges a slot's A dwords into one dwordx2/x4 load; ROCm 7.2's clang
+      // lowers __builtin_amdgcn_raw_buffer_load_b128 to a single dword load)
 #pragma unroll
       for (int k = 0; k < A; ++k)
-        hreg[sl][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (int)hv, so + 4 * k, 0));
+        hreg[sl][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (int)(hv + 4u * k), so, 0));
     }
   } else {
     const int a_src = valid ? a : blockIdx.x * P.EPB * D;   // idle lanes read a valid row
