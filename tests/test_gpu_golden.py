@@ -22,7 +22,10 @@ def test_kernel_replays_golden(name, precision):
     aux = kw.pop("aux", ())
     phys = Physics.PYB if kw.pop("physics", "dyn") == "pyb" else Physics.DYN
     sw = QuadSwarm(num_envs=mg.E, precision=precision, physics=phys, aux=aux, **kw)
-    np.testing.assert_allclose(sw.reset(mg.SEED).cpu().numpy(), GOLD[f"{name}/obs0"], atol=1e-7)
+    # reset obs: fp64 to float32 rounding; fp32 kernel within 2e-6 (hardware sin/cos of
+    # the Spiral phase, ~1e-6 absolute)
+    np.testing.assert_allclose(sw.reset(mg.SEED).cpu().numpy(), GOLD[f"{name}/obs0"],
+                               atol=1e-7 if precision == 8 else 2e-6)
     act = torch.zeros((mg.E, sw.num_drones, sw.act_dim), device=sw.device)
     steps = mg.STEPS if precision == 8 else 10   # fp32: short open-loop horizon
     atol = 2e-6 if precision == 8 else 2e-3
