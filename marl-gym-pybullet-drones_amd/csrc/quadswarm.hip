@@ -59,6 +59,7 @@ struct qs_handle {
   long long log_cap = 0;
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
+  int* rq = nullptr;            // deferred reset-search queue (2 + E ints), MultiHover layouts that can reject
   uint64_t seed = 0;
   bool reset_done = false;
   std::vector<double> orig_host;
@@ -74,6 +75,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.ep_len_sec = s.episode_len_sec;
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
   P.env_offset = s.env_offset;
+  P.reset_queue = h->rq;
   const double dt = 1.0 / s.pyb_freq;
   P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq); P.ctrl_hz = T(s.ctrl_freq);
   P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
@@ -111,6 +113,11 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
     ok = qs::launch_task<T, qs::kTaskMarl>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
   if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
+  if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none): one workgroup each
+    const int rgrid = P.E < 1024 ? P.E : 1024;
+    hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
+    HIP_TRY(hipGetLastError());
+  }
   return QS_OK;
 }
 
@@ -196,6 +203,18 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
     }
     for (int k = 0; k < 3; ++k) h->orig_host[i * 3 + k] = xyz[k];
   }
+  // MultiHover reset draws are rejected when two drones come within 0.5 m
+  // (MH:96-101).  The U(±0.25) noise moves a pair by < 0.5 per axis, so a layout
+  // whose every pair is >= 1 m apart in x or y never rejects (the bench's grid);
+  // otherwise (the reference's default diagonal layout) rejected envs are queued
+  // for reset_search_kernel instead of being searched inside the step.
+  bool may_reject = false;
+  if (s.task == QS_TASK_MULTIHOVER && s.num_drones <= qs::kResetMaxD)
+    for (int i = 0; i < s.num_drones; ++i)
+      for (int j = i + 1; j < s.num_drones; ++j)
+        if (std::fabs(h->orig_host[i * 3] - h->orig_host[j * 3]) < 1.0 &&
+            std::fabs(h->orig_host[i * 3 + 1] - h->orig_host[j * 3 + 1]) < 1.0)
+          may_reject = true;
   const size_t rs = (size_t)s.precision;
   const size_t N = d.num_agents;
   h->log_cap = std::max<long long>(1 << 16, 4LL * s.num_envs);
@@ -208,6 +227,10 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   hipError_t e7 = hipMalloc((void**)&h->log_count, sizeof(unsigned long long));
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
   if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
+  if (may_reject && getenv("QS_INKERNEL_RESET_SEARCH") == nullptr) {
+    if (hipMalloc((void**)&h->rq, sizeof(int) * (2 + (size_t)s.num_envs)) != hipSuccess) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
+    if (hipMemset(h->rq, 0, sizeof(int) * 2)) { cleanup(); return fail(QS_E_HIP, "qs_create: memset"); }
+  }
   if (s.precision == 8) {
     if (hipMemcpy(h->orig, h->orig_host.data(), 8 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }
   } else {
@@ -241,7 +264,7 @@ extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
   (void)hipSetDevice(h->device);   // teardown: best effort, nothing to report to
-  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->log_count, h->err, h->stamps};
+  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->log_count, h->err, h->stamps, h->rq};
   for (void* p : ptrs) if (p) (void)hipFree(p);
   delete h;
   return QS_OK;

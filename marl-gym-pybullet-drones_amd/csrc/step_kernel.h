@@ -217,6 +217,7 @@ template <class T> struct Params {
   unsigned long long* log_count;
   long long log_cap;
   int* err;               // [1] reset search overflow flag
+  int* reset_queue;       // deferred MultiHover reset searches: [0] count, [1] blocks done, [2..] env ids; or NULL
   int stage_rows;         // obs rows staged in LDS per pass
   unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
   // per-step I/O
@@ -359,6 +360,26 @@ template <class T> struct Shared {
   int32_t rec[kBlock * kEnvRec];   // per-env records on their way out
 };
 
+// Drone d's position for reset try `try_idx` (MultiHoverAviary.reset, MH:83-95):
+// the original layout plus U(-0.25, 0.25)³ noise, z clipped to [0.1, 1].
+template <class T>
+__device__ __forceinline__ void reset_candidate(const Params<T>& P, const T orig[3], int d, uint32_t try_idx,
+                                                uint32_t genv, uint32_t episode, T& px, T& py, T& pz) {
+  using F = M<T>;
+  U4 r = philox(U4{try_idx, genv, episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
+  T n0 = T(0.5) * u01<T>(r.x) - T(0.25), n1 = T(0.5) * u01<T>(r.y) - T(0.25), n2 = T(0.5) * u01<T>(r.z) - T(0.25);
+  px = F::add_rn(orig[0], n0);
+  py = F::add_rn(orig[1], n1);
+  pz = clampv(F::add_rn(orig[2], n2), T(0.1), T(1.0));
+}
+// MH:96-101 pair test: closer than 0.5 m (the same _rn operation order as the oracle).
+template <class T> __device__ __forceinline__ bool too_close(T ax, T ay, T az, T bx, T by, T bz) {
+  using F = M<T>;
+  T dx = F::sub_rn(ax, bx), dy = F::sub_rn(ay, by), dz = F::sub_rn(az, bz);
+  T ss = F::add_rn(F::add_rn(F::mul_rn(dx, dx), F::mul_rn(dy, dy)), F::mul_rn(dz, dz));
+  return F::sqrt_(ss) < T(0.5);
+}
+
 // Reset search (MultiHoverAviary.reset rejection loop, MH:83-102), group g
 // (= threads g*D .. g*D+D-1) evaluates `try_idx` for its env.
 // Writes cand positions for its group and flags rejection in s.reject[g].
@@ -368,12 +389,8 @@ __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3]
   using F = M<T>;
   const int tid = threadIdx.x;
   if (active) {
-    U4 r = philox(U4{try_idx, genv, episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
-    T n0 = T(0.5) * u01<T>(r.x) - T(0.25), n1 = T(0.5) * u01<T>(r.y) - T(0.25), n2 = T(0.5) * u01<T>(r.z) - T(0.25);
-    T px = F::add_rn(orig[0], n0);
-    T py = F::add_rn(orig[1], n1);
-    T pz = F::add_rn(orig[2], n2);
-    pz = clampv(pz, T(0.1), T(1.0));
+    T px, py, pz;
+    reset_candidate(P, orig, d, try_idx, genv, episode, px, py, pz);
     s.cand[tid][0] = px; s.cand[tid][1] = py; s.cand[tid][2] = pz;
   }
   __syncthreads();
@@ -381,13 +398,8 @@ __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3]
     const int base = g * P.D;
     T px = s.cand[tid][0], py = s.cand[tid][1], pz = s.cand[tid][2];
     bool bad = pz < T(0.1);
-    for (int j = d + 1; j < P.D; ++j) {
-      T dx = F::sub_rn(px, s.cand[base + j][0]);
-      T dy = F::sub_rn(py, s.cand[base + j][1]);
-      T dz = F::sub_rn(pz, s.cand[base + j][2]);
-      T ss = F::add_rn(F::add_rn(F::mul_rn(dx, dx), F::mul_rn(dy, dy)), F::mul_rn(dz, dz));
-      if (F::sqrt_(ss) < T(0.5)) bad = true;
-    }
+    for (int j = d + 1; j < P.D; ++j)
+      if (too_close(px, py, pz, s.cand[base + j][0], s.cand[base + j][1], s.cand[base + j][2])) bad = true;
     if (bad) s.reject[g] = 1;
   }
   __syncthreads();
@@ -1317,6 +1329,18 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       for (int k = 0; k < P.EPB; ++k) {
         if (!s.need[k]) continue;   // block-uniform (LDS)
         const int ek = blockIdx.x * P.EPB + k;
+        if (P.reset_queue) {
+          // deferred: reset_search_kernel (next launch, same stream) finds the first
+          // accepted try with a whole workgroup per env and rewrites the env's
+          // position, target and obs; try 0 stands in until then
+          if (tid == 0) {
+            const int slot = atomicAdd(&P.reset_queue[0], 1);
+            P.reset_queue[2 + slot] = ek;
+            s.need[k] = 0;
+          }
+          __syncthreads();
+          continue;
+        }
         const uint32_t genv_k = (uint32_t)(P.env_offset + ek);
         // episode number of env k lives in its drone-0 thread; broadcast via LDS
         __syncthreads();
@@ -1347,10 +1371,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       }
       if (do_reset) {
         uint32_t wt = (s.need[lenv] == 2) ? s.win_try[lenv] : 0u;
-        U4 r = philox(U4{wt, genv, (uint32_t)episode, (uint32_t)((STREAM_RESET << 24) | d)}, P.k0, P.k1);
-        init[0] = F::add_rn(orig[0], T(0.5) * u01<T>(r.x) - T(0.25));
-        init[1] = F::add_rn(orig[1], T(0.5) * u01<T>(r.y) - T(0.25));
-        init[2] = clampv(F::add_rn(orig[2], T(0.5) * u01<T>(r.z) - T(0.25)), T(0.1), T(1.0));
+        reset_candidate(P, orig, d, wt, genv, (uint32_t)episode, init[0], init[1], init[2]);
       }
     } else {
       if (do_reset) { init[0] = orig[0]; init[1] = orig[1]; init[2] = orig[2]; }
@@ -1428,6 +1449,80 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) SA.st(QS_F_TARGET + i, tgt[i]);
     }
+  }
+}
+
+
+// ------------------------------------------------- deferred reset search
+// MultiHoverAviary.reset's rejection loop (MH:83-102) for the envs the step
+// kernel queued (try 0 rejected).  A workgroup per queued env: thread t tests
+// try base + t as a whole candidate (all D drones, every pair), the smallest
+// accepted index wins — the sequential order of the reference loop and of the
+// in-kernel search, so the draws are bit-identical.  The last workgroup empties
+// the queue for the next launch.  D <= kResetMaxD.
+constexpr int kResetBlock = 256;
+constexpr int kResetMaxD = 8;
+template <class T>
+__global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) {
+  __shared__ int s_win;
+  int* const rq = P.reset_queue;
+  const int n = rq[0];
+  const int D = P.D;
+  T orig[kResetMaxD][3];
+#pragma unroll
+  for (int d = 0; d < kResetMaxD; ++d)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) orig[d][k] = d < D ? P.orig_xyz[d * 3 + k] : T(0);
+  for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+    const int e = rq[2 + idx];
+    const uint32_t genv = (uint32_t)(P.env_offset + e);
+    const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
+    uint32_t win = 0;
+    for (uint32_t base = 1;; base += kResetBlock) {
+      const uint32_t t = base + threadIdx.x;
+      bool ok = true;
+      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
+#pragma unroll
+      for (int d = 0; d < kResetMaxD; ++d) {
+        if (d < D && ok) {
+          reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
+          if (pz[d] < T(0.1)) ok = false;
+#pragma unroll
+          for (int j = 0; j < d; ++j)
+            if (too_close(px[j], py[j], pz[j], px[d], py[d], pz[d])) ok = false;
+        }
+      }
+      if (threadIdx.x == 0) s_win = 0x7fffffff;
+      __syncthreads();
+      if (ok) atomicMin(&s_win, (int)threadIdx.x);
+      __syncthreads();
+      const int w = s_win;
+      __syncthreads();   // s_win is rewritten next iteration
+      if (w != 0x7fffffff) { win = base + (uint32_t)w; break; }
+      if (base + kResetBlock >= kMaxResetTries) {
+        if (threadIdx.x == 0) atomicExch(P.err, 1);
+        break;   // win = 0, as the in-kernel search
+      }
+    }
+    if ((int)threadIdx.x < D) {
+      const int d = threadIdx.x;
+      T ix, iy, iz;
+      T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};
+      reset_candidate(P, od, d, win, genv, episode, ix, iy, iz);
+      const size_t a = (size_t)e * D + d, N = (size_t)P.N;
+      P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
+      P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
+      P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(d + 1));   // MH:106
+      if (P.obs) {
+        float* o = P.obs + a * (size_t)P.O;
+        o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&rq[1], 1) == (int)gridDim.x - 1) { rq[0] = 0; rq[1] = 0; }
   }
 }
 
