@@ -563,10 +563,12 @@ template <class T> __device__ T marl_reward(int task, const T (*p)[3], const T (
 // 30 Hz, Spiral 48 Hz): the substep count, history length and obs width are
 // then constants (fully unrolled substeps, constant obs offsets); CF = 0 reads
 // them from P.
-// AUX = false compiles out the ground-effect / drag / downwash forces (the
-// common P.aux == 0 case): a run-time force branch inside the unrolled substeps
-// cost 0.65 µs of the 10.5 µs C3 launch.
-template <class T, int TASK, int ACT, int CF, int PHYS, bool AUX>
+// AUXM selects the extra-force code: 0 compiles out the ground-effect / drag /
+// downwash forces (the common P.aux == 0 case: a run-time force branch inside
+// the unrolled substeps cost 0.65 µs of the 10.5 µs C3 launch); 1 = downwash
+// only (C5's PYB_DW), kept on the fp32 fast substep; 2 = any combination
+// through the general substep (the P.aux bits decide at run time).
+template <class T, int TASK, int ACT, int CF, int PHYS, int AUXM>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   using F = M<T>;
   constexpr int A = Act<ACT>::A;
@@ -645,7 +647,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   for (int i = 0; i < 4; ++i) q[i] = SA.ld(QS_F_QUAT + i);
   {   // last rpm: read only by the drag model (zero offset range otherwise: no traffic)
     SoA<T> LR = SA;
-    LR.voff = (AUX && (P.aux & QS_AUX_DRAG)) ? SA.voff : kOOB;
+    LR.voff = (AUXM != 0 && (P.aux & QS_AUX_DRAG)) ? SA.voff : kOOB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) lrpm[i] = LR.ld(QS_F_LAST_RPM + i);
   }
@@ -842,7 +844,31 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // gyroscopic term reduced with IXX == IYY, and the PYB world-frame exp map
     // applied as the equivalent right product q ⊗ exp(ω_body dt/2) (R(q)ω = q ω q*).
     // Same mathematics as the general path below; fp32 rounding only.
-    constexpr bool kFastSub = sizeof(T) == 4 && !AUX && CF != 0;
+    constexpr bool kFastSub = sizeof(T) == 4 && AUXM != 2 && CF != 0;
+    // _downwash (BaseAviary.py:798-811) for the fast substep: the body-z force of the
+    // drones above, from the neighbours' substep-start positions (LDS).  fp32 forms:
+    // (PROP_R/(4dz))² and (dxy/β)² from reciprocals (no square root), exp as exp2.
+    auto downwash_f32 = [&]() -> float {
+      __syncthreads();
+      s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
+      __syncthreads();
+      float f = 0.f;
+      if (valid) {
+        const int base = lenv * D;
+        for (int j = 0; j < D; ++j) {
+          const float dz = float(s.cand[base + j][2]) - float(pos[2]);
+          const float dx = float(s.cand[base + j][0]) - float(pos[0]), dy = float(s.cand[base + j][1]) - float(pos[1]);
+          const float d2 = dx * dx + dy * dy;
+          if (dz > 0.f && d2 < 100.f) {
+            const float r = __builtin_amdgcn_rcpf(dz);
+            const float alpha = float(cf2x::DW1 * (cf2x::PROP_R / 4) * (cf2x::PROP_R / 4)) * (r * r);
+            const float rb = __builtin_amdgcn_rcpf(float(cf2x::DW2) * dz + float(cf2x::DW3));
+            f -= alpha * __builtin_amdgcn_exp2f((d2 * (rb * rb)) * float(-0.5 / M_LN2));
+          }
+        }
+      }
+      return f;
+    };
     if constexpr (kFastSub) {
 #pragma clang fp contract(fast)
       constexpr double kDt = 1.0 / 240.0;   // CF != 0 ⇒ pyb_freq == 240 (step_launch_impl.h)
@@ -869,11 +895,16 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       };
       if constexpr (PHYS == QS_PHYS_PYB) {
         const float kd = float(kDt * kPybDamping);
-        const float g1 = thrust_z * dtm, g2 = 2.0f * g1, c8 = g1 - float(cf2x::GRAVITY * kDt / cf2x::M);
+        float g1 = thrust_z * dtm, g2 = 2.0f * g1, c8 = g1 - float(cf2x::GRAVITY * kDt / cf2x::M);
         const float bx = float(kDt / IXX) * pbx, by = float(kDt / IYY) * pby, bz = float(kDt / IZZ) * tz;
         constexpr float amax2 = float((0.25 * M_PI / kDt) * (0.25 * M_PI / kDt));
 #pragma unroll
         for (int sub = 0; sub < S; ++sub) {
+          if constexpr (AUXM == 1) {
+            g1 = (thrust_z + downwash_f32()) * dtm;
+            g2 = 2.0f * g1;
+            c8 = g1 - float(cf2x::GRAVITY * kDt / cf2x::M);
+          }
           const float x = q[0], y = q[1], z = q[2], qw = q[3];
           const float m = __builtin_fmaf(-kd, sqrtf(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]), 1.0f - kd);
           const float mw = __builtin_fmaf(-kd, sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]), 1.0f - kd);
@@ -913,10 +944,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         angv[1] = Rn[3] * w[0] + Rn[4] * w[1] + Rn[5] * w[2];
         angv[2] = Rn[6] * w[0] + Rn[7] * w[1] + Rn[8] * w[2];
       } else {
-        const float gk = thrust_z * s2 * dtm, c8 = (thrust_z - float(cf2x::GRAVITY)) * dtm;
+        float gk = thrust_z * s2 * dtm, c8 = (thrust_z - float(cf2x::GRAVITY)) * dtm;
         const float ax = float(kDt / IXX) * tx, ay = float(kDt / IYY) * ty, az = float(kDt / IZZ) * tz;
 #pragma unroll
         for (int sub = 0; sub < S; ++sub) {
+          if constexpr (AUXM == 1) {
+            const float zb = thrust_z + downwash_f32();
+            gk = zb * s2 * dtm;
+            c8 = (zb - float(cf2x::GRAVITY)) * dtm;
+          }
           const float x = q[0], y = q[1], z = q[2], qw = q[3];
           vel[0] = vel[0] + gk * (x * z + qw * y);
           vel[1] = vel[1] + gk * (y * z - qw * x);
@@ -968,7 +1004,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       const T sq = sizeof(T) == 8 ? T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) : s2;
       quat_to_zaxis_s(q, sq, R2, R5, R8);
       T zb = thrust_z, txe = 0, tye = 0, fwx = 0, fwy = 0, fwz = 0;
-      if (AUX && P.aux) {
+      if (AUXM != 0 && P.aux) {
         // no contraction here: the four ground-effect torque arms cancel exactly
         // for a level drone only in plain multiply-then-add arithmetic
 #pragma clang fp contract(off)

@@ -10,17 +10,20 @@ template <class T, int TASK, int ACT> static void launch_one(int grid, size_t ld
                                                              int ctrl_freq, int pyb_freq, int phys) {
   constexpr int kCF = TASK == QS_TASK_SPIRAL ? 48 : 30;   // SpiralAviary.py:28; MH:20 and the MARL tasks
   const bool cf = ctrl_freq == kCF && pyb_freq == 240;
-  // the default control frequency without extra forces is the hot configuration:
-  // fully compile-time (constant substeps/history, no force branch)
-  const bool aux = P.aux != 0;
+  // the default control frequency is compile-time (constant substeps/history);
+  // no extra forces / downwash only / general force set (step_kernel AUXM)
+  const int auxm = P.aux == 0 ? 0 : (P.aux == QS_AUX_DW ? 1 : 2);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, st, P); };
   if (phys == QS_PHYS_DYN) {
-    if (cf && !aux) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, false>), dim3(grid), dim3(kBlock), lds, st, P);
-    else if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, true>), dim3(grid), dim3(kBlock), lds, st, P);
-    else hipLaunchKernelGGL((step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN, true>), dim3(grid), dim3(kBlock), lds, st, P);
+    if (!cf) go(step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN, 2>);
+    else if (auxm == 0) go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, 0>);
+    else if (auxm == 1) go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, 1>);
+    else go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, 2>);
   } else {
-    if (cf && !aux) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, false>), dim3(grid), dim3(kBlock), lds, st, P);
-    else if (cf) hipLaunchKernelGGL((step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, true>), dim3(grid), dim3(kBlock), lds, st, P);
-    else hipLaunchKernelGGL((step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB, true>), dim3(grid), dim3(kBlock), lds, st, P);
+    if (!cf) go(step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB, 2>);
+    else if (auxm == 0) go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, 0>);
+    else if (auxm == 1) go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, 1>);
+    else go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_PYB, 2>);
   }
 }
 
