@@ -96,6 +96,18 @@ int qs_mlp_tanh_bwd(int64_t K, int32_t N, const float* dh, const float* dout, in
 int qs_mlp_sum_partials(int32_t G, int64_t P, const float* partial, float* d0, int64_t n0, float* d1, int64_t n1,
                         float* d2, void* stream);
 
+/* n (<= 16) qs_mlp_sum_partials reductions in one launch; argument i of each
+ * array describes task i exactly as the single-task call. */
+int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial,
+                              float* const* d0, const int64_t* n0, float* const* d1, const int64_t* n1,
+                              float* const* d2, void* stream);
+
+/* qs_adam_gated followed by qs_adam_commit, in one launch: `work` is a device
+ * uint32 counter, zero before the first call (the kernel leaves it zero). */
+int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step,
+                 float lr, float beta1, float beta2, float eps, const float* gate_val, float gate_thr, void* work,
+                 void* stream);
+
 const char* qs_learner_last_error(void);
 
 #ifdef __cplusplus

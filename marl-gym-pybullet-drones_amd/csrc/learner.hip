@@ -392,6 +392,83 @@ __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_partials_kernel(int G, l
   float* dst = j < n0 ? d0 + j : (j < n0 + n1 ? d1 + (j - n0) : d2 + (j - n0 - n1));
   *dst += t;
 }
+
+// Several partial-sum reductions in one launch (the bias and weight-gradient
+// sums of a whole minibatch backward): blocks [start[i], start[i+1]) serve task i.
+constexpr int kMlpMaxTasks = 16;
+struct MlpSumTask {
+  const float* partial;
+  float* d0;
+  float* d1;
+  float* d2;
+  long long P, n0, n1;
+  int G;
+};
+struct MlpSumTasks {
+  MlpSumTask t[kMlpMaxTasks];
+  int start[kMlpMaxTasks + 1];
+  int n;
+};
+__global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks tasks) {
+  constexpr int W = kMlpSumBlock / 64;
+  __shared__ float lds[W][64];
+  int ti = 0;
+  while (ti + 1 < tasks.n && (int)blockIdx.x >= tasks.start[ti + 1]) ++ti;
+  const MlpSumTask& T = tasks.t[ti];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long j = (long long)(blockIdx.x - tasks.start[ti]) * 64 + lane;
+  float t = 0.f;
+  if (j < T.P) {
+    int g = wv;
+    for (; g + 3 * W < T.G; g += 4 * W) {
+      const float a = T.partial[(size_t)g * T.P + j], b = T.partial[(size_t)(g + W) * T.P + j];
+      const float c = T.partial[(size_t)(g + 2 * W) * T.P + j], d = T.partial[(size_t)(g + 3 * W) * T.P + j];
+      t = (((t + a) + b) + c) + d;
+    }
+    for (; g < T.G; g += W) t += T.partial[(size_t)g * T.P + j];
+  }
+  lds[wv][lane] = t;
+  __syncthreads();
+  if (wv != 0 || j >= T.P) return;
+  t = lds[0][lane];
+  for (int k = 1; k < W; ++k) t += lds[k][lane];
+  float* dst = j < T.n0 ? T.d0 + j : (j < T.n0 + T.n1 ? T.d1 + (j - T.n0) : T.d2 + (j - T.n0 - T.n1));
+  *dst += t;
+}
+
+// torch.optim.Adam step and its step-count commit in one launch: every block
+// reads the count first; the last block to finish increments it (gate permitting).
+__global__ void adam_step_kernel(long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                 float* __restrict__ v, float* step, float lr, float b1, float b2, float eps,
+                                 const float* gate_val, float gate_thr, unsigned* done) {
+  __shared__ bool last;
+  if (gate_ok(gate_val, gate_thr)) {
+    const double t = (double)(*step) + 1.0;
+    const float bc1 = (float)(1.0 - pow((double)b1, t));
+    const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, t));
+    const float step_size = lr / bc1;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+      const float gi = g[i];
+      float mi = m[i];
+      mi = mi + (1.0f - b1) * (gi - mi);
+      float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+      m[i] = mi;
+      v[i] = vi;
+      const float denom = sqrtf(vi) / bc2_sqrt + eps;
+      p[i] = p[i] - step_size * (mi / denom);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *done = 0;
+    if (gate_ok(gate_val, gate_thr)) *step = *step + 1.0f;
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -531,6 +608,41 @@ int qs_mlp_sum_partials(int32_t G, int64_t P, const float* partial, float* d0, i
                      partial, d0, (long long)n0, d1, (long long)n1, d2);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials: ") + hipGetErrorString(e));
+}
+
+int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial,
+                              float* const* d0, const int64_t* n0, float* const* d1, const int64_t* n1,
+                              float* const* d2, void* stream) {
+  if (n <= 0 || n > kMlpMaxTasks || !G || !P || !partial || !d0 || !n0 || !d1 || !n1 || !d2)
+    return fail(QS_E_INVALID, "qs_mlp_sum_partials_multi: bad argument (1..16 tasks)");
+  MlpSumTasks T{};
+  T.n = n;
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (G[i] <= 0 || P[i] <= 0 || !partial[i] || !d0[i] || n0[i] <= 0 || n0[i] > P[i] || n1[i] < 0 ||
+        n0[i] + n1[i] > P[i] || (n0[i] < P[i] && !d1[i]) || (n0[i] + n1[i] < P[i] && !d2[i]))
+      return fail(QS_E_INVALID, "qs_mlp_sum_partials_multi: bad task");
+    T.t[i] = MlpSumTask{partial[i], d0[i], d1[i], d2[i], (long long)P[i], (long long)n0[i], (long long)n1[i], (int)G[i]};
+    T.start[i] = blocks;
+    blocks += (int)((P[i] + 63) / 64);
+  }
+  T.start[n] = blocks;
+  hipLaunchKernelGGL(mlp_sum_multi_kernel, dim3(blocks), dim3(kMlpSumBlock), 0, (hipStream_t)stream, T);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials_multi: ") + hipGetErrorString(e));
+}
+
+int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step, float lr,
+                 float beta1, float beta2, float eps, const float* gate_val, float gate_thr, void* work, void* stream) {
+  if (n <= 0 || !params || !grads || !exp_avg || !exp_avg_sq || !step || !work)
+    return fail(QS_E_INVALID, "qs_adam_step: bad argument");
+  const int block = 256;
+  long long grid = (n + block - 1) / block;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(adam_step_kernel, dim3((unsigned)grid), dim3(block), 0, (hipStream_t)stream, (long long)n, params,
+                     grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, gate_val, gate_thr, (unsigned*)work);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_step: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -61,6 +61,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            # include/qs_learner.h
            "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_ppo_heads_work_bytes",
            "qs_mlp_bias_tanh", "qs_mlp_bwd_blocks", "qs_mlp_tanh_bwd", "qs_mlp_sum_partials",
+           "qs_mlp_sum_partials_multi", "qs_adam_step",
            "qs_learner_last_error")
 
 _lib = None
@@ -109,6 +110,8 @@ def load():
     L.qs_mlp_bwd_blocks.argtypes = [i64]
     L.qs_mlp_tanh_bwd.argtypes = [i64, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp]
     L.qs_mlp_sum_partials.argtypes = [ctypes.c_int32, i64, vp, vp, i64, vp, i64, vp, vp]
+    L.qs_mlp_sum_partials_multi.argtypes = [ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.qs_adam_step.argtypes = [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, f32, vp, vp]
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):

@@ -74,6 +74,53 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_DEFER = None   # reductions queued while a minibatch backward runs (deferred_sums)
+
+
+def _sum_partials(G, P, part, d0, n0, d1=None, n1=0, d2=None):
+    """d += Σ_g part[g] (qs_mlp_sum_partials), or queued for one multi-task launch."""
+    if _DEFER is not None:
+        _DEFER.append((G, P, part, d0, n0, d1, n1, d2))
+        return
+    L.check(L.load().qs_mlp_sum_partials(G, P, L.ptr(part), L.ptr(d0), n0, L.ptr(d1), n1, L.ptr(d2), _stream()),
+            "qs_mlp_sum_partials")
+
+
+def _flush_sums(tasks):
+    lib = L.load()
+    for i in range(0, len(tasks), 16):   # qs_mlp_sum_partials_multi takes up to 16 tasks
+        chunk = tasks[i:i + 16]
+        n = len(chunk)
+        arr = lambda ct, vals: (ct * n)(*vals)
+        vp = ctypes.c_void_p
+        L.check(lib.qs_mlp_sum_partials_multi(
+            n, arr(ctypes.c_int32, [t[0] for t in chunk]), arr(ctypes.c_int64, [t[1] for t in chunk]),
+            arr(vp, [t[2].data_ptr() for t in chunk]), arr(vp, [t[3].data_ptr() for t in chunk]),
+            arr(ctypes.c_int64, [t[4] for t in chunk]),
+            arr(vp, [t[5].data_ptr() if t[5] is not None else None for t in chunk]),
+            arr(ctypes.c_int64, [t[6] for t in chunk]),
+            arr(vp, [t[7].data_ptr() if t[7] is not None else None for t in chunk]), _stream()),
+            "qs_mlp_sum_partials_multi")
+
+
+class deferred_sums:
+    """Within the block, the MLP backward's bias / weight-gradient reductions are
+    queued and issued as one qs_mlp_sum_partials_multi launch at exit (8 small
+    launches per PPO minibatch become one)."""
+
+    def __enter__(self):
+        global _DEFER
+        self._prev, _DEFER = _DEFER, []
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFER
+        tasks, _DEFER = _DEFER, self._prev
+        if exc[0] is None and tasks:
+            _flush_sums(tasks)
+        return False
+
+
 def _splitk_into(dst, dy, x):
     """dst += dyᵀ·x (a weight gradient) as S row-chunk GEMMs + a fixed-order sum."""
     K = x.shape[0]
@@ -82,8 +129,7 @@ def _splitk_into(dst, dy, x):
         dst.addmm_(dy.t(), x)
         return
     part = torch.bmm(dy.reshape(S, K // S, -1).transpose(1, 2), x.reshape(S, K // S, -1))
-    L.check(L.load().qs_mlp_sum_partials(S, part[0].numel(), L.ptr(part), L.ptr(dst), dst.numel(), None, 0, None,
-                                         _stream()), "qs_mlp_sum_partials")
+    _sum_partials(S, part[0].numel(), part, dst, dst.numel())
 
 
 class _TanhMLP3(torch.autograd.Function):
@@ -122,16 +168,14 @@ class _TanhMLP3(torch.autograd.Function):
         part = torch.empty((G, N2 * (1 + A) + A), device=x.device, dtype=torch.float32)
         L.check(lib.qs_mlp_tanh_bwd(K, N2, None, L.ptr(dout), A, L.ptr(w3), L.ptr(h2), L.ptr(dz2), L.ptr(part), st),
                 "qs_mlp_tanh_bwd")
-        L.check(lib.qs_mlp_sum_partials(G, part.shape[1], L.ptr(part), L.ptr(b2.grad), N2, L.ptr(w3.grad), A * N2,
-                                        L.ptr(b3.grad), st), "qs_mlp_sum_partials")
+        _sum_partials(G, part.shape[1], part, b2.grad, N2, w3.grad, A * N2, b3.grad)
         dh1 = torch.mm(dz2, w2)
         _splitk_into(w2.grad, dz2, h1)
         # first tanh (in place on dh1): b1 gradient
         part1 = torch.empty((G, N1), device=x.device, dtype=torch.float32)
         L.check(lib.qs_mlp_tanh_bwd(K, N1, L.ptr(dh1), None, 0, None, L.ptr(h1), L.ptr(dh1), L.ptr(part1), st),
                 "qs_mlp_tanh_bwd")
-        L.check(lib.qs_mlp_sum_partials(G, N1, L.ptr(part1), L.ptr(b1.grad), N1, None, 0, None, st),
-                "qs_mlp_sum_partials")
+        _sum_partials(G, N1, part1, b1.grad, N1)
         _splitk_into(w1.grad, dh1, x)
         dx = dh1 @ w1 if ctx.needs_input_grad[0] else None
         return dx, None, None, None, None, None, None
@@ -305,6 +349,7 @@ class FlatBuffers:
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.step = torch.zeros(1, device=dev)
+        self._adam_work = torch.zeros(1, dtype=torch.int32, device=dev)   # qs_adam_step's block counter
         self.offsets = []
         off = 0
         for p in self.params:
@@ -317,12 +362,13 @@ class FlatBuffers:
         self.lr, self.betas, self.eps = lr, betas, eps
 
     def adam(self, gate_val=None, gate_thr=0.0):
+        """One gated Adam step and its step-count commit (qs_adam_step, one launch)."""
         lib = L.load()
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        L.check(lib.qs_adam_gated(self.n, L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.exp_avg),
-                                  L.ptr(self.exp_avg_sq), L.ptr(self.step), self.lr, self.betas[0], self.betas[1],
-                                  self.eps, L.ptr(gate_val), float(gate_thr), st), "qs_adam_gated")
-        L.check(lib.qs_adam_commit(L.ptr(self.step), L.ptr(gate_val), float(gate_thr), st), "qs_adam_commit")
+        L.check(lib.qs_adam_step(self.n, L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.exp_avg),
+                                 L.ptr(self.exp_avg_sq), L.ptr(self.step), self.lr, self.betas[0], self.betas[1],
+                                 self.eps, L.ptr(gate_val), float(gate_thr), L.ptr(self._adam_work), st),
+                "qs_adam_step")
 
     # torch.optim.Adam state_dict format (checkpoint compatibility, MP:203-229)
     def state_dict(self):
@@ -476,7 +522,8 @@ class MAPPOAgent:
                                  L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), st), "qs_ppo_heads")
-        torch.autograd.backward([mean, v], [self._dmean, self._dv])
+        with deferred_sums():
+            torch.autograd.backward([mean, v], [self._dmean, self._dv])
         if world > 1 or self._force_allreduce:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)

@@ -88,10 +88,18 @@ def test_fused_tanh_mlp_matches_autograd(rows, din, hidden, A):
     for p, w in zip(net.parameters(), want):
         scale = float(w.abs().max())
         torch.testing.assert_close(p.grad - 0.25, w, rtol=1e-4, atol=1e-5 * scale + 1e-7)
-    # a graph replay gives bit-identical gradients (fixed-order reductions)
+    # a rerun gives bit-identical gradients (fixed-order reductions), also with the
+    # reductions deferred into one multi-task launch (the learner's minibatch path)
     grads = [p.grad.clone() for p in net.parameters()]
     for p in net.parameters():
         p.grad.fill_(0.25)
     net(x).backward(g)
+    for p, q in zip(net.parameters(), grads):
+        assert torch.equal(p.grad, q)
+    from gym_pybullet_drones_amd.mappo.agent import deferred_sums
+    for p in net.parameters():
+        p.grad.fill_(0.25)
+    with deferred_sums():
+        net(x).backward(g)
     for p, q in zip(net.parameters(), grads):
         assert torch.equal(p.grad, q)
