@@ -428,6 +428,7 @@ class MAPPOAgent:
         self.actor_lr, self.critic_lr = actor_lr, critic_lr
         self._opt_ready = False
         self._graph = None
+        self._g_k = 0
         self.to(self.device)
 
     # ------------------------------------------------------------ plumbing
@@ -561,12 +562,19 @@ class MAPPOAgent:
         else:
             self._iteration(rollouts.sample(idx), acc)
 
-    def _capture(self, rollouts):
-        """Capture one update iteration as a HIP graph over static index/accumulator tensors."""
+    @staticmethod
+    def _chunk(nmb, cap=128):
+        """Minibatch iterations per captured graph: the largest divisor of nmb <= cap."""
+        return max(k for k in range(1, min(nmb, cap) + 1) if nmb % k == 0)
+
+    def _capture(self, rollouts, k=1):
+        """Capture k consecutive update iterations as one HIP graph over a static
+        index buffer (k minibatch slices) and accumulator."""
         mb = self.mini_batch_size
-        self._g_idx = torch.zeros(mb, dtype=torch.long, device=self.device)
+        self._g_perm = torch.zeros(k * mb, dtype=torch.long, device=self.device)
+        self._g_idx = self._g_perm[:mb]
         self._g_acc = torch.zeros(4, dtype=torch.float64, device=self.device)
-        self._g_rollouts = rollouts
+        self._g_rollouts, self._g_k = rollouts, k
         # warm-up on a side stream (torch.cuda.graph requirement), with a snapshot/restore of
         # the parameters and optimizer state so the warm-up leaves no trace
         snap = [t.clone() for t in (self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq,
@@ -580,7 +588,8 @@ class MAPPOAgent:
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._step_minibatch(rollouts, self._g_idx, self._g_acc)
+            for i in range(k):
+                self._step_minibatch(rollouts, self._g_perm[i * mb:(i + 1) * mb], self._g_acc)
         for t, v in zip((self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq, self.actor_opt.step,
                          self.critic_opt.flat, self.critic_opt.exp_avg, self.critic_opt.exp_avg_sq,
                          self.critic_opt.step), snap):
@@ -588,27 +597,31 @@ class MAPPOAgent:
         self._graph = g
 
     def update(self, rollouts, device='cuda', generator=None):
-        """AG:702-772: opt_epochs × minibatches; per-epoch means of the loss stats."""
+        """AG:702-772: opt_epochs × minibatches; per-epoch means of the loss stats.
+        With graphs, a replay runs k minibatch iterations (one index copy and one
+        graph launch per k minibatches)."""
         results = defaultdict(list)
         total_steps = rollouts.max_length * rollouts.batch_size
-        num_mini_batch = total_steps // self.mini_batch_size
+        mb = self.mini_batch_size
+        num_mini_batch = total_steps // mb
         assert num_mini_batch != 0, 'num_mini_batch is 0'
         graphs = self.use_graphs and self.device.type == 'cuda' and (_dist_world() == 1 or self.graph_collectives)
-        if graphs and (self._graph is None or self._g_rollouts is not rollouts):
-            self._capture(rollouts)
+        k = self._chunk(num_mini_batch)
+        if graphs and (self._graph is None or self._g_rollouts is not rollouts or self._g_k != k):
+            self._capture(rollouts, k)
         per_epoch = []
         for epoch in range(self.opt_epochs):
             perm = torch.randperm(total_steps, device=self.device, generator=generator)
             if graphs:
                 self._g_acc.zero_()
-                for i in range(num_mini_batch):
-                    self._g_idx.copy_(perm[i * self.mini_batch_size:(i + 1) * self.mini_batch_size])
+                for c in range(num_mini_batch // k):
+                    self._g_perm.copy_(perm[c * k * mb:(c + 1) * k * mb])
                     self._graph.replay()
                 per_epoch.append(self._g_acc.clone())
             else:
                 acc = torch.zeros(4, dtype=torch.float64, device=self.device)
                 for i in range(num_mini_batch):
-                    self._step_minibatch(rollouts, perm[i * self.mini_batch_size:(i + 1) * self.mini_batch_size], acc)
+                    self._step_minibatch(rollouts, perm[i * mb:(i + 1) * mb], acc)
                 per_epoch.append(acc)
         stats = (torch.stack(per_epoch) / num_mini_batch).cpu()   # one host sync per update
         for j, k in enumerate(['policy_loss', 'value_loss', 'entropy_loss', 'approx_kl']):
