@@ -434,6 +434,18 @@ template <class V> __device__ __forceinline__ void nt_store(V* p, V v) {
   if constexpr (QS_NT_OBS) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f3v __attribute__((ext_vector_type(3)));
+// A consecutive floats (A-aligned row of [N][A]) as one non-temporal vector store.
+template <int A> __device__ __forceinline__ void store_act(float* p, const float* v) {
+  if constexpr (A == 4) nt_store(reinterpret_cast<f4v*>(p), f4v{v[0], v[1], v[2], v[3]});
+  else if constexpr (A == 2) nt_store(reinterpret_cast<f2v*>(p), f2v{v[0], v[1]});
+  else if constexpr (A == 3) { nt_store(reinterpret_cast<f2v*>(p), f2v{v[0], v[1]}); nt_store(p + 2, v[2]); }
+  else {
+#pragma unroll
+    for (int k = 0; k < A; ++k) nt_store(p + k, v[k]);
+  }
+}
 
 // Raw-buffer access to the SoA state: descriptor over the whole [F][N] array
 // (wave-uniform, from kernel arguments), field base in soffset (SGPR), lane's
@@ -806,13 +818,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // with the history LDS-DMA (issued last) still streaming.
     wait_vm0();
     if (valid) {
-      if (P.act_out) {
-#pragma unroll
-        for (int k = 0; k < A; ++k) nt_store(P.act_out + (size_t)a * A + k, act[k]);
-      }
+      // one vector store per lane for the A components (a wave writes whole
+      // lines; per-component dword stores left 16-B-strided partial lines)
+      if (P.act_out) store_act<A>(P.act_out + (size_t)a * A, act);
       // action_buffer.append(action) (BaseRLAviary.py:187): ring slot total % H
-#pragma unroll
-      for (int k = 0; k < A; ++k) nt_store(P.hist + ((size_t)wslot * N + a) * A + k, act[k]);
+      store_act<A>(P.hist + ((size_t)wslot * N + a) * A, act);
       if constexpr (kPid) {   // PID integrators are final: store now, drains under the substeps
 #pragma unroll
         for (int i = 0; i < 9; ++i) SA.st(QS_F_PID_INT_POS + i, pid[i]);
@@ -1428,7 +1438,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
   QS_STAMP(5);
   // ---------------- obs output
+#ifdef QS_X_NOOBS
+  if (false) {
+#else
   if (P.obs) {
+#endif
     if (P.mode == MODE_RESET_MASK) {
       if (valid && do_reset) write_obs_row(P.obs + (size_t)a * O, obs_sc);
     } else {
