@@ -256,3 +256,32 @@ def test_no_autoreset_facade():
     z = obs[:, 2]
     assert (z < 0.03).any()
     env.close()
+
+
+@pytest.mark.parametrize("precision", [8, 4])
+def test_deferred_reset_search_matches_inkernel(precision, monkeypatch):
+    """The MultiHover reset rejection search queued to reset_search_kernel (layouts
+    that can reject, e.g. the reference's default diagonal layout) draws exactly
+    what the in-kernel sequential search draws: state and obs bit-identical over a
+    rollout with many resets (random RPM actions end episodes every ~20 steps)."""
+    from gym_pybullet_drones_amd.envs import QuadSwarm
+    cfg = dict(task="multihover", num_drones=4, act="rpm")
+    runs = []
+    for inkernel in (False, True):
+        if inkernel:
+            monkeypatch.setenv("QS_INKERNEL_RESET_SEARCH", "1")
+        sw = QuadSwarm(num_envs=96, precision=precision, **cfg)
+        obs = [sw.reset(9).cpu().numpy()]
+        n_done = 0
+        for _ in range(60):
+            r = sw.step(None)
+            obs.append(r.obs.cpu().numpy())
+            n_done += int((r.terminated | r.truncated).sum())
+        torch.cuda.synchronize()
+        runs.append((np.stack(obs), sw.get_state(0).cpu().numpy(), sw.get_state(1).cpu().numpy(), n_done))
+        assert sw.reset_error() == 0
+        sw.close()
+        monkeypatch.delenv("QS_INKERNEL_RESET_SEARCH", raising=False)
+    assert runs[0][3] > 50   # resets happened
+    for a, b in zip(runs[0][:3], runs[1][:3]):
+        np.testing.assert_array_equal(a, b)
