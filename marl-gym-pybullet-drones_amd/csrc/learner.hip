@@ -459,10 +459,9 @@ __global__ void adam_step_kernel(long long n, float* __restrict__ p, const float
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(done, 1u) == gridDim.x - 1;
-  }
+  // no fence: nothing is handed over but the arrival count (every block read
+  // *step before counting itself; p/m/v are read by later launches only)
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (last && threadIdx.x == 0) {
     *done = 0;

@@ -114,7 +114,7 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
   if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none): one workgroup each
-    const int rgrid = P.E < 1024 ? P.E : 1024;
+    const int rgrid = 1024;   // several workgroups per queued env when few are queued
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }
@@ -228,8 +228,13 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
   if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
   if (may_reject && getenv("QS_INKERNEL_RESET_SEARCH") == nullptr) {
-    if (hipMalloc((void**)&h->rq, sizeof(int) * (2 + (size_t)s.num_envs)) != hipSuccess) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
-    if (hipMemset(h->rq, 0, sizeof(int) * 2)) { cleanup(); return fail(QS_E_HIP, "qs_create: memset"); }
+    const size_t qn = 2 + 3 * (size_t)s.num_envs;   // count, done, env ids, per-slot best try, stopped count
+    if (hipMalloc((void**)&h->rq, sizeof(int) * qn) != hipSuccess) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
+    if (hipMemset(h->rq, 0, sizeof(int) * (2 + (size_t)s.num_envs)) ||
+        hipMemset(h->rq + 2 + s.num_envs, 0x7f, sizeof(int) * (size_t)s.num_envs) ||   // qs::kResetNone
+        hipMemset(h->rq + 2 + 2 * (size_t)s.num_envs, 0, sizeof(int) * (size_t)s.num_envs)) {
+      cleanup(); return fail(QS_E_HIP, "qs_create: memset");
+    }
   }
   if (s.precision == 8) {
     if (hipMemcpy(h->orig, h->orig_host.data(), 8 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }

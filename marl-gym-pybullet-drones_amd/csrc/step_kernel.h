@@ -346,7 +346,7 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T 
 
 // --------------------------------------------------- LDS workspace layout
 template <class T> struct Shared {
-  T cand[kBlock][3];        // reset candidates / downwash snapshot / MARL-task positions
+  alignas(16) T cand[kBlock][3];   // reset candidates / downwash snapshot (fp32: float4 per drone) / MARL-task positions
   T velw[kBlock][3];        // MARL-task velocities (Flock alignment and speed)
   T rew[kBlock];            // per-drone reward terms
   uint8_t bits[kBlock];     // per-drone termination reason bits
@@ -558,6 +558,47 @@ template <class T> __device__ T marl_reward(int task, const T (*p)[3], const T (
   }
   return total;
 }
+// ------------------------------------------------------ fp32 downwash terms
+// _downwash (BaseAviary.py:798-811) on a drone dz below a neighbour at
+// horizontal distance² d2: α·exp(−½(dxy/β)²), α = DW1·(PROP_R/(4dz))²,
+// β = DW2·dz + DW3.  fp32: reciprocals instead of divisions, exp as exp2.
+__device__ __forceinline__ float dw_term(float dz, float d2) {
+  const float r = __builtin_amdgcn_rcpf(dz);
+  const float alpha = float(cf2x::DW1 * (cf2x::PROP_R / 4) * (cf2x::PROP_R / 4)) * (r * r);
+  const float rb = __builtin_amdgcn_rcpf(float(cf2x::DW2) * dz + float(cf2x::DW3));
+  return alpha * __builtin_amdgcn_exp2f((d2 * (rb * rb)) * float(-0.5 / M_LN2));
+}
+// DPP row_ror:K — a lane reads lane (i − K) mod 16 of its 16-lane row.
+template <int K> __device__ __forceinline__ float row_ror(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + K, 0xF, 0xF, false));
+}
+// D = 16: an env is one DPP row.  The pair term depends on |Δz| and Δxy² only,
+// so each unordered pair is formed once: for K = 1..7 a lane forms the pair with
+// its row neighbour K away, keeps the term when that drone is above it and hands
+// it back (row_ror 16−K) when it is below; the K = 8 pairs are seen from both
+// ends and each end keeps what is its own.  8 pair terms per drone instead of
+// 16, no LDS, no barrier; the sum order differs from the reference's j loop
+// (fp32 rounding only).
+template <int K> __device__ __forceinline__ void dw16_pair(float px, float py, float pz, float& f) {
+  const float qx = row_ror<K>(px), qy = row_ror<K>(py), qz = row_ror<K>(pz);
+  const float dz = qz - pz, dx = qx - px, dy = qy - py;
+  const float d2 = dx * dx + dy * dy;
+  const bool near = d2 < 100.f;
+  const float t = dw_term(fabsf(dz), d2);
+  f = (near && dz > 0.f) ? f - t : f;
+  if constexpr (K < 8) {
+    const float back = row_ror<16 - K>((near && dz < 0.f) ? t : 0.f);
+    f = f - back;
+  }
+}
+__device__ __forceinline__ float downwash16(float px, float py, float pz) {
+  float f = 0.f;
+  dw16_pair<1>(px, py, pz, f); dw16_pair<2>(px, py, pz, f); dw16_pair<3>(px, py, pz, f);
+  dw16_pair<4>(px, py, pz, f); dw16_pair<5>(px, py, pz, f); dw16_pair<6>(px, py, pz, f);
+  dw16_pair<7>(px, py, pz, f); dw16_pair<8>(px, py, pz, f);
+  return f;
+}
+
 #ifdef QS_STAMPS_BUILD
 #define QS_STAMP(k)                                                                         \
   do {                                                                                      \
@@ -856,25 +897,26 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // Same mathematics as the general path below; fp32 rounding only.
     constexpr bool kFastSub = sizeof(T) == 4 && AUXM != 2 && CF != 0;
     // _downwash (BaseAviary.py:798-811) for the fast substep: the body-z force of the
-    // drones above, from the neighbours' substep-start positions (LDS).  fp32 forms:
-    // (PROP_R/(4dz))² and (dxy/β)² from reciprocals (no square root), exp as exp2.
+    // drones above, from the neighbours' substep-start positions.  D = 16 through
+    // DPP (downwash16); otherwise one float4 per drone in LDS, four neighbours in
+    // flight, the pair test as a select (no branch in the unrolled loop).
     auto downwash_f32 = [&]() -> float {
+      const float px = float(pos[0]), py = float(pos[1]), pz = float(pos[2]);
+      if (D == 16) return downwash16(px, py, pz);   // wave-uniform
+      float4* const nb = reinterpret_cast<float4*>(&s.cand[0][0]);
       __syncthreads();
-      s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
+      nb[tid] = make_float4(px, py, pz, 0.f);
       __syncthreads();
       float f = 0.f;
       if (valid) {
-        const int base = lenv * D;
+        const float4* const en = nb + lenv * D;
+#pragma unroll 4
         for (int j = 0; j < D; ++j) {
-          const float dz = float(s.cand[base + j][2]) - float(pos[2]);
-          const float dx = float(s.cand[base + j][0]) - float(pos[0]), dy = float(s.cand[base + j][1]) - float(pos[1]);
+          const float4 q4 = en[j];
+          const float dz = q4.z - pz, dx = q4.x - px, dy = q4.y - py;
           const float d2 = dx * dx + dy * dy;
-          if (dz > 0.f && d2 < 100.f) {
-            const float r = __builtin_amdgcn_rcpf(dz);
-            const float alpha = float(cf2x::DW1 * (cf2x::PROP_R / 4) * (cf2x::PROP_R / 4)) * (r * r);
-            const float rb = __builtin_amdgcn_rcpf(float(cf2x::DW2) * dz + float(cf2x::DW3));
-            f -= alpha * __builtin_amdgcn_exp2f((d2 * (rb * rb)) * float(-0.5 / M_LN2));
-          }
+          const float t = dw_term(dz, d2);
+          f = (dz > 0.f && d2 < 100.f) ? f - t : f;
         }
       }
       return f;
@@ -1505,30 +1547,55 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
 // ------------------------------------------------- deferred reset search
 // MultiHoverAviary.reset's rejection loop (MH:83-102) for the envs the step
-// kernel queued (try 0 rejected).  A workgroup per queued env: thread t tests
-// try base + t as a whole candidate (all D drones, every pair), the smallest
-// accepted index wins — the sequential order of the reference loop and of the
-// in-kernel search, so the draws are bit-identical.  The last workgroup empties
-// the queue for the next launch.  D <= kResetMaxD.
+// kernel queued (try 0 rejected).  Queue (int32): [0] count, [1] blocks done,
+// [2, 2+E) env ids, then per queue slot the best accepted try so far (win) and
+// the number of workgroups that stopped searching it.
+// B = gridDim / count workgroups share an env: workgroup j tests chunks
+// j, j+B, j+2B, … of 256 tries (thread t: try 1 + 256·chunk + t, a whole
+// candidate), publishes its smallest accepted try with atomicMin and stops, and
+// stops as well once the best try is below its next chunk.  When all B have
+// stopped every chunk below the best try has been tested, so it is the first
+// accepted try of the sequential loop; the last one to stop writes the env's
+// position, target and obs row.  The last workgroup of the launch empties the
+// queue.  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
 constexpr int kResetMaxD = 8;
+constexpr int kResetNone = 0x7f7f7f7f;   // "no accepted try yet" (the queue's memset byte 0x7f)
 template <class T>
 __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) {
-  __shared__ int s_win;
+  __shared__ int s_win, s_best;
+  __shared__ bool s_last;
   int* const rq = P.reset_queue;
   const int n = rq[0];
-  const int D = P.D;
+  if (n == 0) return;   // nothing queued (the usual step): the queue is empty already
+  const int D = P.D, E = P.E;
+  int* const qwin = rq + 2 + E;
+  int* const qstop = qwin + E;
   T orig[kResetMaxD][3];
 #pragma unroll
   for (int d = 0; d < kResetMaxD; ++d)
 #pragma unroll
     for (int k = 0; k < 3; ++k) orig[d][k] = d < D ? P.orig_xyz[d * 3 + k] : T(0);
-  for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+  const int G = gridDim.x;
+  const int B = n > 0 && n <= G ? G / n : 1;            // workgroups per env
+  const int first = n <= G ? (int)blockIdx.x % (n > 0 ? n : 1) : (int)blockIdx.x;
+  const int j = n <= G ? (int)blockIdx.x / (n > 0 ? n : 1) : 0;
+  const bool active = n > 0 && (n > G || (int)blockIdx.x < n * B);
+  for (int idx = first; active && idx < n; idx += (n <= G ? n : G)) {
     const int e = rq[2 + idx];
     const uint32_t genv = (uint32_t)(P.env_offset + e);
     const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
-    uint32_t win = 0;
-    for (uint32_t base = 1;; base += kResetBlock) {
+    for (uint32_t c = (uint32_t)j;; c += (uint32_t)B) {
+      const uint32_t base = 1u + c * kResetBlock;
+      // the best try so far, read once for the workgroup: the exit must be
+      // workgroup-uniform (the body holds barriers); a stale value only delays it
+      if (threadIdx.x == 0) s_best = __hip_atomic_load(&qwin[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if ((int)base > s_best) break;
+      if (base >= kMaxResetTries) {
+        if (threadIdx.x == 0) atomicExch(P.err, 1);
+        break;
+      }
       const uint32_t t = base + threadIdx.x;
       bool ok = true;
       T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
@@ -1538,42 +1605,56 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
           reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
           if (pz[d] < T(0.1)) ok = false;
 #pragma unroll
-          for (int j = 0; j < d; ++j)
-            if (too_close(px[j], py[j], pz[j], px[d], py[d], pz[d])) ok = false;
+          for (int i = 0; i < d; ++i)
+            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
         }
       }
-      if (threadIdx.x == 0) s_win = 0x7fffffff;
+      if (threadIdx.x == 0) s_win = kResetNone;
       __syncthreads();
-      if (ok) atomicMin(&s_win, (int)threadIdx.x);
+      if (ok) atomicMin(&s_win, (int)t);
       __syncthreads();
       const int w = s_win;
-      __syncthreads();   // s_win is rewritten next iteration
-      if (w != 0x7fffffff) { win = base + (uint32_t)w; break; }
-      if (base + kResetBlock >= kMaxResetTries) {
-        if (threadIdx.x == 0) atomicExch(P.err, 1);
-        break;   // win = 0, as the in-kernel search
+      __syncthreads();   // s_win is rewritten next chunk
+      if (w != kResetNone) {
+        if (threadIdx.x == 0) atomicMin(&qwin[idx], w);
+        break;            // this workgroup's later chunks hold only larger tries
       }
     }
-    if ((int)threadIdx.x < D) {
-      const int d = threadIdx.x;
-      T ix, iy, iz;
-      T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};
-      reset_candidate(P, od, d, win, genv, episode, ix, iy, iz);
-      const size_t a = (size_t)e * D + d, N = (size_t)P.N;
-      P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
-      P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
-      P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(d + 1));   // MH:106
-      if (P.obs) {
-        float* o = P.obs + a * (size_t)P.O;
-        o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
-      }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // the atomicMin above is performed before this workgroup counts itself
+      // stopped; both are atomics, so no fence (≈3.5 µs each, MI355X_MICROARCH.md)
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s_last = atomicAdd(&qstop[idx], 1) == B - 1;
+      // the last to stop reads the best try with an atomic read-modify-write,
+      // which returns the coherent value (a cached load may be stale)
+      if (s_last) s_best = atomicOr(&qwin[idx], 0);
     }
+    __syncthreads();
+    if (s_last) {   // every workgroup of this env has stopped: s_best is the first accepted try
+      const int wv = s_best;
+      const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;   // cap reached: try 0, as the in-kernel search
+      if ((int)threadIdx.x < D) {
+        const int d = threadIdx.x;
+        T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};
+        T ix, iy, iz;
+        reset_candidate(P, od, d, win, genv, episode, ix, iy, iz);
+        const size_t a = (size_t)e * D + d, N = (size_t)P.N;
+        P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
+        P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
+        P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(d + 1));   // MH:106
+        if (P.obs) {
+          float* o = P.obs + a * (size_t)P.O;
+          o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
+        }
+      }
+      if (threadIdx.x == 0) { qwin[idx] = kResetNone; qstop[idx] = 0; }   // ready for the next launch
+    }
+    __syncthreads();
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&rq[1], 1) == (int)gridDim.x - 1) { rq[0] = 0; rq[1] = 0; }
-  }
+  // every workgroup read n before counting itself: the last one empties the queue
+  if (threadIdx.x == 0 && atomicAdd(&rq[1], 1) == G - 1) { rq[0] = 0; rq[1] = 0; }
 }
 
 }  // namespace qs
