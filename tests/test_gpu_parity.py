@@ -258,22 +258,24 @@ def test_no_autoreset_facade():
     env.close()
 
 
-@pytest.mark.parametrize("precision", [8, 4])
-def test_deferred_reset_search_matches_inkernel(precision, monkeypatch):
+@pytest.mark.parametrize("precision,num_envs,steps", [(8, 96, 60), (4, 96, 60), (4, 2304, 30)])
+def test_deferred_reset_search_matches_inkernel(precision, num_envs, steps, monkeypatch):
     """The MultiHover reset rejection search queued to reset_search_kernel (layouts
     that can reject, e.g. the reference's default diagonal layout) draws exactly
     what the in-kernel sequential search draws: state and obs bit-identical over a
-    rollout with many resets (random RPM actions end episodes every ~20 steps)."""
+    rollout with many resets (random RPM actions end episodes every ~20 steps).
+    96 envs: several workgroups share each queued env; 2304 envs: the reset queues
+    more envs than the search launch has workgroups (one workgroup walks several)."""
     from gym_pybullet_drones_amd.envs import QuadSwarm
     cfg = dict(task="multihover", num_drones=4, act="rpm")
     runs = []
     for inkernel in (False, True):
         if inkernel:
             monkeypatch.setenv("QS_INKERNEL_RESET_SEARCH", "1")
-        sw = QuadSwarm(num_envs=96, precision=precision, **cfg)
+        sw = QuadSwarm(num_envs=num_envs, precision=precision, **cfg)
         obs = [sw.reset(9).cpu().numpy()]
         n_done = 0
-        for _ in range(60):
+        for _ in range(steps):
             r = sw.step(None)
             obs.append(r.obs.cpu().numpy())
             n_done += int((r.terminated | r.truncated).sum())
@@ -282,6 +284,6 @@ def test_deferred_reset_search_matches_inkernel(precision, monkeypatch):
         assert sw.reset_error() == 0
         sw.close()
         monkeypatch.delenv("QS_INKERNEL_RESET_SEARCH", raising=False)
-    assert runs[0][3] > 50   # resets happened
+    assert runs[0][3] > (50 if num_envs < 1024 else 0)   # resets happened
     for a, b in zip(runs[0][:3], runs[1][:3]):
         np.testing.assert_array_equal(a, b)
