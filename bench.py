@@ -7,20 +7,32 @@ actions drawn in-kernel), obs written into an on-device rollout
 buffer slot each step.  A "step" = one control step of every env on the rank
 (one fused HIP launch: action→PID→8 substeps→obs/reward/done/auto-reset).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-envs are sharded (weak scaling, 16 384 envs per rank, global env ids offset by
-rank) with no data-path collective; value = all ranks' agent-steps ÷ max-over-
-ranks wall time.
+Steady state: after the reset the envs' episode clocks are staggered uniformly
+over the 242-step MultiHover episode (578 for Spiral), as in a long-running
+vectorised rollout whose envs have drifted apart, so any timed window of K steps
+holds K/242 of the envs' truncations and auto-resets.  The default K = 484 is two
+full episodes; `--steps K` is honoured exactly.
+
+Multi-GPU: `python bench.py --gpus N` (no WORLD_SIZE in the environment) starts
+`torch.distributed.run --nproc-per-node N` on this script as a child process
+before anything touches a GPU, and exits with its status; under torchrun (the
+driver's form) each rank runs directly.  Envs are sharded (weak scaling, 16 384
+envs per rank, global env ids offset by rank) with no data-path collective;
+value = all ranks' agent-steps ÷ max-over-ranks wall time.
 
 Extra JSON fields:
   pyb           the same rollout under Physics.PYB (the kernel's restatement of
-                Bullet's step, the reference's training default): agent-steps/s,
-                kernel ms and roofline fraction (same algorithmic bytes).
-  mappo         full MAPPO on the same C3 envs (BASELINE config 3): agent-steps/s of
-                MAPPO.train_step = T-step rollout with the shared actor + simulator,
+                Bullet's step, the reference's training default).
+  mappo         full MAPPO on the same C3 envs (BASELINE config 3) with the
+                reference's rollout length T = 256 (learn_mappo.py:665): agent-steps/s
+                of MAPPO.train_step = T-step rollout with the shared actor + simulator,
                 last value, GAE, advantage normalisation and the PPO update
-                (opt_epochs x minibatches, centralized critic) — SURVEY §8(d)'s
-                "full MAPPO" figure; with N ranks the gradients are all-reduced.
+                (10 epochs x T·E/mini_batch_size minibatches, centralized critic) —
+                SURVEY §8(d)'s "full MAPPO" figure; with N ranks the gradients are
+                all-reduced.  `learner_roofline`: the update's algorithmic fp32 FLOP
+                (MLP forward + backward, counted in DESIGN.md §4c) ÷ its device time
+                vs the 157.3 TFLOP/s fp32 MFMA peak.
+  mappo_t32     the same with T = 32 (round-1 leg, kept for comparison).
   roofline      the step kernel: §8(d) algorithmic bytes per agent-step (418 B,
                 C3 ONE_D_PID) × agents per launch ÷ mean launch time from HIP
                 events on the launch stream, vs 8 TB/s.
@@ -35,6 +47,8 @@ Extra JSON fields:
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -49,26 +63,47 @@ from gym_pybullet_drones_amd.envs.swarm import grid_layout  # noqa: E402
 METRIC = "agent-steps/sec, MultiHover 8-drone MAPPO @ 1/2/4/8 GPU vs PyBullet CPU"
 BYTES_PER_AGENT_STEP = {"one_d_pid": 418.0, "vel": 790.0, "rpm": 720.0}
 HBM_PEAK_GBS = 8000.0
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector rate
+EPISODE_STEPS = {"multihover": 242, "spiral": 578}   # SURVEY §8 derived sizes
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--steps", type=int, default=484, help="timed control steps (default: two MultiHover episodes)")
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs", type=int, default=16384, help="envs per GPU")
     p.add_argument("--drones", type=int, default=8)
     p.add_argument("--act", default="one_d_pid")
     p.add_argument("--slots", type=int, default=32, help="rollout-buffer slots the obs ring cycles through")
+    p.add_argument("--no-stagger", action="store_true", help="start every env at episode step 0")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--mappo", type=int, default=1, help="also time full MAPPO train steps (0 = skip)")
     p.add_argument("--pyb", type=int, default=1, help="also time the rollout under Physics.PYB (0 = skip)")
     p.add_argument("--configs", type=int, default=1, help="also time BASELINE configs C2, C3-VEL, C4, C5 (N=1 only)")
-    p.add_argument("--mappo-steps", type=int, default=32, help="rollout_steps T of the MAPPO leg")
-    p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO leg")
-    p.add_argument("--mappo-iters", type=int, default=3, help="timed train steps (after one warm-up)")
+    p.add_argument("--mappo-steps", type=int, default=256, help="rollout_steps T of the MAPPO leg (learn_mappo.py:665)")
+    p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO legs")
+    p.add_argument("--mappo-iters", type=int, default=2, help="timed train steps (after one warm-up)")
+    p.add_argument("--mappo-t32", type=int, default=1, help="also time the T=32 MAPPO leg (0 = skip)")
     return p.parse_args()
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """--gpus N without a launcher: run N ranks of this script under torchrun as a
+    child process (never an exec) and return its exit status.  Nothing here has
+    touched a GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def cpu_baseline(args, seconds):
@@ -127,10 +162,23 @@ EXTRA_CONFIGS = {
 }
 
 
+def stagger_episodes(sw, task):
+    """Spread the envs' episode clocks uniformly over one episode (steady state of a
+    long vectorised rollout): env e starts at control step ⌊e·L/E⌋ of its episode."""
+    from gym_pybullet_drones_amd import _lib as L
+    E, L_ep = sw.num_envs, EPISODE_STEPS.get(task, 242)
+    env = sw.get_state(L.STATE_ENV).clone()
+    phase = (torch.arange(E, device=env.device, dtype=torch.int64) * L_ep // E).to(torch.int32)
+    env[L.E_STEP_COUNTER] = phase * sw.substeps
+    env[L.E_EP_LEN] = phase
+    sw.set_state(L.STATE_ENV, env)
+
+
 def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D=None, act=None, aux=()):
-    """The timed random-policy rollout: `steps` control steps of E envs per rank, as
-    replays of a HIP graph of `slots` step launches.  Returns (agent-steps/s over all
-    ranks, max-over-ranks seconds, mean step-kernel ms on the launch stream, steps)."""
+    """The timed random-policy rollout: exactly `args.steps` control steps of E envs
+    per rank, as replays of HIP graphs of step launches (one per rollout-buffer slot).
+    Returns (agent-steps/s over all ranks, max-over-ranks seconds, mean step-kernel
+    ms on the launch stream, steps, resets inside the timed window)."""
     from gym_pybullet_drones_amd.envs import QuadSwarm
     from gym_pybullet_drones_amd.utils.enums import Physics
     E = args.envs if E is None else E
@@ -141,63 +189,84 @@ def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D
     sw = QuadSwarm(task, num_envs=E, num_drones=D, act=act, precision=4, physics=phys, aux=aux,
                    initial_xyzs=layout, env_offset=rank * E)
     O, A = sw.obs_dim, sw.act_dim
-    obs_buf = torch.empty((args.slots, E, D, O), dtype=torch.float32, device=sw.device)
-    act_buf = torch.empty((args.slots, E, D, A), dtype=torch.float32, device=sw.device)
-    rew_buf = torch.empty((args.slots, E), dtype=torch.float32, device=sw.device)
-    te_buf = torch.empty((args.slots, E), dtype=torch.uint8, device=sw.device)
-    tr_buf = torch.empty((args.slots, E), dtype=torch.uint8, device=sw.device)
+    slots = max(1, min(args.slots, args.steps))
+    obs_buf = torch.empty((slots, E, D, O), dtype=torch.float32, device=sw.device)
+    act_buf = torch.empty((slots, E, D, A), dtype=torch.float32, device=sw.device)
+    rew_buf = torch.empty((slots, E), dtype=torch.float32, device=sw.device)
+    te_buf = torch.zeros((slots, E), dtype=torch.uint8, device=sw.device)
+    tr_buf = torch.zeros((slots, E), dtype=torch.uint8, device=sw.device)
     sw.reset(0, obs=obs_buf[0])
+    if not args.no_stagger:
+        stagger_episodes(sw, task)
+    done_count = torch.zeros((), dtype=torch.int64, device=sw.device)
 
-    def step(t):
-        k = t % args.slots
+    def step(k):
         sw.step(None, obs=obs_buf[k], reward=rew_buf[k], terminated=te_buf[k], truncated=tr_buf[k],
                 actions_out=act_buf[k])
 
-    # The rollout loop is captured once as a HIP graph of `slots` step launches
-    # (one per rollout-buffer slot) and replayed: the host launches one graph
-    # per `slots` steps instead of one kernel per step.
     for t in range(args.warmup):
-        step(t)
+        step(t % slots)
     torch.cuda.synchronize()
+    # The rollout loop is captured as a HIP graph of `slots` step launches (one per
+    # rollout-buffer slot), plus one of the remainder so that exactly `steps` run;
+    # the host launches one graph per `slots` steps instead of one kernel per step.
+    n_full, rem = divmod(args.steps, slots)
     stream = torch.cuda.Stream()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=stream):
-        for k in range(args.slots):
-            step(k)
+    graphs = []
+    for n in ([slots] if n_full else []) + ([rem] if rem else []):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for k in range(n):
+                step(k)
+        graphs.append((g, n))
     torch.cuda.synchronize()
+    plan = [graphs[0]] * n_full + ([graphs[-1]] if rem else [])
+    _, ended0 = sw.episode_log(cap=0)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    n_rep = (args.steps + args.slots - 1) // args.slots
-    steps = n_rep * args.slots
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_rep)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     cur = torch.cuda.current_stream()
     t0 = time.perf_counter()
-    for r in range(n_rep):
-        ev[r][0].record(cur)
-        graph.replay()
-        ev[r][1].record(cur)
+    for (g, n), (a, b) in zip(plan, ev):
+        a.record(cur)
+        g.replay()
+        b.record(cur)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     # mean step-kernel duration on the launch stream: graph time / launches per graph
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) / args.slots
+    kern_ms = float(sum(a.elapsed_time(b) for a, b in ev)) / args.steps
     if dist:
         t = torch.tensor([elapsed], device=sw.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # sanity of the window: every reset succeeded, outputs finite, episodes ended in it
     assert sw.reset_error() == 0
-    assert torch.isfinite(obs_buf[:min(args.slots, steps)]).all()
-    del graph
+    assert torch.isfinite(obs_buf).all()
+    _, ended1 = sw.episode_log(cap=0)
+    del graphs, plan
     sw.close()
-    return E * D * world * steps / elapsed, elapsed, kern_ms, steps
+    return E * D * world * args.steps / elapsed, elapsed, kern_ms, args.steps, int(ended1 - ended0)
 
 
-def mappo_leg(args, rank, world, dist):
+def mappo_flops(T, E, D, O, A, H=256, epochs=10):
+    """Algorithmic fp32 FLOP of one MAPPO train step: the update's
+    MLP forward + backward over epochs × T·E env-timesteps (actor on D agent rows of
+    O inputs each, centralized critic on one row of D·O), and the rollout's actor
+    forwards.  2 FLOP per MAC; the first layer has no input gradient."""
+    actor_row = 2 * (2 * O * H + 3 * H * H + 3 * H * A)
+    critic_row = 2 * (2 * D * O * H + 3 * H * H + 3 * H)
+    update = epochs * T * E * (D * actor_row + critic_row)
+    rollout = T * E * D * 2 * (O * H + H * H + H * A)
+    return update, rollout
+
+
+def mappo_leg(args, rank, world, dist, T):
     """Full MAPPO train steps on the bench's C3 envs (learn_mappo.py:196-203 hyper-parameters,
-    hidden 256, opt_epochs 10; minibatch scaled to the 128x larger env batch)."""
+    hidden 256, opt_epochs 10; minibatch scaled to the ~100x larger env batch)."""
     from gym_pybullet_drones_amd.envs import MultiHoverAviary
     from gym_pybullet_drones_amd.mappo import MAPPO
     from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
@@ -206,25 +275,19 @@ def mappo_leg(args, rank, world, dist):
     env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act, physics=Physics.DYN,
                                                initial_xyzs=grid_layout(D) if D >= 6 else None)
     m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
-              rollout_steps=args.mappo_steps, rollout_batch_size=E, opt_epochs=10,
+              rollout_steps=T, rollout_batch_size=E, opt_epochs=10,
               mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
     m.reset()
-    try:
-        m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
-    except RuntimeError as e:   # every rank runs the same capture, so they fall back together
-        print(f"[bench] update-graph capture with collectives failed ({e}); eager update iterations",
-              file=sys.stderr, flush=True)
-        torch.cuda.synchronize()
-        m.agent.graph_collectives = False
-        m.agent._graph = None
-        m.train_step()
+    m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
+    m.time_phases = True
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    phases = []
     t0 = time.perf_counter()
     for _ in range(args.mappo_iters):
-        m.train_step()
+        phases.append(m.train_step()['phase_ms'])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -234,20 +297,33 @@ def mappo_leg(args, rank, world, dist):
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    O, A = m.obs_dim, m.agent.ac.act_dim
     graphed = world == 1 or m.agent.graph_collectives
     m.close()
-    T = args.mappo_steps
+    ph = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
+    upd_flop, roll_flop = mappo_flops(T, E, D, O, A)
+    upd_tflops = upd_flop / (ph["update"] * 1e-3) / 1e12
     return {"value": T * E * D * world / dt, "unit": "agent-steps/s", "ms_per_train_step": dt * 1e3,
-            "train_steps": args.mappo_iters,
+            "train_steps": args.mappo_iters, "phase_ms": ph,
+            "learner_roofline": {"bound": "mfma", "achieved": upd_tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
+                                 "unit": "TFLOP/s", "frac": upd_tflops / FP32_MFMA_PEAK_TFLOPS,
+                                 "flop_per_update": upd_flop, "rollout_actor_flop": roll_flop,
+                                 "train_step_tflops": (upd_flop + roll_flop) / dt / 1e12,
+                                 "what": "PPO update: MLP fwd+bwd FLOP / update device time, fp32"},
             "config": {"rollout_steps": T, "envs_per_gpu": E, "drones": D, "hidden": 256, "opt_epochs": 10,
                        "mini_batch_size": args.mappo_mb,
                        "minibatches_per_epoch": T * E // args.mappo_mb,
-                       "graphs": "rollout + update" if graphed else "rollout", "grad_allreduce": ("one fused all-reduce per minibatch" + (", captured in the update graph" if graphed else "")) if world > 1
-                       else None}}
+                       "reference": "learn_mappo.py: T=256, 176 envs, mini_batch_size 32 (1408 minibatches/epoch)",
+                       "graphs": "rollout + update" if graphed else "rollout",
+                       "grad_allreduce": ("one fused all-reduce per minibatch" + (", captured in the update graph"
+                                                                                   if graphed else ""))
+                       if world > 1 else None}}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -257,37 +333,41 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     E, D = args.envs, args.drones
-    value, elapsed, kern_ms, args.steps = sim_leg(args, rank, world, dist, "dyn")
+    value, elapsed, kern_ms, steps, eps_done = sim_leg(args, rank, world, dist, "dyn")
     nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
     pyb = None
     if args.pyb:   # the same rollout under Physics.PYB (the reference's training default)
-        pv, _, pk, _ = sim_leg(args, rank, world, dist, "pyb")
+        pv, _, pk, _, _ = sim_leg(args, rank, world, dist, "pyb")
         pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
                "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
-    mappo = mappo_leg(args, rank, world, dist) if args.mappo else None
+    mappo = mappo_leg(args, rank, world, dist, args.mappo_steps) if args.mappo else None
+    mappo32 = mappo_leg(args, rank, world, dist, 32) if (args.mappo and args.mappo_t32) else None
     configs = None
     if args.configs and world == 1:   # the other BASELINE configs, one GPU each
         configs = {}
         for name, c in EXTRA_CONFIGS.items():
-            v, el, km, st = sim_leg(args, rank, world, dist, c["physics"], c["task"], c["envs"], c["drones"], c["act"],
-                                    c["aux"])
+            v, el, km, st, ne = sim_leg(args, rank, world, dist, c["physics"], c["task"], c["envs"], c["drones"],
+                                        c["act"], c["aux"])
             nb = c["bytes"] * c["envs"] * c["drones"]
             configs[name] = {"workload": c["label"], "value": v, "unit": "agent-steps/s", "kernel_ms": km,
                              "bytes_per_agent_step": c["bytes"],
-                             "roofline_frac": nb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                             "roofline_frac": nb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "episodes_ended_in_timed_window": ne}
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_src = pmc_traffic(E, D, args.act)
         line = {
-            "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"MultiHover {D}-drone x {E} envs/GPU, ActionType.{args.act.upper()}, "
-                                   "Physics.DYN, random-policy rollout (C3 env config; MAPPO learner not in "
-                                   "the timed step)",
+                                   "Physics.DYN, random-policy rollout (C3 env config; MAPPO learner in the "
+                                   "'mappo' field)",
                        "envs_per_gpu": E, "drones": D, "total_envs": E * world, "act": args.act,
-                       "physics": "dyn", "parallelism": f"env-shard x{world}", "precision": "fp32"},
+                       "physics": "dyn", "parallelism": f"env-shard x{world}", "precision": "fp32",
+                       "episode_phases": "uniform over 242 steps" if not args.no_stagger else "synchronised",
+                       "episodes_ended_in_timed_window_rank0": eps_done},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,
@@ -296,6 +376,7 @@ def main():
             "cpu_baseline": cpu,
             "pyb": pyb,
             "mappo": mappo,
+            "mappo_t32": mappo32,
             "configs": configs,
         }
         print(json.dumps(line), flush=True)

@@ -114,7 +114,9 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
   if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none): one workgroup each
-    const int rgrid = 1024;   // several workgroups per queued env when few are queued
+    // Several workgroups per queued env when few are queued; the grid is sized
+    // from E so a small shard does not pay 1024 empty workgroups every step.
+    const int rgrid = std::min(1024, std::max(64, P.E * 4));
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }
@@ -169,6 +171,20 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
     case QS_ACT_PID: A = 3; break;
     case QS_ACT_ONE_D_RPM: case QS_ACT_ONE_D_PID: A = 1; break;
     default: return fail(QS_E_INVALID, "qs_create: bad act_type");
+  }
+  {
+    // The kernels address every buffer through 32-bit buffer-resource ranges and
+    // offsets (step_kernel.h: state, history, obs rows, env records): refuse a
+    // shard whose largest buffer would not fit below 2^31 bytes instead of
+    // letting the offsets wrap.  (C3 at 16 384 envs uses 15 MB.)
+    const int64_t Nn = (int64_t)s.num_envs * s.num_drones;
+    const int64_t H = s.ctrl_freq / 2;
+    const int64_t O = 12 + H * A + (s.task == QS_TASK_SPIRAL ? 11 : 0);
+    const int64_t biggest = std::max({(int64_t)QS_AGENT_FIELDS * Nn * s.precision, H * Nn * A * 4, Nn * O * 4,
+                                      (int64_t)qs::kEnvRec * s.num_envs * 4});
+    if (biggest >= (int64_t(1) << 31))
+      return fail(QS_E_INVALID, "qs_create: num_envs * num_drones too large for one handle (a state buffer would "
+                                "exceed 2^31 bytes); shard the envs over more handles");
   }
   HIP_TRY(hipSetDevice(device));
   auto* h = new (std::nothrow) qs_handle();

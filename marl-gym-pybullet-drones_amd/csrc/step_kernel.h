@@ -346,7 +346,10 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T 
 
 // --------------------------------------------------- LDS workspace layout
 template <class T> struct Shared {
-  alignas(16) T cand[kBlock][3];   // reset candidates / downwash snapshot (fp32: float4 per drone) / MARL-task positions
+  union {
+    alignas(16) T cand[kBlock][3];  // reset candidates / MARL-task positions
+    alignas(16) float4 dw4[kBlock]; // fp32 downwash snapshot during the substeps (one float4 per drone)
+  };
   T velw[kBlock][3];        // MARL-task velocities (Flock alignment and speed)
   T rew[kBlock];            // per-drone reward terms
   uint8_t bits[kBlock];     // per-drone termination reason bits
@@ -386,7 +389,6 @@ template <class T> __device__ __forceinline__ bool too_close(T ax, T ay, T az, T
 template <class T>
 __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3], int g, int d, uint32_t try_idx,
                                uint32_t genv, uint32_t episode, bool active) {
-  using F = M<T>;
   const int tid = threadIdx.x;
   if (active) {
     T px, py, pz;
@@ -903,7 +905,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     auto downwash_f32 = [&]() -> float {
       const float px = float(pos[0]), py = float(pos[1]), pz = float(pos[2]);
       if (D == 16) return downwash16(px, py, pz);   // wave-uniform
-      float4* const nb = reinterpret_cast<float4*>(&s.cand[0][0]);
+      float4* const nb = s.dw4;
       __syncthreads();
       nb[tid] = make_float4(px, py, pz, 0.f);
       __syncthreads();
@@ -1440,7 +1442,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           if (tid < P.EPB) s.reject[tid] = 0;
           if (tid == 0) s.win_group = 1 << 30;
           __syncthreads();
-          const bool act_ = lenv < P.EPB;
+          const bool act_ = lenv < P.EPB && base + (uint32_t)lenv < kMaxResetTries;   // tries [0, cap)
           eval_candidate(P, s, orig, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
           if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
           __syncthreads();
@@ -1592,12 +1594,9 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       if (threadIdx.x == 0) s_best = __hip_atomic_load(&qwin[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       if ((int)base > s_best) break;
-      if (base >= kMaxResetTries) {
-        if (threadIdx.x == 0) atomicExch(P.err, 1);
-        break;
-      }
+      if (base >= kMaxResetTries) break;   // cap: tries >= kMaxResetTries are never accepted (as in-kernel)
       const uint32_t t = base + threadIdx.x;
-      bool ok = true;
+      bool ok = t < kMaxResetTries;
       T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
 #pragma unroll
       for (int d = 0; d < kResetMaxD; ++d) {
@@ -1633,7 +1632,10 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     __syncthreads();
     if (s_last) {   // every workgroup of this env has stopped: s_best is the first accepted try
       const int wv = s_best;
-      const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;   // cap reached: try 0, as the in-kernel search
+      // no try below the cap accepted (every workgroup has stopped): flag the
+      // error and keep try 0, as the in-kernel search does
+      if (wv == kResetNone && threadIdx.x == 0) atomicExch(P.err, 1);
+      const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;
       if ((int)threadIdx.x < D) {
         const int d = threadIdx.x;
         T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};

@@ -363,6 +363,8 @@ class FlatBuffers:
 
     def adam(self, gate_val=None, gate_thr=0.0):
         """One gated Adam step and its step-count commit (qs_adam_step, one launch)."""
+        if self.flat.device.type != 'cuda':
+            raise RuntimeError("FlatBuffers.adam is the HIP qs_adam_step kernel: the parameters must be on the GPU")
         lib = L.load()
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         L.check(lib.qs_adam_step(self.n, L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.exp_avg),
@@ -435,19 +437,20 @@ class MAPPOAgent:
     def to(self, device):
         self.device = torch.device(device)
         self.ac.to(self.device)
-        if self.device.type == 'cuda':
-            na = sum(p.numel() for p in self.ac.actor.parameters())
-            nc = sum(p.numel() for p in self.ac.critic.parameters())
-            # [actor grads | critic grads | approx_kl]: the one buffer every rank all-reduces
-            self._reduce_buf = torch.zeros(na + nc + 1, device=self.device)
-            self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[:na])
-            self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr, grad=self._reduce_buf[na:na + nc])
-            self._kl = self._reduce_buf[na + nc:]
-            if _dist_world() > 1:   # identical initial weights on every rank
-                tdist.broadcast(self.actor_opt.flat, 0)
-                tdist.broadcast(self.critic_opt.flat, 0)
-            self._opt_ready = True
-            self._graph = None
+        # The flat buffers exist on any device (the gloo tests drive the multi-rank
+        # update on CPU tensors); the optimizer step itself is the HIP kernel.
+        na = sum(p.numel() for p in self.ac.actor.parameters())
+        nc = sum(p.numel() for p in self.ac.critic.parameters())
+        # [actor grads | critic grads | approx_kl]: the one buffer every rank all-reduces
+        self._reduce_buf = torch.zeros(na + nc + 1, device=self.device)
+        self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[:na])
+        self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr, grad=self._reduce_buf[na:na + nc])
+        self._kl = self._reduce_buf[na + nc:]
+        if _dist_world() > 1:   # identical initial weights on every rank
+            tdist.broadcast(self.actor_opt.flat, 0)
+            tdist.broadcast(self.critic_opt.flat, 0)
+        self._opt_ready = True
+        self._graph = None
 
     def train(self):
         self.ac.train()
@@ -463,6 +466,8 @@ class MAPPOAgent:
         self.ac.load_state_dict(state_dict['ac'])   # copies into the flat-buffer views in place
         self.actor_opt.load_state_dict(state_dict['actor_opt'])
         self.critic_opt.load_state_dict(state_dict['critic_opt'])
+        # a captured update graph has lr / betas / eps baked in as kernel arguments
+        self._graph = None
 
     # ------------------------------------------------------------- losses
     def compute_policy_loss(self, batch, agent_idx=None):
@@ -525,12 +530,7 @@ class MAPPOAgent:
                                  L.ptr(self._heads_work), st), "qs_ppo_heads")
         with deferred_sums():
             torch.autograd.backward([mean, v], [self._dmean, self._dv])
-        if world > 1 or self._force_allreduce:
-            tdist.all_reduce(self._reduce_buf)
-            self._reduce_buf.div_(world)
-        gate = self._kl if self.target_kl > 0 else None
-        self.actor_opt.adam(gate, 1.5 * self.target_kl)
-        self.critic_opt.adam(None, 0.0)
+        self._exchange_and_step(world)
 
     def _iteration(self, batch, acc):
         """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.
@@ -547,14 +547,24 @@ class MAPPOAgent:
         self._reduce_buf.zero_()
         (policy_loss + self.entropy_coef * entropy_loss + value_loss).backward()
         self._kl.copy_(approx_kl.detach().float().reshape(1))
+        self._exchange_and_step(world)
+        acc += torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
+                            entropy_loss.detach().double(), approx_kl.detach().double()])
+
+    def _exchange_and_step(self, world):
+        """The rank exchange of one minibatch iteration and the two optimizer steps.
+        `_reduce_buf` holds [actor grads | critic grads | approx_kl] of this rank's
+        minibatch; one all-reduce (sum) and a division by the world size turn it
+        into the global-minibatch gradient and the global approx_kl mean (AG:731),
+        so every rank evaluates the same KL gate on the same value and applies the
+        same steps: actor Adam only if approx_kl <= 1.5·target_kl, critic always
+        (AG:731-760)."""
         if world > 1 or self._force_allreduce:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
         gate = self._kl if self.target_kl > 0 else None
         self.actor_opt.adam(gate, 1.5 * self.target_kl)
         self.critic_opt.adam(None, 0.0)
-        acc += torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
-                            entropy_loss.detach().double(), approx_kl.detach().double()])
 
     def _step_minibatch(self, rollouts, idx, acc):
         if self.fused_heads and self._fused_heads_ok(rollouts):

@@ -17,9 +17,14 @@ What changes:
   * total_steps counts env-steps over all ranks.
 Reference quirks kept (SURVEY §7 hard-5): v placeholders are zeros, terminal_v
 is zero (TimeLimit.truncated is never set), rewards are the per-env mean tiled
-over agents, termination_counts stay empty because auto-reset replaces the info
-(subproc_vec_env.py:195-206), obs are normalised twice on a done when
-norm_obs=True and reference_compat=True (MP:804, 1037).
+over agents, obs are normalised twice on a done when norm_obs=True and
+reference_compat=True (MP:804, 1037).
+termination_counts (MP:720-735) are counted from the kernel's per-drone reason
+bits at every terminal state: one count per (drone, reason), the categories of
+the reason strings (crash / flip / out_of_bounds, MH:225-238).  The reference's
+vectorised loop reads the post-auto-reset info, whose reasons MultiHover clears
+before building it (MH:109, subproc_vec_env.py:195-206), so its counts come out
+empty there; these are the counts it was written to collect.
 """
 import os
 import random
@@ -47,11 +52,34 @@ def get_random_state():
 
 
 def set_random_state(st):
+    '''safe_control_gym/utils/utils.py:91-110.  The torch generator states go back as
+    CPU ByteTensors (a checkpoint loaded with map_location='cuda' holds them on the GPU).'''
     random.setstate(st['random'])
-    np.random.set_state(st['numpy'])
-    torch.set_rng_state(st['torch'])
+    np_state = st['numpy']
+    if isinstance(np_state, (list, tuple)) and len(np_state) == 5:
+        np_state = (np_state[0], np.asarray(np_state[1], dtype=np.uint32), *np_state[2:])
+    np.random.set_state(np_state)
+    torch.set_rng_state(torch.as_tensor(st['torch']).cpu().to(torch.uint8))
     if 'torch_cuda' in st and torch.cuda.is_available():
-        torch.cuda.set_rng_state(st['torch_cuda'])
+        torch.cuda.set_rng_state(torch.as_tensor(st['torch_cuda']).cpu().to(torch.uint8))
+
+
+def _numpy_safe_globals():
+    """The numpy reconstructors a torch.save of numpy arrays / scalars / RNG states
+    refers to (data only: they rebuild arrays from dtype + bytes)."""
+    try:
+        from numpy._core import multiarray as ma   # numpy >= 2
+    except ImportError:   # pragma: no cover
+        from numpy.core import multiarray as ma
+    dts = [type(np.dtype(t)) for t in (np.float64, np.float32, np.float16, np.int64, np.int32, np.int16, np.int8,
+                                       np.uint64, np.uint32, np.uint16, np.uint8, np.bool_)]
+    return [np.dtype, np.ndarray, ma._reconstruct, ma.scalar] + dts
+
+
+def load_checkpoint(path, map_location=None):
+    """torch.load with weights_only=True plus the numpy allow-list (MP:231-270 files)."""
+    with torch.serialization.safe_globals(_numpy_safe_globals()):
+        return torch.load(path, map_location=map_location, weights_only=True)
 
 
 class ExperimentLogger:
@@ -249,9 +277,11 @@ class MAPPO:
         torch.save(state_dict, path)
 
     def load(self, path):
-        '''MP:231-270.  Checkpoints written by this class contain only tensors, numpy arrays and
-        RNG tuples; loading them needs weights_only=False like the reference.'''
-        state = torch.load(path, map_location=self.device, weights_only=False)
+        '''MP:231-270, with the same keys.  The file is read with torch.load(weights_only=True):
+        nothing in it is executed.  The reference's checkpoints hold numpy arrays (obs, RNG
+        and normaliser states), so the numpy array / dtype / scalar reconstructors are
+        allow-listed (load_checkpoint).'''
+        state = load_checkpoint(path, map_location=self.device)
         self.agent.load_state_dict(state['agent'])
         self.obs_normalizer.load_state_dict(state['obs_normalizer'])
         self.reward_normalizer.load_state_dict(state['reward_normalizer'])
@@ -263,8 +293,15 @@ class MAPPO:
                     set_random_state(state['random_state'])
                 except Exception as e:
                     print(f"Warning: could not restore random state: {e}")
-            if state.get('env_random_state') is not None and hasattr(self.env, 'set_env_random_state'):
-                self.env.set_env_random_state(state['env_random_state'])
+            env_rs = state.get('env_random_state')
+            # this class's own format; the reference's is a list of per-worker numpy
+            # MT19937 states (subproc_vec_env.py:101-109), which has no counterpart in
+            # the counter-based Philox streams and is skipped like an unreadable state
+            if isinstance(env_rs, dict) and 'seed' in env_rs and hasattr(self.env, 'set_env_random_state'):
+                self.env.set_env_random_state(env_rs)
+            elif env_rs is not None:
+                print("Warning: env_random_state is not in this simulator's format (per-worker numpy states); "
+                      "the env RNG continues from its current counters")
 
     def select_action(self, obs, info=None):
         '''MP:272-287: deterministic (dist.mode) actions for evaluation.'''
@@ -284,6 +321,8 @@ class MAPPO:
             self._te = torch.zeros((self.rollout_steps, E), dtype=torch.uint8, device=self.device)
             self._tr = torch.zeros((self.rollout_steps, E), dtype=torch.uint8, device=self.device)
             self._raw_obs = torch.zeros((E, D, self.obs_dim), device=self.device)
+            # per-drone termination reason bits of every step (QS_REASON_*)
+            self._reasons = torch.zeros((self.rollout_steps, E, D), dtype=torch.uint8, device=self.device)
         return self._rollouts
 
     def _rollout_step(self, rollouts, t, warmup=False):
@@ -296,7 +335,7 @@ class MAPPO:
         target = self._raw_obs if self.norm_obs else rollouts.next_obs_slots[t + 1]
         if not warmup:
             swarm.step(rollouts.act[t], obs=target, reward=self._rew_raw[t], terminated=self._te[t],
-                       truncated=self._tr[t])
+                       truncated=self._tr[t], reasons=self._reasons[t])
         done = (self._te[t] | self._tr[t]).float()
         rew = self._rew_raw[t]
         if self.norm_obs:
@@ -335,6 +374,11 @@ class MAPPO:
         rollouts = self._buffer()
         rollouts.reset()
         start = time.time()
+        # optional device-time split of the train step (bench.py's learner roofline):
+        # rollout | last value + GAE + advantage normalisation | PPO update
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if getattr(self, 'time_phases', False) else None
+        if ev:
+            ev[0].record()
         rollouts.next_obs_slots[0].copy_(self.obs)
         # the quirk path (norm_obs + double normalisation on done) needs a host branch per step
         graph_ok = self.use_graphs and not self.norm_obs and not self.norm_reward   # no collective in a step
@@ -351,6 +395,8 @@ class MAPPO:
                     if bool(done.any()):   # MP:1037: re-normalise (and re-update stats) on any done
                         rollouts.next_obs_slots[t + 1].copy_(self.obs_normalizer(rollouts.next_obs_slots[t + 1]))
         rollouts.t, rollouts.full = 0, True
+        if ev:
+            ev[1].record()
         self.obs = rollouts.next_obs_slots[self.rollout_steps].clone()
         self.total_steps += self.rollout_steps * self.num_envs * self.world
         with torch.inference_mode():
@@ -360,17 +406,35 @@ class MAPPO:
         rollouts.compute_returns_and_advantages(last_val, gamma=self.gamma, use_gae=self.use_gae,
                                                 gae_lambda=self.gae_lambda)
         rollouts.adv = normalize_advantages(rollouts.adv)
+        if ev:
+            ev[2].record()
         results = self.agent.update(rollouts, self.device)
+        if ev:
+            ev[3].record()
+            ev[3].synchronize()
+            results['phase_ms'] = {'rollout': ev[0].elapsed_time(ev[1]), 'gae': ev[1].elapsed_time(ev[2]),
+                                   'update': ev[2].elapsed_time(ev[3])}
         self.env.sync_from_device()
         step_means = self._rew_raw.mean(dim=1).double().cpu().numpy()
         results.update({'step': self.total_steps, 'elapsed_time': time.time() - start,
                         'step_reward_mean': step_means.mean(), 'step_reward_std': step_means.std(),
                         'step_reward_total': step_means.sum(),
-                        'termination_counts': defaultdict(int)})
+                        'termination_counts': self._termination_counts()})
         rew_sum = float(rollouts.rew_env.double().sum().item()) * self.num_agents
         self.episode_return += rew_sum / self.rollout_steps
         self.episode_length += self.rollout_steps
         return results
+
+    def _termination_counts(self):
+        '''MP:720-735: one count per (drone, reason) at the terminal states of this
+        rollout (this rank's envs), keyed like the reference's counter.'''
+        counts = defaultdict(int)
+        bits = self._reasons
+        per = torch.stack([((bits & b) != 0).sum() for b in (1, 2, 4)]).cpu().tolist()
+        for name, n in zip(('crash', 'flip', 'out_of_bounds'), per):
+            if n:
+                counts[name] += int(n)
+        return counts
 
     # -------------------------------------------------------------- learn
     def learn(self, env=None, **kwargs):
@@ -451,4 +515,6 @@ class MAPPO:
         if len(ep_returns):
             self.logger.add_scalars({'ep_length': ep_lengths.mean(), 'ep_return': ep_returns.mean(),
                                      'ep_return_std': ep_returns.std()}, step, prefix='stat')
+        if results.get('termination_counts'):   # MP:1305-1310
+            self.logger.add_scalars(dict(results['termination_counts']), step, prefix='termination')
         self.logger.dump_scalars()

@@ -235,27 +235,39 @@ class VecRecordEpisodeStatistics(VecEnvWrapper):
         return self.venv.reset(**kwargs)
 
     def step_wait(self):
+        """Same bookkeeping as record_episode_statistics.py:144-172: the return
+        grows by the env's mean reward, the length by one; trackers read the
+        env's info (its terminal_info on done); a finished episode is written to
+        info['n'][i]['episode'], queued, and its per-env counters restart."""
         obs, reward, done, info = self.venv.step_wait()
-        for i, (r, d) in enumerate(zip(reward, done)):
-            self.episode_return[i] += float(np.mean(r))
-            self.episode_length[i] += 1
-            for key in self.episode_stats:
-                inf = info["n"][i]["terminal_info"] if d else info["n"][i]
-                if key in inf:
-                    self.episode_stats[key][i] += inf[key]
-            if d:
-                info["n"][i]["episode"] = {"r": self.episode_return[i], "l": self.episode_length[i]}
-                self.return_queue.append(deepcopy(self.episode_return[i]))
-                self.length_queue.append(deepcopy(self.episode_length[i]))
-                self.episode_return[i] = 0
-                self.episode_length[i] = 0
-                for key in self.episode_stats:
-                    info["n"][i]["episode"][key] = deepcopy(self.episode_stats[key][i])
-                    if key in self.accumulated_stats:
-                        self.accumulated_stats[key] += deepcopy(self.episode_stats[key][i])
-                    if key in self.queued_stats:
-                        self.queued_stats[key].append(deepcopy(self.episode_stats[key][i]))
-                    self.episode_stats[key][i] *= 0
+        infos = info["n"]
+        # vectorised over envs: mean over agents of each env's reward
+        self.episode_return += np.asarray(reward, np.float64).reshape(self.num_envs, -1).mean(axis=1)
+        self.episode_length += 1
+        ended = np.flatnonzero(np.asarray(done, bool))
+        if self.episode_stats:
+            ended_set = set(ended.tolist())
+            for i in range(self.num_envs):
+                src = infos[i]["terminal_info"] if i in ended_set else infos[i]
+                for key, vals in self.episode_stats.items():
+                    if key in src:
+                        vals[i] += src[key]
+        for i in ended:
+            ep_r, ep_l = float(self.episode_return[i]), float(self.episode_length[i])
+            summary = {"r": ep_r, "l": ep_l}
+            self.return_queue.append(ep_r)
+            self.length_queue.append(ep_l)
+            for key, vals in self.episode_stats.items():
+                value = deepcopy(vals[i])
+                summary[key] = value
+                if key in self.accumulated_stats:
+                    self.accumulated_stats[key] += deepcopy(value)
+                if key in self.queued_stats:
+                    self.queued_stats[key].append(deepcopy(value))
+                vals[i] *= 0
+            infos[i]["episode"] = summary
+        self.episode_return[ended] = 0
+        self.episode_length[ended] = 0
         return obs, reward, done, info
 
     def sync_from_device(self):
