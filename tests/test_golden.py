@@ -17,7 +17,8 @@ def _cases():
     return make_golden
 
 
-@pytest.mark.parametrize("name", ["mh_rpm_d4", "mh_onedpid_d8", "mh_vel_d3", "spiral_vel_d5", "mh_dw_d16"])
+@pytest.mark.parametrize("name", ["mh_rpm_d4", "mh_onedpid_d8", "mh_vel_d3", "spiral_vel_d5", "mh_dw_d16",
+                                  "mh_onedpid_d8_pyb"])
 def test_oracle_reproduces_golden(name):
     mg = _cases()
     s = qs_oracle.OracleSim(num_envs=mg.E, precision=8, **mg.CASES[name])

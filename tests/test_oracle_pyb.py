@@ -137,8 +137,9 @@ def test_pyb_ground_plane():
 
 def test_pyb_differs_from_dyn_only_by_bullet_terms():
     """Same start, small actions: PYB and DYN agree to first order over one step (the
-    damping, the prop-arm 0.028 vs L/√2 and the roll-torque sign convention are the
-    differences)."""
+    damping and the prop arm 0.028 vs L/√2 are the differences; the roll and pitch
+    torque signs agree: props at (±0.028, ±0.028) give τx = −0.028(f0+f1−f2−f3), the
+    sign of BaseAviary.py:849's −(f0+f1−f2−f3)·L/√2)."""
     rng = np.random.default_rng(3)
     a = rng.uniform(-0.1, 0.1, (1, 2, 1)).astype(np.float32)
     out = {}
