@@ -541,30 +541,45 @@ class MAPPOAgent:
         gradient buffers; with several ranks the actor gradient, the critic
         gradient and approx_kl then travel in ONE all-reduce (gradient mean and
         the KL mean every rank gates on, AG:731)."""
-        world = _dist_world()
+        self._local_grads(batch, acc)
+        self._exchange_and_step(_dist_world())
+
+    def _local_grads(self, batch, acc):
+        """This rank's minibatch: both losses, one backward into `_reduce_buf`'s
+        gradient views, approx_kl into its last slot, loss stats into acc."""
         policy_loss, entropy_loss, approx_kl = self.compute_policy_loss(batch)
         value_loss = self.compute_value_loss(batch)
         self._reduce_buf.zero_()
         (policy_loss + self.entropy_coef * entropy_loss + value_loss).backward()
         self._kl.copy_(approx_kl.detach().float().reshape(1))
-        self._exchange_and_step(world)
         acc += torch.stack([policy_loss.detach().double(), value_loss.detach().double(),
                             entropy_loss.detach().double(), approx_kl.detach().double()])
 
-    def _exchange_and_step(self, world):
-        """The rank exchange of one minibatch iteration and the two optimizer steps.
-        `_reduce_buf` holds [actor grads | critic grads | approx_kl] of this rank's
-        minibatch; one all-reduce (sum) and a division by the world size turn it
-        into the global-minibatch gradient and the global approx_kl mean (AG:731),
-        so every rank evaluates the same KL gate on the same value and applies the
-        same steps: actor Adam only if approx_kl <= 1.5·target_kl, critic always
-        (AG:731-760)."""
+    def _exchange(self, world):
+        """The rank exchange of one minibatch iteration.  `_reduce_buf` holds
+        [actor grads | critic grads | approx_kl] of this rank's minibatch; one
+        all-reduce (sum) and a division by the world size turn it into the
+        global-minibatch gradient and the global approx_kl mean (AG:731), so every
+        rank evaluates the same KL gate on the same value.  Runs on any device
+        (tests/test_distributed_cpu.py drives it on CPU tensors with gloo)."""
         if world > 1 or self._force_allreduce:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
+
+    def _actor_gate_open(self):
+        """AG:731-734: the actor steps only if approx_kl <= 1.5·target_kl (a device
+        tensor; the HIP Adam reads it on the device, this is the host view)."""
+        return self.target_kl <= 0 or bool(self._kl.item() <= 1.5 * self.target_kl)
+
+    def _optimizer_steps(self):
+        """Actor Adam gated by the KL value on the device, critic Adam always (AG:731-760)."""
         gate = self._kl if self.target_kl > 0 else None
         self.actor_opt.adam(gate, 1.5 * self.target_kl)
         self.critic_opt.adam(None, 0.0)
+
+    def _exchange_and_step(self, world):
+        self._exchange(world)
+        self._optimizer_steps()
 
     def _step_minibatch(self, rollouts, idx, acc):
         if self.fused_heads and self._fused_heads_ok(rollouts):

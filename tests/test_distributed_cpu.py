@@ -9,6 +9,11 @@
   moments merged across ranks equal the single-process result on the
   concatenated data; approx_kl / gradient averaging (all_reduce / world) equals
   the gradient of the mean over the global minibatch.
+* MAPPOAgent's own update exchange (agent.py _local_grads → _exchange → KL gate,
+  the code the GPU path runs, here on CPU tensors): identical initial weights on
+  every rank (broadcast), ONE all-reduce of the packed [actor grads | critic
+  grads | approx_kl] buffer, whose result is the single-process gradient of the
+  global minibatch, and the same KL-gate decision on every rank.
 """
 import os
 import socket
@@ -98,6 +103,64 @@ def _grad_worker(rank, world):
     return grad.numpy()
 
 
+D_, O_, A_, MB_ = 3, 10, 2, 6
+
+
+def _agent(seed, target_kl):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "marl-gym-pybullet-drones_amd")]
+    from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
+    from gym_pybullet_drones_amd.utils.spaces import Box
+    torch.manual_seed(seed)
+    obs_space = Box(np.full((D_, O_), -np.inf, np.float32), np.full((D_, O_), np.inf, np.float32), dtype=np.float32)
+    act_space = Box(-np.ones((D_, A_), np.float32), np.ones((D_, A_), np.float32), dtype=np.float32)
+    return MAPPOAgent(obs_space, act_space, hidden_dim=16, device="cpu", use_graphs=False, fused_heads=False,
+                      target_kl=target_kl, entropy_coef=0.01)
+
+
+def _update_batch(n):
+    g = torch.Generator().manual_seed(3)
+    obs = torch.randn(n, D_, O_, generator=g)
+    return {"obs": obs, "act": torch.randn(n, D_, A_, generator=g),
+            "logp": torch.randn(n, D_, 1, generator=g) * 0.1 - 2.0,
+            "adv": torch.randn(n, D_, 1, generator=g, dtype=torch.float64),
+            "ret": torch.randn(n, D_, 1, generator=g, dtype=torch.float64),
+            "v": torch.zeros(n, D_, 1), "global_obs": obs.reshape(n, D_ * O_)}
+
+
+def _update_worker_for(target_kl):
+    def work(rank, world):
+        agent = _agent(100 + rank, target_kl)   # different init per rank: the broadcast equalises it
+        w0 = torch.cat([agent.actor_opt.flat, agent.critic_opt.flat]).clone()
+        full = _update_batch(world * MB_)
+        mine = {k: v[rank * MB_:(rank + 1) * MB_] for k, v in full.items()}
+        acc = torch.zeros(4, dtype=torch.float64)
+        agent._local_grads(mine, acc)
+        calls = []
+        orig = dist.all_reduce
+
+        def counting(t, *a, **kw):
+            calls.append(t.numel())
+            return orig(t, *a, **kw)
+
+        dist.all_reduce = counting
+        try:
+            agent._exchange(world)
+        finally:
+            dist.all_reduce = orig
+        return w0.numpy(), agent._reduce_buf.clone().numpy(), agent._actor_gate_open(), calls
+    return work
+
+
+def _upd_worker_open(rank, world):
+    return _update_worker_for(10.0)(rank, world)
+
+
+def _upd_worker_kl(rank, world):
+    return _update_worker_for(1e-4)(rank, world)
+
+
 # -------------------------------------------------------------------- tests
 def test_env_shards_union_equals_unsharded():
     import qs_oracle
@@ -137,3 +200,21 @@ def test_gradient_average_equals_global_minibatch_gradient():
     want = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()
     for r in res:
         np.testing.assert_allclose(r, want, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("worker,target_kl", [(_upd_worker_open, 10.0), (_upd_worker_kl, 1e-4)])
+def test_agent_update_exchange_two_ranks(worker, target_kl):
+    res = spawn(worker)
+    single = _agent(100, target_kl)   # rank 0's weights (the broadcast source)
+    acc = torch.zeros(4, dtype=torch.float64)
+    single._local_grads(_update_batch(2 * MB_), acc)
+    want = single._reduce_buf.numpy()
+    n = want.size
+    for w0, buf, gate, calls in res:
+        np.testing.assert_array_equal(w0, res[0][0])   # identical initial weights on both ranks
+        np.testing.assert_array_equal(w0, torch.cat([single.actor_opt.flat, single.critic_opt.flat]).numpy())
+        assert calls == [n]                              # one packed all-reduce per minibatch
+        np.testing.assert_allclose(buf, want, rtol=2e-5, atol=1e-7)   # = the global-minibatch gradient and KL
+        assert gate == single._actor_gate_open()
+    assert res[0][2] == res[1][2]
+    np.testing.assert_array_equal(res[0][1], res[1][1])   # every rank holds the same reduced values

@@ -1,0 +1,263 @@
+"""The drop-in Python surfaces on the GPU path, against the oracle and against
+plain-torch restatements of the reference's own code.
+
+  * SwarmVecEnv: the VecEnv 4-tuple with {'n': infos}, auto-reset with
+    terminal_observation / terminal_info and MultiHover's reason strings
+    (subproc_vec_env.py:188-206, MultiHoverAviary.py:216-241, 274-285).
+  * VecRecordEpisodeStatistics (record_episode_statistics.py:97-172).
+  * MAPPO with norm_obs=True and the reference's double normalisation on a
+    done (mappo.py:804, 1037; normalization.py:13-120).
+  * MAPPO.load of a checkpoint written in the reference's layout from plain
+    torch modules and torch.optim.Adam (mappo.py:203-270, agent.py:557-600).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import qs_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _reason_strings(bits, tobs):
+    """MultiHoverAviary._computeTerminated's strings (MH:225-238), restated from the
+    terminal observation [x y z roll pitch yaw ...] and the per-drone reason bits."""
+    out = []
+    for i, b in enumerate(bits):
+        x, y, z, roll, pitch = (float(v) for v in tobs[i, :5])
+        if b & 1:
+            out.append(f"Drone {i} crashed (z={z:.2f})")
+        if b & 2:
+            out.append(f"Drone {i} flipped (roll={roll:.2f}, pitch={pitch:.2f})")
+        if b & 4:
+            out.append(f"Drone {i} out of bounds (pos=[{x:.2f}, {y:.2f}, {z:.2f}])")
+    return out
+
+
+def _venv_and_oracle(E=16, D=4, seed=5):
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    from gym_pybullet_drones_amd.vec_env import SwarmVecEnv
+    venv = SwarmVecEnv(task="multihover", num_envs=E, num_drones=D, act=ActionType.RPM, seed=seed, precision=8)
+    orc = qs_oracle.OracleSim(task="multihover", num_envs=E, num_drones=D, act="rpm", precision=8)
+    return venv, orc
+
+
+def test_vecenv_contract_matches_oracle():
+    E, D = 16, 4
+    venv, orc = _venv_and_oracle(E, D)
+    obs, info = venv.reset()
+    o = orc.reset(5)
+    assert isinstance(obs, np.ndarray) and obs.shape == (E, D, venv.observation_space.shape[1])
+    assert obs.dtype == np.float32
+    np.testing.assert_allclose(obs, o, rtol=0, atol=1e-7)
+    assert set(info) == {"n"} and len(info["n"]) == E
+    assert all(i == {"answer": 42, "termination_reasons": []} for i in info["n"])
+    assert venv.action_space.shape == (D, 4) and venv.observation_space.shape == (D, 72)
+    rng = np.random.default_rng(1)
+    n_done = n_reasons = 0
+    for t in range(150):
+        act = (rng.normal(size=(E, D, 4)) * 0.8).astype(np.float32)   # raw Normal samples, |a| > 1 too
+        obs, rews, dones, info = venv.step(act)
+        c = orc.step(act)
+        assert obs.dtype == np.float32 and rews.dtype == np.float64 and dones.dtype == bool
+        assert rews.shape == (E,) and dones.shape == (E,) and len(info["n"]) == E
+        np.testing.assert_allclose(obs, c["obs"], rtol=2e-7, atol=1e-7, err_msg=f"t={t}")
+        np.testing.assert_allclose(rews, c["reward"], rtol=1e-12, atol=1e-12)
+        want_done = (c["terminated"] | c["truncated"]).astype(bool)
+        np.testing.assert_array_equal(dones, want_done, err_msg=f"t={t}")
+        for i, inf in enumerate(info["n"]):
+            if dones[i]:
+                n_done += 1
+                # the reset env's info, with the finished episode's obs and info attached
+                assert inf["answer"] == 42 and inf["termination_reasons"] == []
+                np.testing.assert_allclose(inf["terminal_observation"], c["terminal_obs"][i], rtol=2e-7, atol=1e-7)
+                want = _reason_strings(c["reasons"][i], c["terminal_obs"][i]) if c["terminated"][i] else []
+                assert inf["terminal_info"]["termination_reasons"] == want, (t, i)
+                assert inf["terminal_info"]["answer"] == 42
+                n_reasons += len(want)
+            else:
+                assert "terminal_observation" not in inf and "terminal_info" not in inf
+                assert inf == {"answer": 42, "termination_reasons": []}
+    assert n_done > 20 and n_reasons > 0
+    venv.close()
+
+
+def test_vec_record_episode_statistics():
+    from gym_pybullet_drones_amd.vec_env import VecRecordEpisodeStatistics
+    E, D = 16, 4
+    venv, orc = _venv_and_oracle(E, D)
+    env = VecRecordEpisodeStatistics(venv, deque_size=10)
+    env.add_tracker("answer", 0, mode="accumulate")
+    env.add_tracker("answer_q", 0, mode="queue")   # absent from the infos: stays 0
+    env.reset()
+    orc.reset(5)
+    rng = np.random.default_rng(2)
+    steps = 0
+    episodes = []
+    for _ in range(150):
+        act = (rng.normal(size=(E, D, 4)) * 0.8).astype(np.float32)
+        _, rews, dones, info = env.step(act)
+        orc.step(act)
+        steps += 1
+        for i in np.flatnonzero(dones):
+            ep = info["n"][i]["episode"]
+            assert set(ep) == {"r", "l", "answer", "answer_q"}
+            assert ep["answer"] == 42 * ep["l"] and ep["answer_q"] == 0
+            episodes.append((ep["r"], ep["l"]))
+    recs, total = orc.episode_log()
+    assert total == len(episodes) and total > 20
+    # the oracle's log is in (step, env) order, the wrapper's queue too
+    np.testing.assert_allclose([e[0] for e in episodes], recs["ret"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_array_equal([e[1] for e in episodes], recs["len"])
+    assert list(env.return_queue) == [e[0] for e in episodes[-10:]]
+    assert list(env.length_queue) == [e[1] for e in episodes[-10:]]
+    assert env.accumulated_stats["answer"] == 42 * sum(e[1] for e in episodes)
+    assert len(env.queued_stats["answer_q"]) == 10
+    env.close()
+
+
+class _NpRunningMeanStd:
+    """normalization.py:13-60 (numpy, float64)."""
+
+    def __init__(self, shape, epsilon=1e-4):
+        self.mean, self.var, self.count = np.zeros(shape), np.ones(shape), epsilon
+
+    def update(self, arr):
+        bm, bv, bc = arr.mean(0), arr.var(0), arr.shape[0]
+        delta = bm - self.mean
+        tot = self.count + bc
+        m2 = self.var * self.count + bv * bc + delta ** 2 * self.count * bc / tot
+        self.mean, self.var, self.count = self.mean + delta * bc / tot, m2 / tot, tot
+
+
+@pytest.mark.parametrize("reference_compat", [True, False])
+def test_norm_obs_and_double_normalisation(reference_compat, tmp_path):
+    """Every obs-normaliser call of a train_step is recorded and replayed through a
+    numpy MeanStdNormalizer (normalization.py:89-120): same statistics and outputs.
+    With reference_compat, a step with any done normalises the already
+    normalised obs a second time (and updates the statistics with them) — MP:1037."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    env_func = lambda seed=None, **kw: MultiHoverAviary(num_drones=4, act=ActionType.RPM)
+    T, E = 12, 16
+    m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=64, rollout_batch_size=E,
+              rollout_steps=T, mini_batch_size=32, opt_epochs=1, norm_obs=True, reference_compat=reference_compat)
+    calls = []
+
+    class Recorder:   # every obs-normaliser call, its input and output
+        def __init__(self, inner):
+            self.inner = inner
+
+        def __call__(self, x, out=None):
+            y = self.inner(x, out)
+            calls.append((x.detach().double().cpu().numpy().copy(), y.detach().double().cpu().numpy().copy()))
+            return y
+
+        def __getattr__(self, name):
+            return getattr(self.inner, name)
+
+    m.obs_normalizer = Recorder(m.obs_normalizer)
+    m.reset()
+    m.train_step()
+    n_done_steps = int(((m._te | m._tr).any(dim=1)).sum())
+    assert n_done_steps > 0
+    assert len(calls) == 1 + T + (n_done_steps if reference_compat else 0)
+    rms = _NpRunningMeanStd(calls[0][0].shape[1:])
+    for k, (x, y) in enumerate(calls):
+        rms.update(x)
+        want = np.clip((x - rms.mean) / np.sqrt(rms.var + 1e-8), -10, 10)
+        np.testing.assert_allclose(y, want, rtol=1e-6, atol=1e-6, err_msg=f"call {k}")
+    if reference_compat:   # the second call of a done step takes the first call's output
+        k = 1
+        te = (m._te | m._tr).any(dim=1).cpu().numpy()
+        for t in range(T):
+            k += 1
+            if te[t]:
+                np.testing.assert_allclose(calls[k][0], calls[k - 1][1].astype(np.float32), rtol=0, atol=0)
+                k += 1
+    np.testing.assert_allclose(m.obs_normalizer.inner.rms.mean.cpu().numpy(), rms.mean, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(m.obs_normalizer.inner.rms.var.cpu().numpy(), rms.var, rtol=1e-9, atol=1e-12)
+    # the rollout buffer holds the last normalised obs of each step
+    np.testing.assert_allclose(m._rollouts.next_obs_slots[T].cpu().numpy(), calls[-1][1], rtol=0, atol=1e-6)
+    m.close()
+
+
+class _RefMLP(nn.Module):
+    """Parameter layout of safe_control_gym's MLP (neural_networks.py:18-54)."""
+
+    def __init__(self, i, o, h):
+        super().__init__()
+        self.fcs = nn.ModuleList([nn.Linear(i, h), nn.Linear(h, h), nn.Linear(h, o)])
+
+
+class _RefActor(nn.Module):
+    def __init__(self, O, A, h):
+        super().__init__()
+        self.pi_net = _RefMLP(O, A, h)                    # AG:99
+        self.logstd = nn.Parameter(-0.5 * torch.ones(A))  # AG:107
+
+
+class _RefCritic(nn.Module):
+    def __init__(self, G, h):
+        super().__init__()
+        self.v_net = _RefMLP(G, 1, h)                     # AG:182
+
+
+class _RefAC(nn.Module):
+    def __init__(self, D, O, A, h):
+        super().__init__()
+        self.actor = _RefActor(O, A, h)
+        self.critic = _RefCritic(D * O, h)
+
+
+def test_load_reference_layout_checkpoint(tmp_path):
+    """A checkpoint written the reference's way — agent.state_dict() of plain torch
+    modules with torch.optim.Adam state (AG:588-600), numpy obs and RNG states
+    (MP:203-229) — loads into this MAPPO; the next Adam step on both sides, from
+    the same gradients, gives the same parameters."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    D, h, E = 3, 64, 8
+    env_func = lambda seed=None, **kw: MultiHoverAviary(num_drones=D, act=ActionType.ONE_D_PID)
+    m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=h, rollout_batch_size=E,
+              rollout_steps=8, mini_batch_size=16, opt_epochs=1)
+    m.reset()
+    O, A = m.obs_dim, 1
+    torch.manual_seed(7)
+    ref = _RefAC(D, O, A, h).cuda()
+    a_opt = torch.optim.Adam(ref.actor.parameters(), 3e-4)
+    c_opt = torch.optim.Adam(ref.critic.parameters(), 1e-3)
+    for _ in range(3):   # give the optimizers some state
+        for opt, mod in ((a_opt, ref.actor), (c_opt, ref.critic)):
+            opt.zero_grad()
+            for p in mod.parameters():
+                p.grad = torch.randn_like(p)
+            opt.step()
+    obs = np.random.default_rng(0).normal(size=(E, D, O)).astype(np.float32)
+    ck = {"agent": {"ac": ref.state_dict(), "actor_opt": a_opt.state_dict(), "critic_opt": c_opt.state_dict()},
+          "obs_normalizer": {}, "reward_normalizer": {}, "total_steps": 1234, "obs": obs,
+          "random_state": {"random": __import__("random").getstate(), "numpy": np.random.get_state(),
+                           "torch": torch.get_rng_state()},
+          "env_random_state": [np.random.RandomState(i).get_state() for i in range(2)]}   # per-worker states
+    path = str(tmp_path / "ref.pt")
+    torch.save(ck, path)
+    m.load(path)
+    assert m.total_steps == 1234
+    np.testing.assert_array_equal(m.obs.cpu().numpy(), obs)
+    for (name, p), q in zip(ref.named_parameters(), m.agent.ac.parameters()):
+        assert torch.equal(p.detach(), q.detach()), name
+    # one more step from identical gradients on both sides
+    for opt, mod, fb in ((a_opt, ref.actor, m.agent.actor_opt), (c_opt, ref.critic, m.agent.critic_opt)):
+        opt.zero_grad()
+        g = [torch.randn_like(p) for p in mod.parameters()]
+        for p, gi in zip(mod.parameters(), g):
+            p.grad = gi.clone()
+        opt.step()
+        fb.grad.copy_(torch.cat([gi.reshape(-1) for gi in g]))
+        fb.adam()
+        for p, q in zip(mod.parameters(), fb.params):
+            torch.testing.assert_close(q.detach(), p.detach(), rtol=1e-6, atol=1e-7)
+    m.close()
