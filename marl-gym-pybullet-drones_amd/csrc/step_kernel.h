@@ -344,6 +344,55 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T 
   }
 }
 
+// Drone–drone contact of the PYB mode, the oracle's drone_contacts
+// (oracle/qs_oracle.cpp): pairs i < j of one env in drone
+// order, inelastic and frictionless push-out between the collision cylinders.
+// p / v / ez: the env's positions, velocities and tilted half-heights in LDS.
+template <class T>
+__device__ void contact_pairs(T (*p)[3], T (*v)[3], const T* ez, int D) {
+  using F = M<T>;
+  const T r2 = T(2 * kCylR);
+  for (int i = 0; i < D; ++i)
+    for (int j = i + 1; j < D; ++j) {
+      const T dx = p[j][0] - p[i][0], dy = p[j][1] - p[i][1], dz = p[j][2] - p[i][2];
+      const T d2 = dx * dx + dy * dy;
+      if (!(d2 < r2 * r2)) continue;
+      const T pz = (ez[i] + ez[j]) - F::abs_(dz);
+      if (!(pz > T(0))) continue;
+      const T dxy = F::sqrt_(d2);
+      const T pxy = r2 - dxy;
+      if (pz < pxy) {   // vertical: j above i when dz >= 0
+        const T sg = dz >= T(0) ? T(1) : T(-1);
+        const T half = T(0.5) * pz;
+        p[i][2] = p[i][2] - sg * half;
+        p[j][2] = p[j][2] + sg * half;
+        const T rel = (v[j][2] - v[i][2]) * sg;
+        if (rel < T(0)) {
+          const T m = T(0.5) * (v[i][2] + v[j][2]);
+          v[i][2] = m;
+          v[j][2] = m;
+        }
+      } else {          // horizontal, along the centre line
+        T nx = T(1), ny = T(0);
+        if (dxy > T(0)) { nx = dx / dxy; ny = dy / dxy; }
+        const T half = T(0.5) * pxy;
+        p[i][0] = p[i][0] - nx * half; p[i][1] = p[i][1] - ny * half;
+        p[j][0] = p[j][0] + nx * half; p[j][1] = p[j][1] + ny * half;
+        const T rel = (v[j][0] - v[i][0]) * nx + (v[j][1] - v[i][1]) * ny;
+        if (rel < T(0)) {
+          const T hr = T(0.5) * rel;
+          v[i][0] = v[i][0] + hr * nx; v[i][1] = v[i][1] + hr * ny;
+          v[j][0] = v[j][0] - hr * nx; v[j][1] = v[j][1] - hr * ny;
+        }
+      }
+    }
+}
+
+__device__ __forceinline__ float wave_min(float x) {
+  for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
 // --------------------------------------------------- LDS workspace layout
 template <class T> struct Shared {
   union {
@@ -890,6 +939,50 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     const T s2 = T(2) * F::rcp(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     T R[9];   // PYB: rotation of the current pose, carried across substeps
     if constexpr (PHYS == QS_PHYS_PYB) quat_to_rot(q, R);
+    // Drone–drone contact (PYB; Bullet keeps every drone's collision cylinder,
+    // cf2x.urdf:31-36, BaseAviary.py:484-503).  Broad phase: Mw = the wave's
+    // smallest horizontal centre distance at the step start.  A drone that has
+    // moved at most B = (Mw − 2r)/2 − margin horizontally cannot close a gap to
+    // 2r with another drone that has also moved at most B, so the exact pair
+    // pass (contact_pairs, one lane per env over LDS) runs only from the first
+    // substep at which some drone of the wave has moved farther, and then for
+    // the rest of the step.  |Δxy| per substep <= dt (|vx| + |vy|).
+    float c_budget = 0.f, c_moved = 0.f;
+    bool c_slow = false;
+    if constexpr (PHYS == QS_PHYS_PYB) {
+      if (D > 1) {
+        __syncthreads();
+        s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1];
+        __syncthreads();
+        float m2 = 1e30f;
+        if (valid) {
+          const int base = lenv * D;
+          for (int j = 0; j < D; ++j) {
+            const float dx = float(s.cand[base + j][0] - pos[0]), dy = float(s.cand[base + j][1] - pos[1]);
+            const float q2 = dx * dx + dy * dy;
+            m2 = (j != d && q2 < m2) ? q2 : m2;
+          }
+        }
+        c_budget = 0.5f * (sqrtf(wave_min(m2)) - float(2 * kCylR)) - 1e-4f;
+        c_slow = c_budget <= 0.f;
+      }
+    }
+    // after the substep's integration and ground check (pos, vel final); r8 = R22
+    auto contacts = [&](T r8) {
+      if (D < 2) return;
+      c_moved += float(dt) * (fabsf(float(vel[0])) + fabsf(float(vel[1])));
+      if (!c_slow) c_slow = __ballot(valid && c_moved > c_budget) != 0;   // wave-uniform
+      if (!c_slow) return;
+      __syncthreads();
+      s.cand[tid][0] = pos[0]; s.cand[tid][1] = pos[1]; s.cand[tid][2] = pos[2];
+      s.velw[tid][0] = vel[0]; s.velw[tid][1] = vel[1]; s.velw[tid][2] = vel[2];
+      s.rew[tid] = T(kCylHalfLen) * F::abs_(r8) + T(kCylR) * F::sqrt_(T(1) - r8 * r8 > T(0) ? T(1) - r8 * r8 : T(0));
+      __syncthreads();
+      if (valid && d == 0) contact_pairs<T>(&s.cand[tid], &s.velw[tid], &s.rew[tid], D);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { pos[i] = s.cand[tid][i]; vel[i] = s.velw[tid][i]; }
+    };
     // fp32 without extra forces at pyb_freq 240 (the hot configurations): the
     // substep is restated algebraically with every per-control-step constant
     // hoisted — the thrust, gravity and torque terms premultiplied by dt/M and
@@ -991,6 +1084,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
               if (vel[2] < 0.f) vel[2] = 0.f;
             }
           }
+          contacts(1.0f - 2.0f * (q[0] * q[0] + q[1] * q[1]));   // drone–drone (rare: broad phase above)
         }
         T Rn[9];   // getBaseVelocity: world angular velocity at the new pose
         quat_to_rot(q, Rn);
@@ -1169,6 +1263,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
             if (vel[2] < T(0)) vel[2] = T(0);
           }
         }
+        contacts(R[8]);   // drone–drone (rare: broad phase above)
         if (sub == S - 1) {   // getBaseVelocity: world angular velocity at the new pose
           angv[0] = R[0] * w[0] + R[1] * w[1] + R[2] * w[2];
           angv[1] = R[3] * w[0] + R[4] * w[1] + R[5] * w[2];

@@ -487,6 +487,64 @@ void pyb_dynamics(const Params<R>& P, Drone<R>& d, const R rpm[4], const Snap<R>
   }
 }
 
+// Drone–drone contact of the PYB mode (Bullet keeps every drone's collision
+// cylinder live: assets/cf2x.urdf:31-36, BaseAviary.py:484-491, the collision
+// filter at BA:500-503 is commented out).  Restated like the ground plane:
+// inelastic and frictionless, equal masses.  Pair (i, j), i < j in drone order,
+// once per substep after every drone's step and ground check:
+//   overlap if the centres are closer than 2r horizontally and closer than the
+//   two tilted half-heights e = h|R22| + r·sqrt(1 − R22²) vertically;
+//   separated along the axis of the smaller penetration (vertical, or the
+//   horizontal centre line), each drone moved by half of it; if the pair is
+//   approaching along that axis both take the mean of their velocity
+//   components on it (the inelastic response), tangential velocity unchanged.
+template <class R> void drone_contacts(Drone<R>* dr, int D) {
+  const R r2 = R(2 * kCylR), h = R(kCylHalfLen), rr = R(kCylR);
+  std::vector<R> ez(D);
+  for (int i = 0; i < D; ++i) {
+    R rot[3][3];
+    quat_to_matrix(dr[i].quat, rot);
+    const R c = rot[2][2];
+    ez[i] = h * std::fabs(c) + rr * std::sqrt(std::max(R(0), R(1) - c * c));
+  }
+  for (int i = 0; i < D; ++i)
+    for (int j = i + 1; j < D; ++j) {
+      Drone<R>& a = dr[i];
+      Drone<R>& b = dr[j];
+      const R dx = b.pos[0] - a.pos[0], dy = b.pos[1] - a.pos[1], dz = b.pos[2] - a.pos[2];
+      const R d2 = dx * dx + dy * dy;
+      if (!(d2 < r2 * r2)) continue;
+      const R pz = (ez[i] + ez[j]) - std::fabs(dz);
+      if (!(pz > R(0))) continue;
+      const R dxy = std::sqrt(d2);
+      const R pxy = r2 - dxy;
+      if (pz < pxy) {   // vertical separation; j is above i when dz >= 0
+        const R sg = dz >= R(0) ? R(1) : R(-1);
+        const R half = R(0.5) * pz;
+        a.pos[2] = a.pos[2] - sg * half;
+        b.pos[2] = b.pos[2] + sg * half;
+        const R rel = (b.vel[2] - a.vel[2]) * sg;
+        if (rel < R(0)) {
+          const R m = R(0.5) * (a.vel[2] + b.vel[2]);
+          a.vel[2] = m;
+          b.vel[2] = m;
+        }
+      } else {          // horizontal separation along the centre line
+        R nx = R(1), ny = R(0);
+        if (dxy > R(0)) { nx = dx / dxy; ny = dy / dxy; }
+        const R half = R(0.5) * pxy;
+        a.pos[0] = a.pos[0] - nx * half; a.pos[1] = a.pos[1] - ny * half;
+        b.pos[0] = b.pos[0] + nx * half; b.pos[1] = b.pos[1] + ny * half;
+        const R rel = (b.vel[0] - a.vel[0]) * nx + (b.vel[1] - a.vel[1]) * ny;
+        if (rel < R(0)) {
+          const R hr = R(0.5) * rel;
+          a.vel[0] = a.vel[0] + hr * nx; a.vel[1] = a.vel[1] + hr * ny;
+          b.vel[0] = b.vel[0] - hr * nx; b.vel[1] = b.vel[1] - hr * ny;
+        }
+      }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // The vectorised env (oracle of qs_handle).
 // ---------------------------------------------------------------------------
@@ -823,6 +881,7 @@ template <class R> struct Sim {
         if (P.physics == QS_PHYS_PYB) pyb_dynamics(P, drones[e * D + d], &rpm[d * 4], snaps.data(), d);
         else dynamics(P, drones[e * D + d], &rpm[d * 4], snaps.data(), d);
       }
+      if (P.physics == QS_PHYS_PYB && D > 1) drone_contacts(&drones[e * D], D);   // Bullet's drone–drone contacts
       for (int d = 0; d < D; ++d)  // last_clipped_action = clipped_action (BA:372)
         for (int m = 0; m < 4; ++m) drones[e * D + d].last_rpm[m] = rpm[d * 4 + m];
     }

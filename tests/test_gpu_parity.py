@@ -299,3 +299,57 @@ def test_deferred_reset_search_matches_inkernel(precision, num_envs, steps, monk
     assert runs[0][3] > (50 if num_envs < 1024 else 0)   # resets happened
     for a, b in zip(runs[0][:3], runs[1][:3]):
         np.testing.assert_array_equal(a, b)
+
+
+def _collision_course_state(orc, rng, frac=0.5):
+    """A state where `frac` of the envs have their drones packed into a 0.3 m box at
+    z = 1 with horizontal velocities up to 2 m/s (drone–drone contacts within a few
+    substeps), the rest keep their reset layout (no contact possible)."""
+    st = orc.get_state(0)
+    E, D = orc.E, orc.D
+    for e in range(int(E * frac)):
+        sl = slice(e * D, (e + 1) * D)
+        st[0:2, sl] = rng.uniform(-0.15, 0.15, (2, D))
+        st[2, sl] = 1.0 + rng.uniform(-0.02, 0.02, D)
+        st[7:9, sl] = rng.uniform(-2, 2, (2, D))
+        st[9, sl] = rng.uniform(-0.5, 0.5, D)
+    return st
+
+
+@pytest.mark.parametrize("precision", [8, 4])
+def test_drone_contact_parity(precision):
+    """Physics.PYB drone–drone contact (oracle drone_contacts): the
+    kernel's broad phase + per-env pair pass against the oracle's every-substep
+    pair pass, teacher-forced from states on a collision course (half the envs of
+    each wave) — fp64 to 1e-12, fp32 to the teacher-forced bounds."""
+    cfg = dict(task="multihover", num_drones=4, act="one_d_rpm", physics="pyb",
+               initial_xyzs=[[0, 0, 1], [1, 0, 1], [0, 1, 1], [1, 1, 1]])
+    E = 48   # 3 waves of 16 envs
+    sw, orc = make_pair(cfg, E, precision)
+    sw.reset(0)
+    orc.reset(0)
+    rng = np.random.default_rng(4)
+    truth = qs_oracle.OracleSim(num_envs=E, precision=8, **cfg)
+    truth.reset(0)
+    st = _collision_course_state(truth, rng)
+    truth.set_state(0, st)
+    contacts = 0
+    for t in range(12):
+        for block in (0, 1, 2, 3):
+            b = truth.get_state(block)
+            orc.set_state(block, b)
+            sw.set_state(block, torch.as_tensor(b))
+        before = truth.get_state(0)
+        acts = np.zeros((E, 4, 1), np.float32)   # hover rpm: only the contacts move the drones apart
+        r = sw.step(torch.as_tensor(acts, device=sw.device))
+        c = orc.step(acts)
+        truth.step(acts)
+        torch.cuda.synchronize()
+        after = orc.get_state(0)
+        # count drones whose horizontal velocity changed by more than the damping can do
+        dv = np.abs(after[7:9] - before[7:9]).max(axis=0)
+        contacts += int((dv > 0.05).sum())
+        assert_close(f"state t={t}", sw.get_state(0).cpu().numpy(), after, STATE_TOL[precision])
+        assert_close(f"obs t={t}", r.obs.cpu().numpy(), c["obs"], OBS_TOL[precision])
+    assert contacts > 20
+    sw.close()
