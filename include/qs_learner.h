@@ -8,13 +8,15 @@
  *     E×D×T on the host, float64
  *   MAPPOAgent.update optimizer steps (mappo/agent.py:731-734,  qs_adam_gated +
  *     757-760): torch.optim.Adam.step, actor step skipped         qs_adam_commit
- *     unless approx_kl <= 1.5*target_kl (host .item() sync)
+ *     unless approx_kl <= 1.5*target_kl (host .item() sync)        qs_adam_step, qs_adam_multi
  *   compute_policy_loss / compute_value_loss forward and their   qs_ppo_heads
  *     autograd backward down to the actor mean and critic value
  *     (mappo/agent.py:602-683): ~60 small torch kernels
  *   MLP forward/backward (neural_networks.py:18-54) outside the   qs_mlp_bias_tanh,
  *     GEMMs: bias + tanh, the linear head, tanh backward and the   qs_mlp_tanh_bwd,
  *     bias / weight-gradient reductions (torch autograd kernels)   qs_mlp_sum_partials
+ *   the same MLP at hidden 256, forward and backward fused on     qs_mlp3_fwd,
+ *     MFMA (nn.Linear + torch.tanh autograd in the reference)      qs_mlp3_bwd
  *
  * All pointers are device pointers; every call is asynchronous on `stream`
  * (hipStream_t as void*) and contains no host synchronisation, so it can be
@@ -102,11 +104,44 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
                               float* const* d0, const int64_t* n0, float* const* d1, const int64_t* n1,
                               float* const* d2, void* stream);
 
+/* Fused tanh MLP with two hidden layers of N = 256 and a linear head of
+ * A <= 4 outputs (the learner's actor and critic at the reference's
+ * hidden_dim 256, learn_mappo.py:196), on the f32-input MFMA, activations
+ * transposed and register-resident (learner.hip).
+ * qs_mlp3_pack: W1 [N][I], W2 [N][N] → pack[qs_mlp3_pack_floats(I)], the
+ *   weights in MFMA-operand order; repack after every weight update.
+ * qs_mlp3_fwd: H1ᵀ = tanh(W1·Xᵀ + b1), H2ᵀ = tanh(W2·H1ᵀ + b2),
+ *   out = H2·W3ᵀ + b3; X [K][I] (I <= 1024), W3 [A][N]; writes H1T, H2T
+ *   [N][K] (saved for the backward) and out [K][A].
+ * qs_mlp3_bwd: given dout [K][A]: dZ2ᵀ = (W3ᵀ·doutᵀ) ⊙ (1 − H2ᵀ²) and
+ *   dZ1ᵀ = (W2ᵀ·dZ2ᵀ) ⊙ (1 − H1ᵀ²) [N][K], and per 128-row block g of
+ *   qs_mlp3_tiles(K) the partial sums partA[g][N + A·N + A] =
+ *   [Σ dZ2 | Σ dout_a·H2 | Σ dout_a] and partB[g][N] = Σ dZ1 over the block's
+ *   rows (reduce with qs_mlp_sum_partials; the weight gradients are
+ *   dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·X). */
+int32_t qs_mlp3_tiles(int64_t K);
+int64_t qs_mlp3_pack_floats(int32_t I);
+int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* pack, void* stream);
+int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
+                const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream);
+int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, const float* H1T, const float* H2T,
+                const float* pack, const float* W3, float* dZ2T, float* dZ1T, float* partA, float* partB,
+                void* stream);
+
 /* qs_adam_gated followed by qs_adam_commit, in one launch: `work` is a device
  * uint32 counter, zero before the first call (the kernel leaves it zero). */
 int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step,
                  float lr, float beta1, float beta2, float eps, const float* gate_val, float gate_thr, void* work,
                  void* stream);
+
+/* qs_adam_step over nseg (<= 4) flat buffers in one launch (the learner's
+ * actor, gated on approx_kl, and critic, AG:731-760): segment i is exactly the
+ * single-buffer call with argument i of every array (host arrays of device
+ * pointers / values).  work: device uint32[4], zero before the first call. */
+int qs_adam_multi(int32_t nseg, float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr, const float* beta1,
+                  const float* beta2, const float* eps, const float* const* gate_val, const float* gate_thr, void* work,
+                  void* stream);
 
 const char* qs_learner_last_error(void);
 

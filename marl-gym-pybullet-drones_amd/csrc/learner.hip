@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 
@@ -468,6 +469,419 @@ __global__ void adam_step_kernel(long long n, float* __restrict__ p, const float
     if (gate_ok(gate_val, gate_thr)) *step = *step + 1.0f;
   }
 }
+
+// ------------------------------------------------ fused 256-wide tanh MLP (MFMA)
+// The reference MLP (neural_networks.py:18-54) with two tanh hidden layers of
+// N = 256 and a linear head of A <= 4 outputs, on the f32-input MFMA
+// (v_mfma_f32_32x32x2_f32: exact fp32 FMA chains at the fp32 rate), for the
+// large batches of the actor update (>= 512 tiles of 32 rows).
+//
+// Transposed, register-resident formulation.  A tile is 32 rows (batch
+// samples) r; the kernels compute Zᵀ = W·Xᵀ so that a 32×32 accumulator holds
+// hidden units m on its 16 registers and samples r on its lanes (C/D map:
+// lane l = 32h + c holds column c and rows (i & 3) + 8 (i >> 2) + 4h of
+// register i).  That is exactly the B-operand map of the next product, which
+// sums over the hidden index (B[k][col]: lane 32h + c supplies column c and
+// k-slot h), so tanh(Z1ᵀ + b1) feeds layer 2 straight from registers: no LDS
+// round trip for the activations, no transposes.  The weights are the A
+// operands: qs_mlp3_pack lays them out in MFMA-step order (lane-contiguous
+// float4 = 4 steps), and a workgroup of 4 waves (4 tiles) streams them through
+// a double-buffered 16-KB LDS window, one chunk = 64 MFMA steps of every wave.
+// Hᵀ and dZᵀ are stored [N][K] (a register store is two 128-B row segments).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kM3N = 256;       // hidden width of the fused path
+constexpr int kM3NB = 8;        // 32-wide hidden blocks
+constexpr int kM3Steps2 = 128;  // MFMA steps of a 256-deep contraction (2 k per step)
+constexpr int kM3ChunkF = 8192; // floats per streamed chunk (32 KB = 128 steps x 64 lanes)
+constexpr int kM3Waves = 4;     // waves (tiles) per workgroup
+constexpr int kM3Block = 64 * kM3Waves;
+
+__device__ __forceinline__ int m3_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }   // C/D row of reg i
+__device__ __forceinline__ int m3_ip(int I) { return (I + 15) & ~15; }                        // padded input width
+
+// Raw buffer access: lanes past the batch get offset kM3OOB, which the
+// hardware drops on stores and reads as 0 — no per-element branches.
+constexpr unsigned kM3OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t m3_rsrc(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float m3_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void m3_st(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
+
+// tanh as 1 − 2/(e^{2x} + 1) with the hardware exp2 and rcp: five VALU
+// instructions, no branches, saturates to ±1; absolute error a few 1e-7
+// (fp32 rounding level of the activations).
+__device__ __forceinline__ float m3_tanh(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);   // e^{2x}
+  return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+
+// Σ over the 32 lanes of each half-wave, for each of the 16 registers:
+// returns in lane 32h + c the sum of register j = 8b4 + 4b3 + 2b2 + b1 (b = bits of c).
+__device__ __forceinline__ float m3_lane_sum16(const float* v) {
+  const int c = threadIdx.x & 31;
+  float a8[8], a4[4], a2[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool up = c & 16;
+    const float keep = up ? v[j + 8] : v[j], send = up ? v[j] : v[j + 8];
+    a8[j] = keep + __shfl_xor(send, 16, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool up = c & 8;
+    const float keep = up ? a8[j + 4] : a8[j], send = up ? a8[j] : a8[j + 4];
+    a4[j] = keep + __shfl_xor(send, 8, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const bool up = c & 4;
+    const float keep = up ? a4[j + 2] : a4[j], send = up ? a4[j] : a4[j + 2];
+    a2[j] = keep + __shfl_xor(send, 4, 64);
+  }
+  const bool up = c & 2;
+  const float t = (up ? a2[1] : a2[0]) + __shfl_xor(up ? a2[0] : a2[1], 2, 64);
+  return t + __shfl_xor(t, 1, 64);
+}
+__device__ __forceinline__ int m3_lane_sum16_reg() {
+  const int c = threadIdx.x & 31;
+  return 8 * ((c >> 4) & 1) + 4 * ((c >> 3) & 1) + 2 * ((c >> 2) & 1) + ((c >> 1) & 1);
+}
+
+// Packed weights (float offsets; qs_mlp3_pack_floats):
+//   W1p  [Ip/8 q][8 mb][64 lane][4]: step s = 4q + e, lane 32h + c → W1[32mb + c][2s + h]
+//   W2p  [8 mb][32 q][64][4]:  step s = 16 nb + i → W2[32mb + c][32nb + row(i, h)]
+//   W2Tp [8 nb][32 q][64][4]:  step s = 16 mb + i → W2[32mb + row(i, h)][32nb + c]
+__device__ __forceinline__ size_t m3_w1p_floats(int Ip) { return (size_t)(Ip / 8) * kM3NB * 256; }
+__device__ __forceinline__ size_t m3_w2_floats() { return (size_t)kM3NB * 32 * 256; }
+
+__global__ void mlp3_pack_kernel(int I, const float* __restrict__ W1, const float* __restrict__ W2,
+                                 float* __restrict__ pack) {
+  const int Ip = m3_ip(I);
+  const size_t n1 = m3_w1p_floats(Ip), n2 = m3_w2_floats();
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n1 + 2 * n2; t += (size_t)gridDim.x * blockDim.x) {
+    const size_t u = t < n1 ? t : (t < n1 + n2 ? t - n1 : t - n1 - n2);
+    const int e = u & 3, lane = (u >> 2) & 63, c = lane & 31, h = lane >> 5;
+    const size_t rest = u >> 8;
+    float v;
+    if (t < n1) {
+      const int mb = rest % kM3NB, q = rest / kM3NB, k = 2 * (4 * q + e) + h;
+      v = k < I ? W1[(size_t)(32 * mb + c) * I + k] : 0.f;
+    } else {
+      const int q = rest % 32, blk = rest / 32, st = 4 * q + e, i = st & 15, other = st >> 4;
+      if (t < n1 + n2) v = W2[(size_t)(32 * blk + c) * kM3N + 32 * other + m3_row(i, h)];   // blk = mb, other = nb
+      else v = W2[(size_t)(32 * other + m3_row(i, h)) * kM3N + 32 * blk + c];               // blk = nb, other = mb
+    }
+    pack[t] = v;
+  }
+}
+
+// Double-buffered chunk stream: the workgroup's 256 threads load a 16-KB chunk
+// of `src` into registers one chunk ahead of its LDS write, and every wave
+// consumes chunk c from buf[c & 1] after the barrier that makes it visible.
+struct M3Stream {
+  const float4* src;
+  float4* buf;   // LDS [2][kM3ChunkF / 4]
+  float4 st[kM3ChunkF / 4 / kM3Block];
+  __device__ __forceinline__ void load(int c) {
+#pragma unroll
+    for (int j = 0; j < kM3ChunkF / 4 / kM3Block; ++j) st[j] = src[(size_t)c * (kM3ChunkF / 4) + j * kM3Block + threadIdx.x];
+  }
+  __device__ __forceinline__ void store(int c) {
+#pragma unroll
+    for (int j = 0; j < kM3ChunkF / 4 / kM3Block; ++j) buf[(c & 1) * (kM3ChunkF / 4) + j * kM3Block + threadIdx.x] = st[j];
+  }
+  // LDS-only fences around a plain barrier: the LDS writes are complete and
+  // ordered, but the next chunk's global loads stay in flight (a full
+  // __syncthreads would drain vmcnt)
+  __device__ __forceinline__ static void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  }
+};
+
+// Stream `n` chunks: body(c, chunk) with chunk = the LDS float4 window of chunk c.
+template <class Body>
+__device__ __forceinline__ void m3_stream(M3Stream& S, int n, Body body) {
+  S.load(0);
+  S.store(0);
+  if (n > 1) S.load(1);
+  for (int c = 0; c < n; ++c) {
+    M3Stream::sync();
+    if (c + 1 < n) S.store(c + 1);
+    if (c + 2 < n) S.load(c + 2);
+    body(c, S.buf + (c & 1) * (kM3ChunkF / 4));
+  }
+  M3Stream::sync();
+}
+
+template <int A>
+__global__ void __launch_bounds__(kM3Block) mlp3_fwd_kernel(long long K, int I, const float* __restrict__ X,
+                                                            const float* __restrict__ pack, const float* __restrict__ b1,
+                                                            const float* __restrict__ b2, const float* __restrict__ W3,
+                                                            const float* __restrict__ b3, float* __restrict__ H1T,
+                                                            float* __restrict__ H2T, float* __restrict__ out) {
+  __shared__ float4 wbuf[2 * kM3ChunkF / 4];
+  __shared__ float sb1[kM3N], sb2[kM3N], sw3[A * kM3N];   // biases and head weights, read in the epilogues
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  const long long r = ((long long)blockIdx.x * kM3Waves + w) * 32 + c;
+  const bool rv = r < K;
+  const int Ip = m3_ip(I);
+  for (int j = threadIdx.x; j < kM3N; j += kM3Block) { sb1[j] = b1[j]; sb2[j] = b2[j]; }
+  for (int j = threadIdx.x; j < A * kM3N; j += kM3Block) sw3[j] = W3[j];
+  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, (size_t)K * I * 4), h1r = m3_rsrc(H1T, (size_t)K * kM3N * 4),
+                               h2r = m3_rsrc(H2T, (size_t)K * kM3N * 4);
+  const unsigned xoff = rv ? (unsigned)(r * I * 4) : kM3OOB, roff = rv ? (unsigned)(r * 4) : kM3OOB;
+  const unsigned kstride = (unsigned)(K * 4);
+  M3Stream S{reinterpret_cast<const float4*>(pack), wbuf};
+  // layer 1: Z1ᵀ = W1·Xᵀ; chunk = 4 k-quads x 8 blocks; B = X[r][2s + h]
+  f32x16 acc[kM3NB];
+#pragma unroll
+  for (int mb = 0; mb < kM3NB; ++mb) acc[mb] = f32x16{};
+  m3_stream(S, Ip / 32 + ((Ip & 16) ? 1 : 0), [&](int ch, const float4* wc) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int q = 4 * ch + qq;
+      if (q >= Ip / 8) break;
+      float xb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 2 * (4 * q + e) + h;
+        xb[e] = m3_ld(xr, k < I ? xoff + 4u * k : kM3OOB);
+      }
+#pragma unroll
+      for (int mb = 0; mb < kM3NB; ++mb) {
+        const float4 wv = wc[(qq * kM3NB + mb) * 64 + lane];
+        acc[mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, xb[0], acc[mb], 0, 0, 0);
+        acc[mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, xb[1], acc[mb], 0, 0, 0);
+        acc[mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, xb[2], acc[mb], 0, 0, 0);
+        acc[mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, xb[3], acc[mb], 0, 0, 0);
+      }
+    }
+  });
+  // bias + tanh in the accumulators → H1ᵀ registers (the B operand of layer 2) and HBM
+  float hb[kM3Steps2];
+#pragma unroll
+  for (int nb = 0; nb < kM3NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = 32 * nb + m3_row(i, h);
+      const float v = m3_tanh(acc[nb][i] + sb1[m]);
+      hb[nb * 16 + i] = v;
+      m3_st(h1r, roff + (unsigned)m * kstride, v);
+    }
+  // layer 2: Z2ᵀ[mb] = W2[mb]·H1ᵀ, one chunk (128 steps) per block; the
+  // epilogue of block mb − 1 (bias + tanh, H2ᵀ store, head) sits in block mb's
+  // basic block, beside its MFMAs
+  S.src = reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip));
+  float hs[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) hs[a] = 0.f;
+  f32x16 zp = f32x16{};
+  auto epi2 = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = 32 * mb + m3_row(i, h);
+      const float v = m3_tanh(zp[i] + sb2[m]);
+      m3_st(h2r, roff + (unsigned)m * kstride, v);
+#pragma unroll
+      for (int a = 0; a < A; ++a) hs[a] += v * sw3[a * kM3N + m];
+    }
+  };
+  m3_stream(S, kM3NB, [&](int mb, const float4* wc) {
+    f32x16 z = f32x16{};
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const float4 wv = wc[q * 64 + lane];
+      z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, hb[4 * q + 0], z, 0, 0, 0);
+      z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, hb[4 * q + 1], z, 0, 0, 0);
+      z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, hb[4 * q + 2], z, 0, 0, 0);
+      z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, hb[4 * q + 3], z, 0, 0, 0);
+      if (q == 0 && mb > 0) epi2(mb - 1);
+    }
+    zp = z;
+  });
+  epi2(kM3NB - 1);
+  // head: out[r][a] = Σ_m H2ᵀ[m][r]·W3[a][m] + b3[a] (the two halves hold the two m sets)
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    const float t = hs[a] + __shfl_xor(hs[a], 32, 64);
+    if (h == 0 && rv) out[r * A + a] = t + b3[a];
+  }
+}
+
+// partA[tile][N + A·N + A] = [Σ_r dZ2ᵀ | Σ_r dout_a·H2ᵀ | Σ_r dout_a], partB[tile][N] = Σ_r dZ1ᵀ.
+template <int A>
+__global__ void __launch_bounds__(kM3Block) mlp3_bwd_kernel(long long K, const float* __restrict__ dout,
+                                                            const float* __restrict__ H1T, const float* __restrict__ H2T,
+                                                            const float* __restrict__ pack, int Ip,
+                                                            const float* __restrict__ W3, float* __restrict__ dZ2T,
+                                                            float* __restrict__ dZ1T, float* __restrict__ partA,
+                                                            float* __restrict__ partB) {
+  constexpr int N = kM3N, PA = N + A * N + A;
+  __shared__ float4 wbuf[2 * kM3ChunkF / 4];
+  __shared__ float sw3[A * kM3N];
+  __shared__ float spa[kM3Waves][PA], spb[kM3Waves][N];   // per-wave (tile) partials, combined per workgroup
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  const long long tile = (long long)blockIdx.x * kM3Waves + w;
+  const long long r = tile * 32 + c;
+  const bool rv = r < K;
+  for (int j = threadIdx.x; j < A * kM3N; j += kM3Block) sw3[j] = W3[j];
+  const size_t hbytes = (size_t)K * kM3N * 4;
+  const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), h2r = m3_rsrc(H2T, hbytes), z2r = m3_rsrc(dZ2T, hbytes),
+                               z1r = m3_rsrc(dZ1T, hbytes);
+  const unsigned roff = rv ? (unsigned)(r * 4) : kM3OOB, kstride = (unsigned)(K * 4);
+  float dv[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) dv[a] = rv ? dout[r * A + a] : 0.f;
+  float* pa = spa[w];
+  const int jr = m3_lane_sum16_reg();
+#pragma unroll
+  for (int a = 0; a < A; ++a) {   // Σ_r dout_a over the tile (half 0 holds the 32 rows)
+    float t = h == 0 ? dv[a] : 0.f;
+    for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) pa[N + A * N + a] = t;
+  }
+  // 1. dZ2ᵀ = (W3ᵀ·doutᵀ) ⊙ (1 − H2ᵀ²) in registers (the B operand of dH1ᵀ); bias / head partials
+  float zb[kM3Steps2];
+#pragma unroll
+  for (int mb = 0; mb < kM3NB; ++mb) {
+    float hw[A][16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = 32 * mb + m3_row(i, h);
+      const float hv = m3_ld(h2r, roff + (unsigned)m * kstride);
+      float g = 0.f;
+#pragma unroll
+      for (int a = 0; a < A; ++a) { g += dv[a] * sw3[a * N + m]; hw[a][i] = dv[a] * hv; }
+      const float zz = g * (1.f - hv * hv);
+      zb[mb * 16 + i] = zz;
+      m3_st(z2r, roff + (unsigned)m * kstride, zz);
+    }
+    const float sdb = m3_lane_sum16(zb + mb * 16);
+    float sdw[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) sdw[a] = m3_lane_sum16(hw[a]);
+    if ((c & 1) == 0) {   // tiles past K write zeros: every partial row is defined
+      const int m = 32 * mb + m3_row(jr, h);
+      pa[m] = sdb;
+#pragma unroll
+      for (int a = 0; a < A; ++a) pa[N + a * N + m] = sdw[a];
+    }
+  }
+  // 2. dH1ᵀ[nb] = (W2ᵀ)[nb]·dZ2ᵀ, one chunk per block; the epilogue of block
+  // nb − 1 (dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²), store, Σ_r) beside block nb's MFMAs
+  M3Stream S{reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip) + m3_w2_floats()), wbuf};
+  // H1ᵀ of block nb is loaded at the start of block nb and used one block later
+  // (the epilogue's loads never stall the MFMA chain)
+  f32x16 dp = f32x16{};
+  float h1p[16], h1n[16];
+  auto epi1 = [&](int nb) {
+    float z1[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = 32 * nb + m3_row(i, h);
+      z1[i] = dp[i] * (1.f - h1p[i] * h1p[i]);
+      m3_st(z1r, roff + (unsigned)n * kstride, z1[i]);
+    }
+    const float sdb = m3_lane_sum16(z1);
+    if ((c & 1) == 0) spb[w][32 * nb + m3_row(jr, h)] = sdb;
+  };
+  m3_stream(S, kM3NB, [&](int nb, const float4* wc) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) h1n[i] = m3_ld(h1r, roff + (unsigned)(32 * nb + m3_row(i, h)) * kstride);
+    f32x16 d = f32x16{};
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const float4 wv = wc[q * 64 + lane];
+      d = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, zb[4 * q + 0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, zb[4 * q + 1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, zb[4 * q + 2], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, zb[4 * q + 3], d, 0, 0, 0);
+      if (q == 16 && nb > 0) epi1(nb - 1);
+    }
+    dp = d;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) h1p[i] = h1n[i];
+  });
+  epi1(kM3NB - 1);
+  // the workgroup's four tiles → one partial row, waves in order (a fixed summation order)
+  __syncthreads();
+  for (int j = threadIdx.x; j < PA; j += kM3Block)
+    partA[(size_t)blockIdx.x * PA + j] = ((spa[0][j] + spa[1][j]) + spa[2][j]) + spa[3][j];
+  for (int j = threadIdx.x; j < N; j += kM3Block)
+    partB[(size_t)blockIdx.x * N + j] = ((spb[0][j] + spb[1][j]) + spb[2][j]) + spb[3][j];
+}
+
+
+// torch.optim.Adam over several flat parameter buffers in one launch (the
+// actor's, KL-gated, and the critic's): blocks [start[i], start[i+1]) serve
+// segment i.  Thread 0 of each block forms the bias corrections once from the
+// step count (fp64, as torch's host-side step_size), and the last block of a
+// segment to finish commits its step count (gate permitting).
+constexpr int kAdamMaxSeg = 4;
+constexpr int kAdamBlock = 256;
+struct AdamSeg {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  float* step;
+  const float* gate;
+  long long n;
+  float lr, b1, b2, eps, thr;
+};
+struct AdamSegs {
+  AdamSeg s[kAdamMaxSeg];
+  int start[kAdamMaxSeg + 1];
+  int n;
+};
+// A segment gets at most kAdamSegBlocks workgroups (grid-stride): the
+// last-block arrival count is one atomic per workgroup on one address, and those
+// serialise at the L2 — a few dozen cost well under a microsecond, a thousand
+// cost ~10 µs.
+constexpr int kAdamSegBlocks = 64;
+__global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsigned* done) {
+  __shared__ float sc[2];
+  __shared__ bool last;
+  int si = 0;
+  while (si + 1 < S.n && (int)blockIdx.x >= S.start[si + 1]) ++si;
+  const AdamSeg& A = S.s[si];
+  const int nb = S.start[si + 1] - S.start[si];
+  const bool open = gate_ok(A.gate, A.thr);
+  if (threadIdx.x == 0) {
+    const double t = (double)(*A.step) + 1.0;
+    sc[0] = (float)(1.0 - pow((double)A.b1, t));        // bias_correction1
+    sc[1] = (float)sqrt(1.0 - pow((double)A.b2, t));   // sqrt(bias_correction2)
+  }
+  __syncthreads();
+  if (open) {
+    const float step_size = A.lr / sc[0], bc2_sqrt = sc[1];
+    const long long stride = (long long)nb * kAdamBlock;
+    for (long long i = (long long)(blockIdx.x - S.start[si]) * kAdamBlock + threadIdx.x; i < A.n; i += stride) {
+      const float gi = A.g[i];
+      const float mi = A.m[i] + (1.0f - A.b1) * (gi - A.m[i]);
+      const float vi = A.v[i] * A.b2 + (1.0f - A.b2) * gi * gi;
+      A.m[i] = mi;
+      A.v[i] = vi;
+      const float denom = sqrtf(vi) / bc2_sqrt + A.eps;
+      A.p[i] = A.p[i] - step_size * (mi / denom);
+    }
+  }
+  __syncthreads();
+  // every block read *step before counting itself; p/m/v go to later launches only
+  if (threadIdx.x == 0) last = atomicAdd(&done[si], 1u) == (unsigned)nb - 1;
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    done[si] = 0;
+    if (open) *A.step = *A.step + 1.0f;
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -629,6 +1043,88 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
   hipLaunchKernelGGL(mlp_sum_multi_kernel, dim3(blocks), dim3(kMlpSumBlock), 0, (hipStream_t)stream, T);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials_multi: ") + hipGetErrorString(e));
+}
+
+int32_t qs_mlp3_tiles(int64_t K) { return (int32_t)((K + 127) / 128); }   // partial rows: one per workgroup
+
+int64_t qs_mlp3_pack_floats(int32_t I) {
+  const int64_t Ip = (I + 15) & ~15;
+  return (Ip / 8) * kM3NB * 256 + 2 * (int64_t)kM3NB * 32 * 256;
+}
+
+int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* pack, void* stream) {
+  if (I <= 0 || I > 1024 || N != kM3N || !W1 || !W2 || !pack) return fail(QS_E_INVALID, "qs_mlp3_pack: bad argument");
+  const int64_t n = qs_mlp3_pack_floats(I);
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(mlp3_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (int)I, W1, W2, pack);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_pack: ") + hipGetErrorString(e));
+}
+
+int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
+                const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream) {
+  if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !X || !pack ||
+      !b1 || !b2 || !W3 || !b3 || !H1T || !H2T || !out)
+    return fail(QS_E_INVALID, "qs_mlp3_fwd: bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
+  const unsigned grid = (unsigned)((K + 127) / 128);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3Block), 0, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1, b2,
+                       W3, b3, H1T, H2T, out);
+  };
+  switch (A) {
+    case 1: go(mlp3_fwd_kernel<1>); break;
+    case 2: go(mlp3_fwd_kernel<2>); break;
+    case 3: go(mlp3_fwd_kernel<3>); break;
+    default: go(mlp3_fwd_kernel<4>); break;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_fwd: ") + hipGetErrorString(e));
+}
+
+int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, const float* H1T, const float* H2T,
+                const float* pack, const float* W3, float* dZ2T, float* dZ1T, float* partA, float* partB,
+                void* stream) {
+  if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !dout ||
+      !H1T || !H2T || !pack || !W3 || !dZ2T || !dZ1T || !partA || !partB)
+    return fail(QS_E_INVALID, "qs_mlp3_bwd: bad argument (N must be 256, 1 <= A <= 4)");
+  const unsigned grid = (unsigned)((K + 127) / 128);
+  const int Ip = (I + 15) & ~15;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3Block), 0, (hipStream_t)stream, (long long)K, dout, H1T, H2T, pack, Ip,
+                       W3, dZ2T, dZ1T, partA, partB);
+  };
+  switch (A) {
+    case 1: go(mlp3_bwd_kernel<1>); break;
+    case 2: go(mlp3_bwd_kernel<2>); break;
+    case 3: go(mlp3_bwd_kernel<3>); break;
+    default: go(mlp3_bwd_kernel<4>); break;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_bwd: ") + hipGetErrorString(e));
+}
+
+int qs_adam_multi(int32_t nseg, float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr, const float* beta1,
+                  const float* beta2, const float* eps, const float* const* gate_val, const float* gate_thr, void* work,
+                  void* stream) {
+  if (nseg <= 0 || nseg > kAdamMaxSeg || !params || !grads || !exp_avg || !exp_avg_sq || !step || !n || !lr || !beta1 ||
+      !beta2 || !eps || !gate_val || !gate_thr || !work)
+    return fail(QS_E_INVALID, "qs_adam_multi: bad argument (1..4 segments)");
+  AdamSegs S{};
+  S.n = nseg;
+  int blocks = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (n[i] <= 0 || !params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i] || !step[i])
+      return fail(QS_E_INVALID, "qs_adam_multi: bad segment");
+    S.s[i] = AdamSeg{params[i], grads[i], exp_avg[i], exp_avg_sq[i], step[i], gate_val[i], (long long)n[i], lr[i],
+                     beta1[i], beta2[i], eps[i], gate_thr[i]};
+    S.start[i] = blocks;
+    blocks += (int)std::min<int64_t>((n[i] + kAdamBlock - 1) / kAdamBlock, kAdamSegBlocks);
+  }
+  S.start[nseg] = blocks;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(kAdamBlock), 0, (hipStream_t)stream, S, (unsigned*)work);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_multi: ") + hipGetErrorString(e));
 }
 
 int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step, float lr,

@@ -61,7 +61,8 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            # include/qs_learner.h
            "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_ppo_heads_work_bytes",
            "qs_mlp_bias_tanh", "qs_mlp_bwd_blocks", "qs_mlp_tanh_bwd", "qs_mlp_sum_partials",
-           "qs_mlp_sum_partials_multi", "qs_adam_step",
+           "qs_mlp_sum_partials_multi", "qs_adam_step", "qs_mlp3_tiles", "qs_mlp3_pack_floats",
+           "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_bwd", "qs_adam_multi",
            "qs_learner_last_error")
 
 _lib = None
@@ -112,11 +113,18 @@ def load():
     L.qs_mlp_sum_partials.argtypes = [ctypes.c_int32, i64, vp, vp, i64, vp, i64, vp, vp]
     L.qs_mlp_sum_partials_multi.argtypes = [ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.qs_adam_step.argtypes = [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, f32, vp, vp]
+    L.qs_adam_multi.argtypes = [ctypes.c_int32] + [vp] * 14
+    L.qs_mlp3_tiles.argtypes = [i64]
+    L.qs_mlp3_pack_floats.argtypes = [ctypes.c_int32]
+    L.qs_mlp3_pack.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp]
+    L.qs_mlp3_fwd.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 10
+    L.qs_mlp3_bwd.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 10
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):
             getattr(L, name).restype = i32
     L.qs_ppo_heads_work_bytes.restype = i64
+    L.qs_mlp3_pack_floats.restype = i64
     _lib = L
     return L
 

@@ -132,10 +132,28 @@ def _splitk_into(dst, dy, x):
     _sum_partials(S, part[0].numel(), part, dst, dst.numel())
 
 
+def _splitk_nt(dst, a, b, b_rows_are_k):
+    """dst[N][M] += a·bᵀ (b [M][K], b_rows_are_k False: b [K][M]) with a [N][K]: a
+    weight gradient from transposed activations, as S K-chunk GEMMs + a fixed-order sum."""
+    K = a.shape[1]
+    S = _splitk_chunks(K)
+    bk = b.t() if b_rows_are_k else b   # [K][M] view
+    if S == 1:
+        dst.addmm_(a, bk)
+        return
+    a3 = a.view(a.shape[0], S, K // S).transpose(0, 1)                                  # [S][N][K/S]
+    b3 = b.view(b.shape[0], S, K // S).permute(1, 2, 0) if b_rows_are_k else b.view(S, K // S, -1)   # [S][K/S][M]
+    part = torch.bmm(a3, b3)
+    _sum_partials(S, part[0].numel(), part, dst, dst.numel())
+
+
 class _TanhMLP3(torch.autograd.Function):
     """The reference MLP with two tanh hidden layers and a linear head
-    (neural_networks.py:18-54), forward and backward, on the MI355X path:
-    hipBLASLt GEMMs for the contractions, HIP kernels for everything between them
+    (neural_networks.py:18-54), forward and backward, on the MI355X path.
+    Hidden width 256 (the reference MAPPO's hidden_dim, learn_mappo.py:196):
+    qs_mlp3_fwd / qs_mlp3_bwd fuse both layers, bias + tanh and the head on the
+    f32 MFMA with the pre-activations kept on chip; the weight gradients are
+    split-K GEMMs.  Other widths: hipBLASLt GEMMs for the contractions, HIP kernels for everything between them
     (qs_mlp_bias_tanh: bias + tanh, and the head's row dot products in the same
     pass; qs_mlp_tanh_bwd: the head backward fused with tanh's, and the bias /
     head-weight gradient partials; qs_mlp_sum_partials: fixed-order reductions,
@@ -147,6 +165,19 @@ class _TanhMLP3(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, w3, b3):
         lib, st = L.load(), _stream()
         K, N1, N2, A = x.shape[0], w1.shape[0], w2.shape[0], w3.shape[0]
+        # the fused kernels fill the chip from 512 tiles of 32 rows (the actor's minibatch)
+        ctx.fused = N1 == N2 == 256 and A <= 4 and x.shape[1] <= 1024 and K >= 16384
+        if ctx.fused:   # qs_mlp3_fwd: both layers and the head on MFMA, activations kept transposed [N][K]
+            I = x.shape[1]
+            pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device=x.device, dtype=torch.float32)
+            L.check(lib.qs_mlp3_pack(I, N1, L.ptr(w1), L.ptr(w2), L.ptr(pack), st), "qs_mlp3_pack")
+            h1 = torch.empty((N1, K), device=x.device, dtype=x.dtype)
+            h2 = torch.empty((N2, K), device=x.device, dtype=x.dtype)
+            out = torch.empty((K, A), device=x.device, dtype=x.dtype)
+            L.check(lib.qs_mlp3_fwd(K, I, N1, A, L.ptr(x), L.ptr(pack), L.ptr(b1), L.ptr(b2), L.ptr(w3), L.ptr(b3),
+                                    L.ptr(h1), L.ptr(h2), L.ptr(out), st), "qs_mlp3_fwd")
+            ctx.save_for_backward(x, w1, b1, w2, b2, w3, b3, h1, h2, pack)
+            return out
         h1 = torch.mm(x, w1.t())
         L.check(lib.qs_mlp_bias_tanh(K, N1, L.ptr(h1), L.ptr(b1), L.ptr(h1), 0, None, None, None, st), "qs_mlp_bias_tanh")
         h2 = torch.mm(h1, w2.t())
@@ -158,10 +189,25 @@ class _TanhMLP3(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x, w1, b1, w2, b2, w3, b3, h1, h2 = ctx.saved_tensors
+        x, w1, b1, w2, b2, w3, b3, h1, h2 = ctx.saved_tensors[:9]
         lib, st = L.load(), _stream()
         K, N1, N2, A = x.shape[0], w1.shape[0], w2.shape[0], w3.shape[0]
         dout = dout.contiguous()
+        if ctx.fused:   # qs_mlp3_bwd: head + tanh backward, dH1ᵀ = W2ᵀ·dZ2ᵀ on MFMA, tanh backward, bias partials
+            pack = ctx.saved_tensors[9]
+            G = int(lib.qs_mlp3_tiles(K))
+            dz2 = torch.empty_like(h2)   # [N][K]
+            dz1 = torch.empty_like(h1)
+            part_a = torch.empty((G, N2 * (1 + A) + A), device=x.device, dtype=torch.float32)
+            part_b = torch.empty((G, N1), device=x.device, dtype=torch.float32)
+            L.check(lib.qs_mlp3_bwd(K, x.shape[1], N2, A, L.ptr(dout), L.ptr(h1), L.ptr(h2), L.ptr(pack), L.ptr(w3),
+                                    L.ptr(dz2), L.ptr(dz1), L.ptr(part_a), L.ptr(part_b), st), "qs_mlp3_bwd")
+            _sum_partials(G, part_a.shape[1], part_a, b2.grad, N2, w3.grad, A * N2, b3.grad)
+            _sum_partials(G, N1, part_b, b1.grad, N1)
+            _splitk_nt(w2.grad, dz2, h1, True)    # dW2 = dZ2ᵀ·H1
+            _splitk_nt(w1.grad, dz1, x, False)    # dW1 = dZ1ᵀ·X
+            dx = dz1.t() @ w1 if ctx.needs_input_grad[0] else None
+            return dx, None, None, None, None, None, None
         G = int(lib.qs_mlp_bwd_blocks(K))
         # head + second tanh: dz2 = (dout·w3) ⊙ (1 − h2²); b2, w3, b3 gradients
         dz2 = torch.empty_like(h2)
@@ -372,6 +418,26 @@ class FlatBuffers:
                                  self.eps, L.ptr(gate_val), float(gate_thr), L.ptr(self._adam_work), st),
                 "qs_adam_step")
 
+    @staticmethod
+    def adam_multi(segs, work):
+        """One gated Adam step of several FlatBuffers in one launch (qs_adam_multi).
+        segs: [(buffers, gate_val tensor or None, gate_thr)]; work: device int32[4]."""
+        fb0 = segs[0][0]
+        if fb0.flat.device.type != 'cuda':
+            raise RuntimeError("FlatBuffers.adam_multi is the HIP qs_adam_multi kernel: the parameters must be on the GPU")
+        n = len(segs)
+        vp = ctypes.c_void_p
+        arr = lambda ct, vals: (ct * n)(*vals)
+        ptrs = lambda f: arr(vp, [f(s) for s in segs])
+        L.check(L.load().qs_adam_multi(
+            n, ptrs(lambda s: s[0].flat.data_ptr()), ptrs(lambda s: s[0].grad.data_ptr()),
+            ptrs(lambda s: s[0].exp_avg.data_ptr()), ptrs(lambda s: s[0].exp_avg_sq.data_ptr()),
+            ptrs(lambda s: s[0].step.data_ptr()), arr(ctypes.c_int64, [s[0].n for s in segs]),
+            arr(ctypes.c_float, [s[0].lr for s in segs]), arr(ctypes.c_float, [s[0].betas[0] for s in segs]),
+            arr(ctypes.c_float, [s[0].betas[1] for s in segs]), arr(ctypes.c_float, [s[0].eps for s in segs]),
+            ptrs(lambda s: s[1].data_ptr() if s[1] is not None else None), arr(ctypes.c_float, [s[2] for s in segs]),
+            L.ptr(work), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "qs_adam_multi")
+
     # torch.optim.Adam state_dict format (checkpoint compatibility, MP:203-229)
     def state_dict(self):
         state = {}
@@ -446,6 +512,7 @@ class MAPPOAgent:
         self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[:na])
         self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr, grad=self._reduce_buf[na:na + nc])
         self._kl = self._reduce_buf[na + nc:]
+        self._adam_work = torch.zeros(4, dtype=torch.int32, device=self.device)   # qs_adam_multi's block counters
         if _dist_world() > 1:   # identical initial weights on every rank
             tdist.broadcast(self.actor_opt.flat, 0)
             tdist.broadcast(self.critic_opt.flat, 0)
@@ -572,10 +639,11 @@ class MAPPOAgent:
         return self.target_kl <= 0 or bool(self._kl.item() <= 1.5 * self.target_kl)
 
     def _optimizer_steps(self):
-        """Actor Adam gated by the KL value on the device, critic Adam always (AG:731-760)."""
+        """Actor Adam gated by the KL value on the device, critic Adam always
+        (AG:731-760): both in one qs_adam_multi launch."""
         gate = self._kl if self.target_kl > 0 else None
-        self.actor_opt.adam(gate, 1.5 * self.target_kl)
-        self.critic_opt.adam(None, 0.0)
+        FlatBuffers.adam_multi([(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)],
+                               self._adam_work)
 
     def _exchange_and_step(self, world):
         self._exchange(world)
