@@ -1682,14 +1682,16 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     const int e = rq[2 + idx];
     const uint32_t genv = (uint32_t)(P.env_offset + e);
     const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
+    int best = kResetNone;   // the env's best try as of the previous chunk (workgroup-uniform)
     for (uint32_t c = (uint32_t)j;; c += (uint32_t)B) {
       const uint32_t base = 1u + c * kResetBlock;
-      // the best try so far, read once for the workgroup: the exit must be
-      // workgroup-uniform (the body holds barriers); a stale value only delays it
-      if (threadIdx.x == 0) s_best = __hip_atomic_load(&qwin[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      if ((int)base > s_best) break;
+      // the exit must be workgroup-uniform (the body holds barriers); the best
+      // try is read one chunk ahead — its ~µs atomic round trip runs under this
+      // chunk's Philox work — and a stale value only delays the exit
+      if ((int)base > best) break;
       if (base >= kMaxResetTries) break;   // cap: tries >= kMaxResetTries are never accepted (as in-kernel)
+      int next_best = 0;
+      if (threadIdx.x == 0) next_best = __hip_atomic_load(&qwin[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t t = base + threadIdx.x;
       bool ok = t < kMaxResetTries;
       T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
@@ -1706,9 +1708,11 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       if (threadIdx.x == 0) s_win = kResetNone;
       __syncthreads();
       if (ok) atomicMin(&s_win, (int)t);
+      if (threadIdx.x == 0) s_best = next_best;
       __syncthreads();
       const int w = s_win;
-      __syncthreads();   // s_win is rewritten next chunk
+      best = s_best;
+      __syncthreads();   // s_win / s_best are rewritten next chunk
       if (w != kResetNone) {
         if (threadIdx.x == 0) atomicMin(&qwin[idx], w);
         break;            // this workgroup's later chunks hold only larger tries
