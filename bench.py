@@ -320,6 +320,29 @@ def mappo_leg(args, rank, world, dist, T):
                        if world > 1 else None}}
 
 
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2   # wave64 VALU instr/s: 1024 SIMDs, one per 2 cycles (the fp32 vector rate)
+
+
+def valu_roofline(name, kernel_ms):
+    """VALU bound of a config's step kernel: its VALU issue cycles per launch
+    (profiles/r02_valu.json: SQ_INSTS_VALU, transcendentals at 4x) over the
+    SIMD-cycles of the measured launch time."""
+    path = os.path.join(ROOT, "profiles", "r02_valu.json")
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"].get(name)
+    except (OSError, ValueError):
+        return None
+    if not k:
+        return None
+    cycles = k["valu_cycles_per_launch"]
+    avail = 1024 * 2.4e9 * kernel_ms * 1e-3
+    return {"bound": "valu", "achieved": cycles / 2 / (kernel_ms * 1e-3), "peak": VALU_ISSUE_PEAK,
+            "unit": "wave64 VALU instr/s (2-cycle issue, transcendentals 8)", "frac": cycles / avail,
+            "valu_lane_instr_per_agent_step": k["valu_lane_instr_per_agent_step"],
+            "source": "profiles/r02_valu.json"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -354,6 +377,9 @@ def main():
                              "bytes_per_agent_step": c["bytes"],
                              "roofline_frac": nb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "episodes_ended_in_timed_window": ne}
+            vr = valu_roofline(name, km)
+            if vr:
+                configs[name]["valu_roofline"] = vr
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_src = pmc_traffic(E, D, args.act)

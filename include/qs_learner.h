@@ -112,7 +112,7 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
  *   weights in MFMA-operand order; repack after every weight update.
  * qs_mlp3_fwd: H1ᵀ = tanh(W1·Xᵀ + b1), H2ᵀ = tanh(W2·H1ᵀ + b2),
  *   out = H2·W3ᵀ + b3; X [K][I] (I <= 1024), W3 [A][N]; writes H1T, H2T
- *   [N][K] (saved for the backward) and out [K][A].
+ *   [N][K] (saved for the backward; both NULL for inference) and out [K][A].
  * qs_mlp3_bwd: given dout [K][A]: dZ2ᵀ = (W3ᵀ·doutᵀ) ⊙ (1 − H2ᵀ²) and
  *   dZ1ᵀ = (W2ᵀ·dZ2ᵀ) ⊙ (1 − H1ᵀ²) [N][K], and per 128-row block g of
  *   qs_mlp3_tiles(K) the partial sums partA[g][N + A·N + A] =

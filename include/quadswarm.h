@@ -215,12 +215,14 @@ int qs_step(qs_handle* h, const float* actions, const qs_step_out* out,
  * dir = 0: handle → buf (get), dir = 1: buf → handle (set). */
 int qs_state_io(qs_handle* h, int block, void* buf, int dir, void* stream);
 
-/* Completed-episode log (device ring, appended in-kernel on done).
- * Each record: {double return; int32 length; int32 env; int32 seq_hi;
- * int32 seq_lo}: seq = the global step index at which it completed.
- * qs_episode_log copies up to `cap` most-recent records to `dst` (device)
- * and writes the total number of records ever logged to *total (host,
- * synchronous). */
+/* Completed-episode log: a ring per env (max(8, 65536 / num_envs) slots,
+ * appended in-kernel on done, no atomics).  Each record: {double return;
+ * int32 length; int32 env; int64 seq}: seq = the step index at which it
+ * completed.  qs_episode_log merges the rings in (seq, env) order — the
+ * order the reference's env loop logs them — copies up to `cap` most-recent
+ * records to `dst` (device) and writes the total number of episodes ever
+ * logged to *total (host, synchronous).  An env that completes more episodes
+ * than its ring holds between two reads keeps only its latest ones. */
 typedef struct qs_episode_rec {
   double ret;
   int32_t len;

@@ -634,8 +634,10 @@ __global__ void __launch_bounds__(kM3Block) mlp3_fwd_kernel(long long K, int I, 
   const int Ip = m3_ip(I);
   for (int j = threadIdx.x; j < kM3N; j += kM3Block) { sb1[j] = b1[j]; sb2[j] = b2[j]; }
   for (int j = threadIdx.x; j < A * kM3N; j += kM3Block) sw3[j] = W3[j];
-  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, (size_t)K * I * 4), h1r = m3_rsrc(H1T, (size_t)K * kM3N * 4),
-                               h2r = m3_rsrc(H2T, (size_t)K * kM3N * 4);
+  // H1T / H2T may be NULL (inference): a zero-size descriptor drops every store
+  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, (size_t)K * I * 4),
+                               h1r = m3_rsrc(H1T, H1T ? (size_t)K * kM3N * 4 : 0),
+                               h2r = m3_rsrc(H2T, H2T ? (size_t)K * kM3N * 4 : 0);
   const unsigned xoff = rv ? (unsigned)(r * I * 4) : kM3OOB, roff = rv ? (unsigned)(r * 4) : kM3OOB;
   const unsigned kstride = (unsigned)(K * 4);
   M3Stream S{reinterpret_cast<const float4*>(pack), wbuf};
@@ -1064,7 +1066,7 @@ int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* 
 int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
                 const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream) {
   if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !X || !pack ||
-      !b1 || !b2 || !W3 || !b3 || !H1T || !H2T || !out)
+      !b1 || !b2 || !W3 || !b3 || (!H1T) != (!H2T) || !out)
     return fail(QS_E_INVALID, "qs_mlp3_fwd: bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
   const unsigned grid = (unsigned)((K + 127) / 128);
   auto go = [&](auto kern) {

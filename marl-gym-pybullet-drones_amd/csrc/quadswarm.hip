@@ -55,8 +55,7 @@ struct qs_handle {
   float* hist = nullptr;
   void* orig = nullptr;        // [D][3] real
   qs_episode_rec* log = nullptr;
-  unsigned long long* log_count = nullptr;
-  long long log_cap = 0;
+  int log_per_env = 0;
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
   int* rq = nullptr;            // deferred reset-search queue (2 + E ints), MultiHover layouts that can reject
@@ -81,7 +80,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
   P.sp_cx = T(s.target_center[0]); P.sp_cy = T(s.target_center[1]); P.sp_cz = T(s.target_center[2]);
   P.st = (T*)h->st; P.env = h->env; P.hist = h->hist; P.orig_xyz = (const T*)h->orig;
-  P.log = h->log; P.log_count = h->log_count; P.log_cap = h->log_cap; P.err = h->err;
+  P.log = h->log; P.log_per_env = h->log_per_env; P.err = h->err;
   P.stamps = h->stamps;
 }
 
@@ -233,14 +232,15 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
           may_reject = true;
   const size_t rs = (size_t)s.precision;
   const size_t N = d.num_agents;
-  h->log_cap = std::max<long long>(1 << 16, 4LL * s.num_envs);
+  // per-env episode rings: at least 8 slots each, 65 536 records in all for small batches
+  h->log_per_env = (int)std::max<int64_t>(8, ((int64_t)1 << 16) / std::max(1, s.num_envs));
   auto cleanup = [&]() { qs_destroy(h); };
   hipError_t e1 = hipMalloc(&h->st, rs * QS_AGENT_FIELDS * N);
   hipError_t e2 = hipMalloc((void**)&h->env, sizeof(int32_t) * qs::kEnvRec * s.num_envs);
   hipError_t e3 = hipMalloc((void**)&h->hist, sizeof(float) * d.hist_len * N * A);
   hipError_t e5 = hipMalloc(&h->orig, rs * 3 * s.num_drones);
-  hipError_t e6 = hipMalloc((void**)&h->log, sizeof(qs_episode_rec) * h->log_cap);
-  hipError_t e7 = hipMalloc((void**)&h->log_count, sizeof(unsigned long long));
+  hipError_t e6 = hipMalloc((void**)&h->log, sizeof(qs_episode_rec) * h->log_per_env * (size_t)s.num_envs);
+  hipError_t e7 = hipSuccess;
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
   if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
   if (may_reject && getenv("QS_INKERNEL_RESET_SEARCH") == nullptr) {
@@ -260,7 +260,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   }
   if (hipMemset(h->st, 0, rs * QS_AGENT_FIELDS * N) || hipMemset(h->env, 0, sizeof(int32_t) * qs::kEnvRec * s.num_envs) ||
       hipMemset(h->hist, 0, sizeof(float) * d.hist_len * N * A) ||
-      hipMemset(h->log_count, 0, sizeof(unsigned long long)) || hipMemset(h->err, 0, sizeof(int))) {
+      hipMemset(h->err, 0, sizeof(int))) {
     cleanup(); return fail(QS_E_HIP, "qs_create: memset");
   }
 #ifdef QS_STAMPS_BUILD
@@ -285,7 +285,7 @@ extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
   (void)hipSetDevice(h->device);   // teardown: best effort, nothing to report to
-  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->log_count, h->err, h->stamps, h->rq};
+  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->err, h->stamps, h->rq};
   for (void* p : ptrs) if (p) (void)hipFree(p);
   delete h;
   return QS_OK;
@@ -306,7 +306,6 @@ int qs_reset(qs_handle* h, uint64_t seed, float* obs, void* stream) {
   HIP_TRY(hipMemsetAsync(h->st, 0, rs * QS_AGENT_FIELDS * N, st));
   HIP_TRY(hipMemsetAsync(h->env, 0, sizeof(int32_t) * qs::kEnvRec * d.num_envs, st));
   HIP_TRY(hipMemsetAsync(h->hist, 0, sizeof(float) * d.hist_len * N * d.act_dim, st));
-  HIP_TRY(hipMemsetAsync(h->log_count, 0, sizeof(unsigned long long), st));
   HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(int), st));
   h->seed = seed;
   int rc;
@@ -402,21 +401,30 @@ int qs_episode_log(qs_handle* h, qs_episode_rec* dst, int64_t cap, int64_t* tota
   if (!h || !total) return fail(QS_E_INVALID, "qs_episode_log: null argument");
   hipStream_t st = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(h->device));
-  unsigned long long cnt = 0;
-  HIP_TRY(hipMemcpyAsync(&cnt, h->log_count, sizeof(cnt), hipMemcpyDeviceToHost, st));
+  const int E = h->dims.num_envs, R = h->log_per_env;
+  std::vector<int32_t> rec((size_t)E * qs::kEnvRec);
+  HIP_TRY(hipMemcpyAsync(rec.data(), h->env, rec.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  *total = (int64_t)cnt;
+  int64_t cnt = 0;
+  for (int e = 0; e < E; ++e) cnt += rec[(size_t)e * qs::kEnvRec + qs::kEnvLogWord];
+  *total = cnt;
   if (!dst || cap <= 0 || cnt == 0) return QS_OK;
-  const long long avail = std::min<long long>((long long)cnt, h->log_cap);
-  const long long k = std::min<long long>(avail, cap);
-  // most recent k records, in ring order, wrapped
-  const long long first = (long long)cnt - k;
-  for (long long done = 0; done < k;) {
-    long long idx = (first + done) % h->log_cap;
-    long long run = std::min<long long>(k - done, h->log_cap - idx);
-    HIP_TRY(hipMemcpyAsync(dst + done, h->log + idx, sizeof(qs_episode_rec) * run, hipMemcpyDeviceToDevice, st));
-    done += run;
+  // the per-env rings hold each env's last min(logged, R) episodes: merge them in
+  // (step, env) order — the order the reference's env loop logs them — and keep
+  // the most recent `cap`
+  std::vector<qs_episode_rec> ring((size_t)E * R), all;
+  HIP_TRY(hipMemcpyAsync(ring.data(), h->log, ring.size() * sizeof(qs_episode_rec), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (int e = 0; e < E; ++e) {
+    const int64_t n = rec[(size_t)e * qs::kEnvRec + qs::kEnvLogWord];
+    for (int64_t i = std::max<int64_t>(0, n - R); i < n; ++i) all.push_back(ring[(size_t)e * R + (size_t)(i % R)]);
   }
+  std::sort(all.begin(), all.end(), [](const qs_episode_rec& a, const qs_episode_rec& b) {
+    return a.seq != b.seq ? a.seq < b.seq : a.env < b.env;
+  });
+  const size_t k = std::min<size_t>(all.size(), (size_t)cap);
+  HIP_TRY(hipMemcpyAsync(dst, all.data() + (all.size() - k), k * sizeof(qs_episode_rec), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
   return QS_OK;
 }
 

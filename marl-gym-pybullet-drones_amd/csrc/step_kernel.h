@@ -38,11 +38,13 @@ namespace qs {
 // the workgroup barriers below cost nothing (no inter-wave coupling).
 constexpr int kBlock = 64;
 // Per-env record, kEnvRec int32 words: the QS_ENV_FIELDS counters (words 0-3,
-// QS_E_* order), the episode return as f64 (words 4-5), padding.  32 B per env
+// QS_E_* order), the episode return as f64 (words 4-5), the number of episodes
+// this env has logged (word 6, kEnvLogWord), padding.  32 B per env
 // make a wave's envs (D = 8) one 256-B span, loaded and stored whole: written
 // field by field, [field][E] arrays took partial-line writes.
 constexpr int kEnvRec = 8;
 constexpr int kEnvRetWord = 4;
+constexpr int kEnvLogWord = 6;
 constexpr uint32_t kMaxResetTries = 1u << 24;
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
 enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
@@ -213,9 +215,8 @@ template <class T> struct Params {
   int32_t* env;           // [E][kEnvRec] per-env records (see kEnvRec)
   float* hist;            // [H][N][A]
   const T* orig_xyz;      // [D][3]
-  qs_episode_rec* log;    // [log_cap]
-  unsigned long long* log_count;
-  long long log_cap;
+  qs_episode_rec* log;    // [E][log_per_env] per-env rings of completed episodes
+  int log_per_env;
   int* err;               // [1] reset search overflow flag
   int* reset_queue;       // deferred MultiHover reset searches: [0] count, [1] blocks done, [2..] env ids; or NULL
   int stage_rows;         // obs rows staged in LDS per pass
@@ -739,6 +740,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   int32_t step_counter = (int32_t)c01.x, episode = (int32_t)c01.y;
   int32_t total = (int32_t)c23.x, ep_len = (int32_t)c23.y;
   const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvRetWord * 4, 0));
+  const int32_t log_n0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(env_r, (int)ev, kEnvLogWord * 4, 0);
   issue_fence();
   T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
 #pragma unroll
@@ -840,6 +842,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   T angv[3] = {0, 0, 0}, rpy[3] = {0, 0, 0};
   double ep_ret_out = ep_ret0;   // VecRecordEpisodeStatistics accumulators after this call
   int32_t ep_len_out = ep_len;
+  int32_t log_n = log_n0;        // episodes logged by this env
   bool done_env = false;
   int obs_sc = step_counter;   // step_counter seen by _computeObs (before BaseAviary.py:382)
 
@@ -1407,16 +1410,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       ep_len_out = dn ? 0 : len;
       s.done[lenv] = dn;
     }
-    // Episode log (VecRecordEpisodeStatistics, record_episode_statistics.py:155-166).
-    // The atomic's returned slot makes a wave wait for all its outstanding
-    // stores, so only waves holding a finished episode take this branch.
-    if (__ballot(dn) != 0ull) {
-      if (dn) {
-        unsigned long long slot = atomicAdd(P.log_count, 1ull);
-        qs_episode_rec rec;
-        rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
-        P.log[slot % (unsigned long long)P.log_cap] = rec;
-      }
+    // Episode log (VecRecordEpisodeStatistics, record_episode_statistics.py:155-166):
+    // each env appends to its own ring, slot = its logged count mod log_per_env —
+    // no atomic (a returned global slot made the finishing waves wait ~µs for it
+    // and for all their outstanding stores, and they set the launch's tail).
+    if (dn) {
+      qs_episode_rec rec;
+      rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
+      P.log[(size_t)e * P.log_per_env + (unsigned)log_n % (unsigned)P.log_per_env] = rec;
+      log_n = log_n + 1;
     }
     if (P.reasons && valid) P.reasons[a] = kMarl ? 0 : bits;
     step_counter += S;   // BaseAviary.py:382
@@ -1621,7 +1623,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     r[QS_E_STEP_COUNTER] = step_counter; r[QS_E_EPISODE] = episode; r[QS_E_TOTAL_STEPS] = total;
     r[QS_E_EP_LEN] = ep_len_out;
     r[kEnvRetWord] = (int32_t)(unsigned)rb; r[kEnvRetWord + 1] = (int32_t)(unsigned)(rb >> 32);
-    r[6] = 0; r[7] = 0;
+    r[kEnvLogWord] = log_n; r[7] = 0;
   }
   __syncthreads();
   {

@@ -250,7 +250,24 @@ class MLP(nn.Module):
         return (n1 in ok_n and n2 in ok_n and a <= (1 if n2 == 512 else 4)
                 and all(p.grad is not None and p.grad.is_contiguous() for p in self.parameters()))
 
+    def _infer_fused(self, x):
+        """Inference forward (the rollout's batched actor, AG:389-415) through
+        qs_mlp3_fwd without the saved activations."""
+        lib, st = L.load(), _stream()
+        f0, f1, f2 = self.fcs
+        K, I, A = x.shape[0], x.shape[1], f2.out_features
+        pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device=x.device, dtype=torch.float32)
+        L.check(lib.qs_mlp3_pack(I, 256, L.ptr(f0.weight), L.ptr(f1.weight), L.ptr(pack), st), "qs_mlp3_pack")
+        out = torch.empty((K, A), device=x.device, dtype=x.dtype)
+        L.check(lib.qs_mlp3_fwd(K, I, 256, A, L.ptr(x), L.ptr(pack), L.ptr(f0.bias), L.ptr(f1.bias), L.ptr(f2.weight),
+                                L.ptr(f2.bias), None, None, L.ptr(out), st), "qs_mlp3_fwd")
+        return out
+
     def forward(self, x):
+        if (not torch.is_grad_enabled() and self._tanh3 and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32
+                and x.shape[0] >= 16384 and x.shape[1] <= 1024 and self.fcs[0].out_features == 256
+                and self.fcs[1].out_features == 256 and self.fcs[2].out_features <= 4):
+            return self._infer_fused(x.contiguous())
         if self._fused_ok(x):
             f0, f1, f2 = self.fcs
             return _TanhMLP3.apply(x.contiguous(), f0.weight, f0.bias, f1.weight, f1.bias, f2.weight, f2.bias)

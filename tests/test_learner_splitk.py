@@ -104,3 +104,20 @@ def test_fused_tanh_mlp_matches_autograd(rows, din, hidden, A):
         net(x).backward(g)
     for p, q in zip(net.parameters(), grads):
         assert torch.equal(p.grad, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,din,A", [(32768, 27, 1), (20000, 72, 4)])
+def test_fused_inference_forward(rows, din, A):
+    """The rollout's no-grad actor forward through qs_mlp3_fwd (no saved activations)
+    against the plain nn.Linear / torch.tanh forward."""
+    torch.manual_seed(2)
+    net = MLP(din, A, [256, 256], act='tanh').cuda()
+    x = torch.randn(rows, din, device="cuda")
+    with torch.no_grad():
+        got = net(x)
+        out = x
+        for i, fc in enumerate(net.fcs):
+            out = fc(out)
+            out = torch.tanh(out) if i < len(net.fcs) - 1 else out
+    torch.testing.assert_close(got, out, rtol=1e-5, atol=1e-5)
