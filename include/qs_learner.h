@@ -114,12 +114,12 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
  *   out = H2·W3ᵀ + b3; X [K][I] (I <= 1024), W3 [A][N]; writes H1T, H2T
  *   [N][K] (saved for the backward; both NULL for inference) and out [K][A].
  * qs_mlp3_bwd: given dout [K][A]: dZ2ᵀ = (W3ᵀ·doutᵀ) ⊙ (1 − H2ᵀ²) and
- *   dZ1ᵀ = (W2ᵀ·dZ2ᵀ) ⊙ (1 − H1ᵀ²) [N][K], and per 128-row block g of
- *   qs_mlp3_tiles(K) the partial sums partA[g][N + A·N + A] =
+ *   dZ1ᵀ = (W2ᵀ·dZ2ᵀ) ⊙ (1 − H1ᵀ²) [N][K], and per row block g of
+ *   qs_mlp3_tiles(K, I) (32 rows when K < 16 384 or I > 64, else 128) the partial sums partA[g][N + A·N + A] =
  *   [Σ dZ2 | Σ dout_a·H2 | Σ dout_a] and partB[g][N] = Σ dZ1 over the block's
  *   rows (reduce with qs_mlp_sum_partials; the weight gradients are
  *   dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·X). */
-int32_t qs_mlp3_tiles(int64_t K);
+int32_t qs_mlp3_tiles(int64_t K, int32_t I);
 int64_t qs_mlp3_pack_floats(int32_t I);
 int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* pack, void* stream);
 int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,

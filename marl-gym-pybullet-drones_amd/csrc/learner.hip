@@ -497,7 +497,7 @@ constexpr int kM3Waves = 4;     // waves (tiles) per workgroup
 constexpr int kM3Block = 64 * kM3Waves;
 
 __device__ __forceinline__ int m3_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }   // C/D row of reg i
-__device__ __forceinline__ int m3_ip(int I) { return (I + 15) & ~15; }                        // padded input width
+__device__ __forceinline__ int m3_ip(int I) { return (I + 31) & ~31; }   // padded input width: whole groups of 4 k-quads
 
 // Raw buffer access: lanes past the batch get offset kM3OOB, which the
 // hardware drops on stores and reads as 0 — no per-element branches.
@@ -580,7 +580,7 @@ __global__ void mlp3_pack_kernel(int I, const float* __restrict__ W1, const floa
   }
 }
 
-// Double-buffered chunk stream: the workgroup's 256 threads load a 16-KB chunk
+// Double-buffered chunk stream: the workgroup's 256 threads load a 32-KB chunk
 // of `src` into registers one chunk ahead of its LDS write, and every wave
 // consumes chunk c from buf[c & 1] after the barrier that makes it visible.
 struct M3Stream {
@@ -645,7 +645,7 @@ __global__ void __launch_bounds__(kM3Block) mlp3_fwd_kernel(long long K, int I, 
   f32x16 acc[kM3NB];
 #pragma unroll
   for (int mb = 0; mb < kM3NB; ++mb) acc[mb] = f32x16{};
-  m3_stream(S, Ip / 32 + ((Ip & 16) ? 1 : 0), [&](int ch, const float4* wc) {
+  m3_stream(S, Ip / 32, [&](int ch, const float4* wc) {
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int q = 4 * ch + qq;
@@ -884,6 +884,206 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
     if (open) *A.step = *A.step + 1.0f;
   }
 }
+
+// ---- wide variant: one 32-row tile per workgroup of 8 waves, wave w owning
+// hidden block w (batches of < 16 384 rows, e.g. the critic's 4 096: 128 tiles
+// would leave most SIMDs idle with one wave per tile).  The waves exchange
+// their activation blocks through LDS before each contraction over the hidden
+// index; each wave streams its own weight block from L2 (no sharing, no LDS).
+constexpr int kM3WWaves = 8;
+constexpr int kM3WBlock = 64 * kM3WWaves;
+constexpr int kM3WMaxI = 1024;                                            // widest input the fused path takes
+constexpr int kM3WLds = 32 * (kM3WMaxI + 1);                             // floats: X tile (row stride Ip + 1), then the exchange
+static_assert(kM3WLds >= kM3Steps2 * 64, "wide LDS too small");
+
+__device__ __forceinline__ void m3w_share(float* xs, const float* mine, float* all, int w) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xs[(w * 16 + i) * 64 + lane] = mine[i];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kM3Steps2; ++k) all[k] = xs[k * 64 + lane];
+}
+
+// Σ_k over the 128 MFMA steps of block blk of a [8 blk][32 q][64][4] packed
+// matrix (W2p or W2Tp) with the B operand in registers.  A wave's block is
+// private to it, so it streams straight from L2 into a ring of eight float4
+// (eight k-quads = 32 MFMAs ahead), no LDS.
+__device__ __forceinline__ f32x16 m3w_contract(const float4* __restrict__ mat, int blk, const float* bv) {
+  const float4* p = mat + (size_t)blk * 32 * 64 + (threadIdx.x & 63);
+  float4 ring[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) ring[b] = p[b * 64];
+  f32x16 z = f32x16{};
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const float4 wv = ring[q & 7];
+    if (q + 8 < 32) ring[q & 7] = p[(q + 8) * 64];
+    __builtin_amdgcn_sched_barrier(0);   // keep the load eight k-quads ahead (the scheduler would sink it)
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, bv[4 * q + 0], z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, bv[4 * q + 1], z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, bv[4 * q + 2], z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, bv[4 * q + 3], z, 0, 0, 0);
+  }
+  return z;
+}
+
+template <int A>
+__global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I, const float* __restrict__ X,
+                                                              const float* __restrict__ pack,
+                                                              const float* __restrict__ b1,
+                                                              const float* __restrict__ b2,
+                                                              const float* __restrict__ W3,
+                                                              const float* __restrict__ b3, float* __restrict__ H1T,
+                                                              float* __restrict__ H2T, float* __restrict__ out) {
+  // LDS: the X tile during layer 1, then the H1ᵀ exchange
+  __shared__ float lds[kM3WLds];
+  __shared__ float hp[kM3WWaves][A][64];
+  float* xs = lds;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  const long long r0 = (long long)blockIdx.x * 32, r = r0 + c;
+  const bool rv = r < K;
+  const int Ip = m3_ip(I), S = Ip + 1;   // odd row stride: the 32 rows of a read hit 32 banks
+  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, (size_t)K * I * 4),
+                               h1r = m3_rsrc(H1T, H1T ? (size_t)K * kM3N * 4 : 0),
+                               h2r = m3_rsrc(H2T, H2T ? (size_t)K * kM3N * 4 : 0);
+  const unsigned roff = rv ? (unsigned)(r * 4) : kM3OOB;
+  const unsigned kstride = (unsigned)(K * 4);
+  // the tile's 32 rows are contiguous in X: every wave reads them coalesced,
+  // once, instead of each of the 8 waves gathering every lane's row
+  for (int row = w; row < 32; row += kM3WWaves) {
+    const unsigned base = r0 + row < K ? (unsigned)((r0 + row) * I * 4) : kM3OOB;
+    for (int k = lane; k < Ip; k += 64) lds[row * S + k] = m3_ld(xr, k < I ? base + 4u * k : kM3OOB);
+  }
+  __syncthreads();
+  // layer 1, block w: W1p (the wave's block, one coalesced float4 per k-quad)
+  // from L2, software-pipelined eight k-quads ahead (Ip is a multiple of 32)
+  const float4* w1p = reinterpret_cast<const float4*>(pack) + w * 64 + lane;
+  const float* xrow = lds + c * S + h;
+  f32x16 acc = f32x16{};
+  const int nq = Ip / 8;   // a multiple of 4
+  float4 wq[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    if (b < nq) wq[b] = w1p[(size_t)b * kM3NB * 64];
+  for (int q0 = 0; q0 < nq; q0 += 8) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      if (b >= 4 && q0 + b >= nq) break;
+      const float4 wv = wq[b];
+      if (q0 + 8 + b < nq) wq[b] = w1p[(size_t)(q0 + 8 + b) * kM3NB * 64];
+      __builtin_amdgcn_sched_barrier(0);   // keep the load eight k-quads ahead
+      const float* xk = xrow + 8 * (q0 + b);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, xk[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, xk[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, xk[4], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, xk[6], acc, 0, 0, 0);
+    }
+  }
+  __syncthreads();   // the X tile is dead: the LDS is reused below
+  float mine[16], hb[kM3Steps2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = 32 * w + m3_row(i, h);
+    mine[i] = m3_tanh(acc[i] + b1[m]);
+    m3_st(h1r, roff + (unsigned)m * kstride, mine[i]);
+  }
+  m3w_share(xs, mine, hb, w);
+  // layer 2, block w: Z2ᵀ[w] = W2[w]·H1ᵀ
+  const f32x16 z = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip)), w, hb);
+  float hs[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) hs[a] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = 32 * w + m3_row(i, h);
+    const float v = m3_tanh(z[i] + b2[m]);
+    m3_st(h2r, roff + (unsigned)m * kstride, v);
+#pragma unroll
+    for (int a = 0; a < A; ++a) hs[a] += v * W3[a * kM3N + m];
+  }
+  // head: halves, then the 8 waves in order
+#pragma unroll
+  for (int a = 0; a < A; ++a) hp[w][a][lane] = hs[a] + __shfl_xor(hs[a], 32, 64);
+  __syncthreads();
+  if (w == 0 && h == 0 && rv)
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      float t = hp[0][a][lane];
+#pragma unroll
+      for (int k = 1; k < kM3WWaves; ++k) t += hp[k][a][lane];
+      out[r * A + a] = t + b3[a];
+    }
+}
+
+template <int A>
+__global__ void __launch_bounds__(kM3WBlock) mlp3w_bwd_kernel(long long K, const float* __restrict__ dout,
+                                                              const float* __restrict__ H1T,
+                                                              const float* __restrict__ H2T,
+                                                              const float* __restrict__ pack, int Ip,
+                                                              const float* __restrict__ W3, float* __restrict__ dZ2T,
+                                                              float* __restrict__ dZ1T, float* __restrict__ partA,
+                                                              float* __restrict__ partB) {
+  constexpr int N = kM3N, PA = N + A * N + A;
+  __shared__ float xs[kM3Steps2 * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  const long long r = (long long)blockIdx.x * 32 + c;
+  const bool rv = r < K;
+  const size_t hbytes = (size_t)K * kM3N * 4;
+  const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), h2r = m3_rsrc(H2T, hbytes), z2r = m3_rsrc(dZ2T, hbytes),
+                               z1r = m3_rsrc(dZ1T, hbytes);
+  const unsigned roff = rv ? (unsigned)(r * 4) : kM3OOB, kstride = (unsigned)(K * 4);
+  float dv[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) dv[a] = rv ? dout[r * A + a] : 0.f;
+  float* pa = partA + (size_t)blockIdx.x * PA;
+  const int jr = m3_lane_sum16_reg();
+  float h1v[16];   // H1ᵀ of block w, used after the contraction
+#pragma unroll
+  for (int i = 0; i < 16; ++i) h1v[i] = m3_ld(h1r, roff + (unsigned)(32 * w + m3_row(i, h)) * kstride);
+  if (w == 0)
+#pragma unroll
+    for (int a = 0; a < A; ++a) {   // Σ_r dout_a over the tile
+      float t = h == 0 ? dv[a] : 0.f;
+      for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) pa[N + A * N + a] = t;
+    }
+  // dZ2ᵀ block w; its bias / head partials (this wave's 32 hidden units)
+  float mine[16], hw[A][16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = 32 * w + m3_row(i, h);
+    const float hv = m3_ld(h2r, roff + (unsigned)m * kstride);
+    float g = 0.f;
+#pragma unroll
+    for (int a = 0; a < A; ++a) { g += dv[a] * W3[a * N + m]; hw[a][i] = dv[a] * hv; }
+    mine[i] = g * (1.f - hv * hv);
+    m3_st(z2r, roff + (unsigned)m * kstride, mine[i]);
+  }
+  const float sdb = m3_lane_sum16(mine);
+  float sdw[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) sdw[a] = m3_lane_sum16(hw[a]);
+  if ((c & 1) == 0) {   // tiles past K write zeros: every partial row is defined
+    const int m = 32 * w + m3_row(jr, h);
+    pa[m] = sdb;
+#pragma unroll
+    for (int a = 0; a < A; ++a) pa[N + a * N + m] = sdw[a];
+  }
+  float zb[kM3Steps2];
+  m3w_share(xs, mine, zb, w);
+  // dH1ᵀ block w = (W2ᵀ)[w]·dZ2ᵀ; dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²)
+  const f32x16 d = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip) + m3_w2_floats()), w, zb);
+  float z1[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int n = 32 * w + m3_row(i, h);
+    z1[i] = d[i] * (1.f - h1v[i] * h1v[i]);
+    m3_st(z1r, roff + (unsigned)n * kstride, z1[i]);
+  }
+  const float s1 = m3_lane_sum16(z1);
+  if ((c & 1) == 0) partB[(size_t)blockIdx.x * N + 32 * w + m3_row(jr, h)] = s1;
+}
 }  // namespace
 
 extern "C" {
@@ -1047,10 +1247,14 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials_multi: ") + hipGetErrorString(e));
 }
 
-int32_t qs_mlp3_tiles(int64_t K) { return (int32_t)((K + 127) / 128); }   // partial rows: one per workgroup
+// the 8-wave-per-tile kernels below 512 tiles (too few waves otherwise) and for
+// wide inputs (their X tile is staged through LDS once, where the 4-tile
+// kernel gathers every lane's row per k-quad)
+static bool m3_wide(int64_t K, int32_t I) { return K < 16384 || I > 64; }
+int32_t qs_mlp3_tiles(int64_t K, int32_t I) { return (int32_t)(m3_wide(K, I) ? (K + 31) / 32 : (K + 127) / 128); }   // partial rows
 
 int64_t qs_mlp3_pack_floats(int32_t I) {
-  const int64_t Ip = (I + 15) & ~15;
+  const int64_t Ip = (I + 31) & ~31;
   return (Ip / 8) * kM3NB * 256 + 2 * (int64_t)kM3NB * 32 * 256;
 }
 
@@ -1068,16 +1272,17 @@ int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, cons
   if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !X || !pack ||
       !b1 || !b2 || !W3 || !b3 || (!H1T) != (!H2T) || !out)
     return fail(QS_E_INVALID, "qs_mlp3_fwd: bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
-  const unsigned grid = (unsigned)((K + 127) / 128);
+  const bool wide = m3_wide(K, I);
+  const unsigned grid = (unsigned)qs_mlp3_tiles(K, I);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3Block), 0, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1, b2,
-                       W3, b3, H1T, H2T, out);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(wide ? kM3WBlock : kM3Block), 0, (hipStream_t)stream, (long long)K,
+                       (int)I, X, pack, b1, b2, W3, b3, H1T, H2T, out);
   };
   switch (A) {
-    case 1: go(mlp3_fwd_kernel<1>); break;
-    case 2: go(mlp3_fwd_kernel<2>); break;
-    case 3: go(mlp3_fwd_kernel<3>); break;
-    default: go(mlp3_fwd_kernel<4>); break;
+    case 1: wide ? go(mlp3w_fwd_kernel<1>) : go(mlp3_fwd_kernel<1>); break;
+    case 2: wide ? go(mlp3w_fwd_kernel<2>) : go(mlp3_fwd_kernel<2>); break;
+    case 3: wide ? go(mlp3w_fwd_kernel<3>) : go(mlp3_fwd_kernel<3>); break;
+    default: wide ? go(mlp3w_fwd_kernel<4>) : go(mlp3_fwd_kernel<4>); break;
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_fwd: ") + hipGetErrorString(e));
@@ -1089,17 +1294,18 @@ int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, c
   if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !dout ||
       !H1T || !H2T || !pack || !W3 || !dZ2T || !dZ1T || !partA || !partB)
     return fail(QS_E_INVALID, "qs_mlp3_bwd: bad argument (N must be 256, 1 <= A <= 4)");
-  const unsigned grid = (unsigned)((K + 127) / 128);
-  const int Ip = (I + 15) & ~15;
+  const bool wide = m3_wide(K, I);
+  const unsigned grid = (unsigned)qs_mlp3_tiles(K, I);
+  const int Ip = (I + 31) & ~31;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3Block), 0, (hipStream_t)stream, (long long)K, dout, H1T, H2T, pack, Ip,
-                       W3, dZ2T, dZ1T, partA, partB);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(wide ? kM3WBlock : kM3Block), 0, (hipStream_t)stream, (long long)K,
+                       dout, H1T, H2T, pack, Ip, W3, dZ2T, dZ1T, partA, partB);
   };
   switch (A) {
-    case 1: go(mlp3_bwd_kernel<1>); break;
-    case 2: go(mlp3_bwd_kernel<2>); break;
-    case 3: go(mlp3_bwd_kernel<3>); break;
-    default: go(mlp3_bwd_kernel<4>); break;
+    case 1: wide ? go(mlp3w_bwd_kernel<1>) : go(mlp3_bwd_kernel<1>); break;
+    case 2: wide ? go(mlp3w_bwd_kernel<2>) : go(mlp3_bwd_kernel<2>); break;
+    case 3: wide ? go(mlp3w_bwd_kernel<3>) : go(mlp3_bwd_kernel<3>); break;
+    default: wide ? go(mlp3w_bwd_kernel<4>) : go(mlp3_bwd_kernel<4>); break;
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_bwd: ") + hipGetErrorString(e));

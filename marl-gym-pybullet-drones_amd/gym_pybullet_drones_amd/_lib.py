@@ -114,7 +114,7 @@ def load():
     L.qs_mlp_sum_partials_multi.argtypes = [ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.qs_adam_step.argtypes = [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp, f32, vp, vp]
     L.qs_adam_multi.argtypes = [ctypes.c_int32] + [vp] * 14
-    L.qs_mlp3_tiles.argtypes = [i64]
+    L.qs_mlp3_tiles.argtypes = [i64, i32]
     L.qs_mlp3_pack_floats.argtypes = [ctypes.c_int32]
     L.qs_mlp3_pack.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp]
     L.qs_mlp3_fwd.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 10

@@ -165,8 +165,7 @@ class _TanhMLP3(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, w3, b3):
         lib, st = L.load(), _stream()
         K, N1, N2, A = x.shape[0], w1.shape[0], w2.shape[0], w3.shape[0]
-        # the fused kernels fill the chip from 512 tiles of 32 rows (the actor's minibatch)
-        ctx.fused = N1 == N2 == 256 and A <= 4 and x.shape[1] <= 1024 and K >= 16384
+        ctx.fused = N1 == N2 == 256 and A <= 4 and x.shape[1] <= 1024
         if ctx.fused:   # qs_mlp3_fwd: both layers and the head on MFMA, activations kept transposed [N][K]
             I = x.shape[1]
             pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device=x.device, dtype=torch.float32)
@@ -195,7 +194,7 @@ class _TanhMLP3(torch.autograd.Function):
         dout = dout.contiguous()
         if ctx.fused:   # qs_mlp3_bwd: head + tanh backward, dH1ᵀ = W2ᵀ·dZ2ᵀ on MFMA, tanh backward, bias partials
             pack = ctx.saved_tensors[9]
-            G = int(lib.qs_mlp3_tiles(K))
+            G = int(lib.qs_mlp3_tiles(K, x.shape[1]))
             dz2 = torch.empty_like(h2)   # [N][K]
             dz1 = torch.empty_like(h1)
             part_a = torch.empty((G, N2 * (1 + A) + A), device=x.device, dtype=torch.float32)
@@ -265,7 +264,7 @@ class MLP(nn.Module):
 
     def forward(self, x):
         if (not torch.is_grad_enabled() and self._tanh3 and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32
-                and x.shape[0] >= 16384 and x.shape[1] <= 1024 and self.fcs[0].out_features == 256
+                and x.shape[1] <= 1024 and self.fcs[0].out_features == 256
                 and self.fcs[1].out_features == 256 and self.fcs[2].out_features <= 4):
             return self._infer_fused(x.contiguous())
         if self._fused_ok(x):

@@ -13,13 +13,15 @@ from gym_pybullet_drones_amd import _lib as L  # noqa: E402
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 I = int(sys.argv[2]) if len(sys.argv) > 2 else 27
 A = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+if os.environ.get("QS_LIB"):
+    L.LIB_PATH = os.environ["QS_LIB"]
 lib = L.load()
 f = lambda *s: torch.randn(*s, device="cuda") * 0.1
 x, w1, b1, w2, b2, w3, b3 = f(K, I), f(256, I), f(256), f(256, 256), f(256), f(A, 256), f(A)
 pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device="cuda")
 h1, h2, out = torch.empty(256, K, device="cuda"), torch.empty(256, K, device="cuda"), torch.empty(K, A, device="cuda")
 dout, dz2, dz1 = f(K, A), torch.empty(256, K, device="cuda"), torch.empty(256, K, device="cuda")
-T = int(lib.qs_mlp3_tiles(K))
+T = int(lib.qs_mlp3_tiles(K, I))
 pa, pb = torch.empty(T, 256 * (1 + A) + A, device="cuda"), torch.empty(T, 256, device="cuda")
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 P = lambda t: L.ptr(t)
