@@ -124,6 +124,12 @@ int64_t qs_mlp3_pack_floats(int32_t I);
 int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* pack, void* stream);
 int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
                 const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream);
+/* qs_mlp3_fwd with the minibatch gather folded in: row r of the batch is
+ * X[rows[r]] (X [·][I], rows int64 [K]), and the gathered rows are written to
+ * Xg [K][I] (may be NULL) for the weight gradients. */
+int qs_mlp3_fwd_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
+                     const float* pack, const float* b1, const float* b2, const float* W3, const float* b3, float* H1T,
+                     float* H2T, float* out, void* stream);
 int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, const float* H1T, const float* H2T,
                 const float* pack, const float* W3, float* dZ2T, float* dZ1T, float* partA, float* partB,
                 void* stream);
@@ -142,6 +148,18 @@ int qs_adam_multi(int32_t nseg, float* const* params, const float* const* grads,
                   float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr, const float* beta1,
                   const float* beta2, const float* eps, const float* const* gate_val, const float* gate_thr, void* work,
                   void* stream);
+
+/* qs_adam_multi with, per segment i: pack[i] (NULL = none) the qs_mlp3_pack
+ * image of a 256-wide tanh MLP whose W1 [256][pack_I[i]] and W2 [256][256]
+ * start at elements w1_off[i] / w2_off[i] of params[i] — every updated W1 / W2
+ * element is also written to its pack positions, so the image stays current
+ * without a qs_mlp3_pack launch (it must be packed once before the first call);
+ * zero_grads != 0: every gradient element is set to 0 after it is read. */
+int qs_adam_multi_pack(int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr,
+                       const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                       const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                       const int32_t* pack_I, int32_t zero_grads, void* work, void* stream);
 
 const char* qs_learner_last_error(void);
 

@@ -108,17 +108,30 @@ constexpr int kHeadsBlock = 256;
 constexpr int kMaxA = 4;
 constexpr int kHeadsSums = 3 + kMaxA;   // policy, approx_kl, value, d logstd[A]
 
-__device__ __forceinline__ double block_sum(double x, double* lds) {
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+// NV block sums at once: one shuffle butterfly per value, one LDS round and one
+// barrier for all of them (the per-value order of block_sum: lanes by
+// butterfly, then the waves in order); valid in thread 0.
+template <int NV>
+__device__ __forceinline__ void block_sum_n(double (&x)[NV], double (*lds)[NV]) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) x[k] += __shfl_xor(x[k], o, 64);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   __syncthreads();
-  if (l == 0) lds[w] = x;
+  if (l == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[w][k] = x[k];
   __syncthreads();
-  double t = 0;
   if (threadIdx.x == 0)
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += lds[k];
-  return t;   // valid in thread 0
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double t = 0;
+      for (int j = 0; j < (int)(blockDim.x >> 6); ++j) t += lds[j][k];
+      x[k] = t;
+    }
 }
+
 
 // A (actions per agent) is a template value: the per-action arrays stay in
 // registers (a run-time A put them in scratch memory and cost ~70 µs a launch).
@@ -129,7 +142,7 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     const double* __restrict__ adv, const double* __restrict__ ret, const float* __restrict__ v, float clip,
     float ent_coef, float* __restrict__ dmean, float* __restrict__ dlogstd, float* __restrict__ dv,
     float* __restrict__ kl_out, double* __restrict__ acc, double* __restrict__ partial, unsigned* __restrict__ count) {
-  __shared__ double lds[kHeadsBlock / 64];
+  __shared__ double ldsn[kHeadsBlock / 64][kHeadsSums];
   __shared__ bool last;
   const int R = mb * D;
   float sd[A], lsd[A], var2[A];
@@ -187,12 +200,10 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     sums[2] = diff * diff;
     dv[r] = (float)(diff / (double)mb);
   }
-#pragma unroll
-  for (int k = 0; k < 3 + A; ++k) {
-    const double t = block_sum(sums[k], lds);
-    if (threadIdx.x == 0) partial[(size_t)blockIdx.x * kHeadsSums + k] = t;
-  }
+  block_sum_n<kHeadsSums>(sums, ldsn);
   if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 3 + A; ++k) partial[(size_t)blockIdx.x * kHeadsSums + k] = sums[k];
     __threadfence();
     last = atomicAdd(count, 1u) == gridDim.x - 1;
   }
@@ -201,13 +212,11 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
   // the last workgroup: every thread sums a fixed strided subset of the
   // partials in workgroup order, then the same fixed-order block reduction
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  double tot[kHeadsSums];
+  double tot[kHeadsSums] = {0, 0, 0, 0, 0, 0, 0};
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
 #pragma unroll
-  for (int k = 0; k < 3 + A; ++k) {
-    double t = 0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) t += partial[(size_t)b * kHeadsSums + k];
-    tot[k] = block_sum(t, lds);
-  }
+    for (int k = 0; k < 3 + A; ++k) tot[k] += partial[(size_t)b * kHeadsSums + k];
+  block_sum_n<kHeadsSums>(tot, ldsn);
   if (threadIdx.x != 0) return;
   *count = 0;   // ready for the next launch (graph replay)
   float ent = 0.0f;   // Normal.entropy summed over A: 0.5 + 0.5·log(2π) + log(scale)
@@ -410,31 +419,66 @@ struct MlpSumTasks {
   int start[kMlpMaxTasks + 1];
   int n;
 };
+// A block is 16 waves; a task's G partial rows are split over Wg = min(16,
+// pow2 ≥ G) wave slices (wave slice w sums rows g ≡ w mod Wg in order, eight
+// rows' loads in flight), and the 16 / Wg wave groups of the block take
+// 256-column spans (lane l: columns l + 64j, j < 4 — every load a coalesced
+// 256-B wave access).  The slices are combined in slice order: per column the
+// same fixed order as mlp_sum_partials_kernel (rows g ≡ w mod 16 in order, then
+// w = 0..15), so both give the same bits.
+constexpr int kMlpSumCols = 4;
+__device__ __forceinline__ int mlp_sum_wg(int G) {
+  int w = 1;
+  while (w < G && w < 16) w <<= 1;
+  return w;
+}
 __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks tasks) {
-  constexpr int W = kMlpSumBlock / 64;
-  __shared__ float lds[W][64];
+  constexpr int W = kMlpSumBlock / 64, C = kMlpSumCols;
+  __shared__ float lds[W][64 * C];
   int ti = 0;
   while (ti + 1 < tasks.n && (int)blockIdx.x >= tasks.start[ti + 1]) ++ti;
   const MlpSumTask& T = tasks.t[ti];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long long j = (long long)(blockIdx.x - tasks.start[ti]) * 64 + lane;
-  float t = 0.f;
-  if (j < T.P) {
-    int g = wv;
-    for (; g + 3 * W < T.G; g += 4 * W) {
-      const float a = T.partial[(size_t)g * T.P + j], b = T.partial[(size_t)(g + W) * T.P + j];
-      const float c = T.partial[(size_t)(g + 2 * W) * T.P + j], d = T.partial[(size_t)(g + 3 * W) * T.P + j];
-      t = (((t + a) + b) + c) + d;
-    }
-    for (; g < T.G; g += W) t += T.partial[(size_t)g * T.P + j];
+  const int Wg = mlp_sum_wg(T.G), ws = wv % Wg, cg = wv / Wg;
+  const long long c0 = ((long long)(blockIdx.x - tasks.start[ti]) * (W / Wg) + cg) * (64 * C) + lane;
+  float t[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) t[j] = 0.f;
+  int g = ws;
+  constexpr int U = 8;   // rows per batch: 32 loads in flight per lane
+  for (; g + (U - 1) * Wg < T.G; g += U * Wg) {
+    float v[U][C];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const long long c = c0 + 64 * j;
+        v[u][j] = c < T.P ? T.partial[(size_t)(g + u * Wg) * T.P + c] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < C; ++j) t[j] += v[u][j];
   }
-  lds[wv][lane] = t;
+  for (; g < T.G; g += Wg)
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const long long c = c0 + 64 * j;
+      if (c < T.P) t[j] += T.partial[(size_t)g * T.P + c];
+    }
+#pragma unroll
+  for (int j = 0; j < C; ++j) lds[wv][lane + 64 * j] = t[j];
   __syncthreads();
-  if (wv != 0 || j >= T.P) return;
-  t = lds[0][lane];
-  for (int k = 1; k < W; ++k) t += lds[k][lane];
-  float* dst = j < T.n0 ? T.d0 + j : (j < T.n0 + T.n1 ? T.d1 + (j - T.n0) : T.d2 + (j - T.n0 - T.n1));
-  *dst += t;
+  if (ws != 0) return;
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const long long c = c0 + 64 * j;
+    if (c >= T.P) continue;
+    float u = lds[cg * Wg][lane + 64 * j];
+    for (int k = 1; k < Wg; ++k) u += lds[cg * Wg + k][lane + 64 * j];
+    float* dst = c < T.n0 ? T.d0 + c : (c < T.n0 + T.n1 ? T.d1 + (c - T.n0) : T.d2 + (c - T.n0 - T.n1));
+    *dst += u;
+  }
 }
 
 // torch.optim.Adam step and its step-count commit in one launch: every block
@@ -823,31 +867,60 @@ __global__ void __launch_bounds__(kM3Block) mlp3_bwd_kernel(long long K, const f
 
 // torch.optim.Adam over several flat parameter buffers in one launch (the
 // actor's, KL-gated, and the critic's): blocks [start[i], start[i+1]) serve
-// segment i.  Thread 0 of each block forms the bias corrections once from the
+// segment i, kAdamPer elements per thread (all loads issued before the
+// arithmetic).  Thread 0 of each block forms the bias corrections once from the
 // step count (fp64, as torch's host-side step_size), and the last block of a
-// segment to finish commits its step count (gate permitting).
+// segment to finish commits its step count (gate permitting).  Optionally per
+// segment: the gradient is zeroed after it is read (the next minibatch's sums
+// accumulate into it), and the updated W1 / W2 of a 256-wide tanh MLP are also
+// written into its qs_mlp3_pack image (W1p; W2p and W2Tp), so no pack launch
+// runs between the step and the next forward.
 constexpr int kAdamMaxSeg = 4;
 constexpr int kAdamBlock = 256;
+constexpr int kAdamPer = 4;
+// A segment gets at most kAdamSegBlocks workgroups (grid-stride): the
+// last-block arrival count is one atomic per workgroup on one address, and those
+// serialise at the L2 — a hundred cost about a microsecond, a thousand ~10 µs.
+constexpr int kAdamSegBlocks = 128;
 struct AdamSeg {
   float* p;
-  const float* g;
+  float* g;
   float* m;
   float* v;
   float* step;
   const float* gate;
-  long long n;
+  float* pack;            // NULL: no pack image
+  long long n, w1, w2;    // elements; offsets of W1 [256][I] and W2 [256][256] in p
   float lr, b1, b2, eps, thr;
+  int I, zero;
 };
 struct AdamSegs {
   AdamSeg s[kAdamMaxSeg];
   int start[kAdamMaxSeg + 1];
   int n;
 };
-// A segment gets at most kAdamSegBlocks workgroups (grid-stride): the
-// last-block arrival count is one atomic per workgroup on one address, and those
-// serialise at the L2 — a few dozen cost well under a microsecond, a thousand
-// cost ~10 µs.
-constexpr int kAdamSegBlocks = 64;
+
+// pack positions (qs_mlp3_pack layout) of W1[m][k] and W2[m][n]
+__device__ __forceinline__ long long m3_pos_w1(int m, int k) {
+  const int st = k >> 1, hh = k & 1, q = st >> 2, e = st & 3, mb = m >> 5, c = m & 31;
+  return ((((long long)q * kM3NB + mb) * 64 + 32 * hh + c) << 2) + e;
+}
+// row(i, h) = (i & 3) + 8 (i >> 2) + 4h  ⇔  i = (x & 3) + 4 (x >> 3), h = (x >> 2) & 1 for x in [0, 32)
+__device__ __forceinline__ long long m3_pos_w2(int blk, int c, int other, int x) {
+  const int i = (x & 3) + 4 * (x >> 3), hh = (x >> 2) & 1, st = 16 * other + i, q = st >> 2, e = st & 3;
+  return ((((long long)blk * 32 + q) * 64 + 32 * hh + c) << 2) + e;
+}
+
+__device__ __forceinline__ double powi_d(double b, unsigned t) {
+  double r = 1.0;
+  while (t) {
+    if (t & 1u) r *= b;
+    b *= b;
+    t >>= 1;
+  }
+  return r;
+}
+
 __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsigned* done) {
   __shared__ float sc[2];
   __shared__ bool last;
@@ -856,23 +929,52 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
   const AdamSeg& A = S.s[si];
   const int nb = S.start[si + 1] - S.start[si];
   const bool open = gate_ok(A.gate, A.thr);
+  const long long stride = (long long)nb * kAdamBlock * kAdamPer;
+  const long long first = (long long)(blockIdx.x - S.start[si]) * kAdamBlock * kAdamPer + threadIdx.x;
+  float gi[kAdamPer], mi[kAdamPer], vi[kAdamPer], pi[kAdamPer];
+  auto load = [&](long long i0) {
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const long long i = i0 + (long long)u * kAdamBlock;
+      if (i < A.n) { gi[u] = A.g[i]; mi[u] = A.m[i]; vi[u] = A.v[i]; pi[u] = A.p[i]; }
+    }
+  };
+  load(first);   // in flight while thread 0 forms the bias corrections
   if (threadIdx.x == 0) {
-    const double t = (double)(*A.step) + 1.0;
-    sc[0] = (float)(1.0 - pow((double)A.b1, t));        // bias_correction1
-    sc[1] = (float)sqrt(1.0 - pow((double)A.b2, t));   // sqrt(bias_correction2)
+    // β^t for the integral step count t by fp64 square-and-multiply (a few
+    // dozen dependent multiplies; the libm pow took microseconds on one lane)
+    const unsigned t = (unsigned)(*A.step) + 1u;
+    sc[0] = (float)(1.0 - powi_d((double)A.b1, t));        // bias_correction1
+    sc[1] = (float)sqrt(1.0 - powi_d((double)A.b2, t));   // sqrt(bias_correction2)
   }
   __syncthreads();
-  if (open) {
-    const float step_size = A.lr / sc[0], bc2_sqrt = sc[1];
-    const long long stride = (long long)nb * kAdamBlock;
-    for (long long i = (long long)(blockIdx.x - S.start[si]) * kAdamBlock + threadIdx.x; i < A.n; i += stride) {
-      const float gi = A.g[i];
-      const float mi = A.m[i] + (1.0f - A.b1) * (gi - A.m[i]);
-      const float vi = A.v[i] * A.b2 + (1.0f - A.b2) * gi * gi;
-      A.m[i] = mi;
-      A.v[i] = vi;
-      const float denom = sqrtf(vi) / bc2_sqrt + A.eps;
-      A.p[i] = A.p[i] - step_size * (mi / denom);
+  const int Ip = (A.I + 31) & ~31;
+  const long long w2p0 = (long long)(Ip / 8) * kM3NB * 256, w2tp0 = w2p0 + (long long)kM3NB * 32 * 256;
+  for (long long i0 = first; i0 < A.n; i0 += stride) {
+    if (i0 != first) load(i0);
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const long long i = i0 + (long long)u * kAdamBlock;
+      if (i >= A.n) break;
+      if (A.zero) A.g[i] = 0.f;
+      if (!open) continue;
+      const float m1 = mi[u] + (1.0f - A.b1) * (gi[u] - mi[u]);
+      const float v1 = vi[u] * A.b2 + (1.0f - A.b2) * gi[u] * gi[u];
+      A.m[i] = m1;
+      A.v[i] = v1;
+      const float denom = sqrtf(v1) / sc[1] + A.eps;
+      const float p1 = pi[u] - (A.lr / sc[0]) * (m1 / denom);
+      A.p[i] = p1;
+      if (A.pack) {
+        if (i >= A.w1 && i < A.w1 + (long long)kM3N * A.I) {
+          const int m = (int)((i - A.w1) / A.I), k = (int)((i - A.w1) - (long long)m * A.I);
+          A.pack[m3_pos_w1(m, k)] = p1;
+        } else if (i >= A.w2 && i < A.w2 + (long long)kM3N * kM3N) {
+          const int m = (int)((i - A.w2) >> 8), n = (int)((i - A.w2) & 255);
+          A.pack[w2p0 + m3_pos_w2(m >> 5, m & 31, n >> 5, n & 31)] = p1;    // W2p:  blk = mb, c = m, other = nb
+          A.pack[w2tp0 + m3_pos_w2(n >> 5, n & 31, m >> 5, m & 31)] = p1;   // W2Tp: blk = nb, c = n, other = mb
+        }
+      }
     }
   }
   __syncthreads();
@@ -892,9 +994,12 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
 // index; each wave streams its own weight block from L2 (no sharing, no LDS).
 constexpr int kM3WWaves = 8;
 constexpr int kM3WBlock = 64 * kM3WWaves;
-constexpr int kM3WMaxI = 1024;                                            // widest input the fused path takes
-constexpr int kM3WLds = 32 * (kM3WMaxI + 1);                             // floats: X tile (row stride Ip + 1), then the exchange
-static_assert(kM3WLds >= kM3Steps2 * 64, "wide LDS too small");
+// dynamic LDS of the wide forward (floats): the X tile (row stride Ip + 1),
+// then the H1ᵀ exchange — sized to the input width so a workgroup can share its
+// CU with another kernel's (the actor's, on the other stream)
+__host__ __device__ constexpr int m3w_lds_floats(int Ip) {
+  return 32 * (Ip + 1) > kM3Steps2 * 64 ? 32 * (Ip + 1) : kM3Steps2 * 64;
+}
 
 __device__ __forceinline__ void m3w_share(float* xs, const float* mine, float* all, int w) {
   const int lane = threadIdx.x & 63;
@@ -935,25 +1040,51 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
                                                               const float* __restrict__ b2,
                                                               const float* __restrict__ W3,
                                                               const float* __restrict__ b3, float* __restrict__ H1T,
-                                                              float* __restrict__ H2T, float* __restrict__ out) {
+                                                              float* __restrict__ H2T, float* __restrict__ out,
+                                                              const long long* __restrict__ rows,
+                                                              float* __restrict__ Xg) {
   // LDS: the X tile during layer 1, then the H1ᵀ exchange
-  __shared__ float lds[kM3WLds];
+  extern __shared__ float lds[];   // m3w_lds_floats(Ip)
   __shared__ float hp[kM3WWaves][A][64];
   float* xs = lds;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   const long long r0 = (long long)blockIdx.x * 32, r = r0 + c;
   const bool rv = r < K;
   const int Ip = m3_ip(I), S = Ip + 1;   // odd row stride: the 32 rows of a read hit 32 banks
-  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, (size_t)K * I * 4),
-                               h1r = m3_rsrc(H1T, H1T ? (size_t)K * kM3N * 4 : 0),
+  const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, H1T ? (size_t)K * kM3N * 4 : 0),
                                h2r = m3_rsrc(H2T, H2T ? (size_t)K * kM3N * 4 : 0);
   const unsigned roff = rv ? (unsigned)(r * 4) : kM3OOB;
   const unsigned kstride = (unsigned)(K * 4);
   // the tile's 32 rows are contiguous in X: every wave reads them coalesced,
   // once, instead of each of the 8 waves gathering every lane's row
-  for (int row = w; row < 32; row += kM3WWaves) {
-    const unsigned base = r0 + row < K ? (unsigned)((r0 + row) * I * 4) : kM3OOB;
-    for (int k = lane; k < Ip; k += 64) lds[row * S + k] = m3_ld(xr, k < I ? base + 4u * k : kM3OOB);
+  // (rows != NULL: tile row r is X row rows[r] — the minibatch gather — and is
+  // also written to Xg[r], the gathered copy the weight gradients read).  Each
+  // wave stages 4 rows; every load of a 256-column pass is issued before the
+  // first LDS write, so the pass costs one memory latency, not sixteen.
+  constexpr int RPW = 32 / kM3WWaves;
+  long long src[RPW];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const long long rr = r0 + w + kM3WWaves * j;
+    src[j] = rr < K ? (rows ? rows[rr] : rr) : -1;
+  }
+  for (int k0 = 0; k0 < Ip; k0 += 256) {
+    float v[RPW][4];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + lane + 64 * u;
+        v[j][u] = src[j] >= 0 && k < I ? X[src[j] * I + k] : 0.f;
+      }
+#pragma unroll
+    for (int j = 0; j < RPW; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + lane + 64 * u, row = w + kM3WWaves * j;
+        if (k < Ip) lds[row * S + k] = v[j][u];
+        if (rows && Xg && src[j] >= 0 && k < I) Xg[(r0 + row) * I + k] = v[j][u];
+      }
   }
   __syncthreads();
   // layer 1, block w: W1p (the wave's block, one coalesced float4 per k-quad)
@@ -1239,7 +1370,10 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
       return fail(QS_E_INVALID, "qs_mlp_sum_partials_multi: bad task");
     T.t[i] = MlpSumTask{partial[i], d0[i], d1[i], d2[i], (long long)P[i], (long long)n0[i], (long long)n1[i], (int)G[i]};
     T.start[i] = blocks;
-    blocks += (int)((P[i] + 63) / 64);
+    int wg = 1;   // mlp_sum_wg
+    while (wg < G[i] && wg < 16) wg <<= 1;
+    const int64_t span = (int64_t)(kMlpSumBlock / 64 / wg) * 64 * kMlpSumCols;   // columns per block
+    blocks += (int)((P[i] + span - 1) / span);
   }
   T.start[n] = blocks;
   hipLaunchKernelGGL(mlp_sum_multi_kernel, dim3(blocks), dim3(kMlpSumBlock), 0, (hipStream_t)stream, T);
@@ -1267,25 +1401,45 @@ int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* 
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_pack: ") + hipGetErrorString(e));
 }
 
-int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
-                const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream) {
+static int mlp3_fwd_launch(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
+                           const float* pack, const float* b1, const float* b2, const float* W3, const float* b3,
+                           float* H1T, float* H2T, float* out, void* stream, const char* name) {
   if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !X || !pack ||
       !b1 || !b2 || !W3 || !b3 || (!H1T) != (!H2T) || !out)
-    return fail(QS_E_INVALID, "qs_mlp3_fwd: bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
-  const bool wide = m3_wide(K, I);
-  const unsigned grid = (unsigned)qs_mlp3_tiles(K, I);
+    return fail(QS_E_INVALID, std::string(name) + ": bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
+  const bool wide = rows || m3_wide(K, I);   // the gathering form is the 8-wave kernel's
+  const unsigned grid = (unsigned)(wide ? (K + 31) / 32 : qs_mlp3_tiles(K, I));
+  const unsigned lds = wide ? (unsigned)(m3w_lds_floats((I + 31) & ~31) * sizeof(float)) : 0u;
+  const long long* rr = (const long long*)rows;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(wide ? kM3WBlock : kM3Block), 0, (hipStream_t)stream, (long long)K,
-                       (int)I, X, pack, b1, b2, W3, b3, H1T, H2T, out);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3Block), 0, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1, b2,
+                       W3, b3, H1T, H2T, out);
+  };
+  auto gow = [&](auto kern) {
+    if (lds > 65536u) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3WBlock), lds, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1,
+                       b2, W3, b3, H1T, H2T, out, rr, Xg);
   };
   switch (A) {
-    case 1: wide ? go(mlp3w_fwd_kernel<1>) : go(mlp3_fwd_kernel<1>); break;
-    case 2: wide ? go(mlp3w_fwd_kernel<2>) : go(mlp3_fwd_kernel<2>); break;
-    case 3: wide ? go(mlp3w_fwd_kernel<3>) : go(mlp3_fwd_kernel<3>); break;
-    default: wide ? go(mlp3w_fwd_kernel<4>) : go(mlp3_fwd_kernel<4>); break;
+    case 1: wide ? gow(mlp3w_fwd_kernel<1>) : go(mlp3_fwd_kernel<1>); break;
+    case 2: wide ? gow(mlp3w_fwd_kernel<2>) : go(mlp3_fwd_kernel<2>); break;
+    case 3: wide ? gow(mlp3w_fwd_kernel<3>) : go(mlp3_fwd_kernel<3>); break;
+    default: wide ? gow(mlp3w_fwd_kernel<4>) : go(mlp3_fwd_kernel<4>); break;
   }
   hipError_t e = hipGetLastError();
-  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_fwd: ") + hipGetErrorString(e));
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string(name) + ": " + hipGetErrorString(e));
+}
+
+int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
+                const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream) {
+  return mlp3_fwd_launch(K, I, N, A, X, nullptr, nullptr, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd");
+}
+
+int qs_mlp3_fwd_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
+                     const float* pack, const float* b1, const float* b2, const float* W3, const float* b3, float* H1T,
+                     float* H2T, float* out, void* stream) {
+  if (!rows) return fail(QS_E_INVALID, "qs_mlp3_fwd_rows: rows is NULL");
+  return mlp3_fwd_launch(K, I, N, A, X, rows, Xg, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd_rows");
 }
 
 int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, const float* H1T, const float* H2T,
@@ -1311,28 +1465,53 @@ int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, c
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_bwd: ") + hipGetErrorString(e));
 }
 
-int qs_adam_multi(int32_t nseg, float* const* params, const float* const* grads, float* const* exp_avg,
-                  float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr, const float* beta1,
-                  const float* beta2, const float* eps, const float* const* gate_val, const float* gate_thr, void* work,
-                  void* stream) {
+static int adam_multi_launch(int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr,
+                             const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                             const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                             const int32_t* pack_I, int32_t zero_grads, void* work, void* stream, const char* name) {
   if (nseg <= 0 || nseg > kAdamMaxSeg || !params || !grads || !exp_avg || !exp_avg_sq || !step || !n || !lr || !beta1 ||
       !beta2 || !eps || !gate_val || !gate_thr || !work)
-    return fail(QS_E_INVALID, "qs_adam_multi: bad argument (1..4 segments)");
+    return fail(QS_E_INVALID, std::string(name) + ": bad argument (1..4 segments)");
   AdamSegs S{};
   S.n = nseg;
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
     if (n[i] <= 0 || !params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i] || !step[i])
-      return fail(QS_E_INVALID, "qs_adam_multi: bad segment");
-    S.s[i] = AdamSeg{params[i], grads[i], exp_avg[i], exp_avg_sq[i], step[i], gate_val[i], (long long)n[i], lr[i],
-                     beta1[i], beta2[i], eps[i], gate_thr[i]};
+      return fail(QS_E_INVALID, std::string(name) + ": bad segment");
+    float* pk = pack ? pack[i] : nullptr;
+    const int I = pk ? pack_I[i] : 0;
+    if (pk && (I <= 0 || I > 1024 || w1_off[i] < 0 || w2_off[i] < 0 || w1_off[i] + (int64_t)kM3N * I > n[i] ||
+               w2_off[i] + (int64_t)kM3N * kM3N > n[i]))
+      return fail(QS_E_INVALID, std::string(name) + ": bad pack segment");
+    S.s[i] = AdamSeg{params[i], grads[i], exp_avg[i], exp_avg_sq[i], step[i], gate_val[i], pk, (long long)n[i],
+                     pk ? (long long)w1_off[i] : 0, pk ? (long long)w2_off[i] : 0, lr[i], beta1[i], beta2[i], eps[i],
+                     gate_thr[i], I, zero_grads ? 1 : 0};
     S.start[i] = blocks;
-    blocks += (int)std::min<int64_t>((n[i] + kAdamBlock - 1) / kAdamBlock, kAdamSegBlocks);
+    blocks += (int)std::min<int64_t>((n[i] + kAdamBlock * kAdamPer - 1) / (kAdamBlock * kAdamPer), kAdamSegBlocks);
   }
   S.start[nseg] = blocks;
   hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(kAdamBlock), 0, (hipStream_t)stream, S, (unsigned*)work);
   hipError_t e = hipGetLastError();
-  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_multi: ") + hipGetErrorString(e));
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string(name) + ": " + hipGetErrorString(e));
+}
+
+int qs_adam_multi(int32_t nseg, float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr, const float* beta1,
+                  const float* beta2, const float* eps, const float* const* gate_val, const float* gate_thr, void* work,
+                  void* stream) {
+  return adam_multi_launch(nseg, params, (float* const*)grads, exp_avg, exp_avg_sq, step, n, lr, beta1, beta2, eps,
+                           gate_val, gate_thr, nullptr, nullptr, nullptr, nullptr, 0, work, stream, "qs_adam_multi");
+}
+
+int qs_adam_multi_pack(int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr,
+                       const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                       const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                       const int32_t* pack_I, int32_t zero_grads, void* work, void* stream) {
+  if (!pack || !w1_off || !w2_off || !pack_I) return fail(QS_E_INVALID, "qs_adam_multi_pack: bad argument");
+  return adam_multi_launch(nseg, params, grads, exp_avg, exp_avg_sq, step, n, lr, beta1, beta2, eps, gate_val,
+                           gate_thr, pack, w1_off, w2_off, pack_I, zero_grads, work, stream, "qs_adam_multi_pack");
 }
 
 int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step, float lr,

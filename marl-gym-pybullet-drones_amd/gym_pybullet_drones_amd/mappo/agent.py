@@ -35,11 +35,11 @@ def get_activation(name):
     return getattr(torch, name) if name in ("tanh", "relu", "sigmoid") else (getattr(F, name) if name else (lambda x: x))
 
 
-def _splitk_chunks(rows):
+def _splitk_chunks(rows, min_rows=1024):
     """Row chunks of the split-K weight gradient: the largest power of two S with
-    rows / S >= 1024 that divides rows (1 = plain GEMM)."""
+    rows / S >= min_rows that divides rows (1 = plain GEMM)."""
     s = 1
-    while rows % (2 * s) == 0 and rows // (2 * s) >= 1024 and s < 64:
+    while rows % (2 * s) == 0 and rows // (2 * s) >= min_rows and s < 64:
         s *= 2
     return s
 
@@ -224,6 +224,100 @@ class _TanhMLP3(torch.autograd.Function):
         _splitk_into(w1.grad, dh1, x)
         dx = dh1 @ w1 if ctx.needs_input_grad[0] else None
         return dx, None, None, None, None, None, None
+
+
+# (rows K, gradient width M) → minimum rows per split-K chunk of the direct
+# iteration's weight gradients (default 1024)
+_SPLITK_MIN_ROWS = {}
+
+
+class _M3Work:
+    """Static workspace and launches of one 256-wide tanh MLP (qs_mlp3_fwd / bwd)
+    at a fixed batch of K rows, outside autograd: the update iteration drives the
+    actor's and the critic's on two streams (MAPPOAgent._iteration_streams).  Same
+    kernels and reductions as _TanhMLP3; every buffer, the split-K partials
+    included, is allocated once, so the captured graph never allocates and
+    nothing is freed while the other stream may still use it."""
+
+    def __init__(self, mlp, K, device):
+        f0, f1, f2 = mlp.fcs
+        lib = L.load()
+        self.mlp, self.K, self.I, self.A = mlp, K, f0.in_features, f2.out_features
+        f32 = dict(device=device, dtype=torch.float32)
+        self.pack = torch.empty(int(lib.qs_mlp3_pack_floats(self.I)), **f32)
+        self.h1, self.h2 = torch.empty((256, K), **f32), torch.empty((256, K), **f32)
+        self.dz1, self.dz2 = torch.empty((256, K), **f32), torch.empty((256, K), **f32)
+        self.out = torch.empty((K, self.A), **f32)
+        G = int(lib.qs_mlp3_tiles(K, self.I))
+        self.G = G
+        self.part_a = torch.empty((G, 256 * (1 + self.A) + self.A), **f32)
+        self.part_b = torch.empty((G, 256), **f32)
+        # split-K chunk counts of dW2 and dW1 (rows per chunk >= the _splitk_min_rows entry)
+        m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 1024), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
+        self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
+        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
+        self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 else None
+
+    def repack(self):
+        """The pack image from the current weights (qs_adam_multi_pack keeps it
+        current across the update's Adam steps)."""
+        f0, f1, _ = self.mlp.fcs
+        L.check(L.load().qs_mlp3_pack(self.I, 256, L.ptr(f0.weight), L.ptr(f1.weight), L.ptr(self.pack), _stream()),
+                "qs_mlp3_pack")
+
+    def forward(self, x, rows=None, xg=None):
+        """out = MLP(x) (x [K][I]); rows: x is the whole table and batch row r is
+        x[rows[r]] (gathered in the kernel, copied to xg)."""
+        lib, st = L.load(), _stream()
+        f0, f1, f2 = self.mlp.fcs
+        tail = (L.ptr(self.pack), L.ptr(f0.bias), L.ptr(f1.bias), L.ptr(f2.weight), L.ptr(f2.bias), L.ptr(self.h1),
+                L.ptr(self.h2), L.ptr(self.out), st)
+        if rows is None:
+            L.check(lib.qs_mlp3_fwd(self.K, self.I, 256, self.A, L.ptr(x), *tail), "qs_mlp3_fwd")
+        else:
+            L.check(lib.qs_mlp3_fwd_rows(self.K, self.I, 256, self.A, L.ptr(x), L.ptr(rows), L.ptr(xg), *tail),
+                    "qs_mlp3_fwd_rows")
+        return self.out
+
+    def pack_segment(self, fb):
+        """(pack, w1 offset, w2 offset, I) of this MLP inside FlatBuffers fb."""
+        f0, f1, _ = self.mlp.fcs
+        ids = [id(p) for p in fb.params]
+        return (self.pack, fb.offsets[ids.index(id(f0.weight))][0], fb.offsets[ids.index(id(f1.weight))][0], self.I)
+
+    def _splitk(self, dst, a, b, b_rows_are_k, part, S):
+        """dst += a·bᵀ over K in S chunks (see _splitk_nt) into the preallocated partials."""
+        K = a.shape[1]
+        bk = b.t() if b_rows_are_k else b
+        if S == 1:
+            dst.addmm_(a, bk)
+            return None
+        a3 = a.view(a.shape[0], S, K // S).transpose(0, 1)
+        b3 = b.view(b.shape[0], S, K // S).permute(1, 2, 0) if b_rows_are_k else b.view(S, K // S, -1)
+        torch.bmm(a3, b3, out=part)
+        return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
+
+    def backward(self, x, dout, tasks):
+        """Gradients of the parameters' .grad views (+=); the fixed-order partial
+        sums are appended to `tasks` (one qs_mlp_sum_partials_multi launch later)."""
+        lib, st = L.load(), _stream()
+        f0, f1, f2 = self.mlp.fcs
+        N, A = 256, self.A
+        L.check(lib.qs_mlp3_bwd(self.K, self.I, N, A, L.ptr(dout), L.ptr(self.h1), L.ptr(self.h2), L.ptr(self.pack),
+                                L.ptr(f2.weight), L.ptr(self.dz2), L.ptr(self.dz1), L.ptr(self.part_a),
+                                L.ptr(self.part_b), st), "qs_mlp3_bwd")
+        tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
+        tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
+        for t in (self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2),    # dW2 = dZ2ᵀ·H1
+                  self._splitk(f0.weight.grad, self.dz1, x, False, self.pw1, self.S1)):        # dW1 = dZ1ᵀ·X
+            if t is not None:
+                tasks.append(t)
+
+
+def _m3_ok(mlp, max_in=1024):
+    f0, f1, f2 = mlp.fcs
+    return (mlp._tanh3 and f0.out_features == 256 and f1.out_features == 256 and f2.out_features <= 4
+            and f0.in_features <= max_in and all(p.grad is not None and p.grad.is_contiguous() for p in mlp.parameters()))
 
 
 class MLP(nn.Module):
@@ -435,9 +529,12 @@ class FlatBuffers:
                 "qs_adam_step")
 
     @staticmethod
-    def adam_multi(segs, work):
+    def adam_multi(segs, work, packs=None, zero_grads=False):
         """One gated Adam step of several FlatBuffers in one launch (qs_adam_multi).
-        segs: [(buffers, gate_val tensor or None, gate_thr)]; work: device int32[4]."""
+        segs: [(buffers, gate_val tensor or None, gate_thr)]; work: device int32[4].
+        packs: per segment None or (pack image, W1 offset, W2 offset, I) of a
+        256-wide tanh MLP kept current by the step; zero_grads: the gradients are
+        zeroed after they are read (qs_adam_multi_pack)."""
         fb0 = segs[0][0]
         if fb0.flat.device.type != 'cuda':
             raise RuntimeError("FlatBuffers.adam_multi is the HIP qs_adam_multi kernel: the parameters must be on the GPU")
@@ -445,14 +542,23 @@ class FlatBuffers:
         vp = ctypes.c_void_p
         arr = lambda ct, vals: (ct * n)(*vals)
         ptrs = lambda f: arr(vp, [f(s) for s in segs])
-        L.check(L.load().qs_adam_multi(
-            n, ptrs(lambda s: s[0].flat.data_ptr()), ptrs(lambda s: s[0].grad.data_ptr()),
-            ptrs(lambda s: s[0].exp_avg.data_ptr()), ptrs(lambda s: s[0].exp_avg_sq.data_ptr()),
-            ptrs(lambda s: s[0].step.data_ptr()), arr(ctypes.c_int64, [s[0].n for s in segs]),
-            arr(ctypes.c_float, [s[0].lr for s in segs]), arr(ctypes.c_float, [s[0].betas[0] for s in segs]),
-            arr(ctypes.c_float, [s[0].betas[1] for s in segs]), arr(ctypes.c_float, [s[0].eps for s in segs]),
-            ptrs(lambda s: s[1].data_ptr() if s[1] is not None else None), arr(ctypes.c_float, [s[2] for s in segs]),
-            L.ptr(work), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "qs_adam_multi")
+        common = (ptrs(lambda s: s[0].flat.data_ptr()), ptrs(lambda s: s[0].grad.data_ptr()),
+                  ptrs(lambda s: s[0].exp_avg.data_ptr()), ptrs(lambda s: s[0].exp_avg_sq.data_ptr()),
+                  ptrs(lambda s: s[0].step.data_ptr()), arr(ctypes.c_int64, [s[0].n for s in segs]),
+                  arr(ctypes.c_float, [s[0].lr for s in segs]), arr(ctypes.c_float, [s[0].betas[0] for s in segs]),
+                  arr(ctypes.c_float, [s[0].betas[1] for s in segs]), arr(ctypes.c_float, [s[0].eps for s in segs]),
+                  ptrs(lambda s: s[1].data_ptr() if s[1] is not None else None),
+                  arr(ctypes.c_float, [s[2] for s in segs]))
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        if packs is None and not zero_grads:
+            L.check(L.load().qs_adam_multi(n, *common, L.ptr(work), st), "qs_adam_multi")
+            return
+        packs = packs or [None] * n
+        L.check(L.load().qs_adam_multi_pack(
+            n, *common, arr(vp, [p[0].data_ptr() if p else None for p in packs]),
+            arr(ctypes.c_int64, [p[1] if p else 0 for p in packs]), arr(ctypes.c_int64, [p[2] if p else 0 for p in packs]),
+            arr(ctypes.c_int32, [p[3] if p else 0 for p in packs]), int(bool(zero_grads)), L.ptr(work), st),
+            "qs_adam_multi_pack")
 
     # torch.optim.Adam state_dict format (checkpoint compatibility, MP:203-229)
     def state_dict(self):
@@ -504,6 +610,7 @@ class MAPPOAgent:
         self.graph_collectives = kwargs.get('graph_collectives', True)
         self._force_allreduce = False   # tests: take the all-reduce path with one rank
         self.fused_heads = fused_heads   # qs_ppo_heads (False: the loss heads as plain torch ops)
+        self.direct = kwargs.get('direct', True)   # the fused MLP kernels without autograd (_iteration_direct)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
                                    share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
@@ -615,6 +722,66 @@ class MAPPOAgent:
             torch.autograd.backward([mean, v], [self._dmean, self._dv])
         self._exchange_and_step(world)
 
+    def _direct_ok(self):
+        return self.direct and _m3_ok(self.ac.actor.pi_net) and _m3_ok(self.ac.critic.v_net)
+
+    def _direct_setup(self, mb, D, O, A):
+        lib = L.load()
+        if getattr(self, '_ws_key', None) == (mb, D, O, A):
+            return
+        self._ws_actor = _M3Work(self.ac.actor.pi_net, mb * D, self.device)
+        self._ws_critic = _M3Work(self.ac.critic.v_net, mb, self.device)
+        self._xg = torch.empty((mb, D * O), device=self.device)
+        self._dmean = torch.empty(mb * D, A, device=self.device)
+        self._dv = torch.empty(mb, 1, device=self.device)
+        self._heads_work = torch.zeros(int(lib.qs_ppo_heads_work_bytes(mb, D)), dtype=torch.uint8, device=self.device)
+        self._ws_key = (mb, D, O, A)
+        self._repack()
+
+    def _repack(self):
+        """Pack images from the current weights, and zeroed gradients: the direct
+        iteration's Adam keeps both from then on (call after any weight change
+        outside the update, e.g. load_state_dict, and before each update)."""
+        if getattr(self, '_ws_key', None) is not None:
+            self._ws_actor.repack()
+            self._ws_critic.repack()
+        self._reduce_buf.zero_()
+
+    def _iteration_direct(self, rollouts, idx, acc):
+        """One minibatch on the 256-wide fused MLP kernels without autograd, in
+        the fewest launches: the critic forward gathers the minibatch's obs rows
+        itself (qs_mlp3_fwd_rows; its gathered copy is the actor's input and the
+        weight gradients' X), qs_ppo_heads, both backwards into the .grad views,
+        one partial-sum launch, the exchange, and one Adam launch that also zeroes
+        the gradients and rewrites the weights' pack images
+        (qs_adam_multi_pack) — no fill, gather or pack launches.  The same
+        kernels and arithmetic as _iteration_fused, so the same bits."""
+        world = _dist_world()
+        D, O, A = rollouts.num_agents, rollouts.obs_dim, self.ac.act_dim
+        mb = idx.shape[0]
+        lib = L.load()
+        self._direct_setup(mb, D, O, A)
+        T, E = rollouts.max_length, rollouts.batch_size
+        xc, xa = self._xg, self._xg.view(mb * D, O)
+        v = self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
+        mean = self._ws_actor.forward(xa)
+        logstd = self.ac.actor.logstd
+        L.check(lib.qs_ppo_heads(mb, D, A, L.ptr(idx), L.ptr(mean), L.ptr(logstd), float(self.action_scale),
+                                 L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
+                                 L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
+                                 L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
+                                 L.ptr(self._heads_work), _stream()), "qs_ppo_heads")
+        tasks = []
+        self._ws_actor.backward(xa, self._dmean, tasks)
+        self._ws_critic.backward(xc, self._dv, tasks)
+        _flush_sums(tasks)
+        self._exchange(world)
+        gate = self._kl if self.target_kl > 0 else None
+        FlatBuffers.adam_multi([(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)],
+                               self._adam_work, packs=[self._ws_actor.pack_segment(self.actor_opt),
+                                                       self._ws_critic.pack_segment(self.critic_opt)],
+                               zero_grads=True)
+
     def _iteration(self, batch, acc):
         """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.
 
@@ -667,7 +834,10 @@ class MAPPOAgent:
 
     def _step_minibatch(self, rollouts, idx, acc):
         if self.fused_heads and self._fused_heads_ok(rollouts):
-            self._iteration_fused(rollouts, idx, acc)
+            if self._direct_ok():
+                self._iteration_direct(rollouts, idx, acc)
+            else:
+                self._iteration_fused(rollouts, idx, acc)
         else:
             self._iteration(rollouts.sample(idx), acc)
 
@@ -718,6 +888,7 @@ class MAPPOAgent:
         k = self._chunk(num_mini_batch)
         if graphs and (self._graph is None or self._g_rollouts is not rollouts or self._g_k != k):
             self._capture(rollouts, k)
+        self._repack()   # the direct iteration's pack images and zeroed gradients
         per_epoch = []
         for epoch in range(self.opt_epochs):
             perm = torch.randperm(total_steps, device=self.device, generator=generator)
