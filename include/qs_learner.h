@@ -161,6 +161,25 @@ int qs_adam_multi_pack(int32_t nseg, float* const* params, float* const* grads, 
                        const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
                        const int32_t* pack_I, int32_t zero_grads, void* work, void* stream);
 
+/* One rank's minibatch step after the backward kernels: the n partial-sum
+ * tasks of qs_mlp_sum_partials_multi (same arguments) and the Adam step of
+ * qs_adam_multi_pack (segments params[nseg] …, pack images as there) in one
+ * launch.  task_seg[i] names the segment whose gradient buffer task i's
+ * destinations lie in; every gradient element the step reads must be the
+ * destination of exactly one task column (a one-row task with partial = the
+ * gradient itself covers an element written elsewhere, e.g. logstd's).  The
+ * gradients are not written: each reduced value goes straight into Adam.
+ * Equals qs_mlp_sum_partials_multi on zeroed gradients followed by
+ * qs_adam_multi_pack, bit for bit.  work: device uint32, zero before the first
+ * call. */
+int qs_mlp_sum_adam(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial, float* const* d0,
+                    const int64_t* n0, float* const* d1, const int64_t* n1, float* const* d2, const int32_t* task_seg,
+                    int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, float* const* step, const int64_t* nel, const float* lr,
+                    const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                    const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                    const int32_t* pack_I, void* work, void* stream);
+
 const char* qs_learner_last_error(void);
 
 #ifdef __cplusplus

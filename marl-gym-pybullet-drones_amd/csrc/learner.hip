@@ -419,6 +419,9 @@ struct MlpSumTasks {
   int start[kMlpMaxTasks + 1];
   int n;
 };
+struct SegOf {
+  int s[kMlpMaxTasks];   // the Adam segment of each task's destination
+};
 // A block is 16 waves; a task's G partial rows are split over Wg = min(16,
 // pow2 ≥ G) wave slices (wave slice w sums rows g ≡ w mod Wg in order, eight
 // rows' loads in flight), and the 16 / Wg wave groups of the block take
@@ -432,7 +435,10 @@ __device__ __forceinline__ int mlp_sum_wg(int G) {
   while (w < G && w < 16) w <<= 1;
   return w;
 }
-__global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks tasks) {
+// fin(ti, c, dst, u): the block's result u for column c of task ti (dst its
+// destination element)
+template <class Fin>
+__device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin) {
   constexpr int W = kMlpSumBlock / 64, C = kMlpSumCols;
   __shared__ float lds[W][64 * C];
   int ti = 0;
@@ -477,8 +483,12 @@ __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks
     float u = lds[cg * Wg][lane + 64 * j];
     for (int k = 1; k < Wg; ++k) u += lds[cg * Wg + k][lane + 64 * j];
     float* dst = c < T.n0 ? T.d0 + c : (c < T.n0 + T.n1 ? T.d1 + (c - T.n0) : T.d2 + (c - T.n0 - T.n1));
-    *dst += u;
+    fin(ti, dst, u);
   }
+}
+
+__global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks tasks) {
+  mlp_sum_block(tasks, [](int, float* dst, float u) { *dst += u; });
 }
 
 // torch.optim.Adam step and its step-count commit in one launch: every block
@@ -911,6 +921,32 @@ __device__ __forceinline__ long long m3_pos_w2(int blk, int c, int other, int x)
   return ((((long long)blk * 32 + q) * 64 + 32 * hh + c) << 2) + e;
 }
 
+// One Adam element (torch.optim.Adam, amsgrad=False, weight_decay=0): the new
+// moments and parameter, and the parameter's pack-image copies.  bc1 =
+// 1 − β1^t, bc2s = sqrt(1 − β2^t).
+__device__ __forceinline__ void adam_elem(const AdamSeg& A, long long i, float g, float p, float m, float v,
+                                          float bc1, float bc2s) {
+  const float m1 = m + (1.0f - A.b1) * (g - m);
+  const float v1 = v * A.b2 + (1.0f - A.b2) * g * g;
+  A.m[i] = m1;
+  A.v[i] = v1;
+  const float denom = sqrtf(v1) / bc2s + A.eps;
+  const float p1 = p - (A.lr / bc1) * (m1 / denom);
+  A.p[i] = p1;
+  if (A.pack) {
+    const int Ip = (A.I + 31) & ~31;
+    const long long w2p0 = (long long)(Ip / 8) * kM3NB * 256, w2tp0 = w2p0 + (long long)kM3NB * 32 * 256;
+    if (i >= A.w1 && i < A.w1 + (long long)kM3N * A.I) {
+      const int mm = (int)((i - A.w1) / A.I), k = (int)((i - A.w1) - (long long)mm * A.I);
+      A.pack[m3_pos_w1(mm, k)] = p1;
+    } else if (i >= A.w2 && i < A.w2 + (long long)kM3N * kM3N) {
+      const int mm = (int)((i - A.w2) >> 8), n = (int)((i - A.w2) & 255);
+      A.pack[w2p0 + m3_pos_w2(mm >> 5, mm & 31, n >> 5, n & 31)] = p1;    // W2p:  blk = mb, c = m, other = nb
+      A.pack[w2tp0 + m3_pos_w2(n >> 5, n & 31, mm >> 5, mm & 31)] = p1;   // W2Tp: blk = nb, c = n, other = mb
+    }
+  }
+}
+
 __device__ __forceinline__ double powi_d(double b, unsigned t) {
   double r = 1.0;
   while (t) {
@@ -948,8 +984,6 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
     sc[1] = (float)sqrt(1.0 - powi_d((double)A.b2, t));   // sqrt(bias_correction2)
   }
   __syncthreads();
-  const int Ip = (A.I + 31) & ~31;
-  const long long w2p0 = (long long)(Ip / 8) * kM3NB * 256, w2tp0 = w2p0 + (long long)kM3NB * 32 * 256;
   for (long long i0 = first; i0 < A.n; i0 += stride) {
     if (i0 != first) load(i0);
 #pragma unroll
@@ -957,24 +991,7 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
       const long long i = i0 + (long long)u * kAdamBlock;
       if (i >= A.n) break;
       if (A.zero) A.g[i] = 0.f;
-      if (!open) continue;
-      const float m1 = mi[u] + (1.0f - A.b1) * (gi[u] - mi[u]);
-      const float v1 = vi[u] * A.b2 + (1.0f - A.b2) * gi[u] * gi[u];
-      A.m[i] = m1;
-      A.v[i] = v1;
-      const float denom = sqrtf(v1) / sc[1] + A.eps;
-      const float p1 = pi[u] - (A.lr / sc[0]) * (m1 / denom);
-      A.p[i] = p1;
-      if (A.pack) {
-        if (i >= A.w1 && i < A.w1 + (long long)kM3N * A.I) {
-          const int m = (int)((i - A.w1) / A.I), k = (int)((i - A.w1) - (long long)m * A.I);
-          A.pack[m3_pos_w1(m, k)] = p1;
-        } else if (i >= A.w2 && i < A.w2 + (long long)kM3N * kM3N) {
-          const int m = (int)((i - A.w2) >> 8), n = (int)((i - A.w2) & 255);
-          A.pack[w2p0 + m3_pos_w2(m >> 5, m & 31, n >> 5, n & 31)] = p1;    // W2p:  blk = mb, c = m, other = nb
-          A.pack[w2tp0 + m3_pos_w2(n >> 5, n & 31, m >> 5, m & 31)] = p1;   // W2Tp: blk = nb, c = n, other = mb
-        }
-      }
+      if (open) adam_elem(A, i, gi[u], pi[u], mi[u], vi[u], sc[0], sc[1]);
     }
   }
   __syncthreads();
@@ -984,6 +1001,42 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
   if (last && threadIdx.x == 0) {
     done[si] = 0;
     if (open) *A.step = *A.step + 1.0f;
+  }
+}
+
+// The minibatch's partial-sum reduction and the Adam step in one launch (one
+// rank: no gradient exchange between them).  Every gradient element of the
+// segments is the destination of exactly one task column; the block that
+// reduces it applies Adam to it at once (the gradient is never written).  Each
+// block forms both segments' bias corrections; the last block to finish
+// commits the step counts (gates permitting).  The per-column summation order
+// is mlp_sum_multi_kernel's, so the step equals sum-then-Adam bit for bit.
+__global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_adam_kernel(MlpSumTasks tasks, AdamSegs S, SegOf seg,
+                                                                   unsigned* done) {
+  __shared__ float sc[kAdamMaxSeg][2];
+  __shared__ bool last;
+  if (threadIdx.x < (unsigned)S.n) {
+    const AdamSeg& A = S.s[threadIdx.x];
+    const unsigned t = (unsigned)(*A.step) + 1u;
+    sc[threadIdx.x][0] = (float)(1.0 - powi_d((double)A.b1, t));
+    sc[threadIdx.x][1] = (float)sqrt(1.0 - powi_d((double)A.b2, t));
+  }
+  __syncthreads();
+  mlp_sum_block(tasks, [&](int ti, float* dst, float u) {
+    const int si = seg.s[ti];
+    const AdamSeg& A = S.s[si];
+    if (!gate_ok(A.gate, A.thr)) return;
+    const long long i = dst - A.g;
+    adam_elem(A, i, u, A.p[i], A.m[i], A.v[i], sc[si][0], sc[si][1]);
+  });
+  __syncthreads();
+  // every block read the step counts before counting itself
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last && threadIdx.x < (unsigned)S.n) {
+    const AdamSeg& A = S.s[threadIdx.x];
+    if (gate_ok(A.gate, A.thr)) *A.step = *A.step + 1.0f;
+    if (threadIdx.x == 0) *done = 0;
   }
 }
 
@@ -1356,18 +1409,18 @@ int qs_mlp_sum_partials(int32_t G, int64_t P, const float* partial, float* d0, i
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials: ") + hipGetErrorString(e));
 }
 
-int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial,
-                              float* const* d0, const int64_t* n0, float* const* d1, const int64_t* n1,
-                              float* const* d2, void* stream) {
+static int build_sum_tasks(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial,
+                           float* const* d0, const int64_t* n0, float* const* d1, const int64_t* n1, float* const* d2,
+                           MlpSumTasks& T, int& blocks, const char* name) {
   if (n <= 0 || n > kMlpMaxTasks || !G || !P || !partial || !d0 || !n0 || !d1 || !n1 || !d2)
-    return fail(QS_E_INVALID, "qs_mlp_sum_partials_multi: bad argument (1..16 tasks)");
-  MlpSumTasks T{};
+    return fail(QS_E_INVALID, std::string(name) + ": bad argument (1..16 tasks)");
+  T = MlpSumTasks{};
   T.n = n;
-  int blocks = 0;
+  blocks = 0;
   for (int i = 0; i < n; ++i) {
     if (G[i] <= 0 || P[i] <= 0 || !partial[i] || !d0[i] || n0[i] <= 0 || n0[i] > P[i] || n1[i] < 0 ||
         n0[i] + n1[i] > P[i] || (n0[i] < P[i] && !d1[i]) || (n0[i] + n1[i] < P[i] && !d2[i]))
-      return fail(QS_E_INVALID, "qs_mlp_sum_partials_multi: bad task");
+      return fail(QS_E_INVALID, std::string(name) + ": bad task");
     T.t[i] = MlpSumTask{partial[i], d0[i], d1[i], d2[i], (long long)P[i], (long long)n0[i], (long long)n1[i], (int)G[i]};
     T.start[i] = blocks;
     int wg = 1;   // mlp_sum_wg
@@ -1376,6 +1429,16 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
     blocks += (int)((P[i] + span - 1) / span);
   }
   T.start[n] = blocks;
+  return QS_OK;
+}
+
+int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial,
+                              float* const* d0, const int64_t* n0, float* const* d1, const int64_t* n1,
+                              float* const* d2, void* stream) {
+  MlpSumTasks T;
+  int blocks;
+  const int rc = build_sum_tasks(n, G, P, partial, d0, n0, d1, n1, d2, T, blocks, "qs_mlp_sum_partials_multi");
+  if (rc != QS_OK) return rc;
   hipLaunchKernelGGL(mlp_sum_multi_kernel, dim3(blocks), dim3(kMlpSumBlock), 0, (hipStream_t)stream, T);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_sum_partials_multi: ") + hipGetErrorString(e));
@@ -1465,15 +1528,15 @@ int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, c
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3_bwd: ") + hipGetErrorString(e));
 }
 
-static int adam_multi_launch(int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
-                             float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr,
-                             const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
-                             const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
-                             const int32_t* pack_I, int32_t zero_grads, void* work, void* stream, const char* name) {
+static int build_adam_segs(int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                           float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr,
+                           const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                           const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                           const int32_t* pack_I, int32_t zero_grads, AdamSegs& S, const char* name) {
   if (nseg <= 0 || nseg > kAdamMaxSeg || !params || !grads || !exp_avg || !exp_avg_sq || !step || !n || !lr || !beta1 ||
-      !beta2 || !eps || !gate_val || !gate_thr || !work)
+      !beta2 || !eps || !gate_val || !gate_thr)
     return fail(QS_E_INVALID, std::string(name) + ": bad argument (1..4 segments)");
-  AdamSegs S{};
+  S = AdamSegs{};
   S.n = nseg;
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -1491,7 +1554,54 @@ static int adam_multi_launch(int32_t nseg, float* const* params, float* const* g
     blocks += (int)std::min<int64_t>((n[i] + kAdamBlock * kAdamPer - 1) / (kAdamBlock * kAdamPer), kAdamSegBlocks);
   }
   S.start[nseg] = blocks;
-  hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(kAdamBlock), 0, (hipStream_t)stream, S, (unsigned*)work);
+  return QS_OK;
+}
+
+static int adam_multi_launch(int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, float* const* step, const int64_t* n, const float* lr,
+                             const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                             const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                             const int32_t* pack_I, int32_t zero_grads, void* work, void* stream, const char* name) {
+  if (!work) return fail(QS_E_INVALID, std::string(name) + ": bad argument (work)");
+  AdamSegs S;
+  const int rc = build_adam_segs(nseg, params, grads, exp_avg, exp_avg_sq, step, n, lr, beta1, beta2, eps, gate_val,
+                                 gate_thr, pack, w1_off, w2_off, pack_I, zero_grads, S, name);
+  if (rc != QS_OK) return rc;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(S.start[nseg]), dim3(kAdamBlock), 0, (hipStream_t)stream, S,
+                     (unsigned*)work);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string(name) + ": " + hipGetErrorString(e));
+}
+
+int qs_mlp_sum_adam(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial, float* const* d0,
+                    const int64_t* n0, float* const* d1, const int64_t* n1, float* const* d2, const int32_t* task_seg,
+                    int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, float* const* step, const int64_t* nel, const float* lr,
+                    const float* beta1, const float* beta2, const float* eps, const float* const* gate_val,
+                    const float* gate_thr, float* const* pack, const int64_t* w1_off, const int64_t* w2_off,
+                    const int32_t* pack_I, void* work, void* stream) {
+  const char* name = "qs_mlp_sum_adam";
+  MlpSumTasks T;
+  int blocks;
+  int rc = build_sum_tasks(n, G, P, partial, d0, n0, d1, n1, d2, T, blocks, name);
+  if (rc != QS_OK) return rc;
+  AdamSegs S;
+  rc = build_adam_segs(nseg, params, grads, exp_avg, exp_avg_sq, step, nel, lr, beta1, beta2, eps, gate_val, gate_thr,
+                       pack, w1_off, w2_off, pack_I, 0, S, name);
+  if (rc != QS_OK) return rc;
+  if (!task_seg || !work) return fail(QS_E_INVALID, std::string(name) + ": bad argument");
+  SegOf seg{};
+  for (int i = 0; i < n; ++i) {   // every destination element inside its segment's gradient buffer
+    if (task_seg[i] < 0 || task_seg[i] >= nseg) return fail(QS_E_INVALID, std::string(name) + ": bad task segment");
+    seg.s[i] = task_seg[i];
+    const float* g0 = grads[task_seg[i]];
+    const float* g1 = g0 + nel[task_seg[i]];
+    auto inside = [&](const float* d, int64_t len) { return len <= 0 || (d >= g0 && d + len <= g1); };
+    if (!inside(d0[i], n0[i]) || !inside(d1[i], n1[i]) || !inside(d2[i], P[i] - n0[i] - n1[i]))
+      return fail(QS_E_INVALID, std::string(name) + ": a task destination lies outside its segment's gradients");
+  }
+  hipLaunchKernelGGL(mlp_sum_adam_kernel, dim3(blocks), dim3(kMlpSumBlock), 0, (hipStream_t)stream, T, S, seg,
+                     (unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string(name) + ": " + hipGetErrorString(e));
 }

@@ -560,6 +560,37 @@ class FlatBuffers:
             arr(ctypes.c_int32, [p[3] if p else 0 for p in packs]), int(bool(zero_grads)), L.ptr(work), st),
             "qs_adam_multi_pack")
 
+    @staticmethod
+    def sum_adam(tasks, task_seg, segs, packs, work):
+        """The partial-sum tasks (see _flush_sums) and the gated Adam step of segs
+        in one launch (qs_mlp_sum_adam): every gradient element of the segments is
+        one task column, reduced straight into its Adam update."""
+        lib = L.load()
+        n, ns = len(tasks), len(segs)
+        if n > 16:
+            raise ValueError("qs_mlp_sum_adam takes at most 16 tasks")
+        vp = ctypes.c_void_p
+        arr = lambda ct, vals: (ct * len(vals))(*vals)
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.check(lib.qs_mlp_sum_adam(
+            n, arr(ctypes.c_int32, [t[0] for t in tasks]), arr(ctypes.c_int64, [t[1] for t in tasks]),
+            arr(vp, [t[2].data_ptr() for t in tasks]), arr(vp, [t[3].data_ptr() for t in tasks]),
+            arr(ctypes.c_int64, [t[4] for t in tasks]),
+            arr(vp, [t[5].data_ptr() if t[5] is not None else None for t in tasks]),
+            arr(ctypes.c_int64, [t[6] for t in tasks]),
+            arr(vp, [t[7].data_ptr() if t[7] is not None else None for t in tasks]),
+            arr(ctypes.c_int32, task_seg), ns,
+            arr(vp, [s[0].flat.data_ptr() for s in segs]), arr(vp, [s[0].grad.data_ptr() for s in segs]),
+            arr(vp, [s[0].exp_avg.data_ptr() for s in segs]), arr(vp, [s[0].exp_avg_sq.data_ptr() for s in segs]),
+            arr(vp, [s[0].step.data_ptr() for s in segs]), arr(ctypes.c_int64, [s[0].n for s in segs]),
+            arr(ctypes.c_float, [s[0].lr for s in segs]), arr(ctypes.c_float, [s[0].betas[0] for s in segs]),
+            arr(ctypes.c_float, [s[0].betas[1] for s in segs]), arr(ctypes.c_float, [s[0].eps for s in segs]),
+            arr(vp, [s[1].data_ptr() if s[1] is not None else None for s in segs]),
+            arr(ctypes.c_float, [s[2] for s in segs]),
+            arr(vp, [p[0].data_ptr() if p else None for p in packs]),
+            arr(ctypes.c_int64, [p[1] if p else 0 for p in packs]), arr(ctypes.c_int64, [p[2] if p else 0 for p in packs]),
+            arr(ctypes.c_int32, [p[3] if p else 0 for p in packs]), L.ptr(work), st), "qs_mlp_sum_adam")
+
     # torch.optim.Adam state_dict format (checkpoint compatibility, MP:203-229)
     def state_dict(self):
         state = {}
@@ -771,16 +802,22 @@ class MAPPOAgent:
                                  L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), _stream()), "qs_ppo_heads")
-        tasks = []
-        self._ws_actor.backward(xa, self._dmean, tasks)
-        self._ws_critic.backward(xc, self._dv, tasks)
-        _flush_sums(tasks)
-        self._exchange(world)
+        ta, tc = [], []
+        self._ws_actor.backward(xa, self._dmean, ta)
+        self._ws_critic.backward(xc, self._dv, tc)
         gate = self._kl if self.target_kl > 0 else None
-        FlatBuffers.adam_multi([(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)],
-                               self._adam_work, packs=[self._ws_actor.pack_segment(self.actor_opt),
-                                                       self._ws_critic.pack_segment(self.critic_opt)],
-                               zero_grads=True)
+        segs = [(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)]
+        packs = [self._ws_actor.pack_segment(self.actor_opt), self._ws_critic.pack_segment(self.critic_opt)]
+        if world == 1 and not self._force_allreduce:
+            # nothing to exchange: the reductions feed Adam in the same launch; logstd's
+            # gradient (written by qs_ppo_heads) rides along as a one-row task
+            g = logstd.grad
+            ta.append((1, g.numel(), g, g, g.numel(), None, 0, None))
+            FlatBuffers.sum_adam(ta + tc, [0] * len(ta) + [1] * len(tc), segs, packs, self._adam_work)
+            return
+        _flush_sums(ta + tc)
+        self._exchange(world)
+        FlatBuffers.adam_multi(segs, self._adam_work, packs=packs, zero_grads=True)
 
     def _iteration(self, batch, acc):
         """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.
