@@ -642,6 +642,7 @@ class MAPPOAgent:
         self._force_allreduce = False   # tests: take the all-reduce path with one rank
         self.fused_heads = fused_heads   # qs_ppo_heads (False: the loss heads as plain torch ops)
         self.direct = kwargs.get('direct', True)   # the fused MLP kernels without autograd (_iteration_direct)
+        self.side_stream = kwargs.get('side_stream', True)   # critic backward beside the actor's (_iteration_direct)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
                                    share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
@@ -803,8 +804,22 @@ class MAPPOAgent:
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), _stream()), "qs_ppo_heads")
         ta, tc = [], []
-        self._ws_actor.backward(xa, self._dmean, ta)
-        self._ws_critic.backward(xc, self._dv, tc)
+        if self.side_stream:
+            # the critic's backward (a 128-workgroup kernel at 4 096 rows: half the
+            # CUs) and its weight-gradient GEMMs on a second stream, beside the
+            # actor's; joined before the reductions (graph capture records the fork
+            # and the join as dependency edges)
+            cur = torch.cuda.current_stream()
+            if getattr(self, '_side', None) is None or self._side.device != cur.device:
+                self._side = torch.cuda.Stream(device=cur.device)
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                self._ws_critic.backward(xc, self._dv, tc)
+            self._ws_actor.backward(xa, self._dmean, ta)
+            cur.wait_stream(self._side)
+        else:
+            self._ws_actor.backward(xa, self._dmean, ta)
+            self._ws_critic.backward(xc, self._dv, tc)
         gate = self._kl if self.target_kl > 0 else None
         segs = [(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)]
         packs = [self._ws_actor.pack_segment(self.actor_opt), self._ws_critic.pack_segment(self.critic_opt)]

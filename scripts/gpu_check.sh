@@ -18,5 +18,6 @@ if [ "${PROFILE:-1}" = "1" ]; then
     python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline > gpurun_out/prof_${TAG}.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof_${TAG}.log
   find gpurun_out/prof_${TAG} -name "*stats*" | head
+  rm -f gpurun_out/prof_${TAG}/*trace*.csv
 fi
 exit 0

@@ -181,6 +181,56 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
+def _hidden256_update(graphs, **variant):
+    """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
+    iteration's configuration) from fixed weights, data and permutations."""
+    from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
+    from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
+    from gym_pybullet_drones_amd.utils.spaces import Box
+    E, D, O, A, T = 32, 8, 27, 1, 8
+    obs_space = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O)))
+    act_space = Box(-np.ones((D, A)), np.ones((D, A)))
+    torch.manual_seed(1)
+    agent = MAPPOAgent(obs_space, act_space, hidden_dim=256, opt_epochs=2, mini_batch_size=T * E // 2,
+                       entropy_coef=0.005, use_graphs=graphs, device="cuda", **variant)
+    torch.manual_seed(2)
+    buf = MAPPOBuffer(obs_space, act_space, T, E, include_global_state=True, device="cuda")
+    buf.next_obs_slots.normal_()
+    buf.act.normal_()
+    with torch.no_grad():
+        d = agent.ac.actor.dist(buf.obs.reshape(-1, O))
+        buf.logp.copy_(d.log_prob(buf.act.reshape(-1, A)).reshape(T, E, D, 1)
+                       + 0.001 * torch.randn(T, E, D, 1, device="cuda"))
+    buf.ret_env.normal_()
+    buf.adv_env.normal_()
+    buf.t, buf.full = 0, True
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(5)
+    res = agent.update(buf, generator=gen)
+    torch.cuda.synchronize()
+    return agent, res
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_direct_update_side_stream_bit_identical(graphs):
+    """The critic backward on its own stream (side_stream) changes no bit of the
+    update; the direct iteration agrees with the autograd-driven fused one."""
+    a_side, r_side = _hidden256_update(graphs)
+    assert a_side._direct_ok()
+    a_one, r_one = _hidden256_update(graphs, side_stream=False)
+    assert torch.equal(a_side.actor_opt.flat, a_one.actor_opt.flat)
+    assert torch.equal(a_side.critic_opt.flat, a_one.critic_opt.flat)
+    assert torch.equal(a_side.actor_opt.exp_avg_sq, a_one.actor_opt.exp_avg_sq)
+    assert r_side == r_one
+    a_fused, r_fused = _hidden256_update(graphs, direct=False)
+    # (the fused path's critic, at 128 rows, is plain torch: ulp-level gradient
+    # differences, which Adam's normalised steps carry up to ~lr/60 per step; 4 steps)
+    torch.testing.assert_close(a_side.actor_opt.flat, a_fused.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
+    torch.testing.assert_close(a_side.critic_opt.flat, a_fused.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
+    for k in r_side:
+        assert r_side[k] == pytest.approx(r_fused[k], rel=1e-5, abs=1e-7)
+
+
 @pytest.mark.parametrize("graphs", [True, False])
 def test_mappo_train_step_and_checkpoint(graphs, tmp_path):
     from gym_pybullet_drones_amd.envs import MultiHoverAviary
