@@ -130,6 +130,14 @@ int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, cons
 int qs_mlp3_fwd_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
                      const float* pack, const float* b1, const float* b2, const float* W3, const float* b3, float* H1T,
                      float* H2T, float* out, void* stream);
+/* qs_mlp3_fwd over groups of G consecutive rows: row r of the batch is
+ * X[rows[r / G]·G + r % G] (K a multiple of G).  The actor's minibatch read
+ * straight from the rollout table [T·E·D][O] with rows = the sampled
+ * env-timesteps and G = num_agents (buffer.py:222-306's per-agent rows of the
+ * sampled (t, env) pairs); no gathered copy is written. */
+int qs_mlp3_fwd_group_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, int32_t G,
+                           const float* pack, const float* b1, const float* b2, const float* W3, const float* b3,
+                           float* H1T, float* H2T, float* out, void* stream);
 int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, const float* H1T, const float* H2T,
                 const float* pack, const float* W3, float* dZ2T, float* dZ1T, float* partA, float* partB,
                 void* stream);

@@ -674,12 +674,16 @@ __device__ __forceinline__ void m3_stream(M3Stream& S, int n, Body body) {
   M3Stream::sync();
 }
 
-template <int A>
+// GATHER: batch row r is X row rows[r / G]·G + r % G (the minibatch's agent
+// rows read straight from the rollout table, which may exceed a buffer
+// descriptor's 4-GB range: plain 64-bit loads)
+template <int A, bool GATHER = false>
 __global__ void __launch_bounds__(kM3Block) mlp3_fwd_kernel(long long K, int I, const float* __restrict__ X,
                                                             const float* __restrict__ pack, const float* __restrict__ b1,
                                                             const float* __restrict__ b2, const float* __restrict__ W3,
                                                             const float* __restrict__ b3, float* __restrict__ H1T,
-                                                            float* __restrict__ H2T, float* __restrict__ out) {
+                                                            float* __restrict__ H2T, float* __restrict__ out,
+                                                            const long long* __restrict__ rows = nullptr, int G = 1) {
   __shared__ float4 wbuf[2 * kM3ChunkF / 4];
   __shared__ float sb1[kM3N], sb2[kM3N], sw3[A * kM3N];   // biases and head weights, read in the epilogues
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
@@ -689,7 +693,9 @@ __global__ void __launch_bounds__(kM3Block) mlp3_fwd_kernel(long long K, int I, 
   for (int j = threadIdx.x; j < kM3N; j += kM3Block) { sb1[j] = b1[j]; sb2[j] = b2[j]; }
   for (int j = threadIdx.x; j < A * kM3N; j += kM3Block) sw3[j] = W3[j];
   // H1T / H2T may be NULL (inference): a zero-size descriptor drops every store
-  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, (size_t)K * I * 4),
+  const float* xrow = X;
+  if constexpr (GATHER) xrow = rv ? X + (rows[r / G] * G + r % G) * (long long)I : X;
+  const __amdgpu_buffer_rsrc_t xr = m3_rsrc(X, GATHER ? 0 : (size_t)K * I * 4),
                                h1r = m3_rsrc(H1T, H1T ? (size_t)K * kM3N * 4 : 0),
                                h2r = m3_rsrc(H2T, H2T ? (size_t)K * kM3N * 4 : 0);
   const unsigned xoff = rv ? (unsigned)(r * I * 4) : kM3OOB, roff = rv ? (unsigned)(r * 4) : kM3OOB;
@@ -708,7 +714,8 @@ __global__ void __launch_bounds__(kM3Block) mlp3_fwd_kernel(long long K, int I, 
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 2 * (4 * q + e) + h;
-        xb[e] = m3_ld(xr, k < I ? xoff + 4u * k : kM3OOB);
+        if constexpr (GATHER) xb[e] = rv && k < I ? xrow[k] : 0.f;
+        else xb[e] = m3_ld(xr, k < I ? xoff + 4u * k : kM3OOB);
       }
 #pragma unroll
       for (int mb = 0; mb < kM3NB; ++mb) {
@@ -1095,7 +1102,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
                                                               const float* __restrict__ b3, float* __restrict__ H1T,
                                                               float* __restrict__ H2T, float* __restrict__ out,
                                                               const long long* __restrict__ rows,
-                                                              float* __restrict__ Xg) {
+                                                              float* __restrict__ Xg, int G) {
   // LDS: the X tile during layer 1, then the H1ᵀ exchange
   extern __shared__ float lds[];   // m3w_lds_floats(Ip)
   __shared__ float hp[kM3WWaves][A][64];
@@ -1119,7 +1126,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
 #pragma unroll
   for (int j = 0; j < RPW; ++j) {
     const long long rr = r0 + w + kM3WWaves * j;
-    src[j] = rr < K ? (rows ? rows[rr] : rr) : -1;
+    src[j] = rr < K ? (rows ? rows[rr / G] * G + rr % G : rr) : -1;
   }
   for (int k0 = 0; k0 < Ip; k0 += 256) {
     float v[RPW][4];
@@ -1465,29 +1472,40 @@ int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* 
 }
 
 static int mlp3_fwd_launch(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
-                           const float* pack, const float* b1, const float* b2, const float* W3, const float* b3,
-                           float* H1T, float* H2T, float* out, void* stream, const char* name) {
+                           int32_t G, const float* pack, const float* b1, const float* b2, const float* W3,
+                           const float* b3, float* H1T, float* H2T, float* out, void* stream, const char* name) {
   if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !X || !pack ||
       !b1 || !b2 || !W3 || !b3 || (!H1T) != (!H2T) || !out)
     return fail(QS_E_INVALID, std::string(name) + ": bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
-  const bool wide = rows || m3_wide(K, I);   // the gathering form is the 8-wave kernel's
+  if (G < 1 || (G > 1 && Xg)) return fail(QS_E_INVALID, std::string(name) + ": bad group size");
+  // the row-gathering form with a gathered copy (G = 1) is the 8-wave kernel's
+  const bool wide = (rows && G == 1) || m3_wide(K, I);
   const unsigned grid = (unsigned)(wide ? (K + 31) / 32 : qs_mlp3_tiles(K, I));
   const unsigned lds = wide ? (unsigned)(m3w_lds_floats((I + 31) & ~31) * sizeof(float)) : 0u;
   const long long* rr = (const long long*)rows;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3Block), 0, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1, b2,
-                       W3, b3, H1T, H2T, out);
+                       W3, b3, H1T, H2T, out, rr, (int)G);
   };
   auto gow = [&](auto kern) {
     if (lds > 65536u) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3WBlock), lds, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1,
-                       b2, W3, b3, H1T, H2T, out, rr, Xg);
+                       b2, W3, b3, H1T, H2T, out, rr, Xg, (int)G);
   };
-  switch (A) {
-    case 1: wide ? gow(mlp3w_fwd_kernel<1>) : go(mlp3_fwd_kernel<1>); break;
-    case 2: wide ? gow(mlp3w_fwd_kernel<2>) : go(mlp3_fwd_kernel<2>); break;
-    case 3: wide ? gow(mlp3w_fwd_kernel<3>) : go(mlp3_fwd_kernel<3>); break;
-    default: wide ? gow(mlp3w_fwd_kernel<4>) : go(mlp3_fwd_kernel<4>); break;
+  if (rows && !wide) {
+    switch (A) {
+      case 1: go(mlp3_fwd_kernel<1, true>); break;
+      case 2: go(mlp3_fwd_kernel<2, true>); break;
+      case 3: go(mlp3_fwd_kernel<3, true>); break;
+      default: go(mlp3_fwd_kernel<4, true>); break;
+    }
+  } else {
+    switch (A) {
+      case 1: wide ? gow(mlp3w_fwd_kernel<1>) : go(mlp3_fwd_kernel<1>); break;
+      case 2: wide ? gow(mlp3w_fwd_kernel<2>) : go(mlp3_fwd_kernel<2>); break;
+      case 3: wide ? gow(mlp3w_fwd_kernel<3>) : go(mlp3_fwd_kernel<3>); break;
+      default: wide ? gow(mlp3w_fwd_kernel<4>) : go(mlp3_fwd_kernel<4>); break;
+    }
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string(name) + ": " + hipGetErrorString(e));
@@ -1495,14 +1513,23 @@ static int mlp3_fwd_launch(int64_t K, int32_t I, int32_t N, int32_t A, const flo
 
 int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const float* pack, const float* b1,
                 const float* b2, const float* W3, const float* b3, float* H1T, float* H2T, float* out, void* stream) {
-  return mlp3_fwd_launch(K, I, N, A, X, nullptr, nullptr, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd");
+  return mlp3_fwd_launch(K, I, N, A, X, nullptr, nullptr, 1, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd");
 }
 
 int qs_mlp3_fwd_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
                      const float* pack, const float* b1, const float* b2, const float* W3, const float* b3, float* H1T,
                      float* H2T, float* out, void* stream) {
   if (!rows) return fail(QS_E_INVALID, "qs_mlp3_fwd_rows: rows is NULL");
-  return mlp3_fwd_launch(K, I, N, A, X, rows, Xg, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd_rows");
+  return mlp3_fwd_launch(K, I, N, A, X, rows, Xg, 1, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd_rows");
+}
+
+int qs_mlp3_fwd_group_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, int32_t G,
+                           const float* pack, const float* b1, const float* b2, const float* W3, const float* b3,
+                           float* H1T, float* H2T, float* out, void* stream) {
+  if (!rows) return fail(QS_E_INVALID, "qs_mlp3_fwd_group_rows: rows is NULL");
+  if (G < 1 || K % G) return fail(QS_E_INVALID, "qs_mlp3_fwd_group_rows: K must be a multiple of G >= 1");
+  return mlp3_fwd_launch(K, I, N, A, X, rows, nullptr, G, pack, b1, b2, W3, b3, H1T, H2T, out, stream,
+                         "qs_mlp3_fwd_group_rows");
 }
 
 int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, const float* H1T, const float* H2T,

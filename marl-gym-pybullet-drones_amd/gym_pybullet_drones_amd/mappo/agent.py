@@ -265,15 +265,19 @@ class _M3Work:
         L.check(L.load().qs_mlp3_pack(self.I, 256, L.ptr(f0.weight), L.ptr(f1.weight), L.ptr(self.pack), _stream()),
                 "qs_mlp3_pack")
 
-    def forward(self, x, rows=None, xg=None):
+    def forward(self, x, rows=None, xg=None, group=1):
         """out = MLP(x) (x [K][I]); rows: x is the whole table and batch row r is
-        x[rows[r]] (gathered in the kernel, copied to xg)."""
+        x[rows[r]] (gathered in the kernel, copied to xg); group G > 1: batch row
+        r is x[rows[r // G]·G + r % G] (no copy)."""
         lib, st = L.load(), _stream()
         f0, f1, f2 = self.mlp.fcs
         tail = (L.ptr(self.pack), L.ptr(f0.bias), L.ptr(f1.bias), L.ptr(f2.weight), L.ptr(f2.bias), L.ptr(self.h1),
                 L.ptr(self.h2), L.ptr(self.out), st)
         if rows is None:
             L.check(lib.qs_mlp3_fwd(self.K, self.I, 256, self.A, L.ptr(x), *tail), "qs_mlp3_fwd")
+        elif group > 1:
+            L.check(lib.qs_mlp3_fwd_group_rows(self.K, self.I, 256, self.A, L.ptr(x), L.ptr(rows), int(group), *tail),
+                    "qs_mlp3_fwd_group_rows")
         else:
             L.check(lib.qs_mlp3_fwd_rows(self.K, self.I, 256, self.A, L.ptr(x), L.ptr(rows), L.ptr(xg), *tail),
                     "qs_mlp3_fwd_rows")
@@ -286,20 +290,26 @@ class _M3Work:
         return (self.pack, fb.offsets[ids.index(id(f0.weight))][0], fb.offsets[ids.index(id(f1.weight))][0], self.I)
 
     def _splitk(self, dst, a, b, b_rows_are_k, part, S):
-        """dst += a·bᵀ over K in S chunks (see _splitk_nt) into the preallocated partials."""
+        """a·bᵀ over K in S chunks (see _splitk_nt) into the preallocated partials;
+        S = 1: dst = a·bᵀ, one GEMM (the direct iteration's .grad views hold
+        nothing else: the single-rank qs_mlp_sum_adam never writes them, the
+        multi-rank Adam zeroes them)."""
         K = a.shape[1]
         bk = b.t() if b_rows_are_k else b
         if S == 1:
-            dst.addmm_(a, bk)
+            torch.mm(a, bk, out=dst)
             return None
         a3 = a.view(a.shape[0], S, K // S).transpose(0, 1)
         b3 = b.view(b.shape[0], S, K // S).permute(1, 2, 0) if b_rows_are_k else b.view(S, K // S, -1)
         torch.bmm(a3, b3, out=part)
         return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
 
-    def backward(self, x, dout, tasks):
+    def backward(self, x, dout, tasks, whole=None):
         """Gradients of the parameters' .grad views (+=); the fixed-order partial
-        sums are appended to `tasks` (one qs_mlp_sum_partials_multi launch later)."""
+        sums are appended to `tasks` (one qs_mlp_sum_partials_multi launch later).
+        A weight gradient small enough for one GEMM (S = 1) is accumulated into its
+        .grad view directly; that view is appended to `whole` (qs_mlp_sum_adam
+        must still visit it: every gradient element is one of its task columns)."""
         lib, st = L.load(), _stream()
         f0, f1, f2 = self.mlp.fcs
         N, A = 256, self.A
@@ -308,10 +318,12 @@ class _M3Work:
                                 L.ptr(self.part_b), st), "qs_mlp3_bwd")
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
-        for t in (self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2),    # dW2 = dZ2ᵀ·H1
-                  self._splitk(f0.weight.grad, self.dz1, x, False, self.pw1, self.S1)):        # dW1 = dZ1ᵀ·X
+        for dst, t in ((f1.weight.grad, self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2)),
+                       (f0.weight.grad, self._splitk(f0.weight.grad, self.dz1, x, False, self.pw1, self.S1))):
             if t is not None:
                 tasks.append(t)
+            elif whole is not None:
+                whole.append(dst)
 
 
 def _m3_ok(mlp, max_in=1024):
@@ -795,39 +807,51 @@ class MAPPOAgent:
         self._direct_setup(mb, D, O, A)
         T, E = rollouts.max_length, rollouts.batch_size
         xc, xa = self._xg, self._xg.view(mb * D, O)
-        v = self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
-        mean = self._ws_actor.forward(xa)
+        if self.side_stream:
+            # the critic forward (which also writes the gathered copy the weight
+            # gradients read) on the second stream, beside the actor forward, which
+            # reads its agent rows straight from the rollout table
+            cur = torch.cuda.current_stream()
+            if getattr(self, '_side', None) is None or self._side.device != cur.device:
+                self._side = torch.cuda.Stream(device=cur.device)
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                v = self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
+            mean = self._ws_actor.forward(rollouts.obs.reshape(T * E * D, O), rows=idx, group=D)
+            cur.wait_stream(self._side)
+        else:
+            v = self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
+            mean = self._ws_actor.forward(xa)
         logstd = self.ac.actor.logstd
         L.check(lib.qs_ppo_heads(mb, D, A, L.ptr(idx), L.ptr(mean), L.ptr(logstd), float(self.action_scale),
                                  L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
                                  L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), _stream()), "qs_ppo_heads")
-        ta, tc = [], []
+        ta, tc, wa, wc = [], [], [], []
         if self.side_stream:
             # the critic's backward (a 128-workgroup kernel at 4 096 rows: half the
             # CUs) and its weight-gradient GEMMs on a second stream, beside the
             # actor's; joined before the reductions (graph capture records the fork
             # and the join as dependency edges)
-            cur = torch.cuda.current_stream()
-            if getattr(self, '_side', None) is None or self._side.device != cur.device:
-                self._side = torch.cuda.Stream(device=cur.device)
             self._side.wait_stream(cur)
             with torch.cuda.stream(self._side):
-                self._ws_critic.backward(xc, self._dv, tc)
-            self._ws_actor.backward(xa, self._dmean, ta)
+                self._ws_critic.backward(xc, self._dv, tc, wc)
+            self._ws_actor.backward(xa, self._dmean, ta, wa)
             cur.wait_stream(self._side)
         else:
-            self._ws_actor.backward(xa, self._dmean, ta)
-            self._ws_critic.backward(xc, self._dv, tc)
+            self._ws_actor.backward(xa, self._dmean, ta, wa)
+            self._ws_critic.backward(xc, self._dv, tc, wc)
         gate = self._kl if self.target_kl > 0 else None
         segs = [(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)]
         packs = [self._ws_actor.pack_segment(self.actor_opt), self._ws_critic.pack_segment(self.critic_opt)]
         if world == 1 and not self._force_allreduce:
             # nothing to exchange: the reductions feed Adam in the same launch; logstd's
             # gradient (written by qs_ppo_heads) rides along as a one-row task
-            g = logstd.grad
-            ta.append((1, g.numel(), g, g, g.numel(), None, 0, None))
+            # (as do the weight gradients formed by one GEMM straight into .grad)
+            for g in [logstd.grad] + wa:
+                ta.append((1, g.numel(), g, g, g.numel(), None, 0, None))
+            tc += [(1, g.numel(), g, g, g.numel(), None, 0, None) for g in wc]
             FlatBuffers.sum_adam(ta + tc, [0] * len(ta) + [1] * len(tc), segs, packs, self._adam_work)
             return
         _flush_sums(ta + tc)

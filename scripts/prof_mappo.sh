@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-mappo}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
-  python3 bench.py --steps 32 --warmup 4 --no-cpu-baseline --mappo-iters 1 > gpurun_out/prof_${TAG}.log 2>&1
+  python3 bench.py --steps 32 --warmup 4 --no-cpu-baseline --mappo-iters 1 --configs 0 --pyb 0 --mappo-t32 0 ${BENCH_EXTRA:-} > gpurun_out/prof_${TAG}.log 2>&1
 rc=$?; echo "rc=$rc"
 python3 - <<PY
 import csv

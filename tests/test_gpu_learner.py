@@ -181,13 +181,13 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
-def _hidden256_update(graphs, **variant):
+def _hidden256_update(graphs, E=32, T=8, **variant):
     """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
     iteration's configuration) from fixed weights, data and permutations."""
     from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
     from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
     from gym_pybullet_drones_amd.utils.spaces import Box
-    E, D, O, A, T = 32, 8, 27, 1, 8
+    D, O, A = 8, 27, 1
     obs_space = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O)))
     act_space = Box(-np.ones((D, A)), np.ones((D, A)))
     torch.manual_seed(1)
@@ -211,18 +211,20 @@ def _hidden256_update(graphs, **variant):
     return agent, res
 
 
+@pytest.mark.parametrize("E,T", [(256, 16), (32, 8)])
 @pytest.mark.parametrize("graphs", [False, True])
-def test_direct_update_side_stream_bit_identical(graphs):
-    """The critic backward on its own stream (side_stream) changes no bit of the
-    update; the direct iteration agrees with the autograd-driven fused one."""
-    a_side, r_side = _hidden256_update(graphs)
+def test_direct_update_side_stream_bit_identical(graphs, E, T):
+    """The critic forward / backward on their own stream (side_stream) change no
+    bit of the update; the direct iteration agrees with the autograd-driven fused
+    one (E=256, T=16: the same kernels at 16 384 actor / 2 048 critic rows)."""
+    a_side, r_side = _hidden256_update(graphs, E, T)
     assert a_side._direct_ok()
-    a_one, r_one = _hidden256_update(graphs, side_stream=False)
+    a_one, r_one = _hidden256_update(graphs, E, T, side_stream=False)
     assert torch.equal(a_side.actor_opt.flat, a_one.actor_opt.flat)
     assert torch.equal(a_side.critic_opt.flat, a_one.critic_opt.flat)
     assert torch.equal(a_side.actor_opt.exp_avg_sq, a_one.actor_opt.exp_avg_sq)
     assert r_side == r_one
-    a_fused, r_fused = _hidden256_update(graphs, direct=False)
+    a_fused, r_fused = _hidden256_update(graphs, E, T, direct=False)
     # (the fused path's critic, at 128 rows, is plain torch: ulp-level gradient
     # differences, which Adam's normalised steps carry up to ~lr/60 per step; 4 steps)
     torch.testing.assert_close(a_side.actor_opt.flat, a_fused.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)

@@ -121,3 +121,56 @@ def test_fused_inference_forward(rows, din, A):
             out = fc(out)
             out = torch.tanh(out) if i < len(net.fcs) - 1 else out
     torch.testing.assert_close(got, out, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("envsteps,D,din,A", [(4096, 8, 27, 1), (256, 8, 27, 1), (600, 5, 72, 4)])
+def test_group_rows_forward_bit_identical(envsteps, D, din, A):
+    """qs_mlp3_fwd_group_rows (batch row r = table row rows[r // D]·D + r % D, the
+    actor's minibatch read from the rollout table) against qs_mlp3_fwd on the
+    gathered rows: the same kernel arithmetic, so identical bits (outputs and the
+    saved activations); 4-wave kernel at 32 768 rows, 8-wave kernel below."""
+    from gym_pybullet_drones_amd.mappo.agent import _M3Work
+    torch.manual_seed(3)
+    net = MLP(din, A, [256, 256], act='tanh').cuda()
+    for p in net.parameters():
+        p.grad = torch.zeros_like(p)
+    table = torch.randn(3 * envsteps * D, din, device="cuda")
+    idx = torch.randperm(3 * envsteps, device="cuda")[:envsteps]
+    rows = (idx[:, None] * D + torch.arange(D, device="cuda")).reshape(-1)
+    w_g, w_p = _M3Work(net, envsteps * D, "cuda"), _M3Work(net, envsteps * D, "cuda")
+    w_g.repack()
+    w_p.repack()
+    got = w_g.forward(table, rows=idx, group=D).clone()
+    want = w_p.forward(table[rows].contiguous()).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    assert torch.equal(w_g.h1, w_p.h1) and torch.equal(w_g.h2, w_p.h2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,din,A", [(128, 216, 1), (1024, 27, 1), (4096, 216, 1), (32768, 27, 1), (1000, 27, 2)])
+def test_m3work_matches_autograd(rows, din, A):
+    """The direct iteration's _M3Work forward + backward (+ the fixed-order sums)
+    against nn.Linear / torch.tanh autograd, including the small batches of the
+    8-wave kernels."""
+    from gym_pybullet_drones_amd.mappo.agent import _M3Work, _flush_sums
+    torch.manual_seed(4)
+    net = MLP(din, A, [256, 256], act='tanh').cuda()
+    ref = copy.deepcopy(net)
+    x = torch.randn(rows, din, device="cuda")
+    g = torch.randn(rows, A, device="cuda") / rows
+    want_out, want = _plain(ref, x, g)
+    for p in net.parameters():
+        p.grad = torch.zeros_like(p)
+    w = _M3Work(net, rows, "cuda")
+    w.repack()
+    out = w.forward(x).clone()
+    tasks = []
+    w.backward(x, g, tasks)
+    _flush_sums(tasks)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, want_out, rtol=1e-5, atol=1e-5)
+    for p, wg in zip(net.parameters(), want):
+        scale = float(wg.abs().max())
+        torch.testing.assert_close(p.grad, wg, rtol=1e-4, atol=1e-5 * scale + 1e-7)
