@@ -142,6 +142,19 @@ int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, c
                 const float* pack, const float* W3, float* dZ2T, float* dZ1T, float* partA, float* partB,
                 void* stream);
 
+/* Weight gradient of a layer over a long batch as fixed-order chunk partials
+ * (the dW = dYᵀ·X of nn.Linear's backward, neural_networks.py:18-54 under
+ * agent.py:702-772's loss.backward()): partial[c][n][m] = Σ_{b in chunk c}
+ * AT[n][b]·B(b, m) for c < C, chunk c = rows [c·K/C, (c+1)·K/C), with
+ * B(b, m) = B[b][m] (b_transposed 0: B [K][M], e.g. the layer input) or
+ * BT[m][b] (b_transposed 1: a transposed activation [M][K]).  AT [N][K].
+ * N % 32 == 0, K a multiple of 64·C, AT (and BT) 16-byte aligned.
+ * Sum the C partials with qs_mlp_sum_partials / qs_mlp_sum_adam.
+ * qs_mlp_wgrad_chunks: the C the learner uses (0: the shape is not taken). */
+int32_t qs_mlp_wgrad_chunks(int64_t K, int32_t N, int32_t M);
+int qs_mlp_wgrad(int64_t K, int32_t N, int32_t M, const float* AT, const float* B, int32_t b_transposed, int32_t C,
+                 float* partial, void* stream);
+
 /* qs_adam_gated followed by qs_adam_commit, in one launch: `work` is a device
  * uint32 counter, zero before the first call (the kernel leaves it zero). */
 int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step,

@@ -1047,6 +1047,74 @@ __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_adam_kernel(MlpSumTasks 
   }
 }
 
+// ---- weight gradients dW = Aᵀ·B over a long batch, as fixed-order partials.
+// partial[c][n][m] = Σ_{b in chunk c} AT[n][b]·B(b, m), B(b, m) = B[b][m]
+// (BT = false: the layer input X, row-major [K][M]) or BT[m][b] (BT = true: a
+// transposed activation [M][K]).  One wave per 32×32 output tile and batch
+// chunk: each MFMA step contracts two batch rows, a lane's float4 of AT (BT)
+// holds four consecutive rows of its n (m), so every operand load is one
+// 16-B vector per lane and no LDS or transpose is needed.  The chunk partials
+// are summed in chunk order by the minibatch's reduction (qs_mlp_sum_adam).
+constexpr int kWgWaves = 4;
+template <bool BT>
+__global__ void __launch_bounds__(64 * kWgWaves) mlp_wgrad_kernel(long long K, int N, int M, int R,
+                                                                  const float* __restrict__ AT,
+                                                                  const float* __restrict__ B,
+                                                                  float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c32 = lane & 31, hf = lane >> 5;
+  const int nb = blockIdx.x * kWgWaves + w;   // 32-row block of N
+  if (nb * 32 >= N) return;                   // (no barriers below)
+  const int mb = blockIdx.y, ch = blockIdx.z;
+  const int m = mb * 32 + c32;
+  const bool mv = m < M;
+  const long long b0 = (long long)ch * R;
+  const float* ap = AT + (size_t)(nb * 32 + c32) * K + b0 + 4 * hf;
+  const float* bp = BT ? B + (size_t)(mv ? m : 0) * K + b0 + 4 * hf : B + (size_t)(b0 + 4 * hf) * M + (mv ? m : 0);
+  // batches of U 8-row steps; the next batch's loads are issued before this
+  // batch's MFMAs (one wave per SIMD: the loads' latency must hide under MFMAs)
+  constexpr int U = 8;
+  f32x16 acc = f32x16{};
+  float4 av[2][U];
+  float bv[2][U][4];
+  auto load = [&](int buf, int r) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      av[buf][u] = *reinterpret_cast<const float4*>(ap + r + 8 * u);
+      if constexpr (BT) {
+        const float4 t = *reinterpret_cast<const float4*>(bp + r + 8 * u);
+        bv[buf][u][0] = t.x; bv[buf][u][1] = t.y; bv[buf][u][2] = t.z; bv[buf][u][3] = t.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[buf][u][q] = mv ? bp[(size_t)(r + 8 * u + q) * M] : 0.f;
+      }
+    }
+  };
+  auto mma = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[buf][u].x, mv ? bv[buf][u][0] : 0.f, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[buf][u].y, mv ? bv[buf][u][1] : 0.f, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[buf][u].z, mv ? bv[buf][u][2] : 0.f, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[buf][u].w, mv ? bv[buf][u][3] : 0.f, acc, 0, 0, 0);
+    }
+  };
+  // R is a multiple of 8·U (qs_mlp_wgrad): batches r = 0, 8U, … alternate buffers
+  load(0, 0);
+  for (int r = 0; r < R; r += 16 * U) {
+    if (r + 8 * U < R) load(1, r + 8 * U);
+    mma(0);
+    if (r + 16 * U < R) load(0, r + 16 * U);
+    if (r + 8 * U < R) mma(1);
+  }
+  if (!mv) return;
+  float* out = partial + (size_t)ch * N * M + m;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int n = nb * 32 + 8 * (j >> 2) + 4 * hf + (j & 3);
+    out[(size_t)n * M] = acc[j];
+  }
+}
+
 // ---- wide variant: one 32-row tile per workgroup of 8 waves, wave w owning
 // hidden block w (batches of < 16 384 rows, e.g. the critic's 4 096: 128 tiles
 // would leave most SIMDs idle with one wave per tile).  The waves exchange
@@ -1662,6 +1730,35 @@ int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, f
                      grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, gate_val, gate_thr, (unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_step: ") + hipGetErrorString(e));
+}
+
+// chunks of qs_mlp_wgrad: the most (a power of two, <= 256) that keeps every
+// chunk a multiple of 64 rows (the kernel's load batch)
+int32_t qs_mlp_wgrad_chunks(int64_t K, int32_t N, int32_t M) {
+  if (K <= 0 || N <= 0 || M <= 0) return 0;
+  const int64_t tiles = (int64_t)((N + 31) / 32) * ((M + 31) / 32);
+  int32_t C = 1;   // chunks of 64·k rows; <= 4 096 waves; partials <= 8 MiB
+  while (C < 256 && K % (128 * (int64_t)C) == 0 && tiles * C * 2 <= 4096 &&
+         (int64_t)2 * C * N * M * 4 <= (int64_t(8) << 20))
+    C *= 2;
+  return K % (64 * (int64_t)C) == 0 ? C : 0;
+}
+
+int qs_mlp_wgrad(int64_t K, int32_t N, int32_t M, const float* AT, const float* B, int32_t b_transposed, int32_t C,
+                 float* partial, void* stream) {
+  if (K <= 0 || N <= 0 || N % 32 || M <= 0 || C <= 0 || K % (64 * (int64_t)C) || !AT || !B || !partial ||
+      ((uintptr_t)AT & 15) || (K & 3) || (b_transposed && ((uintptr_t)B & 15)))
+    return fail(QS_E_INVALID, "qs_mlp_wgrad: bad argument (N % 32 == 0, K a multiple of 64·C, AT/BT 16-B aligned)");
+  const int R = (int)(K / C);
+  const dim3 grid((unsigned)((N / 32 + kWgWaves - 1) / kWgWaves), (unsigned)((M + 31) / 32), (unsigned)C);
+  if (b_transposed)
+    hipLaunchKernelGGL(mlp_wgrad_kernel<true>, grid, dim3(64 * kWgWaves), 0, (hipStream_t)stream, (long long)K, (int)N,
+                       (int)M, R, AT, B, partial);
+  else
+    hipLaunchKernelGGL(mlp_wgrad_kernel<false>, grid, dim3(64 * kWgWaves), 0, (hipStream_t)stream, (long long)K, (int)N,
+                       (int)M, R, AT, B, partial);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_wgrad: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -115,7 +115,12 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none): one workgroup each
     // Several workgroups per queued env when few are queued; the grid is sized
     // from E so a small shard does not pay 1024 empty workgroups every step.
-    const int rgrid = std::min(1024, std::max(64, P.E * 4));
+    static const int cap = [] {   // dev knob QS_RESET_GRID: the search grid's workgroup cap
+      const char* v = getenv("QS_RESET_GRID");
+      const int c = v ? atoi(v) : 0;
+      return c >= 64 && c <= 16384 ? c : 1024;
+    }();
+    const int rgrid = std::min(cap, std::max(64, P.E * 4));
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }

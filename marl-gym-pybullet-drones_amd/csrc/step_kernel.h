@@ -218,7 +218,7 @@ template <class T> struct Params {
   qs_episode_rec* log;    // [E][log_per_env] per-env rings of completed episodes
   int log_per_env;
   int* err;               // [1] reset search overflow flag
-  int* reset_queue;       // deferred MultiHover reset searches: [0] count, [1] blocks done, [2..] env ids; or NULL
+  int* reset_queue;       // deferred MultiHover reset searches: [0] count, [1] envs done, [2..] env ids; or NULL
   int stage_rows;         // obs rows staged in LDS per pass
   unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
   // per-step I/O
@@ -1646,7 +1646,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
 // ------------------------------------------------- deferred reset search
 // MultiHoverAviary.reset's rejection loop (MH:83-102) for the envs the step
-// kernel queued (try 0 rejected).  Queue (int32): [0] count, [1] blocks done,
+// kernel queued (try 0 rejected).  Queue (int32): [0] count, [1] envs written,
 // [2, 2+E) env ids, then per queue slot the best accepted try so far (win) and
 // the number of workgroups that stopped searching it.
 // B = gridDim / count workgroups share an env: workgroup j tests chunks
@@ -1655,7 +1655,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 // stops as well once the best try is below its next chunk.  When all B have
 // stopped every chunk below the best try has been tested, so it is the first
 // accepted try of the sequential loop; the last one to stop writes the env's
-// position, target and obs row.  The last workgroup of the launch empties the
+// position, target and obs row.  The last env written empties the
 // queue.  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
 constexpr int kResetMaxD = 8;
@@ -1751,13 +1751,17 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
           o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
         }
       }
-      if (threadIdx.x == 0) { qwin[idx] = kResetNone; qstop[idx] = 0; }   // ready for the next launch
+      if (threadIdx.x == 0) {
+        qwin[idx] = kResetNone; qstop[idx] = 0;   // ready for the next launch
+        // the last env to be written empties the queue: one same-address atomic
+        // per queued env, not per workgroup (1 024 of them serialise at L2 for
+        // ~16 µs).  Every workgroup with work read n before its env could finish;
+        // one that reads n after the reset had nothing to do.
+        if (atomicAdd(&rq[1], 1) == n - 1) { rq[0] = 0; rq[1] = 0; }
+      }
     }
     __syncthreads();
   }
-  __syncthreads();
-  // every workgroup read n before counting itself: the last one empties the queue
-  if (threadIdx.x == 0 && atomicAdd(&rq[1], 1) == G - 1) { rq[0] = 0; rq[1] = 0; }
 }
 
 }  // namespace qs

@@ -62,7 +62,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_gae", "qs_adam_gated", "qs_adam_commit", "qs_ppo_heads", "qs_ppo_heads_work_bytes",
            "qs_mlp_bias_tanh", "qs_mlp_bwd_blocks", "qs_mlp_tanh_bwd", "qs_mlp_sum_partials",
            "qs_mlp_sum_partials_multi", "qs_adam_step", "qs_mlp3_tiles", "qs_mlp3_pack_floats",
-           "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_adam_multi",
+           "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_mlp_wgrad", "qs_mlp_wgrad_chunks", "qs_adam_multi",
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_learner_last_error")
 
 _lib = None
@@ -120,6 +120,9 @@ def load():
     L.qs_mlp3_fwd.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 10
     L.qs_mlp3_bwd.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 10
     L.qs_mlp3_fwd_rows.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 12
+    L.qs_mlp_wgrad_chunks.argtypes = [i64, ctypes.c_int32, ctypes.c_int32]
+    L.qs_mlp_wgrad_chunks.restype = ctypes.c_int32
+    L.qs_mlp_wgrad.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp]
     L.qs_mlp3_fwd_group_rows.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                          ctypes.c_int32] + [vp] * 9
     L.qs_adam_multi_pack.argtypes = [ctypes.c_int32] + [vp] * 16 + [ctypes.c_int32, vp, vp]

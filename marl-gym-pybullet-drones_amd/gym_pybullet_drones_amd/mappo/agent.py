@@ -239,6 +239,10 @@ class _M3Work:
     included, is allocated once, so the captured graph never allocates and
     nothing is freed while the other stream may still use it."""
 
+    # weight gradients on qs_mlp_wgrad ('w1', 'w2'); default: split-K hipBLASLt GEMMs,
+    # measured faster at the bench's sizes (update 2 446 ms vs 2 781 with 'w1')
+    wgrad = ()
+
     def __init__(self, mlp, K, device):
         f0, f1, f2 = mlp.fcs
         lib = L.load()
@@ -252,11 +256,16 @@ class _M3Work:
         self.G = G
         self.part_a = torch.empty((G, 256 * (1 + self.A) + self.A), **f32)
         self.part_b = torch.empty((G, 256), **f32)
-        # split-K chunk counts of dW2 and dW1 (rows per chunk >= the _splitk_min_rows entry)
+        # dW1 = dZ1ᵀ·X (and dW2 = dZ2ᵀ·H1 when 'w2' is in wgrad): chunk partials of
+        # the MFMA weight-gradient kernel (qs_mlp_wgrad) where it takes the shape;
+        # otherwise split-K GEMMs (rows per chunk >= the _SPLITK_MIN_ROWS entry)
+        self.C2 = int(lib.qs_mlp_wgrad_chunks(K, 256, 256)) if 'w2' in self.wgrad else 0
+        self.C1 = int(lib.qs_mlp_wgrad_chunks(K, 256, self.I)) if 'w1' in self.wgrad else 0
         m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 1024), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
-        self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
-        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
-        self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 else None
+        self.S2 = self.C2 or _splitk_chunks(K, m2)
+        self.S1 = self.C1 or _splitk_chunks(K, m1)
+        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 or self.C2 else None
+        self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 or self.C1 else None
 
     def repack(self):
         """The pack image from the current weights (qs_adam_multi_pack keeps it
@@ -304,6 +313,13 @@ class _M3Work:
         torch.bmm(a3, b3, out=part)
         return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
 
+    def _wgrad(self, dst, at, b, b_transposed, part, C):
+        """Chunk partials of dst = atᵀ-contraction (qs_mlp_wgrad), summed later as one task."""
+        N, M = part.shape[1], part.shape[2]
+        L.check(L.load().qs_mlp_wgrad(self.K, N, M, L.ptr(at), L.ptr(b), int(b_transposed), int(C), L.ptr(part),
+                                      _stream()), "qs_mlp_wgrad")
+        return (C, N * M, part, dst, dst.numel(), None, 0, None)
+
     def backward(self, x, dout, tasks, whole=None):
         """Gradients of the parameters' .grad views (+=); the fixed-order partial
         sums are appended to `tasks` (one qs_mlp_sum_partials_multi launch later).
@@ -318,8 +334,11 @@ class _M3Work:
                                 L.ptr(self.part_b), st), "qs_mlp3_bwd")
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
-        for dst, t in ((f1.weight.grad, self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2)),
-                       (f0.weight.grad, self._splitk(f0.weight.grad, self.dz1, x, False, self.pw1, self.S1))):
+        w2 = (self._wgrad(f1.weight.grad, self.dz2, self.h1, 1, self.pw2, self.C2) if self.C2 else
+              self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2))    # dW2 = dZ2ᵀ·H1
+        w1 = (self._wgrad(f0.weight.grad, self.dz1, x, 0, self.pw1, self.C1) if self.C1 else
+              self._splitk(f0.weight.grad, self.dz1, x, False, self.pw1, self.S1))        # dW1 = dZ1ᵀ·X
+        for dst, t in ((f1.weight.grad, w2), (f0.weight.grad, w1)):
             if t is not None:
                 tasks.append(t)
             elif whole is not None:

@@ -149,12 +149,14 @@ def test_group_rows_forward_bit_identical(envsteps, D, din, A):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wgrad", [('w1',), ('w1', 'w2'), ()])
 @pytest.mark.parametrize("rows,din,A", [(128, 216, 1), (1024, 27, 1), (4096, 216, 1), (32768, 27, 1), (1000, 27, 2)])
-def test_m3work_matches_autograd(rows, din, A):
+def test_m3work_matches_autograd(rows, din, A, wgrad, monkeypatch):
     """The direct iteration's _M3Work forward + backward (+ the fixed-order sums)
     against nn.Linear / torch.tanh autograd, including the small batches of the
-    8-wave kernels."""
+    8-wave kernels, with the weight gradients on qs_mlp_wgrad or split-K GEMMs."""
     from gym_pybullet_drones_amd.mappo.agent import _M3Work, _flush_sums
+    monkeypatch.setattr(_M3Work, "wgrad", wgrad)
     torch.manual_seed(4)
     net = MLP(din, A, [256, 256], act='tanh').cuda()
     ref = copy.deepcopy(net)
@@ -174,3 +176,26 @@ def test_m3work_matches_autograd(rows, din, A):
     for p, wg in zip(net.parameters(), want):
         scale = float(wg.abs().max())
         torch.testing.assert_close(p.grad, wg, rtol=1e-4, atol=1e-5 * scale + 1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N,M,bt", [(32768, 256, 27, 0), (4096, 256, 216, 0), (32768, 256, 256, 1),
+                                      (4096, 256, 256, 1), (2048, 64, 40, 1), (128, 32, 5, 0)])
+def test_wgrad_kernel_matches_matmul(K, N, M, bt):
+    """qs_mlp_wgrad's chunk partials: each chunk equals AT[:, chunk]·B[chunk] (fp64
+    reference, fp32 tolerance) and their sum is the weight gradient."""
+    from gym_pybullet_drones_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(5)
+    at = torch.randn(N, K, device="cuda")
+    b = torch.randn(M, K, device="cuda") if bt else torch.randn(K, M, device="cuda")
+    bk = b.t() if bt else b
+    C = int(lib.qs_mlp_wgrad_chunks(K, N, M))
+    assert C >= 1
+    part = torch.full((C, N, M), float("nan"), device="cuda")
+    L.check(lib.qs_mlp_wgrad(K, N, M, L.ptr(at), L.ptr(b), bt, C, L.ptr(part), None), "qs_mlp_wgrad")
+    torch.cuda.synchronize()
+    R = K // C
+    want = torch.stack([at[:, c * R:(c + 1) * R].double() @ bk[c * R:(c + 1) * R].double() for c in range(C)])
+    torch.testing.assert_close(part.double(), want, rtol=1e-5, atol=1e-5 * R ** 0.5)
+    assert lib.qs_mlp_wgrad(K + 1, N, M, L.ptr(at), L.ptr(b), bt, C, L.ptr(part), None) != 0   # K not a multiple of 32·C
