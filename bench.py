@@ -87,6 +87,7 @@ def parse():
     p.add_argument("--mappo-iters", type=int, default=2, help="timed train steps (after one warm-up)")
     p.add_argument("--mappo-t32", type=int, default=1, help="also time the T=32 MAPPO leg (0 = skip)")
     p.add_argument("--wgrad", default="", help="learner weight gradients on the MFMA qs_mlp_wgrad kernel (w1,w2; '' = GEMMs)")
+    p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
     return p.parse_args()
 
@@ -280,8 +281,12 @@ def mappo_leg(args, rank, world, dist, T):
               rollout_steps=T, rollout_batch_size=E, opt_epochs=10,
               mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
     m.agent.side_stream = bool(args.side_stream)
-    from gym_pybullet_drones_amd.mappo.agent import _M3Work
+    from gym_pybullet_drones_amd.mappo.agent import _M3Work, _SPLITK_MIN_ROWS
     _M3Work.wgrad = tuple(w for w in args.wgrad.split(",") if w)
+    for item in filter(None, args.splitk.split(",")):   # "KxM=rows": split-K chunk rows of a weight gradient
+        km, rows = item.split("=")
+        k, mm = km.split("x")
+        _SPLITK_MIN_ROWS[(int(k), int(mm))] = int(rows)
     m.reset()
     m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
     m.time_phases = True

@@ -1650,14 +1650,16 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 // [2, 2+E) env ids, then per queue slot the best accepted try so far (win) and
 // the number of workgroups that stopped searching it.
 // B = gridDim / count workgroups share an env: workgroup j tests chunks
-// j, j+B, j+2B, … of 256 tries (thread t: try 1 + 256·chunk + t, a whole
-// candidate), publishes its smallest accepted try with atomicMin and stops, and
+// j, j+B, j+2B, … of 1 024 tries (thread t: tries 1 + 1024·chunk + t + 256·q,
+// q < 4, whole candidates; fewer chunk rounds and barriers per try), publishes its smallest accepted try with atomicMin and stops, and
 // stops as well once the best try is below its next chunk.  When all B have
 // stopped every chunk below the best try has been tested, so it is the first
 // accepted try of the sequential loop; the last one to stop writes the env's
 // position, target and obs row.  The last env written empties the
 // queue.  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
+constexpr int kResetPer = 4;                          // candidates per thread and chunk
+constexpr int kResetChunk = kResetBlock * kResetPer;  // tries per chunk
 constexpr int kResetMaxD = 8;
 constexpr int kResetNone = 0x7f7f7f7f;   // "no accepted try yet" (the queue's memset byte 0x7f)
 template <class T>
@@ -1686,7 +1688,7 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
     int best = kResetNone;   // the env's best try as of the previous chunk (workgroup-uniform)
     for (uint32_t c = (uint32_t)j;; c += (uint32_t)B) {
-      const uint32_t base = 1u + c * kResetBlock;
+      const uint32_t base = 1u + c * kResetChunk;
       // the exit must be workgroup-uniform (the body holds barriers); the best
       // try is read one chunk ahead — its ~µs atomic round trip runs under this
       // chunk's Philox work — and a stale value only delays the exit
@@ -1694,22 +1696,28 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       if (base >= kMaxResetTries) break;   // cap: tries >= kMaxResetTries are never accepted (as in-kernel)
       int next_best = 0;
       if (threadIdx.x == 0) next_best = __hip_atomic_load(&qwin[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t t = base + threadIdx.x;
-      bool ok = t < kMaxResetTries;
-      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
+      // kResetPer whole candidates per thread: tries base + threadIdx.x + 256·q
+      int mine = kResetNone;
 #pragma unroll
-      for (int d = 0; d < kResetMaxD; ++d) {
-        if (d < D && ok) {
-          reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
-          if (pz[d] < T(0.1)) ok = false;
+      for (int q = 0; q < kResetPer; ++q) {
+        const uint32_t t = base + threadIdx.x + (uint32_t)(kResetBlock * q);
+        bool ok = t < kMaxResetTries;
+        T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
 #pragma unroll
-          for (int i = 0; i < d; ++i)
-            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
+        for (int d = 0; d < kResetMaxD; ++d) {
+          if (d < D && ok) {
+            reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
+            if (pz[d] < T(0.1)) ok = false;
+#pragma unroll
+            for (int i = 0; i < d; ++i)
+              if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
+          }
         }
+        if (ok && (int)t < mine) mine = (int)t;
       }
       if (threadIdx.x == 0) s_win = kResetNone;
       __syncthreads();
-      if (ok) atomicMin(&s_win, (int)t);
+      if (mine != kResetNone) atomicMin(&s_win, mine);
       if (threadIdx.x == 0) s_best = next_best;
       __syncthreads();
       const int w = s_win;
