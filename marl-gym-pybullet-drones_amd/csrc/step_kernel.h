@@ -1650,15 +1650,18 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 // [2, 2+E) env ids, then per queue slot the best accepted try so far (win) and
 // the number of workgroups that stopped searching it.
 // B = gridDim / count workgroups share an env: workgroup j tests chunks
-// j, j+B, j+2B, … of 1 024 tries (thread t: tries 1 + 1024·chunk + t + 256·q,
-// q < 4, whole candidates; fewer chunk rounds and barriers per try), publishes its smallest accepted try with atomicMin and stops, and
+// j, j+B, j+2B, … of kResetChunk tries (thread t: tries 1 + kResetChunk·chunk +
+// t + 256·q, q < kResetPer, whole candidates), publishes its smallest accepted try with atomicMin and stops, and
 // stops as well once the best try is below its next chunk.  When all B have
 // stopped every chunk below the best try has been tested, so it is the first
 // accepted try of the sequential loop; the last one to stop writes the env's
 // position, target and obs row.  The last env written empties the
 // queue.  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
-constexpr int kResetPer = 4;                          // candidates per thread and chunk
+// candidates per thread and chunk: 4 (1 024-try chunks, a quarter of the
+// barrier rounds) measured slower on C2 (search 31 vs 23 µs): the longer
+// chunk delays every workgroup's exit test
+constexpr int kResetPer = 1;
 constexpr int kResetChunk = kResetBlock * kResetPer;  // tries per chunk
 constexpr int kResetMaxD = 8;
 constexpr int kResetNone = 0x7f7f7f7f;   // "no accepted try yet" (the queue's memset byte 0x7f)

@@ -9,3 +9,6 @@ for v in "" "32768x27=512" "32768x27=4096" "4096x216=256" "4096x216=4096" "32768
   python -c "
 import json; d=json.load(open('gpurun_out/sk_$i.json')); m=d['mappo']; print('[$v]', round(m['phase_ms']['update'],1), round(m['value']/1e6,3))"
 done
+timeout -k 10 300 python bench.py --mappo 0 --pyb 0 --no-cpu-baseline > gpurun_out/bc.json 2>gpurun_out/bc.err || exit 1
+python -c "
+import json; d=json.load(open('gpurun_out/bc.json')); c=d['configs']['C2']; print('C2', c['kernel_ms'], c['roofline_frac'])"
