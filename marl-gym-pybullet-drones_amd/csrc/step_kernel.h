@@ -436,14 +436,17 @@ template <class T> __device__ __forceinline__ bool too_close(T ax, T ay, T az, T
 // Reset search (MultiHoverAviary.reset rejection loop, MH:83-102), group g
 // (= threads g*D .. g*D+D-1) evaluates `try_idx` for its env.
 // Writes cand positions for its group and flags rejection in s.reject[g].
+// The candidate is also returned in c[3] (phase 1 keeps try 0's draw: the
+// usual winner, whose position is then not drawn a second time).
 template <class T>
 __device__ void eval_candidate(const Params<T>& P, Shared<T>& s, const T orig[3], int g, int d, uint32_t try_idx,
-                               uint32_t genv, uint32_t episode, bool active) {
+                               uint32_t genv, uint32_t episode, bool active, T* c = nullptr) {
   const int tid = threadIdx.x;
   if (active) {
     T px, py, pz;
     reset_candidate(P, orig, d, try_idx, genv, episode, px, py, pz);
     s.cand[tid][0] = px; s.cand[tid][1] = py; s.cand[tid][2] = pz;
+    if (c) { c[0] = px; c[1] = py; c[2] = pz; }
   }
   __syncthreads();
   if (active) {
@@ -1414,7 +1417,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // each env appends to its own ring, slot = its logged count mod log_per_env —
     // no atomic (a returned global slot made the finishing waves wait ~µs for it
     // and for all their outstanding stores, and they set the launch's tail).
+#ifdef QS_X_NOLOG
+    if (false) {
+#else
     if (dn) {
+#endif
       qs_episode_rec rec;
       rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
       P.log[(size_t)e * P.log_per_env + (unsigned)log_n % (unsigned)P.log_per_env] = rec;
@@ -1493,7 +1500,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   };
 
   QS_STAMP(4);
+#ifndef QS_X_NOTOBS
   if (valid && done_env && P.mode == MODE_STEP && P.tobs) write_obs_row(P.tobs + (size_t)a * O, obs_sc);
+#endif
 
   // ---------------- auto-reset (worker.step_env → env.reset)
   s.any = 0;
@@ -1503,12 +1512,14 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   if (s.any) {
     if (d == 0 && lenv < P.EPB) s.need[lenv] = do_reset ? 1 : 0;
     if (P.mode != MODE_RESET_ALL && do_reset) episode += 1;
-    T init[3];
+    T init[3] = {orig[0], orig[1], orig[2]};
     if constexpr (kHover) {
       // Phase 1: every group tries index 0 for its own env.
       if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
       __syncthreads();
-      eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset);
+#ifndef QS_X_NORESETDRAW
+      eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset, init);
+#endif
       if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
       __syncthreads();
       // Phase 2: for each still-rejected env, all groups search in parallel,
@@ -1556,10 +1567,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         if (tid == 0) s.need[k] = 2;   // resolved by phase 2 (win_try holds the index)
         __syncthreads();
       }
-      if (do_reset) {
-        uint32_t wt = (s.need[lenv] == 2) ? s.win_try[lenv] : 0u;
-        reset_candidate(P, orig, d, wt, genv, (uint32_t)episode, init[0], init[1], init[2]);
-      }
+      // try 0 accepted (the usual case): its draw is already in init (one Philox
+      // per drone less on the reset path, which sets the launch's tail)
+      if (do_reset && s.need[lenv] == 2)
+        reset_candidate(P, orig, d, s.win_try[lenv], genv, (uint32_t)episode, init[0], init[1], init[2]);
     } else {
       if (do_reset) { init[0] = orig[0]; init[1] = orig[1]; init[2] = orig[2]; }
     }
@@ -1634,7 +1645,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   if (!valid) return;
 
   // ---------------- store state of the envs that (auto-)reset
+#ifdef QS_X_NORESETSTORE
+  if (false) {
+#else
   if (do_reset) {
+#endif
     store_kin();
     if constexpr (kHover) {
 #pragma unroll

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libquadswarm.so")
+LIB_PATH = os.environ.get("QS_DEV_LIB") or os.path.join(_HERE, "lib", "libquadswarm.so")   # QS_DEV_LIB: dev variant builds
 
 QS_OK = 0
 TASK_MULTIHOVER, TASK_SPIRAL, TASK_FLOCK, TASK_MEETUP, TASK_LEADERFOLLOWER = 0, 1, 2, 3, 4
