@@ -181,7 +181,7 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
-def _hidden256_update(graphs, E=32, T=8, **variant):
+def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, **variant):
     """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
     iteration's configuration) from fixed weights, data and permutations."""
     from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
@@ -193,6 +193,7 @@ def _hidden256_update(graphs, E=32, T=8, **variant):
     torch.manual_seed(1)
     agent = MAPPOAgent(obs_space, act_space, hidden_dim=256, opt_epochs=2, mini_batch_size=T * E // 2,
                        entropy_coef=0.005, use_graphs=graphs, device="cuda", **variant)
+    agent._force_allreduce = force_allreduce
     torch.manual_seed(2)
     buf = MAPPOBuffer(obs_space, act_space, T, E, include_global_state=True, device="cuda")
     buf.next_obs_slots.normal_()
@@ -377,6 +378,35 @@ def test_update_graph_captures_the_allreduce():
         assert torch.equal(agents[0].critic_opt.flat, agents[1].critic_opt.flat)
         for k in ('policy_loss', 'value_loss', 'approx_kl'):
             assert res[0][k] == res[1][k]
+    finally:
+        if own:
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_direct_update_allreduce_path_bit_identical(graphs):
+    """The multi-rank form of the 256-wide direct iteration (what every rank of
+    `bench.py --gpus N` runs): partial sums into .grad, the gradient/approx_kl
+    all-reduce (RCCL, one rank, captured in the graph when graphs=True), then the
+    zeroing Adam — bit-identical to the one-rank fused sum+Adam launch, with the
+    critic on the second stream and at 16 384 / 256 actor rows."""
+    import socket
+    import torch.distributed as dist
+    own = not dist.is_initialized()
+    if own:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        for E, T in ((256, 16), (32, 8)):
+            a_one, r_one = _hidden256_update(graphs, E, T)
+            a_ar, r_ar = _hidden256_update(graphs, E, T, force_allreduce=True)
+            assert torch.equal(a_one.actor_opt.flat, a_ar.actor_opt.flat)
+            assert torch.equal(a_one.critic_opt.flat, a_ar.critic_opt.flat)
+            assert torch.equal(a_one.critic_opt.exp_avg_sq, a_ar.critic_opt.exp_avg_sq)
+            assert r_one == r_ar
     finally:
         if own:
             dist.destroy_process_group()
