@@ -89,6 +89,8 @@ def parse():
     p.add_argument("--wgrad", default="", help="learner weight gradients on the MFMA qs_mlp_wgrad kernel (w1,w2; '' = GEMMs)")
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
+    p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
+    p.add_argument("--dry-ms", type=float, default=2.0, help="--dry-run: ms per stand-in step of rank 0 (rank r: (1+r)x)")
     return p.parse_args()
 
 
@@ -107,6 +109,81 @@ def launch_ranks(n):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.run(cmd, env=env).returncode
+
+
+class Ranks:
+    """The bench's rank plumbing: the torchrun environment, the process group (RCCL;
+    gloo on CPU tensors for --dry-run), barrier + device-sync fences around a timed
+    window, and the MAX of a duration over ranks."""
+
+    def __init__(self, dry=False):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dry = dry
+        self.dist = None
+        if not dry:
+            torch.cuda.set_device(self.local)
+        if self.world > 1:
+            import torch.distributed as dist
+            if dry:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.dist = dist
+
+    def sync(self):
+        if not self.dry:
+            torch.cuda.synchronize()
+
+    def fence(self):
+        """Every rank's queued work done, then all ranks together."""
+        self.sync()
+        if self.dist:
+            self.dist.barrier()
+        self.sync()
+
+    def max(self, seconds):
+        if not self.dist:
+            return seconds
+        t = torch.tensor([seconds], dtype=torch.float64, device="cpu" if self.dry else "cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def dry_leg(args, ranks):
+    """--dry-run: the rank plumbing of a sim leg with no GPU (gloo, CPU).  Each
+    control step is a CPU stand-in that takes (1 + rank)·--dry-ms: the fences make
+    every rank's window hold the slowest rank's work, and the reported time is the
+    MAX of the ranks' windows (tests/test_bench_ranks.py checks both)."""
+    def busy(sec):
+        t_end = time.perf_counter() + sec
+        while time.perf_counter() < t_end:
+            pass
+    per_step = (1 + ranks.rank) * args.dry_ms * 1e-3
+    for _ in range(args.warmup):
+        busy(per_step)
+    ranks.fence()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        busy(per_step)
+    ranks.fence()
+    mine = time.perf_counter() - t0
+    every = [mine]
+    if ranks.dist:   # each rank's own window, reported beside the max
+        t = [torch.zeros(1, dtype=torch.float64) for _ in range(ranks.world)]
+        ranks.dist.all_gather(t, torch.tensor([mine], dtype=torch.float64))
+        every = [float(x) for x in t]
+    return every, ranks.max(mine)
+
+
+def _ppid(pid):
+    with open(f"/proc/{pid}/stat") as f:
+        return int(f.read().rsplit(")", 1)[1].split()[1])
 
 
 def cpu_baseline(args, seconds):
@@ -177,7 +254,7 @@ def stagger_episodes(sw, task):
     sw.set_state(L.STATE_ENV, env)
 
 
-def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D=None, act=None, aux=()):
+def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=None, aux=()):
     """The timed random-policy rollout: exactly `args.steps` control steps of E envs
     per rank, as replays of HIP graphs of step launches (one per rollout-buffer slot).
     Returns (agent-steps/s over all ranks, max-over-ranks seconds, mean step-kernel
@@ -190,7 +267,7 @@ def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D
     phys = {"dyn": Physics.DYN, "pyb": Physics.PYB, "pyb_dw": Physics.PYB_DW}[physics]
     layout = grid_layout(D) if (D >= 6 and task == "multihover") else None
     sw = QuadSwarm(task, num_envs=E, num_drones=D, act=act, precision=4, physics=phys, aux=aux,
-                   initial_xyzs=layout, env_offset=rank * E)
+                   initial_xyzs=layout, env_offset=ranks.rank * E)
     O, A = sw.obs_dim, sw.act_dim
     slots = max(1, min(args.slots, args.steps))
     obs_buf = torch.empty((slots, E, D, O), dtype=torch.float32, device=sw.device)
@@ -223,11 +300,14 @@ def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D
                 step(k)
         graphs.append((g, n))
     torch.cuda.synchronize()
+    # one untimed replay of each graph: a graph's first launch also uploads it to
+    # the device (at --steps 20 that upload was 2 µs of every timed step)
+    for g, _ in graphs:
+        g.replay()
+    torch.cuda.synchronize()
     plan = [graphs[0]] * n_full + ([graphs[-1]] if rem else [])
     _, ended0 = sw.episode_log(cap=0)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    ranks.fence()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     cur = torch.cuda.current_stream()
     t0 = time.perf_counter()
@@ -235,24 +315,18 @@ def sim_leg(args, rank, world, dist, physics="dyn", task="multihover", E=None, D
         a.record(cur)
         g.replay()
         b.record(cur)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    ranks.fence()
     elapsed = time.perf_counter() - t0
     # mean step-kernel duration on the launch stream: graph time / launches per graph
     kern_ms = float(sum(a.elapsed_time(b) for a, b in ev)) / args.steps
-    if dist:
-        t = torch.tensor([elapsed], device=sw.device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = ranks.max(elapsed)
     # sanity of the window: every reset succeeded, outputs finite, episodes ended in it
     assert sw.reset_error() == 0
     assert torch.isfinite(obs_buf).all()
     _, ended1 = sw.episode_log(cap=0)
     del graphs, plan
     sw.close()
-    return E * D * world * args.steps / elapsed, elapsed, kern_ms, args.steps, int(ended1 - ended0)
+    return E * D * ranks.world * args.steps / elapsed, elapsed, kern_ms, args.steps, int(ended1 - ended0)
 
 
 def mappo_flops(T, E, D, O, A, H=256, epochs=10):
@@ -267,7 +341,7 @@ def mappo_flops(T, E, D, O, A, H=256, epochs=10):
     return update, rollout
 
 
-def mappo_leg(args, rank, world, dist, T):
+def mappo_leg(args, ranks, T):
     """Full MAPPO train steps on the bench's C3 envs (learn_mappo.py:196-203 hyper-parameters,
     hidden 256, opt_epochs 10; minibatch scaled to the ~100x larger env batch)."""
     from gym_pybullet_drones_amd.envs import MultiHoverAviary
@@ -290,24 +364,15 @@ def mappo_leg(args, rank, world, dist, T):
     m.reset()
     m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
     m.time_phases = True
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    ranks.fence()
     phases = []
     t0 = time.perf_counter()
     for _ in range(args.mappo_iters):
         phases.append(m.train_step()['phase_ms'])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.mappo_iters
-    if dist:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    ranks.fence()
+    dt = ranks.max((time.perf_counter() - t0) / args.mappo_iters)
     O, A = m.obs_dim, m.agent.ac.act_dim
+    world = ranks.world
     graphed = world == 1 or m.agent.graph_collectives
     m.close()
     ph = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
@@ -357,30 +422,35 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ranks = Ranks(dry=args.dry_run)
+    world, rank = ranks.world, ranks.rank
+    if args.dry_run:
+        every, elapsed = dry_leg(args, ranks)
+        if rank == 0:
+            print(json.dumps({
+                "metric": METRIC + " [dry run: CPU stand-in steps, no GPU]", "value": args.steps * world / elapsed,
+                "unit": "stand-in steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": elapsed / args.steps * 1e3, "rank_ms_per_step": [e / args.steps * 1e3 for e in every],
+                "dry_run": {"pid": os.getpid(), "ppid": os.getppid(), "pppid": _ppid(os.getppid()),
+                            "backend": "gloo" if world > 1 else None}}), flush=True)
+        ranks.close()
+        return
     E, D = args.envs, args.drones
-    value, elapsed, kern_ms, steps, eps_done = sim_leg(args, rank, world, dist, "dyn")
+    value, elapsed, kern_ms, steps, eps_done = sim_leg(args, ranks, "dyn")
     nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
     pyb = None
     if args.pyb:   # the same rollout under Physics.PYB (the reference's training default)
-        pv, _, pk, _, _ = sim_leg(args, rank, world, dist, "pyb")
+        pv, _, pk, _, _ = sim_leg(args, ranks, "pyb")
         pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
                "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
-    mappo = mappo_leg(args, rank, world, dist, args.mappo_steps) if args.mappo else None
-    mappo32 = mappo_leg(args, rank, world, dist, 32) if (args.mappo and args.mappo_t32) else None
+    mappo = mappo_leg(args, ranks, args.mappo_steps) if args.mappo else None
+    mappo32 = mappo_leg(args, ranks, 32) if (args.mappo and args.mappo_t32) else None
     configs = None
     if args.configs and world == 1:   # the other BASELINE configs, one GPU each
         configs = {}
         for name, c in EXTRA_CONFIGS.items():
-            v, el, km, st, ne = sim_leg(args, rank, world, dist, c["physics"], c["task"], c["envs"], c["drones"],
+            v, el, km, st, ne = sim_leg(args, ranks, c["physics"], c["task"], c["envs"], c["drones"],
                                         c["act"], c["aux"])
             nb = c["bytes"] * c["envs"] * c["drones"]
             configs[name] = {"workload": c["label"], "value": v, "unit": "agent-steps/s", "kernel_ms": km,
@@ -416,8 +486,7 @@ def main():
             "configs": configs,
         }
         print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    ranks.close()
 
 
 if __name__ == "__main__":

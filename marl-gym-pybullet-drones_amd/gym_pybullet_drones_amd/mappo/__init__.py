@@ -13,8 +13,11 @@ def __getattr__(name):   # keep `import ...mappo` light (torch models load on fi
     if name in ('MAPPOBuffer', 'compute_returns_and_advantages', 'normalize_advantages'):
         from . import buffer
         return getattr(buffer, name)
+    if name in ('normalize_tensor', 'explained_variance'):
+        from . import utils
+        return getattr(utils, name)
     raise AttributeError(name)
 
 
 __all__ = ['MAPPO', 'MAPPOAgent', 'MAPPOActorCritic', 'MLPActor', 'MAPPOBuffer', 'compute_returns_and_advantages',
-           'normalize_advantages', 'MAPPO_CONFIG']
+           'normalize_advantages', 'MAPPO_CONFIG', 'normalize_tensor', 'explained_variance']

@@ -693,11 +693,15 @@ class MAPPOAgent:
         # update on CPU tensors); the optimizer step itself is the HIP kernel.
         na = sum(p.numel() for p in self.ac.actor.parameters())
         nc = sum(p.numel() for p in self.ac.critic.parameters())
-        # [actor grads | critic grads | approx_kl]: the one buffer every rank all-reduces
+        # [critic grads | actor grads | approx_kl]: the buffer the ranks all-reduce, in
+        # one piece (autograd paths) or as two buckets (the direct iteration): the
+        # critic's [:nc], reduced while the actor backward still runs, then the
+        # actor's with approx_kl [nc:]
         self._reduce_buf = torch.zeros(na + nc + 1, device=self.device)
-        self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[:na])
-        self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr, grad=self._reduce_buf[na:na + nc])
-        self._kl = self._reduce_buf[na + nc:]
+        self.critic_opt = FlatBuffers(self.ac.critic, self.critic_lr, grad=self._reduce_buf[:nc])
+        self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[nc:nc + na])
+        self._kl = self._reduce_buf[nc + na:]
+        self._critic_bucket, self._actor_bucket = self._reduce_buf[:nc], self._reduce_buf[nc:]
         self._adam_work = torch.zeros(4, dtype=torch.int32, device=self.device)   # qs_adam_multi's block counters
         if _dist_world() > 1:   # identical initial weights on every rank
             tdist.broadcast(self.actor_opt.flat, 0)
@@ -848,23 +852,36 @@ class MAPPOAgent:
                                  L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
                                  L.ptr(self._heads_work), _stream()), "qs_ppo_heads")
         ta, tc, wa, wc = [], [], [], []
+        multi = world > 1 or self._force_allreduce
         if self.side_stream:
             # the critic's backward (a 128-workgroup kernel at 4 096 rows: half the
             # CUs) and its weight-gradient GEMMs on a second stream, beside the
-            # actor's; joined before the reductions (graph capture records the fork
-            # and the join as dependency edges)
+            # actor's; with several ranks the critic bucket's partial sums and
+            # all-reduce follow on that stream, hidden behind the actor backward.
+            # Joined before Adam (graph capture records the fork and the join as
+            # dependency edges)
             self._side.wait_stream(cur)
             with torch.cuda.stream(self._side):
                 self._ws_critic.backward(xc, self._dv, tc, wc)
+                if multi:
+                    _flush_sums(tc)
+                    self._exchange_bucket(self._critic_bucket, world)
             self._ws_actor.backward(xa, self._dmean, ta, wa)
+            if multi:
+                _flush_sums(ta)
+                self._exchange_bucket(self._actor_bucket, world)
             cur.wait_stream(self._side)
         else:
             self._ws_actor.backward(xa, self._dmean, ta, wa)
             self._ws_critic.backward(xc, self._dv, tc, wc)
+            if multi:
+                _flush_sums(ta + tc)
+                self._exchange_bucket(self._critic_bucket, world)
+                self._exchange_bucket(self._actor_bucket, world)
         gate = self._kl if self.target_kl > 0 else None
         segs = [(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)]
         packs = [self._ws_actor.pack_segment(self.actor_opt), self._ws_critic.pack_segment(self.critic_opt)]
-        if world == 1 and not self._force_allreduce:
+        if not multi:
             # nothing to exchange: the reductions feed Adam in the same launch; logstd's
             # gradient (written by qs_ppo_heads) rides along as a one-row task
             # (as do the weight gradients formed by one GEMM straight into .grad)
@@ -873,8 +890,6 @@ class MAPPOAgent:
             tc += [(1, g.numel(), g, g, g.numel(), None, 0, None) for g in wc]
             FlatBuffers.sum_adam(ta + tc, [0] * len(ta) + [1] * len(tc), segs, packs, self._adam_work)
             return
-        _flush_sums(ta + tc)
-        self._exchange(world)
         FlatBuffers.adam_multi(segs, self._adam_work, packs=packs, zero_grads=True)
 
     def _iteration(self, batch, acc):
@@ -910,6 +925,13 @@ class MAPPOAgent:
         if world > 1 or self._force_allreduce:
             tdist.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
+
+    def _exchange_bucket(self, bucket, world):
+        """One bucket of the direct iteration's exchange (critic gradients, or actor
+        gradients + approx_kl): all-reduce (sum) and divide by the world size on
+        the current stream — the same values as the one-piece `_exchange`."""
+        tdist.all_reduce(bucket)
+        bucket.div_(world)
 
     def _actor_gate_open(self):
         """AG:731-734: the actor steps only if approx_kl <= 1.5·target_kl (a device

@@ -19,12 +19,13 @@ Reference quirks kept (SURVEY §7 hard-5): v placeholders are zeros, terminal_v
 is zero (TimeLimit.truncated is never set), rewards are the per-env mean tiled
 over agents, obs are normalised twice on a done when norm_obs=True and
 reference_compat=True (MP:804, 1037).
-termination_counts (MP:720-735) are counted from the kernel's per-drone reason
-bits at every terminal state: one count per (drone, reason), the categories of
-the reason strings (crash / flip / out_of_bounds, MH:225-238).  The reference's
-vectorised loop reads the post-auto-reset info, whose reasons MultiHover clears
-before building it (MH:109, subproc_vec_env.py:195-206), so its counts come out
-empty there; these are the counts it was written to collect.
+termination_counts (MP:720-735): under reference_compat they are empty, as in the
+reference's vectorised loop, which reads the post-auto-reset info whose reasons
+MultiHover clears before building it (MH:109, subproc_vec_env.py:195-206).  With
+reference_compat=False they are counted from the kernel's per-drone reason bits at
+every terminal state: one count per (drone, reason), the categories of the reason
+strings (crash / flip / out_of_bounds, MH:225-238) — the counts that loop was
+written to collect.
 """
 import os
 import random
@@ -426,9 +427,16 @@ class MAPPO:
         return results
 
     def _termination_counts(self):
-        '''MP:720-735: one count per (drone, reason) at the terminal states of this
-        rollout (this rank's envs), keyed like the reference's counter.'''
+        '''MP:720-735.  reference_compat (default): what the reference's vectorised
+        loop reports — an empty counter, because the worker auto-resets on done and
+        returns the reset's info (subproc_vec_env.py:195-205), whose
+        termination_reasons MultiHoverAviary.reset has just cleared (MH:109); no
+        device read.  reference_compat=False: the counts that loop was written to
+        collect, one per (drone, reason) at the terminal states of this rollout
+        (this rank's envs), keyed like the reference's counter.'''
         counts = defaultdict(int)
+        if getattr(self, 'reference_compat', True):
+            return counts
         bits = self._reasons
         per = torch.stack([((bits & b) != 0).sum() for b in (1, 2, 4)]).cpu().tolist()
         for name, n in zip(('crash', 'flip', 'out_of_bounds'), per):

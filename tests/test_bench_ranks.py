@@ -1,0 +1,49 @@
+"""bench.py's N-rank path on CPU (gloo): `--gpus 2` launches torchrun as a child
+process (never an exec), both ranks time the window between barrier fences, and
+rank 0 reports the MAX over ranks with n_gpus = 2 (bench.py Ranks / dry_leg)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(*extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), *extra], cwd=ROOT, env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    out, err = p.communicate(timeout=240)
+    assert p.returncode == 0, err[-3000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out   # rank 0 alone prints the line
+    return p.pid, json.loads(lines[0])
+
+
+def test_bench_two_ranks_max_over_ranks():
+    dry_ms, steps = 20.0, 6
+    launcher, line = _run_bench("--gpus", "2", "--dry-run", "--dry-ms", str(dry_ms), "--steps", str(steps),
+                                "--warmup", "1")
+    assert line["n_gpus"] == 2 and line["steps"] == steps
+    # rank 1's stand-in step takes 2 x dry_ms: the barrier fences make rank 0's own
+    # window hold rank 1's work too, and the reported time is the MAX of the windows
+    per_rank = line["rank_ms_per_step"]
+    assert len(per_rank) == 2
+    assert min(per_rank) >= 2 * dry_ms
+    assert line["ms_per_step"] == max(per_rank)
+    assert line["value"] == pytest.approx(2 / (line["ms_per_step"] * 1e-3), rel=1e-9)
+    # rank 0 runs in a torchrun child of the launcher: its grandparent is the
+    # process we started, and it is a different process (no exec)
+    d = line["dry_run"]
+    assert d["backend"] == "gloo"
+    assert d["pid"] != launcher and d["ppid"] != launcher
+    assert d["pppid"] == launcher
+
+
+def test_bench_one_rank_dry_run():
+    launcher, line = _run_bench("--dry-run", "--dry-ms", "1", "--steps", "3", "--warmup", "0")
+    assert line["n_gpus"] == 1 and line["dry_run"]["pid"] == launcher and line["dry_run"]["backend"] is None

@@ -11,9 +11,10 @@
   the gradient of the mean over the global minibatch.
 * MAPPOAgent's own update exchange (agent.py _local_grads → _exchange → KL gate,
   the code the GPU path runs, here on CPU tensors): identical initial weights on
-  every rank (broadcast), ONE all-reduce of the packed [actor grads | critic
-  grads | approx_kl] buffer, whose result is the single-process gradient of the
-  global minibatch, and the same KL-gate decision on every rank.
+  every rank (broadcast), ONE all-reduce of the packed [critic grads | actor
+  grads | approx_kl] buffer — or, as the direct iteration exchanges it, two
+  buckets (critic, then actor + approx_kl) — whose result is the single-process
+  gradient of the global minibatch, and the same KL-gate decision on every rank.
 """
 import os
 import socket
@@ -129,7 +130,7 @@ def _update_batch(n):
             "v": torch.zeros(n, D_, 1), "global_obs": obs.reshape(n, D_ * O_)}
 
 
-def _update_worker_for(target_kl):
+def _update_worker_for(target_kl, bucketed=False):
     def work(rank, world):
         agent = _agent(100 + rank, target_kl)   # different init per rank: the broadcast equalises it
         w0 = torch.cat([agent.actor_opt.flat, agent.critic_opt.flat]).clone()
@@ -146,7 +147,11 @@ def _update_worker_for(target_kl):
 
         dist.all_reduce = counting
         try:
-            agent._exchange(world)
+            if bucketed:   # _iteration_direct's order: the critic bucket, then actor + approx_kl
+                agent._exchange_bucket(agent._critic_bucket, world)
+                agent._exchange_bucket(agent._actor_bucket, world)
+            else:
+                agent._exchange(world)
         finally:
             dist.all_reduce = orig
         return w0.numpy(), agent._reduce_buf.clone().numpy(), agent._actor_gate_open(), calls
@@ -159,6 +164,14 @@ def _upd_worker_open(rank, world):
 
 def _upd_worker_kl(rank, world):
     return _update_worker_for(1e-4)(rank, world)
+
+
+def _upd_worker_buckets(rank, world):
+    return _update_worker_for(10.0, bucketed=True)(rank, world)
+
+
+def _upd_worker_buckets_kl(rank, world):
+    return _update_worker_for(1e-4, bucketed=True)(rank, world)
 
 
 # -------------------------------------------------------------------- tests
@@ -202,8 +215,10 @@ def test_gradient_average_equals_global_minibatch_gradient():
         np.testing.assert_allclose(r, want, rtol=1e-12, atol=1e-14)
 
 
-@pytest.mark.parametrize("worker,target_kl", [(_upd_worker_open, 10.0), (_upd_worker_kl, 1e-4)])
-def test_agent_update_exchange_two_ranks(worker, target_kl):
+@pytest.mark.parametrize("worker,target_kl,bucketed", [(_upd_worker_open, 10.0, False), (_upd_worker_kl, 1e-4, False),
+                                                      (_upd_worker_buckets, 10.0, True),
+                                                      (_upd_worker_buckets_kl, 1e-4, True)])
+def test_agent_update_exchange_two_ranks(worker, target_kl, bucketed):
     res = spawn(worker)
     single = _agent(100, target_kl)   # rank 0's weights (the broadcast source)
     acc = torch.zeros(4, dtype=torch.float64)
@@ -213,7 +228,9 @@ def test_agent_update_exchange_two_ranks(worker, target_kl):
     for w0, buf, gate, calls in res:
         np.testing.assert_array_equal(w0, res[0][0])   # identical initial weights on both ranks
         np.testing.assert_array_equal(w0, torch.cat([single.actor_opt.flat, single.critic_opt.flat]).numpy())
-        assert calls == [n]                              # one packed all-reduce per minibatch
+        nc = single.critic_opt.n
+        # one packed all-reduce per minibatch, or the two buckets in the direct iteration's order
+        assert calls == ([nc, n - nc] if bucketed else [n])
         np.testing.assert_allclose(buf, want, rtol=2e-5, atol=1e-7)   # = the global-minibatch gradient and KL
         assert gate == single._actor_gate_open()
     assert res[0][2] == res[1][2]

@@ -386,10 +386,12 @@ def test_update_graph_captures_the_allreduce():
 @pytest.mark.parametrize("graphs", [False, True])
 def test_direct_update_allreduce_path_bit_identical(graphs):
     """The multi-rank form of the 256-wide direct iteration (what every rank of
-    `bench.py --gpus N` runs): partial sums into .grad, the gradient/approx_kl
-    all-reduce (RCCL, one rank, captured in the graph when graphs=True), then the
-    zeroing Adam — bit-identical to the one-rank fused sum+Adam launch, with the
-    critic on the second stream and at 16 384 / 256 actor rows."""
+    `bench.py --gpus N` runs): partial sums into .grad, the exchange as two RCCL
+    all-reduce buckets (one rank; captured in the graph when graphs=True) — the
+    critic's on the second stream right after its backward, overlapping the actor
+    backward, then the actor's with approx_kl — and the zeroing Adam: bit-identical
+    to the one-rank fused sum+Adam launch, at 16 384 / 256 actor rows, with the
+    critic on the second stream and on one stream."""
     import socket
     import torch.distributed as dist
     own = not dist.is_initialized()
@@ -400,9 +402,9 @@ def test_direct_update_allreduce_path_bit_identical(graphs):
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                 device_id=torch.device("cuda", torch.cuda.current_device()))
     try:
-        for E, T in ((256, 16), (32, 8)):
+        for E, T, side in ((256, 16, True), (32, 8, True), (256, 16, False)):
             a_one, r_one = _hidden256_update(graphs, E, T)
-            a_ar, r_ar = _hidden256_update(graphs, E, T, force_allreduce=True)
+            a_ar, r_ar = _hidden256_update(graphs, E, T, force_allreduce=True, side_stream=side)
             assert torch.equal(a_one.actor_opt.flat, a_ar.actor_opt.flat)
             assert torch.equal(a_one.critic_opt.flat, a_ar.critic_opt.flat)
             assert torch.equal(a_one.critic_opt.exp_avg_sq, a_ar.critic_opt.exp_avg_sq)

@@ -1,0 +1,263 @@
+"""One whole MAPPO.train_step against a plain restatement of the reference's
+glue, driven by the same device actions.
+
+The restatement follows gym_pybullet_drones/mappo/mappo.py:647-1184 literally,
+on host numpy / plain torch:
+  * the rollout through the vector-env surface (`env.step(act)` → obs, rew (E,),
+    done, {'n': infos}; MP:712-717) of a second SwarmVecEnv built from the same
+    spec and seed, fed the actions the trainer sampled;
+  * reward tiling to (E, D, 1) (MP:758-772), mask = 1 − done tiled (MP:808-815),
+    terminal_v from infos carrying TimeLimit.truncated (never set: zeros,
+    MP:821-841), global_obs = the concatenated agent obs (MP:857-864, 583-617),
+    v = 0 placeholders (AG:389-415);
+  * the last value of the final obs from the critic, tiled over agents
+    (MP:1050-1067, 1118-1133);
+  * GAE per (env, agent) sequence in float64 (buffer.py:428-614), advantage
+    normalisation with the unbiased std over (T, E, D, 1) (buffer.py:666-695);
+  * opt_epochs × minibatch PPO update with torch.optim.Adam (agent.py:702-772),
+    over the same minibatch permutations.
+Compared: rollout tensors exactly (obs, actions, rewards, masks), the rollout
+log-probabilities and last value to fp32 kernel tolerance, returns / advantages
+to 1e-12, the update's loss statistics to 1e-4 relative and the weights to the
+Adam tolerance used throughout tests/test_gpu_learner.py (lr/60 per step).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+E, D, T, H = 64, 8, 16, 256
+MB, EPOCHS = 128, 2
+ACTOR_LR, CRITIC_LR = 3e-4, 1e-3
+
+
+def _plain_mlp(mlp):
+    """neural_networks.py:18-54 as plain torch layers with the trainer's weights."""
+    f0, f1, f2 = mlp.fcs
+    net = nn.Sequential(nn.Linear(f0.in_features, H), nn.Tanh(), nn.Linear(H, H), nn.Tanh(),
+                        nn.Linear(H, f2.out_features)).cuda()
+    with torch.no_grad():
+        for dst, src in zip((net[0], net[2], net[4]), (f0, f1, f2)):
+            dst.weight.copy_(src.weight)
+            dst.bias.copy_(src.bias)
+    return net
+
+
+def _stagger(swarm, T_win):
+    """Put the envs' episode clocks near their truncation step (242), so that
+    every env of the window's later half is truncated inside it (done → mask 0,
+    auto-reset obs) — the same clocks on both simulators."""
+    from gym_pybullet_drones_amd import _lib as L
+    env = swarm.get_state(L.STATE_ENV).clone()
+    phase = (242 - 1 - (torch.arange(swarm.num_envs, device=env.device) % (2 * T_win))).to(torch.int32)
+    env[L.E_STEP_COUNTER] = phase * swarm.substeps
+    env[L.E_EP_LEN] = phase
+    swarm.set_state(L.STATE_ENV, env)
+
+
+def _ref_gae(rews, vals, masks, terminal_vals, last_val, gamma, lam):
+    """buffer.py:428-614, the multi-agent branch: one backward recursion per
+    (env, agent) sequence, float64."""
+    Tn, N, Dn, _ = rews.shape
+    rets = np.zeros((Tn, N, Dn, 1))
+    advs = np.zeros((Tn, N, Dn, 1))
+    for b in range(N):
+        for a in range(Dn):
+            r, v, m, tv = rews[:, b, a, 0], vals[:, b, a, 0], masks[:, b, a, 0], terminal_vals[:, b, a, 0]
+            lv = last_val[b, a, 0]
+            v_ext = np.concatenate([v, [lv]])
+            ret, adv = lv, 0.0
+            for i in reversed(range(Tn)):
+                ra = r[i] + gamma * tv[i]
+                ret = ra + gamma * m[i] * ret
+                td = ra + gamma * m[i] * v_ext[i + 1] - v[i]
+                adv = adv * lam * gamma * m[i] + td
+                rets[i, b, a, 0] = ret
+                advs[i, b, a, 0] = adv
+    return rets, advs
+
+
+def test_train_step_matches_reference_restatement(tmp_path):
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.envs.swarm import grid_layout
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
+    from gym_pybullet_drones_amd.vec_env import SwarmVecEnv
+
+    env_func = lambda seed=0, **kw: MultiHoverAviary(num_drones=D, act=ActionType.ONE_D_PID, physics=Physics.DYN,
+                                                     initial_xyzs=grid_layout(D))
+    m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=H, rollout_batch_size=E,
+              rollout_steps=T, mini_batch_size=MB, opt_epochs=EPOCHS, actor_lr=ACTOR_LR, critic_lr=CRITIC_LR)
+    m.reset()
+    _stagger(m.env.venv.swarm, T)
+    obs0 = m.obs.clone()
+    O, A = m.obs_dim, m.agent.ac.act_dim
+    actor = _plain_mlp(m.agent.ac.actor.pi_net)
+    logstd = nn.Parameter(m.agent.ac.actor.logstd.detach().clone())
+    critic = _plain_mlp(m.agent.ac.critic.v_net)
+    w_init = [actor[i].weight.detach().clone() for i in (0, 2, 4)]
+
+    # --- record what the trainer hands to GAE and to the update
+    rec = {}
+    rollouts = m._buffer()
+    inner_gae = rollouts.compute_returns_and_advantages
+
+    def gae_spy(last_val, **kw):
+        rec['last_val'] = torch.as_tensor(last_val).detach().clone()
+        rec['gae_kw'] = dict(kw)
+        return inner_gae(last_val, **kw)
+
+    rollouts.compute_returns_and_advantages = gae_spy
+    inner_update = m.agent.update
+
+    def update_spy(r, device='cuda', generator=None):
+        for k in ('obs', 'act', 'logp', 'rew', 'mask', 'v', 'terminal_v', 'ret', 'adv', 'global_obs'):
+            rec[k] = getattr(r, k).detach().clone()
+        g = torch.Generator(device='cuda')
+        g.manual_seed(1234)
+        return inner_update(r, device, generator=g)
+
+    m.agent.update = update_spy
+    res = m.train_step()
+    torch.cuda.synchronize()
+    assert dict(res['termination_counts']) == {}   # reference_compat: the reference's vectorised loop logs {}
+
+    # --- the reference loop (MP:647-1044) on a second simulator, same spec and seed
+    venv = SwarmVecEnv(num_envs=E, seed=0, device=m.device, **env_func().vec_spec())
+    obs, _ = venv.reset()
+    _stagger(venv.swarm, T)
+    np.testing.assert_array_equal(obs, obs0.cpu().numpy())
+    buf = {k: [] for k in ('obs', 'act', 'rew', 'mask', 'v', 'terminal_v', 'global_obs')}
+    acts = rec['act'].cpu().numpy()
+    n_done = 0
+    for t in range(T):
+        act = acts[t]                                                  # the trainer's sample
+        next_obs, rew, done, info = venv.step(act)
+        assert rew.shape == (E,) and done.shape == (E,)
+        rew_t = np.tile(rew[:, None, None], (1, D, 1))                 # MP:758-762
+        mask = np.tile((1 - done.astype(float))[:, None, None], (1, D, 1))   # MP:808-813
+        terminal_v = np.zeros((E, D, 1))                               # MP:821-841
+        for inf in info['n']:
+            assert not inf.get('terminal_info', {}).get('TimeLimit.truncated', False)
+        buf['obs'].append(obs)
+        buf['global_obs'].append(obs.reshape(E, D * O))               # MP:583-617
+        buf['act'].append(act)
+        buf['rew'].append(rew_t.astype(np.float32))                   # stored float32 (buffer.py:176)
+        buf['mask'].append(mask.astype(np.float32))
+        buf['v'].append(np.zeros((E, D, 1), np.float32))
+        buf['terminal_v'].append(terminal_v.astype(np.float32))
+        n_done += int(done.sum())
+        obs = next_obs
+    venv.close()
+    assert n_done > 0, "the window must hold truncations (mask zeros)"
+    ref = {k: np.stack(v) for k, v in buf.items()}
+
+    # rollout tensors: exact
+    for k in ('obs', 'global_obs', 'act', 'rew', 'mask', 'v', 'terminal_v'):
+        np.testing.assert_array_equal(rec[k].cpu().numpy(), ref[k], err_msg=k)
+    np.testing.assert_array_equal(m.obs.cpu().numpy(), obs)   # the obs the next train_step starts from
+
+    # the rollout's log-probabilities (fused inference actor vs plain torch) and the
+    # samples' standardised residuals (the actions are N(mean, exp(logstd)) draws)
+    with torch.no_grad():
+        o = torch.as_tensor(ref['obs']).cuda()
+        mean = actor(o)
+        dist = torch.distributions.Normal(mean, logstd.exp())
+        a = rec['act']
+        logp = dist.log_prob(a).sum(-1, keepdim=True)
+        torch.testing.assert_close(rec['logp'], logp, rtol=1e-5, atol=5e-5)
+        z = ((a - mean) / logstd.exp()).double()
+        assert abs(float(z.mean())) < 5 / np.sqrt(z.numel())
+        assert abs(float(z.std()) - 1) < 5 / np.sqrt(2 * z.numel())
+        # last value (MP:1050-1067): critic of the final obs, tiled over agents
+        lv = critic(torch.as_tensor(obs.reshape(E, D * O)).cuda())
+        last_val = np.tile(lv.cpu().numpy()[:, None, :], (1, D, 1))
+    assert rec['gae_kw'] == {'gamma': m.gamma, 'use_gae': m.use_gae, 'gae_lambda': m.gae_lambda}
+    got_lv = rec['last_val'].reshape(E, -1, 1).expand(E, D, 1).cpu().numpy()
+    np.testing.assert_allclose(got_lv, last_val, rtol=1e-5, atol=2e-6)
+
+    # GAE in float64 from the trainer's own last value: 1e-12
+    rets, advs = _ref_gae(ref['rew'], ref['v'], ref['mask'], ref['terminal_v'], got_lv.astype(np.float32),
+                          m.gamma, m.gae_lambda)
+    np.testing.assert_allclose(rec['ret'].cpu().numpy(), rets, rtol=1e-12, atol=1e-12)
+    adv_t = torch.as_tensor(advs)
+    adv_n = (adv_t - adv_t.mean()) / (adv_t.std() + 1e-8)               # buffer.py:676-685
+    np.testing.assert_allclose(rec['adv'].cpu().numpy(), adv_n.numpy(), rtol=1e-12, atol=1e-12)
+
+    # --- the update (AG:702-772) over the same permutations, torch.optim.Adam
+    aopt = torch.optim.Adam(list(actor.parameters()) + [logstd], ACTOR_LR)
+    copt = torch.optim.Adam(critic.parameters(), CRITIC_LR)
+    cuda = lambda x, dt=None: torch.as_tensor(x, device='cuda', dtype=dt)
+    flat = lambda x: x.reshape(T * E, *x.shape[2:])
+    data = {'obs': flat(cuda(ref['obs'])), 'act': flat(cuda(ref['act'])), 'logp': flat(rec['logp']),
+            'adv': flat(adv_n.cuda()), 'ret': flat(cuda(rets)), 'global_obs': flat(cuda(ref['global_obs']))}
+    g = torch.Generator(device='cuda')
+    g.manual_seed(1234)
+    n_mb = T * E // MB
+    stats = {k: [] for k in ('policy_loss', 'value_loss', 'entropy_loss', 'approx_kl')}
+    steps_taken = 0
+    for _ in range(EPOCHS):
+        perm = torch.randperm(T * E, device='cuda', generator=g)
+        acc = dict.fromkeys(stats, 0.0)
+        for i in range(n_mb):
+            b = {k: v[perm[i * MB:(i + 1) * MB]] for k, v in data.items()}
+            dist = torch.distributions.Normal(actor(b['obs']), logstd.exp())
+            lp = dist.log_prob(b['act']).sum(-1, keepdim=True)
+            ratio = torch.exp(lp - b['logp'])
+            pl = -torch.min(ratio * b['adv'], torch.clamp(ratio, 0.8, 1.2) * b['adv']).mean()
+            el = -dist.entropy().sum(-1).mean()
+            kl = (b['logp'] - lp).mean()
+            if kl <= 1.5 * m.target_kl:
+                aopt.zero_grad()
+                (pl + m.entropy_coef * el).backward()
+                aopt.step()
+                steps_taken += 1
+            v = critic(b['global_obs'])
+            ret = b['ret'].mean(dim=1, keepdim=True).view(v.shape)
+            vl = 0.5 * (v - ret).pow(2).mean()
+            copt.zero_grad()
+            vl.backward()
+            copt.step()
+            for k, x in zip(stats, (pl, vl, el, kl)):
+                acc[k] += float(x)
+        for k in stats:
+            stats[k].append(acc[k] / n_mb)
+    assert steps_taken > 0
+    for k in stats:
+        assert res[k] == pytest.approx(float(np.mean(stats[k])), rel=1e-4, abs=1e-7), k
+    n_steps = EPOCHS * n_mb
+    got_actor = m.agent.ac.actor.pi_net.fcs
+    for (dst, src) in zip((actor[0], actor[2], actor[4]), got_actor):
+        torch.testing.assert_close(src.weight, dst.weight, rtol=0, atol=n_steps * ACTOR_LR / 60)
+        torch.testing.assert_close(src.bias, dst.bias, rtol=0, atol=n_steps * ACTOR_LR / 60)
+    torch.testing.assert_close(m.agent.ac.actor.logstd, logstd, rtol=0, atol=n_steps * ACTOR_LR / 60)
+    for (dst, src) in zip((critic[0], critic[2], critic[4]), m.agent.ac.critic.v_net.fcs):
+        torch.testing.assert_close(src.weight, dst.weight, rtol=0, atol=n_steps * CRITIC_LR / 60)
+        torch.testing.assert_close(src.bias, dst.bias, rtol=0, atol=n_steps * CRITIC_LR / 60)
+    # the typical deviation is far below that bound: Adam's steps agree, not just stay bounded
+    dev = torch.cat([(s.weight - d.weight).abs().flatten() for d, s in zip((actor[0], actor[2], actor[4]),
+                                                                           got_actor)])
+    moved = torch.cat([(d.weight - w0).abs().flatten() for d, w0 in zip((actor[0], actor[2], actor[4]), w_init)])
+    assert float(dev.median()) < 1e-2 * float(moved.median()), (float(dev.median()), float(moved.median()))
+    m.close()
+
+
+def test_train_step_termination_counts_without_reference_compat(tmp_path):
+    """reference_compat=False: the counts the reference's MP:720-735 loop was
+    written to collect — one per (drone, reason) at this rollout's terminal states."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    env_func = lambda seed=0, **kw: MultiHoverAviary(num_drones=4, act=ActionType.RPM)
+    m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=64, rollout_batch_size=32,
+              rollout_steps=40, mini_batch_size=64, opt_epochs=1, reference_compat=False)
+    m.reset()
+    res = m.train_step()
+    counts = dict(res['termination_counts'])
+    bits = m._reasons.cpu().numpy()
+    want = {name: int(((bits & b) != 0).sum()) for name, b in (('crash', 1), ('flip', 2), ('out_of_bounds', 4))}
+    assert counts == {k: v for k, v in want.items() if v}
+    assert sum(counts.values()) > 0   # random RPM actions end episodes within 40 steps
+    m.close()

@@ -1,23 +1,56 @@
 """Host-side trainer logic that needs no GPU."""
 import numpy as np
+import pytest
 import torch
 
 
+def _holder(bits, reference_compat):
+    holder = type("H", (), {})()
+    holder._reasons = torch.as_tensor(bits)
+    holder.reference_compat = reference_compat
+    return holder
+
+
 def test_termination_counts_from_reason_bits():
-    """MAPPO._termination_counts: one count per (drone, reason) at the terminal
-    states of a rollout, under the reference counter's keys (mappo.py:720-735:
-    'crashed' -> crash, 'flipped' -> flip, 'out of bounds' -> out_of_bounds)."""
+    """MAPPO._termination_counts with reference_compat=False: one count per
+    (drone, reason) at the terminal states of a rollout, under the reference
+    counter's keys (mappo.py:720-735: 'crashed' -> crash, 'flipped' -> flip,
+    'out of bounds' -> out_of_bounds)."""
     from gym_pybullet_drones_amd.mappo.mappo import MAPPO
     rng = np.random.default_rng(0)
     T, E, D = 7, 5, 3
     bits = rng.integers(0, 8, size=(T, E, D)).astype(np.uint8)
     bits[rng.random((T, E)) < 0.7] = 0   # most envs do not end at a step
-    holder = type("H", (), {})()
-    holder._reasons = torch.as_tensor(bits)
-    got = MAPPO._termination_counts(holder)
+    got = MAPPO._termination_counts(_holder(bits, False))
     want = {}
     for b in bits.reshape(-1):
         for name, mask in (("crash", 1), ("flip", 2), ("out_of_bounds", 4)):
             if b & mask:
                 want[name] = want.get(name, 0) + 1
     assert dict(got) == want
+
+
+def test_termination_counts_reference_compat_is_empty():
+    """reference_compat: the reference's vectorised loop reads the info of the
+    auto-reset (subproc_vec_env.py:195-205), whose termination_reasons
+    MultiHoverAviary.reset has cleared (MH:109), so its counter stays empty."""
+    from gym_pybullet_drones_amd.mappo.mappo import MAPPO
+    bits = np.full((3, 4, 2), 7, dtype=np.uint8)
+    assert dict(MAPPO._termination_counts(_holder(bits, True))) == {}
+
+
+def test_mappo_utils_match_their_definitions():
+    """mappo/utils.py:6-13: normalize_tensor and explained_variance (re-exported
+    from the package like the reference's module)."""
+    from gym_pybullet_drones_amd.mappo import explained_variance, normalize_tensor
+    rng = np.random.default_rng(3)
+    x = rng.normal(2.0, 3.0, size=(50, 4))
+    got = normalize_tensor(torch.as_tensor(x)).numpy()
+    np.testing.assert_allclose(got, (x - x.mean()) / (x.std(ddof=1) + 1e-8), rtol=1e-12)
+    np.testing.assert_allclose(normalize_tensor(x).numpy(), got, rtol=0)   # numpy input
+    y = rng.normal(size=200)
+    yp = y + 0.1 * rng.normal(size=200)
+    ev = float(explained_variance(torch.as_tensor(yp), torch.as_tensor(y)))
+    assert ev == pytest.approx(1 - np.var(y - yp, ddof=1) / np.var(y, ddof=1), rel=1e-12)
+    with pytest.raises(AssertionError):
+        explained_variance(torch.zeros(2, 2), torch.zeros(2, 2))
