@@ -17,6 +17,8 @@
  *     bias / weight-gradient reductions (torch autograd kernels)   qs_mlp_sum_partials
  *   the same MLP at hidden 256, forward and backward fused on     qs_mlp3_fwd,
  *     MFMA (nn.Linear + torch.tanh autograd in the reference)      qs_mlp3_bwd
+ *   the actor's forward, policy loss and backward of a minibatch  qs_mlp3f_actor,
+ *     (agent.py:602-640, 728-734)                                  qs_value_head
  *
  * All pointers are device pointers; every call is asynchronous on `stream`
  * (hipStream_t as void*) and contains no host synchronisation, so it can be
@@ -154,6 +156,43 @@ int qs_mlp3_bwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* dout, c
 int32_t qs_mlp_wgrad_chunks(int64_t K, int32_t N, int32_t M);
 int qs_mlp_wgrad(int64_t K, int32_t N, int32_t M, const float* AT, const float* B, int32_t b_transposed, int32_t C,
                  float* partial, void* stream);
+
+/* The shared actor's whole minibatch step in one launch (MLPActor AG:87-148
+ * forward, compute_policy_loss AG:602-640, and the backward of
+ * (policy_loss + ent_coef·entropy_loss) down to every actor parameter —
+ * loss.backward() at AG:733): 16-row tiles on the f32 MFMA, activations kept
+ * in registers from the first layer to the last gradient (learner.hip).
+ * Rows: K = mb·D agent rows, row r = agent r % D of env-timestep idx[r / D]
+ * of the rollout table X [·][D][I] (I <= 128); act / logp_old / adv indexed
+ * as in qs_ppo_heads; logstd, action scale, clip, ent_coef as there.
+ * qs_mlp3f_pack: W1 [256][I], W2 [256][256] → pack[qs_mlp3f_pack_floats(I)]
+ *   (W1f | W2f | W2b in 16x16x4 MFMA-step order); qs_adam_multi_pack /
+ *   qs_mlp_sum_adam keep it current when pack_I carries QS_PACK_F16.
+ * qs_mlp3f_actor writes: Xa [K][I] the gathered inputs; H1T, dZ2T, dZ1T
+ *   [256][K] (H1ᵀ = tanh(W1·Xᵀ + b1), dZ2ᵀ, dZ1ᵀ: dW2 = dZ2ᵀ·H1, dW1 =
+ *   dZ1ᵀ·Xa); per workgroup g < qs_mlp3f_tiles(K) (128 rows) the partial
+ *   rows partA[g][256 + 256·A + A] = [Σ dZ2 | Σ dout_a·H2 | Σ dout_a] and
+ *   partB[g][256] = Σ dZ1; and, from the last workgroup, in workgroup order
+ *   (as qs_ppo_heads): dlogstd[A], kl_out[0] = approx_kl, acc[0] += policy,
+ *   acc[2] += entropy, acc[3] += approx_kl (acc[1], the value loss, is
+ *   qs_value_head's).  mean_out [K][A] (may be NULL): the actor output.
+ * work: qs_mlp3f_work_bytes(K) bytes, zeroed once before the first call. */
+#define QS_PACK_F16 (1 << 16)
+int32_t qs_mlp3f_tiles(int64_t K);
+int64_t qs_mlp3f_pack_floats(int32_t I);
+int64_t qs_mlp3f_work_bytes(int64_t K);
+int qs_mlp3f_pack(int32_t I, const float* W1, const float* W2, float* pack, void* stream);
+int qs_mlp3f_actor(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, const int64_t* idx, const float* pack,
+                   const float* b1, const float* b2, const float* W3, const float* b3, const float* logstd,
+                   float action_scale, const float* act, const float* logp_old, const double* adv, float clip,
+                   float ent_coef, float* Xa, float* H1T, float* dZ2T, float* dZ1T, float* partA, float* partB,
+                   float* dlogstd, float* kl_out, double* acc, void* work, float* mean_out, void* stream);
+
+/* The value half of qs_ppo_heads (compute_value_loss AG:642-683, centralized,
+ * unclipped): dv[i] = (v[i] − mean_d ret)/mb and acc[1] += 0.5·mean_i (v −
+ * mean_d ret)², the same arithmetic and order.  work: qs_ppo_heads_work_bytes. */
+int qs_value_head(int32_t mb, int32_t D, const int64_t* idx, const double* ret, const float* v, float* dv,
+                  double* acc, void* work, void* stream);
 
 /* qs_adam_gated followed by qs_adam_commit, in one launch: `work` is a device
  * uint32 counter, zero before the first call (the kernel leaves it zero). */

@@ -30,31 +30,37 @@ namespace {
 thread_local std::string g_err;
 int fail(int code, const std::string& m) { g_err = m; return code; }
 
+// The recurrence in float32, as the reference evaluates it: its arrays are
+// float32 (buffer.py:346-362) and under its pinned numpy 2.2.6 (NEP 50) a
+// float32 scalar op with a Python float (γ, λ) stays float32 with the Python
+// float rounded to float32 first, so every line of buffer.py:590-612 is a
+// float32 operation in source order (no FMA: -ffp-contract=off).  The results
+// are stored to the reference's float64 arrays exactly.
 __global__ void gae_kernel(int T, long long N, const float* __restrict__ rews, const float* __restrict__ vals,
                            const float* __restrict__ masks, const float* __restrict__ tvals,
                            const float* __restrict__ last_val, double gamma, double lam, int use_gae,
                            double* __restrict__ rets, double* __restrict__ advs) {
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  const double lv = (double)last_val[n];
-  double ret = lv, adv = 0.0, vnext = lv;
+  const float g = (float)gamma, lm = (float)lam;
+  const float lv = last_val[n];
+  float ret = lv, adv = 0.0f, vnext = lv;
 #pragma unroll 4
   for (int t = T - 1; t >= 0; --t) {
     const long long k = (long long)t * N + n;
-    const double r = (double)rews[k];
-    const double m = (double)masks[k];
-    const double v = vals ? (double)vals[k] : 0.0;
-    const double tv = tvals ? (double)tvals[k] : 0.0;
-    const double ra = r + gamma * tv;                       // buffer.py:593
-    ret = ra + gamma * m * ret;                             // buffer.py:602
+    const float r = rews[k], m = masks[k];
+    const float v = vals ? vals[k] : 0.0f;
+    const float tv = tvals ? tvals[k] : 0.0f;
+    const float ra = r + g * tv;                            // buffer.py:593
+    ret = ra + (g * m) * ret;                               // buffer.py:602
     if (use_gae) {
-      const double td = ra + gamma * m * vnext - v;         // buffer.py:608
-      adv = adv * lam * gamma * m + td;                     // buffer.py:609
+      const float td = (ra + (g * m) * vnext) - v;          // buffer.py:608
+      adv = ((adv * lm) * g) * m + td;                      // buffer.py:609
     } else {
       adv = ret - v;                                        // buffer.py:606
     }
-    rets[k] = ret;
-    advs[k] = adv;
+    rets[k] = (double)ret;
+    advs[k] = (double)adv;
     vnext = v;
   }
 }
@@ -135,7 +141,7 @@ __device__ __forceinline__ void block_sum_n(double (&x)[NV], double (*lds)[NV]) 
 
 // A (actions per agent) is a template value: the per-action arrays stay in
 // registers (a run-time A put them in scratch memory and cost ~70 µs a launch).
-template <int A>
+template <int A, bool POLICY = true>
 __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
     int mb, int D, const long long* __restrict__ idx, const float* __restrict__ mean,
     const float* __restrict__ logstd, float scale, const float* __restrict__ act, const float* __restrict__ logp_old,
@@ -157,7 +163,7 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
   const double G = -1.0 / (double)R;  // d(-mean(min(...)))/d min_r
   double sums[kHeadsSums] = {0, 0, 0, 0, 0, 0, 0};
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < R) {
+  if (POLICY && r < R) {
     const int i = r / D, d = r - i * D;
     const long long g = idx[i];
     const float* x = act + ((size_t)g * D + d) * A;
@@ -219,6 +225,10 @@ __global__ void __launch_bounds__(kHeadsBlock) ppo_heads_kernel(
   block_sum_n<kHeadsSums>(tot, ldsn);
   if (threadIdx.x != 0) return;
   *count = 0;   // ready for the next launch (graph replay)
+  if constexpr (!POLICY) {   // qs_value_head: the value loss only
+    acc[1] += 0.5 * (tot[2] / (double)mb);
+    return;
+  }
   float ent = 0.0f;   // Normal.entropy summed over A: 0.5 + 0.5·log(2π) + log(scale)
 #pragma unroll
   for (int a = 0; a < A; ++a) ent = a == 0 ? (0.5f + lc) + lsd[a] : ent + ((0.5f + lc) + lsd[a]);
@@ -882,6 +892,471 @@ __global__ void __launch_bounds__(kM3Block) mlp3_bwd_kernel(long long K, const f
 }
 
 
+// ---------------------------------------------------------------- fused actor
+// One launch per PPO minibatch for the shared actor (MLPActor AG:87-148 with
+// the PPO policy loss AG:602-640): forward, the per-row loss head and the
+// backward of every 16-row tile, with the activations of a tile kept in
+// registers from the first layer to the last gradient.
+//
+// Tiles of 16 batch rows on v_mfma_f32_16x16x4_f32, activations transposed
+// (hidden × rows): lane (g, j) of a wave (j = lane & 15, g = lane >> 4) holds
+// hidden units 16·b + 4g + r (r = 0..3) of row j in the C registers of block b.
+// Those registers are exactly the B operand of the next contraction over the
+// hidden index (step (b, r): lane group g supplies hidden 16b + 4g + r), so
+// tanh(Z1ᵀ) feeds layer 2, H2ᵀ feeds the head and dZ2ᵀ feeds dH1ᵀ = W2ᵀ·dZ2ᵀ
+// without an LDS round trip.  A wave holds H1ᵀ (64 VGPRs) and H2ᵀ → dZ2ᵀ (64)
+// of its tile: under 256 registers, so two waves share each SIMD — one wave's
+// epilogues, loss head and barrier waits hide behind the other's MFMAs.
+//
+// A workgroup = 8 waves = 128 rows.  The weights (packed in MFMA-step order by
+// qs_mlp3f_pack: W1f, W2f, W2b) stream through a double-buffered 32-KB LDS
+// window shared by the 8 waves.  The loss head is ppo_heads_kernel's
+// arithmetic per row; per-row inputs are read by index (the minibatch's
+// env-timesteps, D agent rows each, straight from the rollout table).
+// Outputs: H1ᵀ, dZ2ᵀ, dZ1ᵀ [256][K] (the weight-gradient GEMMs' operands),
+// the gathered inputs Xa [K][I], per-workgroup partial rows of the bias / head
+// gradients, and — from the last workgroup, in workgroup order — approx_kl,
+// d logstd and the loss statistics.
+constexpr int kFWaves = 8;
+constexpr int kFBlock = 64 * kFWaves;
+constexpr int kFChunkF = 8192;                   // floats per streamed chunk (32 KB)
+constexpr int kFStage = kFChunkF / 4 / kFBlock;  // float4 per thread per chunk
+constexpr int kFMaxIp = 128;                     // input width bound of the fused path
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ constexpr int f16_ip(int I) { return (I + 31) & ~31; }
+__host__ __device__ constexpr long long f16_w1_floats(int Ip) { return 256LL * Ip; }
+constexpr long long kFW2Floats = 65536;
+
+// pack positions: W1f[q][ob][lane][e] = W1[16ob + (l&15)][16q + 4e + (l>>4)],
+// W2f[ob][ib][lane][e] = W2[16ob + (l&15)][16ib + 4(l>>4) + e],
+// W2b[ib][ob][lane][e] = W2[16ob + 4(l>>4) + e][16ib + (l&15)]
+__device__ __forceinline__ long long f16_pos_w1(int m, int k) {
+  const int kk = k & 15;
+  return ((((long long)(k >> 4) * 16 + (m >> 4)) * 64 + 16 * (kk & 3) + (m & 15)) << 2) + (kk >> 2);
+}
+__device__ __forceinline__ long long f16_pos_w2f(int m, int n) {
+  const int nn = n & 15;
+  return ((((long long)(m >> 4) * 16 + (n >> 4)) * 64 + 16 * (nn >> 2) + (m & 15)) << 2) + (nn & 3);
+}
+__device__ __forceinline__ long long f16_pos_w2b(int m, int n) {
+  const int mm = m & 15;
+  return ((((long long)(n >> 4) * 16 + (m >> 4)) * 64 + 16 * (mm >> 2) + (n & 15)) << 2) + (mm & 3);
+}
+
+__global__ void mlp3f_pack_kernel(int I, const float* __restrict__ W1, const float* __restrict__ W2,
+                                  float* __restrict__ pack) {
+  const int Ip = f16_ip(I);
+  const long long n1 = f16_w1_floats(Ip);
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n1 + 2 * kFW2Floats;
+       t += (long long)gridDim.x * blockDim.x) {
+    // invert the position maps: t → (lane, e, block indices)
+    const long long u = t < n1 ? t : (t < n1 + kFW2Floats ? t - n1 : t - n1 - kFW2Floats);
+    const int e = (int)(u & 3), l = (int)((u >> 2) & 63), jl = l & 15, gl = l >> 4;
+    const long long rest = u >> 8;
+    float v;
+    if (t < n1) {
+      const int ob = (int)(rest & 15), q = (int)(rest >> 4), k = 16 * q + 4 * e + gl;
+      v = k < I ? W1[(size_t)(16 * ob + jl) * I + k] : 0.f;
+    } else {
+      const int lo = (int)(rest & 15), hi = (int)(rest >> 4);
+      if (t < n1 + kFW2Floats) v = W2[(size_t)(16 * hi + jl) * kM3N + 16 * lo + 4 * gl + e];   // W2f: hi = ob, lo = ib
+      else v = W2[(size_t)(16 * lo + 4 * gl + e) * kM3N + 16 * hi + jl];                      // W2b: hi = ib, lo = ob
+    }
+    pack[t] = v;
+  }
+}
+
+// Double-buffered chunk stream for 512 threads (M3Stream's scheme: register
+// staging one chunk ahead of its LDS write, LDS-only fences around the barrier)
+struct FStream {
+  const float4* src;
+  float4* buf;   // LDS [2][kFChunkF / 4]
+  float4 st[kFStage];
+  __device__ __forceinline__ void load(int c) {
+#pragma unroll
+    for (int j = 0; j < kFStage; ++j) st[j] = src[(size_t)c * (kFChunkF / 4) + j * kFBlock + threadIdx.x];
+  }
+  __device__ __forceinline__ void store(int c) {
+#pragma unroll
+    for (int j = 0; j < kFStage; ++j) buf[(c & 1) * (kFChunkF / 4) + j * kFBlock + threadIdx.x] = st[j];
+  }
+};
+
+// n chunks (compile-time N when > 0, so that the body's register arrays are
+// indexed statically); body(c, chunk window)
+template <int N, class Body>
+__device__ __forceinline__ void f_stream(FStream& S, int n, Body body) {
+  if constexpr (N > 0) n = N;
+  S.load(0);
+  S.store(0);
+  if (n > 1) S.load(1);
+  auto step = [&](int c) {
+    M3Stream::sync();
+    if (c + 1 < n) S.store(c + 1);
+    if (c + 2 < n) S.load(c + 2);
+    body(c, S.buf + (c & 1) * (kFChunkF / 4));
+  };
+  if constexpr (N > 0) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) step(c);
+  } else {
+#pragma unroll 1
+    for (int c = 0; c < n; ++c) step(c);
+  }
+  M3Stream::sync();
+}
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Σ over the 16 lanes of each lane group of 64 values v[x] (x = 4·b + r):
+// a transposing butterfly (60 shuffles); lane j of the group ends with the
+// sums of x = 4j + i in out[i], i = 0..3.  Fixed order: replays are bit-identical.
+template <class V>
+__device__ __forceinline__ void f_lane_sum64(V v, float (&out)[4]) {
+  const int j = threadIdx.x & 15;
+  float a[32], b[16], c[8];
+  {
+    const bool up = j & 8;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const float keep = up ? v(i + 32) : v(i), send = up ? v(i) : v(i + 32);
+      a[i] = keep + __shfl_xor(send, 8, 64);
+    }
+  }
+  {
+    const bool up = j & 4;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float keep = up ? a[i + 16] : a[i], send = up ? a[i] : a[i + 16];
+      b[i] = keep + __shfl_xor(send, 4, 64);
+    }
+  }
+  {
+    const bool up = j & 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float keep = up ? b[i + 8] : b[i], send = up ? b[i] : b[i + 8];
+      c[i] = keep + __shfl_xor(send, 2, 64);
+    }
+  }
+  const bool up = j & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float keep = up ? c[i + 4] : c[i], send = up ? c[i] : c[i + 4];
+    out[i] = keep + __shfl_xor(send, 1, 64);
+  }
+}
+
+// LDS layout (floats) of the fused actor kernel; dynamic shared memory
+__host__ __device__ constexpr int f_pa(int A) { return kM3N + A * kM3N + A; }   // b2 | W3[A] | b3[A]
+__host__ __device__ constexpr int f_lds_floats(int A) {
+  return 2 * kFChunkF + (2 + A) * kM3N + kFWaves * (f_pa(A) + kM3N);
+}
+
+// a store of hidden row hh (= 16b + 4g + r) of a [256][K] buffer: the lane's
+// part (row, 4g) in the VGPR offset, the wave-uniform (16b + r)·K·4 in soffset,
+// so the 64 store sites of a tile share one address register
+__device__ __forceinline__ void f_st(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, 0);
+}
+
+template <int A>
+__global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
+    long long K, int I, int D, const float* __restrict__ X, const long long* __restrict__ idx,
+    const float* __restrict__ pack, const float* __restrict__ b1, const float* __restrict__ b2,
+    const float* __restrict__ W3, const float* __restrict__ b3, const float* __restrict__ logstd, float scale,
+    const float* __restrict__ act, const float* __restrict__ logp_old, const double* __restrict__ adv, float clip,
+    float ent_coef, float* __restrict__ Xa, float* __restrict__ H1T, float* __restrict__ dZ2T,
+    float* __restrict__ dZ1T, float* __restrict__ partA, float* __restrict__ partB, double* __restrict__ lossp,
+    float* __restrict__ dlogstd, float* __restrict__ kl_out, double* __restrict__ acc, unsigned* __restrict__ count,
+    float* __restrict__ mean_out) {
+  constexpr int N = kM3N, PA = f_pa(A), NL = 2 + A;   // loss sums: policy, approx_kl, d logstd[A]
+  extern __shared__ float4 f_lds[];
+  float* lf = reinterpret_cast<float*>(f_lds);
+  float* sb1 = lf + 2 * kFChunkF;
+  float* sb2 = sb1 + N;
+  float* sw3 = sb2 + N;                 // [A][N]
+  float* spa = sw3 + A * N;             // [waves][PA]
+  float* spb = spa + kFWaves * PA;      // [waves][N]
+  __shared__ double ldsn[kFWaves][NL];
+  __shared__ bool last;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const long long row = ((long long)blockIdx.x * kFWaves + w) * 16 + j;
+  const bool rv = row < K;
+  const int Ip = f16_ip(I);
+  for (int t = tid; t < N; t += kFBlock) { sb1[t] = b1[t]; sb2[t] = b2[t]; }
+  for (int t = tid; t < A * N; t += kFBlock) sw3[t] = W3[t];
+  // the row's agent obs in the rollout table: env-timestep idx[row / D], agent row % D
+  const long long ei = rv ? row / D : 0;
+  const float* xrow = X + (rv ? (idx[ei] * D + (row - ei * D)) * (long long)I : 0);
+  const size_t hbytes = (size_t)K * N * 4;
+  const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), z2r = m3_rsrc(dZ2T, hbytes), z1r = m3_rsrc(dZ1T, hbytes);
+  const unsigned kstride = (unsigned)(K * 4);
+  const unsigned voff = rv ? (unsigned)(row * 4) + (unsigned)(4 * g) * kstride : kM3OOB;
+  FStream S{reinterpret_cast<const float4*>(pack), f_lds};
+
+  // ---- layer 1: Z1ᵀ = W1·Xᵀ, all 16 hidden blocks at once; step (q, e) contracts k = 16q + 4e + g
+  f32x4 acc1[16];
+#pragma unroll
+  for (int b = 0; b < 16; ++b) acc1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f_stream<0>(S, Ip / 32, [&](int ch, const float4* wc) {
+    float xb[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = 32 * ch + 4 * t + g;   // q = 2ch + (t >> 2), e = t & 3
+      xb[t] = rv && k < I ? xrow[k] : 0.f;
+      if (rv && k < I) Xa[row * I + k] = xb[t];
+    }
+    float4 wv = wc[l];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {   // u = 16·qq + b
+      const int qq = u >> 4, b = u & 15;
+      float4 nx = wv;
+      if (u + 1 < 32) nx = wc[(u + 1) * 64 + l];
+      __builtin_amdgcn_sched_barrier(0);   // the next operand read stays one step ahead of these MFMAs
+      acc1[b] = mfma16(wv.x, xb[4 * qq + 0], acc1[b]);
+      acc1[b] = mfma16(wv.y, xb[4 * qq + 1], acc1[b]);
+      acc1[b] = mfma16(wv.z, xb[4 * qq + 2], acc1[b]);
+      acc1[b] = mfma16(wv.w, xb[4 * qq + 3], acc1[b]);
+      wv = nx;
+    }
+  });
+  float h1[16][4];
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hh = 16 * b + 4 * g + r;
+      h1[b][r] = m3_tanh(acc1[b][r] + sb1[hh]);
+      f_st(h1r, voff, (unsigned)(16 * b + r) * kstride, h1[b][r]);
+    }
+
+  // ---- layer 2: Z2ᵀ = W2·H1ᵀ, two output blocks per chunk (independent accumulators)
+  S.src = reinterpret_cast<const float4*>(pack + f16_w1_floats(Ip));
+  float h2[16][4];
+  float hs[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) hs[a] = 0.f;
+  f_stream<8>(S, 8, [&](int c, const float4* wc) {
+    f32x4 z0 = f32x4{0.f, 0.f, 0.f, 0.f}, z1 = z0;
+    float4 w0 = wc[l], w1 = wc[16 * 64 + l];
+#pragma unroll
+    for (int ib = 0; ib < 16; ++ib) {
+      float4 n0 = w0, n1 = w1;
+      if (ib + 1 < 16) { n0 = wc[(ib + 1) * 64 + l]; n1 = wc[(17 + ib) * 64 + l]; }
+      __builtin_amdgcn_sched_barrier(0);
+      z0 = mfma16(w0.x, h1[ib][0], z0);
+      z1 = mfma16(w1.x, h1[ib][0], z1);
+      z0 = mfma16(w0.y, h1[ib][1], z0);
+      z1 = mfma16(w1.y, h1[ib][1], z1);
+      z0 = mfma16(w0.z, h1[ib][2], z0);
+      z1 = mfma16(w1.z, h1[ib][2], z1);
+      z0 = mfma16(w0.w, h1[ib][3], z0);
+      z1 = mfma16(w1.w, h1[ib][3], z1);
+      w0 = n0;
+      w1 = n1;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h0 = 32 * c + 4 * g + r, hA = h0 + 16;
+      h2[2 * c][r] = m3_tanh(z0[r] + sb2[h0]);
+      h2[2 * c + 1][r] = m3_tanh(z1[r] + sb2[hA]);
+#pragma unroll
+      for (int a = 0; a < A; ++a) hs[a] += h2[2 * c][r] * sw3[a * N + h0] + h2[2 * c + 1][r] * sw3[a * N + hA];
+    }
+  });
+
+  // ---- the loss head of row j (every lane group forms the same values; group 0 counts them)
+  float dout[A];
+  double ls[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) ls[k] = 0.0;
+  {
+    float sd[A], lsd[A], var2[A], mu[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      float t = hs[a] + __shfl_xor(hs[a], 16, 64);
+      t = t + __shfl_xor(t, 32, 64);
+      mu[a] = t + b3[a];
+      sd[a] = expf(logstd[a]);
+      lsd[a] = logf(sd[a]);
+      var2[a] = 2.0f * (sd[a] * sd[a]);
+    }
+    if (mean_out && rv && g == 0)
+#pragma unroll
+      for (int a = 0; a < A; ++a) mean_out[row * A + a] = mu[a];
+    const float lc = (float)log(sqrt(2.0 * M_PI));
+    const float lo = 1.0f - clip, hi = 1.0f + clip;
+    const double G = -1.0 / (double)K;
+    const long long gi = rv ? idx[ei] * D + (row - ei * D) : 0;
+    float t1[A], logp = 0.0f;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float m = mu[a] * scale;
+      t1[a] = (rv ? act[gi * A + a] : 0.f) - m;
+      const float t4 = (float)((double)(-(t1[a] * t1[a])) / (double)var2[a]);
+      const float lp = (t4 - lsd[a]) - lc;
+      logp = a == 0 ? lp : logp + lp;
+    }
+    const float lpo = rv ? logp_old[gi] : 0.f;
+    const float ratio = expf(logp - lpo);
+    const double ad = rv ? adv[idx[ei]] : 0.0;
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
+    const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
+    const double g2 = s2 < s1 ? G : (s1 == s2 ? G / 2 : 0.0);
+    float gr = (float)(g1 * ad);
+    if (ratio >= lo && ratio <= hi) gr = gr + (float)(g2 * ad);
+    const float gl = gr * ratio;
+    const bool cnt = rv && g == 0;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float gt3 = (float)((double)gl / (double)var2[a]);
+      const float gt1 = -gt3 * 2.0f * t1[a];
+      dout[a] = rv ? -gt1 * scale : 0.f;
+      if (cnt) ls[2 + a] = (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
+    }
+    if (cnt) {
+      ls[0] = -(s1 < s2 ? s1 : s2);
+      ls[1] = (double)(lpo - logp);
+    }
+  }
+
+  // ---- head and second-tanh backward: W3 / b3 / b2 partials, dZ2ᵀ = (dout·W3) ⊙ (1 − H2ᵀ²) in place
+  float* pa = spa + w * PA;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    float o4[4];
+    const float da = dout[a];
+    f_lane_sum64([&](int x) { return da * h2[x >> 2][x & 3]; }, o4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pa[N + a * N + 16 * j + 4 * g + i] = o4[i];
+    float t = g == 0 ? dout[a] : 0.f;   // Σ_rows dout_a (group 0's 16 lanes)
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (l == 0) pa[N + A * N + a] = t;
+  }
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hh = 16 * b + 4 * g + r;
+      float gg = 0.f;
+#pragma unroll
+      for (int a = 0; a < A; ++a) gg += dout[a] * sw3[a * N + hh];
+      const float hv = h2[b][r];
+      h2[b][r] = gg * (1.f - hv * hv);
+      f_st(z2r, voff, (unsigned)(16 * b + r) * kstride, h2[b][r]);
+    }
+  {
+    float o4[4];
+    f_lane_sum64([&](int x) { return h2[x >> 2][x & 3]; }, o4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pa[16 * j + 4 * g + i] = o4[i];
+  }
+
+  // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (two hidden blocks per chunk); dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²) in place of H1ᵀ
+  S.src = reinterpret_cast<const float4*>(pack + f16_w1_floats(Ip) + kFW2Floats);
+  f_stream<8>(S, 8, [&](int c, const float4* wc) {
+    f32x4 d0 = f32x4{0.f, 0.f, 0.f, 0.f}, d1 = d0;
+    float4 w0 = wc[l], w1 = wc[16 * 64 + l];
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) {
+      float4 n0 = w0, n1 = w1;
+      if (ob + 1 < 16) { n0 = wc[(ob + 1) * 64 + l]; n1 = wc[(17 + ob) * 64 + l]; }
+      __builtin_amdgcn_sched_barrier(0);
+      d0 = mfma16(w0.x, h2[ob][0], d0);
+      d1 = mfma16(w1.x, h2[ob][0], d1);
+      d0 = mfma16(w0.y, h2[ob][1], d0);
+      d1 = mfma16(w1.y, h2[ob][1], d1);
+      d0 = mfma16(w0.z, h2[ob][2], d0);
+      d1 = mfma16(w1.z, h2[ob][2], d1);
+      d0 = mfma16(w0.w, h2[ob][3], d0);
+      d1 = mfma16(w1.w, h2[ob][3], d1);
+      w0 = n0;
+      w1 = n1;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h0 = 32 * c + 4 * g + r;
+      const float u0 = h1[2 * c][r], u1 = h1[2 * c + 1][r];
+      h1[2 * c][r] = d0[r] * (1.f - u0 * u0);
+      h1[2 * c + 1][r] = d1[r] * (1.f - u1 * u1);
+      f_st(z1r, voff, (unsigned)(32 * c + r) * kstride, h1[2 * c][r]);
+      f_st(z1r, voff, (unsigned)(32 * c + 16 + r) * kstride, h1[2 * c + 1][r]);
+    }
+  });
+  {
+    float o4[4];
+    f_lane_sum64([&](int x) { return h1[x >> 2][x & 3]; }, o4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) spb[w * N + 16 * j + 4 * g + i] = o4[i];
+  }
+  // the loss sums of the wave's rows (group 0), then the waves in order
+#pragma unroll
+  for (int k = 0; k < NL; ++k)
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) ls[k] += __shfl_xor(ls[k], o, 64);
+  if (l == 0)
+#pragma unroll
+    for (int k = 0; k < NL; ++k) ldsn[w][k] = ls[k];
+  __syncthreads();
+  for (int t = tid; t < PA; t += kFBlock) {
+    float s = spa[t];
+#pragma unroll
+    for (int v = 1; v < kFWaves; ++v) s += spa[v * PA + t];
+    partA[(size_t)blockIdx.x * PA + t] = s;
+  }
+  for (int t = tid; t < N; t += kFBlock) {
+    float s = spb[t];
+#pragma unroll
+    for (int v = 1; v < kFWaves; ++v) s += spb[v * N + t];
+    partB[(size_t)blockIdx.x * N + t] = s;
+  }
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      double s = ldsn[0][k];
+#pragma unroll
+      for (int v = 1; v < kFWaves; ++v) s += ldsn[v][k];
+      lossp[(size_t)blockIdx.x * NL + k] = s;
+    }
+    __threadfence();
+    last = atomicAdd(count, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  // the last workgroup: fixed-order sums of the loss partials (ppo_heads_kernel's tail)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double tot[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) tot[k] = 0.0;
+  for (unsigned bb = tid; bb < gridDim.x; bb += kFBlock)
+#pragma unroll
+    for (int k = 0; k < NL; ++k) tot[k] += lossp[(size_t)bb * NL + k];
+  block_sum_n<NL>(tot, ldsn);
+  if (tid != 0) return;
+  *count = 0;
+  const float lc = (float)log(sqrt(2.0 * M_PI));
+  float ent = 0.0f;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    const float lsd = logf(expf(logstd[a]));
+    ent = a == 0 ? (0.5f + lc) + lsd : ent + ((0.5f + lc) + lsd);
+  }
+#pragma unroll
+  for (int a = 0; a < A; ++a) dlogstd[a] = (float)tot[2 + a] - ent_coef;
+  const float akl = (float)(tot[1] / (double)K);
+  *kl_out = akl;
+  acc[0] += tot[0] / (double)K;
+  acc[2] += (double)(-ent);
+  acc[3] += (double)akl;
+}
+
+
 // torch.optim.Adam over several flat parameter buffers in one launch (the
 // actor's, KL-gated, and the critic's): blocks [start[i], start[i+1]) serve
 // segment i, kAdamPer elements per thread (all loads issued before the
@@ -910,6 +1385,7 @@ struct AdamSeg {
   long long n, w1, w2;    // elements; offsets of W1 [256][I] and W2 [256][256] in p
   float lr, b1, b2, eps, thr;
   int I, zero;
+  int kind;               // pack layout: 0 qs_mlp3_pack (32x32 tiles), 1 qs_mlp3f_pack (16x16 tiles)
 };
 struct AdamSegs {
   AdamSeg s[kAdamMaxSeg];
@@ -940,7 +1416,17 @@ __device__ __forceinline__ void adam_elem(const AdamSeg& A, long long i, float g
   const float denom = sqrtf(v1) / bc2s + A.eps;
   const float p1 = p - (A.lr / bc1) * (m1 / denom);
   A.p[i] = p1;
-  if (A.pack) {
+  if (A.pack && A.kind == 1) {
+    const long long w2f0 = f16_w1_floats(f16_ip(A.I)), w2b0 = w2f0 + kFW2Floats;
+    if (i >= A.w1 && i < A.w1 + (long long)kM3N * A.I) {
+      const int mm = (int)((i - A.w1) / A.I), k = (int)((i - A.w1) - (long long)mm * A.I);
+      A.pack[f16_pos_w1(mm, k)] = p1;
+    } else if (i >= A.w2 && i < A.w2 + (long long)kM3N * kM3N) {
+      const int mm = (int)((i - A.w2) >> 8), n = (int)((i - A.w2) & 255);
+      A.pack[w2f0 + f16_pos_w2f(mm, n)] = p1;
+      A.pack[w2b0 + f16_pos_w2b(mm, n)] = p1;
+    }
+  } else if (A.pack) {
     const int Ip = (A.I + 31) & ~31;
     const long long w2p0 = (long long)(Ip / 8) * kM3NB * 256, w2tp0 = w2p0 + (long long)kM3NB * 32 * 256;
     if (i >= A.w1 && i < A.w1 + (long long)kM3N * A.I) {
@@ -1638,13 +2124,14 @@ static int build_adam_segs(int32_t nseg, float* const* params, float* const* gra
     if (n[i] <= 0 || !params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i] || !step[i])
       return fail(QS_E_INVALID, std::string(name) + ": bad segment");
     float* pk = pack ? pack[i] : nullptr;
-    const int I = pk ? pack_I[i] : 0;
+    // pack_I: the MLP's input width, | QS_PACK_F16 for a qs_mlp3f_pack image
+    const int I = pk ? (pack_I[i] & ~QS_PACK_F16) : 0, kind = pk && (pack_I[i] & QS_PACK_F16) ? 1 : 0;
     if (pk && (I <= 0 || I > 1024 || w1_off[i] < 0 || w2_off[i] < 0 || w1_off[i] + (int64_t)kM3N * I > n[i] ||
                w2_off[i] + (int64_t)kM3N * kM3N > n[i]))
       return fail(QS_E_INVALID, std::string(name) + ": bad pack segment");
     S.s[i] = AdamSeg{params[i], grads[i], exp_avg[i], exp_avg_sq[i], step[i], gate_val[i], pk, (long long)n[i],
                      pk ? (long long)w1_off[i] : 0, pk ? (long long)w2_off[i] : 0, lr[i], beta1[i], beta2[i], eps[i],
-                     gate_thr[i], I, zero_grads ? 1 : 0};
+                     gate_thr[i], I, zero_grads ? 1 : 0, kind};
     S.start[i] = blocks;
     blocks += (int)std::min<int64_t>((n[i] + kAdamBlock * kAdamPer - 1) / (kAdamBlock * kAdamPer), kAdamSegBlocks);
   }
@@ -1730,6 +2217,59 @@ int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, f
                      grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, gate_val, gate_thr, (unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_adam_step: ") + hipGetErrorString(e));
+}
+
+int qs_value_head(int32_t mb, int32_t D, const int64_t* idx, const double* ret, const float* v, float* dv, double* acc,
+                  void* work, void* stream) {
+  if (mb <= 0 || D <= 0 || !idx || !ret || !v || !dv || !acc || !work) return fail(QS_E_INVALID, "qs_value_head: bad argument");
+  const unsigned blocks = (unsigned)((mb + kHeadsBlock - 1) / kHeadsBlock);
+  hipLaunchKernelGGL((ppo_heads_kernel<1, false>), dim3(blocks), dim3(kHeadsBlock), 0, (hipStream_t)stream, (int)mb,
+                     (int)D, (const long long*)idx, nullptr, nullptr, 1.0f, nullptr, nullptr, nullptr, ret, v, 0.f, 0.f,
+                     nullptr, nullptr, dv, nullptr, acc, (double*)((char*)work + 64), (unsigned*)work);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_value_head: ") + hipGetErrorString(e));
+}
+
+int32_t qs_mlp3f_tiles(int64_t K) { return K <= 0 ? 0 : (int32_t)((K + 16 * kFWaves - 1) / (16 * kFWaves)); }
+int64_t qs_mlp3f_pack_floats(int32_t I) { return I <= 0 ? 0 : f16_w1_floats(f16_ip(I)) + 2 * kFW2Floats; }
+int64_t qs_mlp3f_work_bytes(int64_t K) { return 64 + (int64_t)qs_mlp3f_tiles(K) * (2 + kMaxA) * (int64_t)sizeof(double); }
+
+int qs_mlp3f_pack(int32_t I, const float* W1, const float* W2, float* pack, void* stream) {
+  if (I <= 0 || f16_ip(I) > kFMaxIp || !W1 || !W2 || !pack) return fail(QS_E_INVALID, "qs_mlp3f_pack: bad argument (I <= 128)");
+  const int64_t n = qs_mlp3f_pack_floats(I);
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(mlp3f_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (int)I, W1, W2, pack);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3f_pack: ") + hipGetErrorString(e));
+}
+
+int qs_mlp3f_actor(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, const int64_t* idx, const float* pack,
+                   const float* b1, const float* b2, const float* W3, const float* b3, const float* logstd,
+                   float action_scale, const float* act, const float* logp_old, const double* adv, float clip,
+                   float ent_coef, float* Xa, float* H1T, float* dZ2T, float* dZ1T, float* partA, float* partB,
+                   float* dlogstd, float* kl_out, double* acc, void* work, float* mean_out, void* stream) {
+  if (K <= 0 || D <= 0 || K % D || K * kM3N * 4 >= (int64_t(1) << 31) || I <= 0 || f16_ip(I) > kFMaxIp || A < 1 ||
+      A > kMaxA || !X || !idx || !pack || !b1 || !b2 || !W3 || !b3 || !logstd || !act || !logp_old || !adv || !Xa ||
+      !H1T || !dZ2T || !dZ1T || !partA || !partB || !dlogstd || !kl_out || !acc || !work)
+    return fail(QS_E_INVALID, "qs_mlp3f_actor: bad argument (K a multiple of D, K·1024 < 2^31, I <= 128, 1 <= A <= 4)");
+  const unsigned grid = (unsigned)qs_mlp3f_tiles(K);
+  unsigned* count = (unsigned*)work;
+  double* lossp = (double*)((char*)work + 64);
+  auto go = [&](auto kern, int AA) {
+    const int lds = f_lds_floats(AA) * (int)sizeof(float);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kFBlock), (unsigned)lds, (hipStream_t)stream, (long long)K, (int)I, (int)D,
+                       X, (const long long*)idx, pack, b1, b2, W3, b3, logstd, action_scale, act, logp_old, adv, clip,
+                       ent_coef, Xa, H1T, dZ2T, dZ1T, partA, partB, lossp, dlogstd, kl_out, acc, count, mean_out);
+  };
+  switch (A) {
+    case 1: go(mlp3f_actor_kernel<1>, 1); break;
+    case 2: go(mlp3f_actor_kernel<2>, 2); break;
+    case 3: go(mlp3f_actor_kernel<3>, 3); break;
+    default: go(mlp3f_actor_kernel<4>, 4); break;
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3f_actor: ") + hipGetErrorString(e));
 }
 
 // chunks of qs_mlp_wgrad: the most (a power of two, <= 256) that keeps every

@@ -63,7 +63,9 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_mlp_bias_tanh", "qs_mlp_bwd_blocks", "qs_mlp_tanh_bwd", "qs_mlp_sum_partials",
            "qs_mlp_sum_partials_multi", "qs_adam_step", "qs_mlp3_tiles", "qs_mlp3_pack_floats",
            "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_mlp_wgrad", "qs_mlp_wgrad_chunks", "qs_adam_multi",
-           "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_learner_last_error")
+           "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
+           "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_learner_last_error")
+QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
 
 _lib = None
 
@@ -127,12 +129,21 @@ def load():
                                          ctypes.c_int32] + [vp] * 9
     L.qs_adam_multi_pack.argtypes = [ctypes.c_int32] + [vp] * 16 + [ctypes.c_int32, vp, vp]
     L.qs_mlp_sum_adam.argtypes = [ctypes.c_int32] + [vp] * 9 + [ctypes.c_int32] + [vp] * 18
+    L.qs_mlp3f_tiles.argtypes = [i64]
+    L.qs_mlp3f_pack_floats.argtypes = [ctypes.c_int32]
+    L.qs_mlp3f_work_bytes.argtypes = [i64]
+    L.qs_mlp3f_pack.argtypes = [ctypes.c_int32, vp, vp, vp, vp]
+    L.qs_mlp3f_actor.argtypes = ([i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 8 + [f32] + [vp] * 3
+                                 + [f32, f32] + [vp] * 12)
+    L.qs_value_head.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 7
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):
             getattr(L, name).restype = i32
     L.qs_ppo_heads_work_bytes.restype = i64
     L.qs_mlp3_pack_floats.restype = i64
+    L.qs_mlp3f_pack_floats.restype = i64
+    L.qs_mlp3f_work_bytes.restype = i64
     _lib = L
     return L
 

@@ -345,6 +345,72 @@ class _M3Work:
                 whole.append(dst)
 
 
+class _F16Work(_M3Work):
+    """The shared actor's minibatch step on qs_mlp3f_actor: forward, the policy
+    loss head and the backward of every 16-row tile in one launch (the
+    activations never leave the registers between the layers), then the
+    split-K weight-gradient GEMMs dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·Xa.  Same partial
+    rows and reduction tasks as _M3Work.backward."""
+
+    def __init__(self, mlp, K, device):
+        f0, f1, f2 = mlp.fcs
+        lib = L.load()
+        self.mlp, self.K, self.I, self.A = mlp, K, f0.in_features, f2.out_features
+        f32 = dict(device=device, dtype=torch.float32)
+        self.pack = torch.empty(int(lib.qs_mlp3f_pack_floats(self.I)), **f32)
+        self.h1, self.dz1, self.dz2 = (torch.empty((256, K), **f32) for _ in range(3))
+        self.xa = torch.empty((K, self.I), **f32)
+        self.G = G = int(lib.qs_mlp3f_tiles(K))
+        self.part_a = torch.empty((G, 256 * (1 + self.A) + self.A), **f32)
+        self.part_b = torch.empty((G, 256), **f32)
+        self.work = torch.zeros(int(lib.qs_mlp3f_work_bytes(K)), dtype=torch.uint8, device=device)
+        self.mean = None   # tests: set to a [K][A] tensor to receive the actor output
+        m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 1024), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
+        self.C2 = self.C1 = 0
+        self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
+        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
+        self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 else None
+
+    def repack(self):
+        f0, f1, _ = self.mlp.fcs
+        L.check(L.load().qs_mlp3f_pack(self.I, L.ptr(f0.weight), L.ptr(f1.weight), L.ptr(self.pack), _stream()),
+                "qs_mlp3f_pack")
+
+    def pack_segment(self, fb):
+        pk, w1, w2, I = super().pack_segment(fb)
+        return pk, w1, w2, I | L.QS_PACK_F16
+
+    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole):
+        """qs_mlp3f_actor over the minibatch's agent rows (env-timesteps idx, D rows
+        each, straight from the rollout table), then the weight gradients."""
+        f0, f1, f2 = self.mlp.fcs
+        logstd = actor.logstd
+        L.check(L.load().qs_mlp3f_actor(
+            self.K, self.I, D, self.A, L.ptr(table), L.ptr(idx), L.ptr(self.pack), L.ptr(f0.bias), L.ptr(f1.bias),
+            L.ptr(f2.weight), L.ptr(f2.bias), L.ptr(logstd), float(actor.action_scale), L.ptr(rollouts.act),
+            L.ptr(rollouts.logp), L.ptr(rollouts.adv_env), float(clip), float(ent_coef), L.ptr(self.xa),
+            L.ptr(self.h1), L.ptr(self.dz2), L.ptr(self.dz1), L.ptr(self.part_a), L.ptr(self.part_b),
+            L.ptr(logstd.grad), L.ptr(kl), L.ptr(acc), L.ptr(self.work), L.ptr(self.mean), _stream()),
+            "qs_mlp3f_actor")
+        N, A = 256, self.A
+        tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
+        tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
+        w2 = self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2)    # dW2 = dZ2ᵀ·H1
+        w1 = self._splitk(f0.weight.grad, self.dz1, self.xa, False, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
+        for dst, t in ((f1.weight.grad, w2), (f0.weight.grad, w1)):
+            if t is not None:
+                tasks.append(t)
+            elif whole is not None:
+                whole.append(dst)
+
+
+def _f16_ok(mlp):
+    """The fused actor step takes the one-action-output actor with inputs <= 128
+    wide (the bench's ONE_D_* actors); other widths keep the two-kernel path."""
+    f0, _, f2 = mlp.fcs
+    return f2.out_features == 1 and f0.in_features <= 128
+
+
 def _m3_ok(mlp, max_in=1024):
     f0, f1, f2 = mlp.fcs
     return (mlp._tanh3 and f0.out_features == 256 and f1.out_features == 256 and f2.out_features <= 4
@@ -673,6 +739,8 @@ class MAPPOAgent:
         self._force_allreduce = False   # tests: take the all-reduce path with one rank
         self.fused_heads = fused_heads   # qs_ppo_heads (False: the loss heads as plain torch ops)
         self.direct = kwargs.get('direct', True)   # the fused MLP kernels without autograd (_iteration_direct)
+        # the direct iteration's actor on qs_mlp3f_actor (forward + loss head + backward in one launch)
+        self.fused_actor = kwargs.get('fused_actor', True)
         self.side_stream = kwargs.get('side_stream', True)   # critic backward beside the actor's (_iteration_direct)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
@@ -796,8 +864,10 @@ class MAPPOAgent:
         lib = L.load()
         if getattr(self, '_ws_key', None) == (mb, D, O, A):
             return
-        self._ws_actor = _M3Work(self.ac.actor.pi_net, mb * D, self.device)
+        f16 = self.fused_actor and _f16_ok(self.ac.actor.pi_net)
+        self._ws_actor = (_F16Work if f16 else _M3Work)(self.ac.actor.pi_net, mb * D, self.device)
         self._ws_critic = _M3Work(self.ac.critic.v_net, mb, self.device)
+        self._vh_work = torch.zeros(int(lib.qs_ppo_heads_work_bytes(mb, D)), dtype=torch.uint8, device=self.device)
         self._xg = torch.empty((mb, D * O), device=self.device)
         self._dmean = torch.empty(mb * D, A, device=self.device)
         self._dv = torch.empty(mb, 1, device=self.device)
@@ -816,13 +886,14 @@ class MAPPOAgent:
 
     def _iteration_direct(self, rollouts, idx, acc):
         """One minibatch on the 256-wide fused MLP kernels without autograd, in
-        the fewest launches: the critic forward gathers the minibatch's obs rows
-        itself (qs_mlp3_fwd_rows; its gathered copy is the actor's input and the
-        weight gradients' X), qs_ppo_heads, both backwards into the .grad views,
-        one partial-sum launch, the exchange, and one Adam launch that also zeroes
-        the gradients and rewrites the weights' pack images
-        (qs_adam_multi_pack) — no fill, gather or pack launches.  The same
-        kernels and arithmetic as _iteration_fused, so the same bits."""
+        the fewest launches.  With the fused actor (_F16Work): the actor's
+        forward, policy loss head and backward in one qs_mlp3f_actor launch plus
+        its weight-gradient GEMMs, beside the critic's forward (which gathers the
+        minibatch rows itself, qs_mlp3_fwd_rows), value head and backward on the
+        second stream; otherwise the two-kernel actor (qs_mlp3_fwd_group_rows /
+        qs_mlp3_bwd) around qs_ppo_heads.  Then one launch reduces every partial
+        sum straight into the KL-gated Adam step (one rank), or the two-bucket
+        exchange and the zeroing Adam (several ranks)."""
         world = _dist_world()
         D, O, A = rollouts.num_agents, rollouts.obs_dim, self.ac.act_dim
         mb = idx.shape[0]
@@ -830,60 +901,98 @@ class MAPPOAgent:
         self._direct_setup(mb, D, O, A)
         T, E = rollouts.max_length, rollouts.batch_size
         xc, xa = self._xg, self._xg.view(mb * D, O)
-        if self.side_stream:
-            # the critic forward (which also writes the gathered copy the weight
-            # gradients read) on the second stream, beside the actor forward, which
-            # reads its agent rows straight from the rollout table
-            cur = torch.cuda.current_stream()
-            if getattr(self, '_side', None) is None or self._side.device != cur.device:
-                self._side = torch.cuda.Stream(device=cur.device)
-            self._side.wait_stream(cur)
-            with torch.cuda.stream(self._side):
-                v = self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
-            mean = self._ws_actor.forward(rollouts.obs.reshape(T * E * D, O), rows=idx, group=D)
-            cur.wait_stream(self._side)
-        else:
-            v = self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
-            mean = self._ws_actor.forward(xa)
         logstd = self.ac.actor.logstd
-        L.check(lib.qs_ppo_heads(mb, D, A, L.ptr(idx), L.ptr(mean), L.ptr(logstd), float(self.action_scale),
-                                 L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
-                                 L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param), float(self.entropy_coef),
-                                 L.ptr(self._dmean), L.ptr(logstd.grad), L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc),
-                                 L.ptr(self._heads_work), _stream()), "qs_ppo_heads")
-        ta, tc, wa, wc = [], [], [], []
         multi = world > 1 or self._force_allreduce
-        if self.side_stream:
-            # the critic's backward (a 128-workgroup kernel at 4 096 rows: half the
-            # CUs) and its weight-gradient GEMMs on a second stream, beside the
-            # actor's; with several ranks the critic bucket's partial sums and
-            # all-reduce follow on that stream, hidden behind the actor backward.
-            # Joined before Adam (graph capture records the fork and the join as
-            # dependency edges)
-            self._side.wait_stream(cur)
-            with torch.cuda.stream(self._side):
-                self._ws_critic.backward(xc, self._dv, tc, wc)
-                if multi:
-                    _flush_sums(tc)
-                    self._exchange_bucket(self._critic_bucket, world)
-            self._ws_actor.backward(xa, self._dmean, ta, wa)
-            if multi:
-                _flush_sums(ta)
-                self._exchange_bucket(self._actor_bucket, world)
-            cur.wait_stream(self._side)
-        else:
-            self._ws_actor.backward(xa, self._dmean, ta, wa)
+        ta, tc, wa, wc = [], [], [], []
+        cur = torch.cuda.current_stream()
+        if self.side_stream and (getattr(self, '_side', None) is None or self._side.device != cur.device):
+            self._side = torch.cuda.Stream(device=cur.device)
+        fused = isinstance(self._ws_actor, _F16Work)
+
+        def critic_fwd():
+            # also writes the gathered copy the weight gradients read
+            return self._ws_critic.forward(rollouts.obs.reshape(T * E, D * O), rows=idx, xg=self._xg)
+
+        def critic_bwd(exchange):
             self._ws_critic.backward(xc, self._dv, tc, wc)
-            if multi:
-                _flush_sums(ta + tc)
+            if exchange:   # the critic bucket: its sums and all-reduce
+                _flush_sums(tc)
                 self._exchange_bucket(self._critic_bucket, world)
-                self._exchange_bucket(self._actor_bucket, world)
+
+        if fused:
+            def critic_all(exchange):
+                v = critic_fwd()
+                L.check(lib.qs_value_head(mb, D, L.ptr(idx), L.ptr(rollouts.ret_env), L.ptr(v), L.ptr(self._dv),
+                                          L.ptr(acc), L.ptr(self._vh_work), _stream()), "qs_value_head")
+                critic_bwd(exchange)
+
+            def actor_all(exchange):
+                self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
+                                    self.clip_param, self.entropy_coef, self._kl, acc, ta, wa)
+                if exchange:
+                    _flush_sums(ta)
+                    self._exchange_bucket(self._actor_bucket, world)
+
+            if self.side_stream:
+                self._side.wait_stream(cur)
+                with torch.cuda.stream(self._side):
+                    critic_all(multi)
+                actor_all(multi)
+                cur.wait_stream(self._side)
+            else:
+                actor_all(False)
+                critic_all(False)
+                if multi:
+                    _flush_sums(ta + tc)
+                    self._exchange_bucket(self._critic_bucket, world)
+                    self._exchange_bucket(self._actor_bucket, world)
+        else:
+            if self.side_stream:
+                # the critic forward (which also writes the gathered copy the weight
+                # gradients read) on the second stream, beside the actor forward, which
+                # reads its agent rows straight from the rollout table
+                self._side.wait_stream(cur)
+                with torch.cuda.stream(self._side):
+                    v = critic_fwd()
+                mean = self._ws_actor.forward(rollouts.obs.reshape(T * E * D, O), rows=idx, group=D)
+                cur.wait_stream(self._side)
+            else:
+                v = critic_fwd()
+                mean = self._ws_actor.forward(xa)
+            L.check(lib.qs_ppo_heads(mb, D, A, L.ptr(idx), L.ptr(mean), L.ptr(logstd), float(self.action_scale),
+                                     L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
+                                     L.ptr(rollouts.ret_env), L.ptr(v), float(self.clip_param),
+                                     float(self.entropy_coef), L.ptr(self._dmean), L.ptr(logstd.grad),
+                                     L.ptr(self._dv), L.ptr(self._kl), L.ptr(acc), L.ptr(self._heads_work), _stream()),
+                    "qs_ppo_heads")
+            if self.side_stream:
+                # the critic's backward (a 128-workgroup kernel at 4 096 rows: half the
+                # CUs) and its weight-gradient GEMMs on a second stream, beside the
+                # actor's; with several ranks the critic bucket's partial sums and
+                # all-reduce follow on that stream, hidden behind the actor backward.
+                # Joined before Adam (graph capture records the fork and the join as
+                # dependency edges)
+                self._side.wait_stream(cur)
+                with torch.cuda.stream(self._side):
+                    critic_bwd(multi)
+                self._ws_actor.backward(xa, self._dmean, ta, wa)
+                if multi:
+                    _flush_sums(ta)
+                    self._exchange_bucket(self._actor_bucket, world)
+                cur.wait_stream(self._side)
+            else:
+                self._ws_actor.backward(xa, self._dmean, ta, wa)
+                critic_bwd(False)
+                if multi:
+                    _flush_sums(ta + tc)
+                    self._exchange_bucket(self._critic_bucket, world)
+                    self._exchange_bucket(self._actor_bucket, world)
         gate = self._kl if self.target_kl > 0 else None
         segs = [(self.actor_opt, gate, 1.5 * self.target_kl), (self.critic_opt, None, 0.0)]
         packs = [self._ws_actor.pack_segment(self.actor_opt), self._ws_critic.pack_segment(self.critic_opt)]
         if not multi:
             # nothing to exchange: the reductions feed Adam in the same launch; logstd's
-            # gradient (written by qs_ppo_heads) rides along as a one-row task
+            # gradient (written by the loss head) rides along as a one-row task
             # (as do the weight gradients formed by one GEMM straight into .grad)
             for g in [logstd.grad] + wa:
                 ta.append((1, g.numel(), g, g, g.numel(), None, 0, None))

@@ -1204,22 +1204,31 @@ void qso_dsl_pid(double pid_state[9], const double cur_pos[3], const double cur_
 
 // compute_returns_and_advantages → _compute_single_agent_returns
 // (mappo/buffer.py:428-614) for data laid out [T][N] (N = E*D agents),
-// terminal_vals [T][N], last_val [N]; float64 like the reference.
+// terminal_vals [T][N], last_val [N].  The reference's arrays are float32 and
+// its pinned numpy 2.2.6 (environment.yml:63) applies NEP 50: a float32 scalar
+// combined with a Python float (γ, λ) stays float32, the Python float rounded
+// to float32 first.  So each line is a float32 operation in source order:
+//   rew_adjusted = rews[i] + γ·tv[i]                    (buffer.py:593)
+//   ret = rew_adjusted + (γ·masks[i])·ret                 (:602, ret starts as last_val)
+//   td = (rew_adjusted + (γ·masks[i])·v_ext[i+1]) − v[i]  (:608)
+//   adv = ((adv·λ)·γ)·masks[i] + td                       (:609; adv = ret − v[i] without GAE)
+// stored into float64 result arrays (exact).  -ffp-contract=off: no FMA.
 void qso_gae(int T, int64_t N, const float* rews, const float* vals, const float* masks, const float* terminal_vals,
              const float* last_val, double gamma, int use_gae, double lam, double* rets, double* advs) {
+  const float g = (float)gamma, lm = (float)lam;
   for (int64_t n = 0; n < N; ++n) {
-    double ret = last_val[n], adv = 0;
+    float ret = last_val[n], adv = 0.0f;
     for (int i = T - 1; i >= 0; --i) {
       const size_t k = (size_t)i * N + n;
-      double rew_adj = (double)rews[k] + gamma * (double)terminal_vals[k];
-      ret = rew_adj + gamma * (double)masks[k] * ret;
-      if (!use_gae) adv = ret - (double)vals[k];
+      const float rew_adj = rews[k] + g * terminal_vals[k];
+      ret = rew_adj + (g * masks[k]) * ret;
+      if (!use_gae) adv = ret - vals[k];
       else {
-        double vnext = (i + 1 < T) ? (double)vals[k + N] : (double)last_val[n];
-        double td = rew_adj + gamma * (double)masks[k] * vnext - (double)vals[k];
-        adv = adv * lam * gamma * (double)masks[k] + td;
+        const float vnext = (i + 1 < T) ? vals[k + N] : last_val[n];
+        const float td = (rew_adj + (g * masks[k]) * vnext) - vals[k];
+        adv = ((adv * lm) * g) * masks[k] + td;
       }
-      rets[k] = ret; advs[k] = adv;
+      rets[k] = (double)ret; advs[k] = (double)adv;
     }
   }
 }

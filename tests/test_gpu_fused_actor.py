@@ -1,0 +1,95 @@
+"""qs_mlp3f_actor (the actor's forward, policy loss head and backward in one
+launch, 16-row tiles on the f32 MFMA) against plain torch autograd of the
+reference's expressions: MLPActor AG:87-148 + compute_policy_loss AG:602-640 and
+the backward of policy_loss + ent_coef·entropy_loss (AG:733)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(I, A, seed):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(I, 256), nn.Tanh(), nn.Linear(256, 256), nn.Tanh(), nn.Linear(256, A)).cuda()
+
+
+@pytest.mark.parametrize("mb,D,I,A", [(4096, 8, 27, 1), (96, 3, 27, 1), (37, 5, 72, 2), (16, 8, 100, 4)])
+def test_fused_actor_matches_autograd(mb, D, I, A):
+    from gym_pybullet_drones_amd import _lib as L
+    lib = L.load()
+    dev = "cuda"
+    net = _net(I, A, 3)
+    logstd = nn.Parameter(torch.full((A,), -0.5, device=dev) + 0.1 * torch.randn(A, device=dev))
+    TE = 3 * mb + 5   # rollout env-timesteps; the minibatch samples mb of them
+    g = torch.Generator(device=dev).manual_seed(1)
+    table = torch.randn(TE, D, I, device=dev, generator=g)
+    act = torch.randn(TE, D, A, device=dev, generator=g)
+    adv = torch.randn(TE, device=dev, dtype=torch.float64, generator=g)
+    idx = torch.randperm(TE, device=dev, generator=g)[:mb]
+    x = table[idx].reshape(mb * D, I)
+    with torch.no_grad():
+        d0 = torch.distributions.Normal(net(x), logstd.exp())
+        lp0 = d0.log_prob(act[idx].reshape(-1, A)).sum(-1) + 0.05 * torch.randn(mb * D, device=dev, generator=g)
+    logp_old = torch.zeros(TE, D, device=dev)
+    logp_old[idx] = lp0.reshape(mb, D)
+    clip, ent = 0.2, 0.01
+    K = mb * D
+    # --- reference: autograd of the torch expressions
+    z1 = net[0](x); h1 = torch.tanh(z1); z2 = net[2](h1); h2 = torch.tanh(z2); mean = net[4](h2)
+    for t in (z1, z2, mean):
+        t.retain_grad()
+    dist = torch.distributions.Normal(mean, logstd.exp())
+    logp = dist.log_prob(act[idx].reshape(-1, A)).sum(-1, keepdim=True)
+    ratio = torch.exp(logp - logp_old[idx].reshape(-1, 1))
+    a_ = adv[idx].repeat_interleave(D).reshape(-1, 1)
+    pl = -torch.min(ratio * a_, torch.clamp(ratio, 1 - clip, 1 + clip) * a_).mean()
+    el = -dist.entropy().sum(-1).mean()
+    kl = (logp_old[idx].reshape(-1, 1) - logp).mean()
+    (pl + ent * el).backward()
+    # --- the fused kernel
+    f32 = dict(device=dev, dtype=torch.float32)
+    pack = torch.empty(int(lib.qs_mlp3f_pack_floats(I)), **f32)
+    import ctypes
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L.check(lib.qs_mlp3f_pack(I, L.ptr(net[0].weight), L.ptr(net[2].weight), L.ptr(pack), stream), "qs_mlp3f_pack")
+    G = int(lib.qs_mlp3f_tiles(K))
+    xa = torch.full((K, I), np.nan, **f32)
+    H1, dZ2, dZ1 = (torch.full((256, K), np.nan, **f32) for _ in range(3))
+    partA = torch.empty((G, 256 * (1 + A) + A), **f32)
+    partB = torch.empty((G, 256), **f32)
+    dls = torch.empty(A, **f32)
+    klo = torch.empty(1, **f32)
+    acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    work = torch.zeros(int(lib.qs_mlp3f_work_bytes(K)), dtype=torch.uint8, device=dev)
+    mean_out = torch.empty((K, A), **f32)
+    for rep in range(2):   # the workspace is left ready for the next call
+        acc.zero_()
+        L.check(lib.qs_mlp3f_actor(K, I, D, A, L.ptr(table), L.ptr(idx), L.ptr(pack), L.ptr(net[0].bias),
+                                   L.ptr(net[2].bias), L.ptr(net[4].weight), L.ptr(net[4].bias), L.ptr(logstd), 1.0,
+                                   L.ptr(act), L.ptr(logp_old), L.ptr(adv), clip, ent, L.ptr(xa), L.ptr(H1), L.ptr(dZ2),
+                                   L.ptr(dZ1), L.ptr(partA), L.ptr(partB), L.ptr(dls), L.ptr(klo), L.ptr(acc),
+                                   L.ptr(work), L.ptr(mean_out), stream), "qs_mlp3f_actor")
+        torch.cuda.synchronize()
+        assert torch.equal(xa, x)
+        torch.testing.assert_close(mean_out, mean.detach(), rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(H1, h1.detach().t(), rtol=0, atol=2e-6)
+        s2 = float(z2.grad.abs().max())
+        torch.testing.assert_close(dZ2, z2.grad.t(), rtol=1e-3, atol=1e-4 * s2)
+        s1 = float(z1.grad.abs().max())
+        torch.testing.assert_close(dZ1, z1.grad.t(), rtol=1e-3, atol=1e-4 * s1)
+        pa, pb = partA.double().sum(0), partB.double().sum(0)
+        for got, want in ((pa[:256], net[2].bias.grad), (pa[256:256 + 256 * A].reshape(A, 256), net[4].weight.grad),
+                          (pa[256 + 256 * A:], net[4].bias.grad), (pb, net[0].bias.grad)):
+            sc = float(want.abs().max())
+            torch.testing.assert_close(got.float(), want, rtol=1e-3, atol=1e-4 * sc)
+        torch.testing.assert_close(dls, logstd.grad, rtol=1e-4, atol=1e-6)
+        assert float(klo) == pytest.approx(float(kl), rel=1e-4, abs=1e-7)
+        assert float(acc[0]) == pytest.approx(float(pl), rel=1e-5, abs=1e-8)
+        assert float(acc[2]) == pytest.approx(float(el), rel=1e-6)
+        assert float(acc[3]) == pytest.approx(float(kl), rel=1e-4, abs=1e-7)
+        # weight gradients from the kernel's activations: dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·Xa
+        for got, want in ((dZ2.double() @ H1.double().t(), net[2].weight.grad), (dZ1.double() @ xa.double(), net[0].weight.grad)):
+            sc = float(want.abs().max())
+            torch.testing.assert_close(got.float(), want, rtol=1e-3, atol=1e-4 * sc)

@@ -1,6 +1,7 @@
 """On-device learner kernels and the MAPPO update, through the C-ABI.
 
-* qs_gae vs the oracle's restatement of _compute_single_agent_returns (float64): 1e-12.
+* qs_gae vs the oracle's restatement of _compute_single_agent_returns (float32, as the
+  reference evaluates it under numpy 2): bit for bit.
 * qs_adam_gated vs torch.optim.Adam (the reference's optimizer): 2e-6 relative, and
   an exact no-op when the KL gate is closed.
 * one PPO minibatch update of MAPPOAgent vs a pure-torch restatement of
@@ -30,8 +31,8 @@ def test_gae_kernel_matches_oracle():
         want_r, want_a = qs_oracle.gae(rews, vals, masks, tv, lv, gamma=0.99, use_gae=use_gae, lam=0.95)
         d = lambda x: torch.as_tensor(x, device="cuda")
         got_r, got_a = gae(d(rews), d(vals), d(masks), d(tv), d(lv), 0.99, use_gae, 0.95)
-        np.testing.assert_allclose(got_r.cpu().numpy(), want_r, rtol=1e-12, atol=1e-12)
-        np.testing.assert_allclose(got_a.cpu().numpy(), want_a, rtol=1e-12, atol=1e-12)
+        np.testing.assert_array_equal(got_r.cpu().numpy(), want_r)   # the same float32 operations, bit for bit
+        np.testing.assert_array_equal(got_a.cpu().numpy(), want_a)
 
 
 def test_gated_adam_matches_torch_adam():

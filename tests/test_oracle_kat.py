@@ -182,8 +182,52 @@ def test_K7_spiral_reference_at_t0():
         np.testing.assert_allclose(x[8:11], vref, atol=1e-7)
 
 
+def _numpy_single_agent_returns(rews, vals, masks, terminal_vals, last_val, gamma, use_gae, gae_lambda):
+    """buffer.py:561-614 line by line on numpy scalars: with numpy >= 2 (the
+    reference pins 2.2.6, environment.yml:63) NEP 50 keeps every float32-scalar
+    expression with the Python floats γ, λ in float32."""
+    T = len(rews)
+    rets, advs = np.zeros(T), np.zeros(T)
+    vals_extended = np.concatenate([vals, [last_val]])
+    ret, adv = last_val, 0
+    for i in reversed(range(T)):
+        rew_adjusted = rews[i] + gamma * terminal_vals[i]
+        ret = rew_adjusted + gamma * masks[i] * ret
+        if not use_gae:
+            adv = ret - vals[i]
+        else:
+            td_error = rew_adjusted + gamma * masks[i] * vals_extended[i + 1] - vals[i]
+            adv = adv * gae_lambda * gamma * masks[i] + td_error
+        rets[i], advs[i] = ret, adv
+    return rets, advs
+
+
+@pytest.mark.parametrize("use_gae", [True, False])
+def test_K8_gae_oracle_equals_reference_numpy_semantics(use_gae):
+    """The oracle's GAE (float32 line by line) equals the reference's numpy code
+    run on float32 arrays under numpy 2 — bit for bit."""
+    assert int(np.__version__.split(".")[0]) >= 2
+    rng = np.random.default_rng(4)
+    T, N = 41, 60
+    r = rng.normal(size=(T, N)).astype(np.float32)
+    v = rng.normal(size=(T, N)).astype(np.float32)
+    m = (rng.random((T, N)) > 0.1).astype(np.float32)
+    tv = (rng.normal(size=(T, N)) * (rng.random((T, N)) > 0.8)).astype(np.float32)
+    last = rng.normal(size=N).astype(np.float32)
+    rets, advs = Q.gae(r, v, m, tv, last, gamma=0.99, use_gae=use_gae, lam=0.95)
+    for n in range(N):
+        want_r, want_a = _numpy_single_agent_returns(r[:, n], v[:, n], m[:, n], tv[:, n], last[n], 0.99, use_gae, 0.95)
+        np.testing.assert_array_equal(rets[:, n], want_r)
+        np.testing.assert_array_equal(advs[:, n], want_a)
+    # and the float32 recursion is what it is: not the float64 one
+    r64, _ = _numpy_single_agent_returns(r[:, 0].astype(np.float64), v[:, 0].astype(np.float64), m[:, 0].astype(np.float64),
+                                         tv[:, 0].astype(np.float64), np.float64(last[0]), 0.99, use_gae, 0.95)
+    assert not np.array_equal(r64, rets[:, 0])
+
+
 def test_K8_gae_zero_values():
-    """V ≡ 0, m ≡ 1 ⇒ ret_t = Σ_k γ^k r_{t+k} + γ^{T-t}·last (buffer.py:586-612)."""
+    """V ≡ 0, m ≡ 1 ⇒ ret_t = Σ_k γ^k r_{t+k} + γ^{T-t}·last (buffer.py:586-612),
+    to float32 accuracy (the reference's recursion is float32)."""
     rng = np.random.default_rng(0)
     T, N, g = 17, 5, 0.99
     r = rng.normal(size=(T, N)).astype(np.float32)
@@ -192,12 +236,12 @@ def test_K8_gae_zero_values():
     rets, advs = Q.gae(r, zeros, np.ones((T, N), np.float32), zeros, last, gamma=g, use_gae=True, lam=0.95)
     for t in range(T):
         want = sum(g ** k * r[t + k].astype(np.float64) for k in range(T - t)) + g ** (T - t) * last.astype(np.float64)
-        np.testing.assert_allclose(rets[t], want, rtol=1e-12)
+        np.testing.assert_allclose(rets[t], want, rtol=2e-6, atol=1e-6)
     # GAE with V ≡ 0: δ_t = r_t (+γ·V_{t+1}=0 except the bootstrap at T-1)
     lam_g = 0.95 * g
     for t in range(T):
         want = sum(lam_g ** k * r[t + k].astype(np.float64) for k in range(T - t)) + lam_g ** (T - 1 - t) * g * last.astype(np.float64)
-        np.testing.assert_allclose(advs[t], want, rtol=1e-12)
+        np.testing.assert_allclose(advs[t], want, rtol=2e-6, atol=1e-6)
 
 
 def test_K8_gae_masks_cut_bootstrap():
