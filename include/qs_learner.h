@@ -200,6 +200,18 @@ int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, f
                  float lr, float beta1, float beta2, float eps, const float* gate_val, float gate_thr, void* work,
                  void* stream);
 
+/* The first layer's weight gradient dW[N][M] = Σ_b AT[N][b]·X[b][M] (AT = dZ1ᵀ
+ * [N][K], X the layer input [K][M]; nn.Linear's dW = dYᵀ·X under AG:733 /
+ * AG:759) as chunk partials partial[c][N][M], c < qs_mlp_wgrad_x_chunks(K, M)
+ * chunks of 128 rows (0: the shape is not taken).  N = 256, M <= 256, K a
+ * multiple of 128, AT 16-byte aligned; at_blocked != 0: AT is laid out
+ * [K/8][N][8].  (Measured slower than split-K GEMMs at the learner's shapes:
+ * opt-in)  Sum with qs_mlp_sum_partials /
+ * qs_mlp_sum_adam (G = chunks, P = N·M). */
+int32_t qs_mlp_wgrad_x_chunks(int64_t K, int32_t M);
+int qs_mlp_wgrad_x(int64_t K, int32_t N, int32_t M, const float* AT, int32_t at_blocked, const float* X,
+                   float* partial, void* stream);
+
 /* qs_adam_step over nseg (<= 4) flat buffers in one launch (the learner's
  * actor, gated on approx_kl, and critic, AG:731-760): segment i is exactly the
  * single-buffer call with argument i of every array (host arrays of device

@@ -445,10 +445,11 @@ __device__ __forceinline__ int mlp_sum_wg(int G) {
   while (w < G && w < 16) w <<= 1;
   return w;
 }
-// fin(ti, c, dst, u): the block's result u for column c of task ti (dst its
-// destination element)
-template <class Fin>
-__device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin) {
+// fin(ti, dst, u, pv): the block's result u for a column of task ti (dst its
+// destination element); pv = pre(ti, dst), issued by the finishing waves before
+// their partial-row loads so that its memory latency overlaps theirs
+template <class Fin, class Pre>
+__device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin, Pre pre) {
   constexpr int W = kMlpSumBlock / 64, C = kMlpSumCols;
   __shared__ float lds[W][64 * C];
   int ti = 0;
@@ -457,6 +458,16 @@ __device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int Wg = mlp_sum_wg(T.G), ws = wv % Wg, cg = wv / Wg;
   const long long c0 = ((long long)(blockIdx.x - tasks.start[ti]) * (W / Wg) + cg) * (64 * C) + lane;
+  auto dst_of = [&](long long c) {
+    return c < T.n0 ? T.d0 + c : (c < T.n0 + T.n1 ? T.d1 + (c - T.n0) : T.d2 + (c - T.n0 - T.n1));
+  };
+  decltype(pre(0, (float*)nullptr)) pv[C];
+  if (ws == 0)
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const long long c = c0 + 64 * j;
+      if (c < T.P) pv[j] = pre(ti, dst_of(c));
+    }
   float t[C];
 #pragma unroll
   for (int j = 0; j < C; ++j) t[j] = 0.f;
@@ -492,13 +503,13 @@ __device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin)
     if (c >= T.P) continue;
     float u = lds[cg * Wg][lane + 64 * j];
     for (int k = 1; k < Wg; ++k) u += lds[cg * Wg + k][lane + 64 * j];
-    float* dst = c < T.n0 ? T.d0 + c : (c < T.n0 + T.n1 ? T.d1 + (c - T.n0) : T.d2 + (c - T.n0 - T.n1));
-    fin(ti, dst, u);
+    fin(ti, dst_of(c), u, pv[j]);
   }
 }
 
 __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks tasks) {
-  mlp_sum_block(tasks, [](int, float* dst, float u) { *dst += u; });
+  mlp_sum_block(tasks, [](int, float* dst, float u, float pv) { *dst = pv + u; },
+                [](int, float* dst) { return *dst; });
 }
 
 // torch.optim.Adam step and its step-count commit in one launch: every block
@@ -1096,20 +1107,43 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
   const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), z2r = m3_rsrc(dZ2T, hbytes), z1r = m3_rsrc(dZ1T, hbytes);
   const unsigned kstride = (unsigned)(K * 4);
   const unsigned voff = rv ? (unsigned)(row * 4) + (unsigned)(4 * g) * kstride : kM3OOB;
+  // One continuous chunk stream over the whole pack (W1f | W2f | W2b): chunk c + 2
+  // is in flight while chunk c is consumed, across the phase boundaries too
+  const int nW1 = Ip / 32, nC = nW1 + 16;
   FStream S{reinterpret_cast<const float4*>(pack), f_lds};
+  auto next = [&](int c) -> const float4* {
+    M3Stream::sync();
+    if (c + 1 < nC) S.store(c + 1);
+    if (c + 2 < nC) S.load(c + 2);
+    return S.buf + (c & 1) * (kFChunkF / 4);
+  };
+  auto xload = [&](int ch, float (&xb)[8]) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = 32 * ch + 4 * t + g;   // q = 2ch + (t >> 2), e = t & 3
+      xb[t] = rv && k < I ? xrow[k] : 0.f;
+    }
+  };
+  float xb[8];
+  S.load(0);
+  xload(0, xb);
+  S.store(0);
+  S.load(1);
 
   // ---- layer 1: Z1ᵀ = W1·Xᵀ, all 16 hidden blocks at once; step (q, e) contracts k = 16q + 4e + g
   f32x4 acc1[16];
 #pragma unroll
   for (int b = 0; b < 16; ++b) acc1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f_stream<0>(S, Ip / 32, [&](int ch, const float4* wc) {
-    float xb[8];
+#pragma unroll 1
+  for (int ch = 0; ch < nW1; ++ch) {
+    const float4* wc = next(ch);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const int k = 32 * ch + 4 * t + g;   // q = 2ch + (t >> 2), e = t & 3
-      xb[t] = rv && k < I ? xrow[k] : 0.f;
+      const int k = 32 * ch + 4 * t + g;
       if (rv && k < I) Xa[row * I + k] = xb[t];
     }
+    float xn[8];
+    if (ch + 1 < nW1) xload(ch + 1, xn);
     float4 wv = wc[l];
 #pragma unroll
     for (int u = 0; u < 32; ++u) {   // u = 16·qq + b
@@ -1123,24 +1157,27 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       acc1[b] = mfma16(wv.w, xb[4 * qq + 3], acc1[b]);
       wv = nx;
     }
-  });
+    if (ch + 1 < nW1)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) xb[t] = xn[t];
+  }
   float h1[16][4];
 #pragma unroll
   for (int b = 0; b < 16; ++b)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int hh = 16 * b + 4 * g + r;
-      h1[b][r] = m3_tanh(acc1[b][r] + sb1[hh]);
+      h1[b][r] = m3_tanh(acc1[b][r] + sb1[16 * b + 4 * g + r]);
       f_st(h1r, voff, (unsigned)(16 * b + r) * kstride, h1[b][r]);
     }
 
   // ---- layer 2: Z2ᵀ = W2·H1ᵀ, two output blocks per chunk (independent accumulators)
-  S.src = reinterpret_cast<const float4*>(pack + f16_w1_floats(Ip));
   float h2[16][4];
   float hs[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) hs[a] = 0.f;
-  f_stream<8>(S, 8, [&](int c, const float4* wc) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float4* wc = next(nW1 + c);
     f32x4 z0 = f32x4{0.f, 0.f, 0.f, 0.f}, z1 = z0;
     float4 w0 = wc[l], w1 = wc[16 * 64 + l];
 #pragma unroll
@@ -1167,7 +1204,7 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
 #pragma unroll
       for (int a = 0; a < A; ++a) hs[a] += h2[2 * c][r] * sw3[a * N + h0] + h2[2 * c + 1][r] * sw3[a * N + hA];
     }
-  });
+  }
 
   // ---- the loss head of row j (every lane group forms the same values; group 0 counts them)
   float dout[A];
@@ -1259,8 +1296,9 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
   }
 
   // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (two hidden blocks per chunk); dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²) in place of H1ᵀ
-  S.src = reinterpret_cast<const float4*>(pack + f16_w1_floats(Ip) + kFW2Floats);
-  f_stream<8>(S, 8, [&](int c, const float4* wc) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float4* wc = next(nW1 + 8 + c);
     f32x4 d0 = f32x4{0.f, 0.f, 0.f, 0.f}, d1 = d0;
     float4 w0 = wc[l], w1 = wc[16 * 64 + l];
 #pragma unroll
@@ -1281,14 +1319,14 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int h0 = 32 * c + 4 * g + r;
       const float u0 = h1[2 * c][r], u1 = h1[2 * c + 1][r];
       h1[2 * c][r] = d0[r] * (1.f - u0 * u0);
       h1[2 * c + 1][r] = d1[r] * (1.f - u1 * u1);
       f_st(z1r, voff, (unsigned)(32 * c + r) * kstride, h1[2 * c][r]);
       f_st(z1r, voff, (unsigned)(32 * c + 16 + r) * kstride, h1[2 * c + 1][r]);
     }
-  });
+  }
+  M3Stream::sync();
   {
     float o4[4];
     f_lane_sum64([&](int x) { return h1[x >> 2][x & 3]; }, o4);
@@ -1515,12 +1553,16 @@ __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_adam_kernel(MlpSumTasks 
     sc[threadIdx.x][1] = (float)sqrt(1.0 - powi_d((double)A.b2, t));
   }
   __syncthreads();
-  mlp_sum_block(tasks, [&](int ti, float* dst, float u) {
+  // the element's parameter and moments are loaded with the partial rows
+  mlp_sum_block(tasks, [&](int ti, float* dst, float u, float3 pmv) {
     const int si = seg.s[ti];
     const AdamSeg& A = S.s[si];
     if (!gate_ok(A.gate, A.thr)) return;
+    adam_elem(A, dst - A.g, u, pmv.x, pmv.y, pmv.z, sc[si][0], sc[si][1]);
+  }, [&](int ti, float* dst) {
+    const AdamSeg& A = S.s[seg.s[ti]];
     const long long i = dst - A.g;
-    adam_elem(A, i, u, A.p[i], A.m[i], A.v[i], sc[si][0], sc[si][1]);
+    return make_float3(A.p[i], A.m[i], A.v[i]);
   });
   __syncthreads();
   // every block read the step counts before counting itself
@@ -1598,6 +1640,66 @@ __global__ void __launch_bounds__(64 * kWgWaves) mlp_wgrad_kernel(long long K, i
   for (int j = 0; j < 16; ++j) {
     const int n = nb * 32 + 8 * (j >> 2) + 4 * hf + (j & 3);
     out[(size_t)n * M] = acc[j];
+  }
+}
+
+// ---- weight gradient of a first layer: dW[256][M] = Σ_b AT[256][b]·X[b][M]
+// (AT = dZ1ᵀ, X the layer input [K][M], M <= 256), as chunk partials
+// partial[c][256][M] over row chunks of kWxR rows.  A workgroup owns one chunk
+// and one 32-column tile of X (staged once in LDS, shared by its 4 waves);
+// wave w owns hidden tiles 2w, 2w + 1 (32x32x2 f32 MFMA).  Every AT operand of
+// the chunk is issued before the first MFMA (one memory round trip per wave):
+// a lane's float4 holds four consecutive rows of its hidden unit, so the
+// contraction index is permuted (step 4u + e, half h ↔ row 8u + 4h + e) on both
+// operands alike.  The partials are summed in chunk order by the minibatch's
+// reduction (qs_mlp_sum_adam).
+constexpr int kWxR = 128;
+constexpr int kWxStride = 33;   // LDS row stride of the X tile (conflict-free column reads)
+template <bool BLOCKED>
+__global__ void __launch_bounds__(256) mlp_wgrad_x_kernel(long long K, int M, const float* __restrict__ AT,
+                                                          const float* __restrict__ X, float* __restrict__ partial) {
+  __shared__ float xs[kWxR * kWxStride];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  const long long r0 = (long long)blockIdx.x * kWxR;
+  const int m0 = blockIdx.y * 32;
+  float4 av[2][kWxR / 8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if constexpr (BLOCKED) {   // AT [K/8][256][8]: a wave's float4s of one u are 1 KB contiguous
+      const float* a = AT + ((size_t)(r0 / 8) * kM3N + 64 * w + 32 * t + c) * 8 + 4 * h;
+#pragma unroll
+      for (int u = 0; u < kWxR / 8; ++u) av[t][u] = *reinterpret_cast<const float4*>(a + (size_t)u * kM3N * 8);
+    } else {
+      const float* a = AT + (size_t)(64 * w + 32 * t + c) * K + r0 + 4 * h;
+#pragma unroll
+      for (int u = 0; u < kWxR / 8; ++u) av[t][u] = *reinterpret_cast<const float4*>(a + 8 * u);
+    }
+  }
+  for (int i = threadIdx.x; i < kWxR * 32; i += 256) {
+    const int r = i >> 5, cc = i & 31;
+    xs[r * kWxStride + cc] = m0 + cc < M ? X[(size_t)(r0 + r) * M + m0 + cc] : 0.f;
+  }
+  __syncthreads();
+  f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+#pragma unroll
+  for (int u = 0; u < kWxR / 8; ++u) {
+    const float* xr = xs + (8 * u + 4 * h) * kWxStride + c;
+    const float b0 = xr[0], b1 = xr[kWxStride], b2 = xr[2 * kWxStride], b3 = xr[3 * kWxStride];
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][u].x, b0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][u].x, b0, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][u].y, b1, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][u].y, b1, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][u].z, b2, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][u].z, b2, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][u].w, b3, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][u].w, b3, acc1, 0, 0, 0);
+  }
+  if (m0 + c >= M) return;
+  float* out = partial + (size_t)blockIdx.x * kM3N * M + m0 + c;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    out[(size_t)(64 * w + m3_row(i, h)) * M] = acc0[i];
+    out[(size_t)(64 * w + 32 + m3_row(i, h)) * M] = acc1[i];
   }
 }
 
@@ -2270,6 +2372,25 @@ int qs_mlp3f_actor(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, c
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp3f_actor: ") + hipGetErrorString(e));
+}
+
+int32_t qs_mlp_wgrad_x_chunks(int64_t K, int32_t M) {
+  return (K > 0 && K % kWxR == 0 && M > 0 && M <= 256) ? (int32_t)(K / kWxR) : 0;
+}
+
+int qs_mlp_wgrad_x(int64_t K, int32_t N, int32_t M, const float* AT, int32_t at_blocked, const float* X,
+                   float* partial, void* stream) {
+  if (K <= 0 || K % kWxR || N != kM3N || M <= 0 || M > 256 || !AT || !X || !partial || ((uintptr_t)AT & 15))
+    return fail(QS_E_INVALID, "qs_mlp_wgrad_x: bad argument (K a multiple of 128, N = 256, M <= 256, AT 16-B aligned)");
+  const dim3 grid((unsigned)(K / kWxR), (unsigned)((M + 31) / 32));
+  if (at_blocked)
+    hipLaunchKernelGGL(mlp_wgrad_x_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, (long long)K, (int)M, AT, X,
+                       partial);
+  else
+    hipLaunchKernelGGL(mlp_wgrad_x_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, (long long)K, (int)M, AT, X,
+                       partial);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_wgrad_x: ") + hipGetErrorString(e));
 }
 
 // chunks of qs_mlp_wgrad: the most (a power of two, <= 256) that keeps every

@@ -365,6 +365,8 @@ class _F16Work(_M3Work):
         self.part_b = torch.empty((G, 256), **f32)
         self.work = torch.zeros(int(lib.qs_mlp3f_work_bytes(K)), dtype=torch.uint8, device=device)
         self.mean = None   # tests: set to a [K][A] tensor to receive the actor output
+        # split-K GEMMs for both weight gradients (qs_mlp_wgrad_x measured slower for dW1:
+        # 19 µs + a 256-row partial sum vs 15.5 µs at 32 768 rows)
         m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 1024), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
         self.C2 = self.C1 = 0
         self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)

@@ -199,3 +199,27 @@ def test_wgrad_kernel_matches_matmul(K, N, M, bt):
     want = torch.stack([at[:, c * R:(c + 1) * R].double() @ bk[c * R:(c + 1) * R].double() for c in range(C)])
     torch.testing.assert_close(part.double(), want, rtol=1e-5, atol=1e-5 * R ** 0.5)
     assert lib.qs_mlp_wgrad(K + 1, N, M, L.ptr(at), L.ptr(b), bt, C, L.ptr(part), None) != 0   # K not a multiple of 32·C
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("blocked", [False, True])
+@pytest.mark.parametrize("K,M", [(32768, 27), (4096, 216), (1024, 72), (128, 256)])
+def test_wgrad_x_matches_fp64_matmul(K, M, blocked):
+    """qs_mlp_wgrad_x: chunk partials of dW = ATᵀ-contraction with the layer
+    input, summed in chunk order, against an fp64 matmul."""
+    import ctypes
+    from gym_pybullet_drones_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(3)
+    at = torch.randn(256, K, device="cuda")
+    x = torch.randn(K, M, device="cuda")
+    C = int(lib.qs_mlp_wgrad_x_chunks(K, M))
+    assert C == K // 128
+    part = torch.full((C, 256, M), float("nan"), device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    src = at.reshape(256, K // 8, 8).permute(1, 0, 2).contiguous() if blocked else at   # [K/8][256][8]
+    L.check(lib.qs_mlp_wgrad_x(K, 256, M, L.ptr(src), int(blocked), L.ptr(x), L.ptr(part), st), "qs_mlp_wgrad_x")
+    want = at.double() @ x.double()
+    got = part.double().sum(0)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-4 * float(want.abs().max()) / 100)
+    assert lib.qs_mlp_wgrad_x_chunks(K + 64, M) == 0 and lib.qs_mlp_wgrad_x_chunks(K, 300) == 0
