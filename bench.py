@@ -89,6 +89,7 @@ def parse():
     p.add_argument("--wgrad", default="", help="learner weight gradients on the MFMA qs_mlp_wgrad kernel (w1,w2; '' = GEMMs)")
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
+    p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
     p.add_argument("--dry-ms", type=float, default=2.0, help="--dry-run: ms per stand-in step of rank 0 (rank r: (1+r)x)")
     return p.parse_args()
@@ -355,7 +356,8 @@ def mappo_leg(args, ranks, T):
               rollout_steps=T, rollout_batch_size=E, opt_epochs=10,
               mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
     m.agent.side_stream = bool(args.side_stream)
-    from gym_pybullet_drones_amd.mappo.agent import _M3Work, _SPLITK_MIN_ROWS
+    from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
+    _F16Work.w1_stream = bool(args.w1_stream)
     _M3Work.wgrad = tuple(w for w in args.wgrad.split(",") if w)
     for item in filter(None, args.splitk.split(",")):   # "KxM=rows": split-K chunk rows of a weight gradient
         km, rows = item.split("=")

@@ -168,9 +168,9 @@ int qs_mlp_wgrad(int64_t K, int32_t N, int32_t M, const float* AT, const float* 
  * qs_mlp3f_pack: W1 [256][I], W2 [256][256] → pack[qs_mlp3f_pack_floats(I)]
  *   (W1f | W2f | W2b in 16x16x4 MFMA-step order); qs_adam_multi_pack /
  *   qs_mlp_sum_adam keep it current when pack_I carries QS_PACK_F16.
- * qs_mlp3f_actor writes: Xa [K][I] the gathered inputs; H1T, dZ2T, dZ1T
- *   [256][K] (H1ᵀ = tanh(W1·Xᵀ + b1), dZ2ᵀ, dZ1ᵀ: dW2 = dZ2ᵀ·H1, dW1 =
- *   dZ1ᵀ·Xa); per workgroup g < qs_mlp3f_tiles(K) (128 rows) the partial
+ * qs_mlp3f_actor writes: Xa [K][I] the gathered inputs; H1T, dZ2T, dZ1T row-major
+ *   [K][256] (H1 = tanh(X·W1ᵀ + b1) and the pre-activation gradients dZ2, dZ1:
+ *   dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·Xa); per workgroup g < qs_mlp3f_tiles(K) (128 rows) the partial
  *   rows partA[g][256 + 256·A + A] = [Σ dZ2 | Σ dout_a·H2 | Σ dout_a] and
  *   partB[g][256] = Σ dZ1; and, from the last workgroup, in workgroup order
  *   (as qs_ppo_heads): dlogstd[A], kl_out[0] = approx_kl, acc[0] += policy,

@@ -924,7 +924,9 @@ __global__ void __launch_bounds__(kM3Block) mlp3_bwd_kernel(long long K, const f
 // window shared by the 8 waves.  The loss head is ppo_heads_kernel's
 // arithmetic per row; per-row inputs are read by index (the minibatch's
 // env-timesteps, D agent rows each, straight from the rollout table).
-// Outputs: H1ᵀ, dZ2ᵀ, dZ1ᵀ [256][K] (the weight-gradient GEMMs' operands),
+// Outputs: H1, dZ2, dZ1 row-major [K][256] (the weight-gradient GEMMs' operands,
+// written as 16-byte stores: four times fewer store instructions than a
+// transposed [256][K] image, whose stores bound the epilogues),
 // the gathered inputs Xa [K][I], per-workgroup partial rows of the bias / head
 // gradients, and — from the last workgroup, in workgroup order — approx_kl,
 // d logstd and the loss statistics.
@@ -1061,18 +1063,64 @@ __device__ __forceinline__ void f_lane_sum64(V v, float (&out)[4]) {
   }
 }
 
+// Σ over the 16 lanes of a lane group of a block's four C registers v[r] (hidden
+// 16b + 4g + r): a transposing butterfly (5 shuffles); lane j gets the sum for
+// r = 2·bit3(j) + bit2(j) (lanes differing in bits 0-1 hold the same value).
+// Fixed order: replays are bit-identical.
+// Lane exchanges within a 16-lane DPP row (VALU moves, no LDS pipe): the value of
+// lane j ^ 8, j ^ 4 (row_shl:4 into banks 0 and 2, row_shr:4 into banks 1 and 3),
+// j ^ 2, j ^ 1 (quad permutes).
+template <int CTRL, int BANKS = 0xF>
+__device__ __forceinline__ float f_dpp(float v, float old = 0.f) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, BANKS, false));
+}
+__device__ __forceinline__ float f_x8(float v) { return f_dpp<0x128>(v); }   // row_ror:8
+__device__ __forceinline__ float f_x4(float v) { return f_dpp<0x114, 0xA>(v, f_dpp<0x104, 0x5>(v)); }
+__device__ __forceinline__ float f_x2(float v) { return f_dpp<0x4E>(v); }    // quad_perm [2,3,0,1]
+__device__ __forceinline__ float f_x1(float v) { return f_dpp<0xB1>(v); }    // quad_perm [1,0,3,2]
+// Σ over the 16 lanes of a row, in every lane
+__device__ __forceinline__ float f_row_sum(float t) {
+  t += f_x8(t);
+  t += f_x4(t);
+  t += f_x2(t);
+  return t + f_x1(t);
+}
+
+__device__ __forceinline__ float f_blk_sum(const float (&v)[4]) {
+  const int j = threadIdx.x & 15;
+  const bool u8 = j & 8, u4 = j & 4;
+  const float a0 = (u8 ? v[2] : v[0]) + f_x8(u8 ? v[0] : v[2]);
+  const float a1 = (u8 ? v[3] : v[1]) + f_x8(u8 ? v[1] : v[3]);
+  float b = (u4 ? a1 : a0) + f_x4(u4 ? a0 : a1);
+  b += f_x2(b);
+  return b + f_x1(b);
+}
+
 // LDS layout (floats) of the fused actor kernel; dynamic shared memory
 __host__ __device__ constexpr int f_pa(int A) { return kM3N + A * kM3N + A; }   // b2 | W3[A] | b3[A]
 __host__ __device__ constexpr int f_lds_floats(int A) {
   return 2 * kFChunkF + (2 + A) * kM3N + kFWaves * (f_pa(A) + kM3N);
 }
 
-// a store of hidden row hh (= 16b + 4g + r) of a [256][K] buffer: the lane's
-// part (row, 4g) in the VGPR offset, the wave-uniform (16b + r)·K·4 in soffset,
-// so the 64 store sites of a tile share one address register
-__device__ __forceinline__ void f_st(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, 0);
+// a lane's four C registers of one block (hidden 16b + 4g + r, r = 0..3, of its
+// row) into a row-major [K][256] buffer: one 16-byte store, the lane's part in
+// the VGPR offset and the block's 64·b bytes in soffset
+typedef unsigned f_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void f_st4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, const float (&v)[4]) {
+#ifndef QS_F_NOSTORE   // dev probe: the kernel without its activation stores
+  const f_u4 u = {__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1]),
+                  __builtin_bit_cast(unsigned, v[2]), __builtin_bit_cast(unsigned, v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)voff, (int)soff, 0);
+#endif
 }
+
+#ifdef QS_F_STAMP   // dev probe: per-wave phase timestamps (s_memtime) of the fused actor kernel
+__device__ unsigned long long g_fstamp[4096 * 8];
+#define F_STAMP(k) do { if ((threadIdx.x & 63) == 0) g_fstamp[((size_t)blockIdx.x * kFWaves + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define F_STAMP(k) do { } while (0)
+#endif
 
 template <int A>
 __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
@@ -1094,6 +1142,7 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
   float* spb = spa + kFWaves * PA;      // [waves][N]
   __shared__ double ldsn[kFWaves][NL];
   __shared__ bool last;
+  F_STAMP(0);
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const long long row = ((long long)blockIdx.x * kFWaves + w) * 16 + j;
   const bool rv = row < K;
@@ -1105,8 +1154,8 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
   const float* xrow = X + (rv ? (idx[ei] * D + (row - ei * D)) * (long long)I : 0);
   const size_t hbytes = (size_t)K * N * 4;
   const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), z2r = m3_rsrc(dZ2T, hbytes), z1r = m3_rsrc(dZ1T, hbytes);
-  const unsigned kstride = (unsigned)(K * 4);
-  const unsigned voff = rv ? (unsigned)(row * 4) + (unsigned)(4 * g) * kstride : kM3OOB;
+  // H1, dZ2, dZ1 are row-major [K][256]: a lane's block of four hidden units is 16 contiguous bytes
+  const unsigned voff = rv ? (unsigned)((row * N + 4 * g) * 4) : kM3OOB;
   // One continuous chunk stream over the whole pack (W1f | W2f | W2b): chunk c + 2
   // is in flight while chunk c is consumed, across the phase boundaries too
   const int nW1 = Ip / 32, nC = nW1 + 16;
@@ -1161,20 +1210,36 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
 #pragma unroll
       for (int t = 0; t < 8; ++t) xb[t] = xn[t];
   }
+  F_STAMP(1);
+  // ---- layer 2: Z2ᵀ = W2·H1ᵀ, two output blocks per chunk (independent accumulators).
+  // H1 = tanh(Z1ᵀ + b1) of block ib + 1 is formed and stored during step ib of the
+  // first chunk: the epilogue runs beside the MFMAs instead of before them
   float h1[16][4];
+  auto epi1 = [&](int b) {
 #pragma unroll
-  for (int b = 0; b < 16; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      h1[b][r] = m3_tanh(acc1[b][r] + sb1[16 * b + 4 * g + r]);
-      f_st(h1r, voff, (unsigned)(16 * b + r) * kstride, h1[b][r]);
-    }
-
-  // ---- layer 2: Z2ᵀ = W2·H1ᵀ, two output blocks per chunk (independent accumulators)
+    for (int r = 0; r < 4; ++r) h1[b][r] = m3_tanh(acc1[b][r] + sb1[16 * b + 4 * g + r]);
+    f_st4(h1r, voff, 64u * b, h1[b]);
+  };
+  epi1(0);
+  F_STAMP(2);
   float h2[16][4];
   float hs[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) hs[a] = 0.f;
+  // the epilogue of chunk c's two blocks (bias + tanh, the head's partial dots) runs
+  // during the first two steps of chunk c + 1
+  f32x4 zp0 = f32x4{0.f, 0.f, 0.f, 0.f}, zp1 = zp0;
+  auto epi2 = [&](int c, int half) {
+    const f32x4& z = half ? zp1 : zp0;
+    const int b = 2 * c + half;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hh = 16 * b + 4 * g + r;
+      h2[b][r] = m3_tanh(z[r] + sb2[hh]);
+#pragma unroll
+      for (int a = 0; a < A; ++a) hs[a] += h2[b][r] * sw3[a * N + hh];
+    }
+  };
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const float4* wc = next(nW1 + c);
@@ -1185,6 +1250,8 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       float4 n0 = w0, n1 = w1;
       if (ib + 1 < 16) { n0 = wc[(ib + 1) * 64 + l]; n1 = wc[(17 + ib) * 64 + l]; }
       __builtin_amdgcn_sched_barrier(0);
+      if (c == 0 && ib + 1 < 16) epi1(ib + 1);
+      if (c > 0 && ib < 2) epi2(c - 1, ib);
       z0 = mfma16(w0.x, h1[ib][0], z0);
       z1 = mfma16(w1.x, h1[ib][0], z1);
       z0 = mfma16(w0.y, h1[ib][1], z0);
@@ -1196,16 +1263,13 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       w0 = n0;
       w1 = n1;
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h0 = 32 * c + 4 * g + r, hA = h0 + 16;
-      h2[2 * c][r] = m3_tanh(z0[r] + sb2[h0]);
-      h2[2 * c + 1][r] = m3_tanh(z1[r] + sb2[hA]);
-#pragma unroll
-      for (int a = 0; a < A; ++a) hs[a] += h2[2 * c][r] * sw3[a * N + h0] + h2[2 * c + 1][r] * sw3[a * N + hA];
-    }
+    zp0 = z0;
+    zp1 = z1;
   }
+  epi2(7, 0);
+  epi2(7, 1);
 
+  F_STAMP(3);
   // ---- the loss head of row j (every lane group forms the same values; group 0 counts them)
   float dout[A];
   double ls[NL];
@@ -1262,22 +1326,34 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
     }
   }
 
-  // ---- head and second-tanh backward: W3 / b3 / b2 partials, dZ2ᵀ = (dout·W3) ⊙ (1 − H2ᵀ²) in place
+#ifdef QS_F_NOHEAD   // dev probe: a constant output gradient, no loss head
+#pragma unroll
+  for (int a = 0; a < A; ++a) dout[a] = 1e-3f;
+#endif
+  // ---- head and second-tanh backward, one hidden block at a time: its W3 partials
+  // Σ_rows dout·H2, dZ2 = (dout·W3) ⊙ (1 − H2²) in place of H2 (stored), its b2
+  // partial Σ_rows dZ2.  Block ob + 1 is prepared during step ob of the first
+  // backward chunk, beside its MFMAs.  Row sums within a block: blk_sum.
   float* pa = spa + w * PA;
+  const int rsel = 2 * ((j >> 3) & 1) + ((j >> 2) & 1);   // the hidden unit 16b + 4g + rsel a lane's block sum is for
+  const bool wsum = (j & 3) == 0;                          // one lane per (g, rsel) writes it
 #pragma unroll
   for (int a = 0; a < A; ++a) {
-    float o4[4];
-    const float da = dout[a];
-    f_lane_sum64([&](int x) { return da * h2[x >> 2][x & 3]; }, o4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pa[N + a * N + 16 * j + 4 * g + i] = o4[i];
-    float t = g == 0 ? dout[a] : 0.f;   // Σ_rows dout_a (group 0's 16 lanes)
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    const float t = f_row_sum(dout[a]);   // Σ_rows dout_a (every row holds the same dout)
     if (l == 0) pa[N + A * N + a] = t;
   }
+  // W3 partials Σ_rows dout·H2 of every block (they need H2 before dZ2 replaces it)
+#ifndef QS_F_NOHEAD
 #pragma unroll
   for (int b = 0; b < 16; ++b)
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float p4[4] = {dout[a] * h2[b][0], dout[a] * h2[b][1], dout[a] * h2[b][2], dout[a] * h2[b][3]};
+      const float sv = f_blk_sum(p4);
+      if (wsum) pa[N + a * N + 16 * b + 4 * g + rsel] = sv;
+    }
+#endif
+  auto prep2 = [&](int b) {   // dZ2 of block b, in place of H2, and its store
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int hh = 16 * b + 4 * g + r;
@@ -1286,16 +1362,21 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       for (int a = 0; a < A; ++a) gg += dout[a] * sw3[a * N + hh];
       const float hv = h2[b][r];
       h2[b][r] = gg * (1.f - hv * hv);
-      f_st(z2r, voff, (unsigned)(16 * b + r) * kstride, h2[b][r]);
     }
-  {
-    float o4[4];
-    f_lane_sum64([&](int x) { return h2[x >> 2][x & 3]; }, o4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pa[16 * j + 4 * g + i] = o4[i];
-  }
+    f_st4(z2r, voff, 64u * b, h2[b]);
+  };
+  prep2(0);
 
+  F_STAMP(4);
   // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (two hidden blocks per chunk); dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²) in place of H1ᵀ
+  // (stored at the chunk's end).  Beside the MFMAs: dZ2 of block ob + 1 during step ob of
+  // chunk 0, the b2 partial of dZ2 block ob during step ob of chunk 1, the b1 partials of
+  // chunk c's dZ1 blocks during the first two steps of chunk c + 1.
+  float* pb = spb + w * N;
+  auto b1sum = [&](int b) {
+    const float sv = f_blk_sum(h1[b]);
+    if (wsum) pb[16 * b + 4 * g + rsel] = sv;
+  };
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const float4* wc = next(nW1 + 8 + c);
@@ -1306,6 +1387,12 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       float4 n0 = w0, n1 = w1;
       if (ob + 1 < 16) { n0 = wc[(ob + 1) * 64 + l]; n1 = wc[(17 + ob) * 64 + l]; }
       __builtin_amdgcn_sched_barrier(0);
+      if (c == 0 && ob + 1 < 16) prep2(ob + 1);
+      if (c == 1) {
+        const float sb = f_blk_sum(h2[ob]);
+        if (wsum) pa[16 * ob + 4 * g + rsel] = sb;
+      }
+      if (c > 0 && ob < 2) b1sum(2 * (c - 1) + ob);
       d0 = mfma16(w0.x, h2[ob][0], d0);
       d1 = mfma16(w1.x, h2[ob][0], d1);
       d0 = mfma16(w0.y, h2[ob][1], d0);
@@ -1322,17 +1409,14 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       const float u0 = h1[2 * c][r], u1 = h1[2 * c + 1][r];
       h1[2 * c][r] = d0[r] * (1.f - u0 * u0);
       h1[2 * c + 1][r] = d1[r] * (1.f - u1 * u1);
-      f_st(z1r, voff, (unsigned)(32 * c + r) * kstride, h1[2 * c][r]);
-      f_st(z1r, voff, (unsigned)(32 * c + 16 + r) * kstride, h1[2 * c + 1][r]);
     }
+    f_st4(z1r, voff, 64u * (2 * c), h1[2 * c]);
+    f_st4(z1r, voff, 64u * (2 * c + 1), h1[2 * c + 1]);
   }
+  b1sum(14);
+  b1sum(15);
   M3Stream::sync();
-  {
-    float o4[4];
-    f_lane_sum64([&](int x) { return h1[x >> 2][x & 3]; }, o4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) spb[w * N + 16 * j + 4 * g + i] = o4[i];
-  }
+  F_STAMP(5);
   // the loss sums of the wave's rows (group 0), then the waves in order
 #pragma unroll
   for (int k = 0; k < NL; ++k)
@@ -1362,6 +1446,7 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       for (int v = 1; v < kFWaves; ++v) s += ldsn[v][k];
       lossp[(size_t)blockIdx.x * NL + k] = s;
     }
+    F_STAMP(6);
     __threadfence();
     last = atomicAdd(count, 1u) == gridDim.x - 1;
   }
@@ -2331,6 +2416,12 @@ int qs_value_head(int32_t mb, int32_t D, const int64_t* idx, const double* ret, 
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_value_head: ") + hipGetErrorString(e));
 }
+
+#ifdef QS_F_STAMP
+int qs_mlp3f_stamps(unsigned long long* host, int64_t n) {   // dev probe: copy out the phase stamps
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fstamp), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int32_t qs_mlp3f_tiles(int64_t K) { return K <= 0 ? 0 : (int32_t)((K + 16 * kFWaves - 1) / (16 * kFWaves)); }
 int64_t qs_mlp3f_pack_floats(int32_t I) { return I <= 0 ? 0 : f16_w1_floats(f16_ip(I)) + 2 * kFW2Floats; }

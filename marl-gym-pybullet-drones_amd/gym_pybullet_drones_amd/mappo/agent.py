@@ -352,13 +352,15 @@ class _F16Work(_M3Work):
     split-K weight-gradient GEMMs dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·Xa.  Same partial
     rows and reduction tasks as _M3Work.backward."""
 
+    w1_stream = True   # dW1 on a third stream beside dW2 (False: after it, one stream)
+
     def __init__(self, mlp, K, device):
         f0, f1, f2 = mlp.fcs
         lib = L.load()
         self.mlp, self.K, self.I, self.A = mlp, K, f0.in_features, f2.out_features
         f32 = dict(device=device, dtype=torch.float32)
         self.pack = torch.empty(int(lib.qs_mlp3f_pack_floats(self.I)), **f32)
-        self.h1, self.dz1, self.dz2 = (torch.empty((256, K), **f32) for _ in range(3))
+        self.h1, self.dz1, self.dz2 = (torch.empty((K, 256), **f32) for _ in range(3))   # row-major (qs_mlp3f_actor)
         self.xa = torch.empty((K, self.I), **f32)
         self.G = G = int(lib.qs_mlp3f_tiles(K))
         self.part_a = torch.empty((G, 256 * (1 + self.A) + self.A), **f32)
@@ -382,6 +384,16 @@ class _F16Work(_M3Work):
         pk, w1, w2, I = super().pack_segment(fb)
         return pk, w1, w2, I | L.QS_PACK_F16
 
+    def _splitk_rm(self, dst, dy, x, part, S):
+        """dst = dyᵀ·x over K rows (dy [K][N], x [K][M], both row-major) as S row-chunk
+        GEMMs into the preallocated partials (S = 1: one GEMM straight into dst)."""
+        K = dy.shape[0]
+        if S == 1:
+            torch.mm(dy.t(), x, out=dst)
+            return None
+        torch.bmm(dy.view(S, K // S, -1).transpose(1, 2), x.view(S, K // S, -1), out=part)
+        return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
+
     def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole):
         """qs_mlp3f_actor over the minibatch's agent rows (env-timesteps idx, D rows
         each, straight from the rollout table), then the weight gradients."""
@@ -397,8 +409,20 @@ class _F16Work(_M3Work):
         N, A = 256, self.A
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
-        w2 = self._splitk(f1.weight.grad, self.dz2, self.h1, True, self.pw2, self.S2)    # dW2 = dZ2ᵀ·H1
-        w1 = self._splitk(f0.weight.grad, self.dz1, self.xa, False, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
+        if self.w1_stream:
+            # dW1's small GEMMs (a few dozen workgroups each) beside dW2's on a third
+            # stream; joined before the caller's reductions
+            cur = torch.cuda.current_stream()
+            if getattr(self, '_s3', None) is None or self._s3.device != cur.device:
+                self._s3 = torch.cuda.Stream(device=cur.device)
+            self._s3.wait_stream(cur)
+            with torch.cuda.stream(self._s3):
+                w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)       # dW2 = dZ2ᵀ·H1
+            cur.wait_stream(self._s3)
+        else:
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)    # dW2 = dZ2ᵀ·H1
+            w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)    # dW1 = dZ1ᵀ·Xa
         for dst, t in ((f1.weight.grad, w2), (f0.weight.grad, w1)):
             if t is not None:
                 tasks.append(t)

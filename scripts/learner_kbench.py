@@ -68,7 +68,7 @@ def main():
     L.check(lib.qs_mlp3f_pack(I, L.ptr(W1), L.ptr(W2), L.ptr(pack), st()), "pack")
     G = int(lib.qs_mlp3f_tiles(K))
     xa = torch.empty(K, I, **f32)
-    H1, dZ2, dZ1 = (torch.empty(256, K, **f32) for _ in range(3))
+    H1, dZ2, dZ1 = (torch.empty(K, 256, **f32) for _ in range(3))   # row-major (qs_mlp3f_actor)
     pA, pB = torch.empty(G, 512 + 1, **f32), torch.empty(G, 256, **f32)
     dls, klo = torch.empty(A, **f32), torch.empty(1, **f32)
     acc = torch.zeros(4, dtype=torch.float64, device=dev)
@@ -82,13 +82,29 @@ def main():
     fl_fused = 2 * K * (32 * 256 + 2 * 256 * 256 + 256)
     report("qs_mlp3f_actor (fwd+head+bwd)", timed(fused), fl_fused)
     fused()
+    if hasattr(lib, "qs_mlp3f_stamps"):   # dev stamp build: phase durations of one launch (cycles)
+        import numpy as np
+        torch.cuda.synchronize()
+        fused()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (G * 8 * 8))()
+        lib.qs_mlp3f_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        assert lib.qs_mlp3f_stamps(buf, G * 8 * 8) == 0
+        st_ = np.frombuffer(buf, dtype=np.uint64).reshape(G * 8, 8).astype(np.int64)
+        t0 = st_[:, 0].min()
+        names = ["start->L1 done", "epi1", "L2", "head+dZ2", "bwd", "sums+partials"]
+        for k, nm in enumerate(names):
+            d = st_[:, k + 1] - st_[:, k]
+            print(f"  phase {nm:16s} median {np.median(d):9.0f}  p10 {np.percentile(d, 10):9.0f}  p90 {np.percentile(d, 90):9.0f}")
+        print(f"  wave start spread {np.percentile(st_[:, 0] - t0, 90):.0f}, end spread (p10..p90 of last stamp) "
+              f"{np.percentile(st_[:, 6] - t0, 10):.0f} .. {np.percentile(st_[:, 6] - t0, 90):.0f}")
     if "fused" in sys.argv[1:]:   # PMC passes: the fused kernel only
         return
     # dW1 = dZ1ᵀ·Xa
     dw1 = torch.empty(256, I, **f32)
     for S in (8, 16, 32, 64):
         part = torch.empty(S, 256, I, **f32)
-        a3 = dZ1.view(256, S, K // S).transpose(0, 1)
+        a3 = dZ1.view(S, K // S, 256).transpose(1, 2)
         b3_ = xa.view(S, K // S, I)
 
         def bmm_dw1():
@@ -98,6 +114,17 @@ def main():
         def sum_dw1():
             L.check(lib.qs_mlp_sum_partials(S, 256 * I, L.ptr(part), L.ptr(dw1), 256 * I, None, 0, None, st()), "sum")
         report(f"   its partial sum (S={S})", timed(sum_dw1))
+    for S in (16, 32, 64):
+        part = torch.empty(S, 256, 256, **f32)
+        a3 = dZ2.view(S, K // S, 256).transpose(1, 2)
+        b3_ = H1.view(S, K // S, 256)
+
+        def bmm_dw2():
+            torch.bmm(a3, b3_, out=part)
+        report(f"dW2 split-K bmm S={S}", timed(bmm_dw2), 2 * K * 256 * 256, 8 * K * 256)
+    dZ1 = dZ1.t().contiguous()   # [256][K] for the qs_mlp_wgrad* variants below
+    H1 = H1.t().contiguous()
+    dZ2 = dZ2.t().contiguous()
     Cx = int(lib.qs_mlp_wgrad_x_chunks(K, I))
     partx = torch.empty(Cx, 256, I, **f32)
 
@@ -117,14 +144,6 @@ def main():
             L.check(lib.qs_mlp_wgrad(K, 256, I, L.ptr(dZ1), L.ptr(xa), 0, C, L.ptr(part), st()), "wgrad")
         report(f"dW1 qs_mlp_wgrad C={C}", timed(wg_dw1), 2 * K * 256 * I, 4 * K * (256 + I))
     # dW2 = dZ2ᵀ·H1
-    for S in (16, 32, 64):
-        part = torch.empty(S, 256, 256, **f32)
-        a3 = dZ2.view(256, S, K // S).transpose(0, 1)
-        b3_ = H1.view(256, S, K // S).permute(1, 2, 0)
-
-        def bmm_dw2():
-            torch.bmm(a3, b3_, out=part)
-        report(f"dW2 split-K bmm S={S}", timed(bmm_dw2), 2 * K * 256 * 256, 8 * K * 256)
     for C in (16, 32, 64):
         part = torch.empty(C, 256, 256, **f32)
 

@@ -56,7 +56,7 @@ def test_fused_actor_matches_autograd(mb, D, I, A):
     L.check(lib.qs_mlp3f_pack(I, L.ptr(net[0].weight), L.ptr(net[2].weight), L.ptr(pack), stream), "qs_mlp3f_pack")
     G = int(lib.qs_mlp3f_tiles(K))
     xa = torch.full((K, I), np.nan, **f32)
-    H1, dZ2, dZ1 = (torch.full((256, K), np.nan, **f32) for _ in range(3))
+    H1, dZ2, dZ1 = (torch.full((K, 256), np.nan, **f32) for _ in range(3))   # row-major
     partA = torch.empty((G, 256 * (1 + A) + A), **f32)
     partB = torch.empty((G, 256), **f32)
     dls = torch.empty(A, **f32)
@@ -74,11 +74,11 @@ def test_fused_actor_matches_autograd(mb, D, I, A):
         torch.cuda.synchronize()
         assert torch.equal(xa, x)
         torch.testing.assert_close(mean_out, mean.detach(), rtol=1e-4, atol=2e-5)
-        torch.testing.assert_close(H1, h1.detach().t(), rtol=0, atol=2e-6)
+        torch.testing.assert_close(H1, h1.detach(), rtol=0, atol=2e-6)
         s2 = float(z2.grad.abs().max())
-        torch.testing.assert_close(dZ2, z2.grad.t(), rtol=1e-3, atol=1e-4 * s2)
+        torch.testing.assert_close(dZ2, z2.grad, rtol=1e-3, atol=1e-4 * s2)
         s1 = float(z1.grad.abs().max())
-        torch.testing.assert_close(dZ1, z1.grad.t(), rtol=1e-3, atol=1e-4 * s1)
+        torch.testing.assert_close(dZ1, z1.grad, rtol=1e-3, atol=1e-4 * s1)
         pa, pb = partA.double().sum(0), partB.double().sum(0)
         for got, want in ((pa[:256], net[2].bias.grad), (pa[256:256 + 256 * A].reshape(A, 256), net[4].weight.grad),
                           (pa[256 + 256 * A:], net[4].bias.grad), (pb, net[0].bias.grad)):
@@ -90,6 +90,6 @@ def test_fused_actor_matches_autograd(mb, D, I, A):
         assert float(acc[2]) == pytest.approx(float(el), rel=1e-6)
         assert float(acc[3]) == pytest.approx(float(kl), rel=1e-4, abs=1e-7)
         # weight gradients from the kernel's activations: dW2 = dZ2ᵀ·H1, dW1 = dZ1ᵀ·Xa
-        for got, want in ((dZ2.double() @ H1.double().t(), net[2].weight.grad), (dZ1.double() @ xa.double(), net[0].weight.grad)):
+        for got, want in ((dZ2.double().t() @ H1.double(), net[2].weight.grad), (dZ1.double().t() @ xa.double(), net[0].weight.grad)):
             sc = float(want.abs().max())
             torch.testing.assert_close(got.float(), want, rtol=1e-3, atol=1e-4 * sc)
