@@ -90,6 +90,8 @@ def parse():
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
     p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
+    p.add_argument("--critic-adam-side", type=int, default=0,
+                   help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
     p.add_argument("--dry-ms", type=float, default=2.0, help="--dry-run: ms per stand-in step of rank 0 (rank r: (1+r)x)")
     return p.parse_args()
@@ -356,6 +358,7 @@ def mappo_leg(args, ranks, T):
               rollout_steps=T, rollout_batch_size=E, opt_epochs=10,
               mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
     m.agent.side_stream = bool(args.side_stream)
+    m.agent.critic_adam_side = bool(args.critic_adam_side)
     from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
     _F16Work.w1_stream = bool(args.w1_stream)
     _M3Work.wgrad = tuple(w for w in args.wgrad.split(",") if w)

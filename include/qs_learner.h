@@ -242,8 +242,11 @@ int qs_adam_multi_pack(int32_t nseg, float* const* params, float* const* grads, 
  * gradient itself covers an element written elsewhere, e.g. logstd's).  The
  * gradients are not written: each reduced value goes straight into Adam.
  * Equals qs_mlp_sum_partials_multi on zeroed gradients followed by
- * qs_adam_multi_pack, bit for bit.  work: device uint32, zero before the first
- * call. */
+ * qs_adam_multi_pack, bit for bit.  work: qs_mlp_sum_adam_work_bytes() of
+ * device memory, zero before the first call (the launch leaves it zero; one
+ * work area per stream that may run the launch concurrently).  At most 2 016
+ * blocks of columns (QS_E_INVALID beyond). */
+int64_t qs_mlp_sum_adam_work_bytes(void);
 int qs_mlp_sum_adam(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial, float* const* d0,
                     const int64_t* n0, float* const* d1, const int64_t* n1, float* const* d2, const int32_t* task_seg,
                     int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,

@@ -1627,21 +1627,32 @@ __global__ void __launch_bounds__(kAdamBlock) adam_multi_kernel(AdamSegs S, unsi
 // block forms both segments' bias corrections; the last block to finish
 // commits the step counts (gates permitting).  The per-column summation order
 // is mlp_sum_multi_kernel's, so the step equals sum-then-Adam bit for bit.
+constexpr int kSumAdamGroup = 32;     // blocks per group word of mlp_sum_adam_kernel's arrival count
+constexpr int kSumAdamStride = 64;    // words between two counter words (256 B)
+constexpr int kSumAdamGroups = 63;    // at most 63 · 32 = 2 016 blocks (qs_mlp_sum_adam_work_bytes)
 __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_adam_kernel(MlpSumTasks tasks, AdamSegs S, SegOf seg,
                                                                    unsigned* done) {
   __shared__ float sc[kAdamMaxSeg][2];
   __shared__ bool last;
+#ifndef QS_SA_NOPOW
   if (threadIdx.x < (unsigned)S.n) {
     const AdamSeg& A = S.s[threadIdx.x];
     const unsigned t = (unsigned)(*A.step) + 1u;
     sc[threadIdx.x][0] = (float)(1.0 - powi_d((double)A.b1, t));
     sc[threadIdx.x][1] = (float)sqrt(1.0 - powi_d((double)A.b2, t));
   }
+#else
+  if (threadIdx.x < (unsigned)S.n) sc[threadIdx.x][0] = sc[threadIdx.x][1] = 1.f;
+#endif
   __syncthreads();
   // the element's parameter and moments are loaded with the partial rows
   mlp_sum_block(tasks, [&](int ti, float* dst, float u, float3 pmv) {
     const int si = seg.s[ti];
     const AdamSeg& A = S.s[si];
+#ifdef QS_SA_NOADAM
+    *dst = u + pmv.x;
+    return;
+#endif
     if (!gate_ok(A.gate, A.thr)) return;
     adam_elem(A, dst - A.g, u, pmv.x, pmv.y, pmv.z, sc[si][0], sc[si][1]);
   }, [&](int ti, float* dst) {
@@ -1649,9 +1660,25 @@ __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_adam_kernel(MlpSumTasks 
     const long long i = dst - A.g;
     return make_float3(A.p[i], A.m[i], A.v[i]);
   });
+#ifdef QS_SA_NOTAIL
+  return;
+#endif
   __syncthreads();
-  // every block read the step counts before counting itself
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  // every block read the step counts before counting itself.  Two-level count:
+  // a block arrives at its group's word (kSumAdamGroup blocks a group), a group's
+  // last block at the top word; the words lie kSumAdamStride apart, in separate
+  // L2 channels (same-address atomics serialise: one word for ~400 blocks was
+  // ~3 µs of tail)
+  if (threadIdx.x == 0) {
+    const unsigned grp = blockIdx.x / kSumAdamGroup, ngrp = (gridDim.x + kSumAdamGroup - 1) / kSumAdamGroup;
+    const unsigned gsz = min((unsigned)kSumAdamGroup, gridDim.x - grp * kSumAdamGroup);
+    unsigned* gw = done + (size_t)kSumAdamStride * (1 + grp);
+    last = false;
+    if (atomicAdd(gw, 1u) == gsz - 1) {
+      *gw = 0;
+      last = atomicAdd(done, 1u) == ngrp - 1;
+    }
+  }
   __syncthreads();
   if (last && threadIdx.x < (unsigned)S.n) {
     const AdamSeg& A = S.s[threadIdx.x];
@@ -2342,6 +2369,8 @@ static int adam_multi_launch(int32_t nseg, float* const* params, float* const* g
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string(name) + ": " + hipGetErrorString(e));
 }
 
+int64_t qs_mlp_sum_adam_work_bytes(void) { return (int64_t)kSumAdamStride * (1 + kSumAdamGroups) * 4; }
+
 int qs_mlp_sum_adam(int32_t n, const int32_t* G, const int64_t* P, const float* const* partial, float* const* d0,
                     const int64_t* n0, float* const* d1, const int64_t* n1, float* const* d2, const int32_t* task_seg,
                     int32_t nseg, float* const* params, float* const* grads, float* const* exp_avg,
@@ -2359,6 +2388,9 @@ int qs_mlp_sum_adam(int32_t n, const int32_t* G, const int64_t* P, const float* 
                        pack, w1_off, w2_off, pack_I, 0, S, name);
   if (rc != QS_OK) return rc;
   if (!task_seg || !work) return fail(QS_E_INVALID, std::string(name) + ": bad argument");
+  if (blocks > kSumAdamGroups * kSumAdamGroup)
+    return fail(QS_E_INVALID, std::string(name) + ": more than " + std::to_string(kSumAdamGroups * kSumAdamGroup) +
+                                  " blocks of columns");
   SegOf seg{};
   for (int i = 0; i < n; ++i) {   // every destination element inside its segment's gradient buffer
     if (task_seg[i] < 0 || task_seg[i] >= nseg) return fail(QS_E_INVALID, std::string(name) + ": bad task segment");

@@ -31,6 +31,16 @@
 
 #include "quadswarm.h"
 
+#ifdef QS_DEV_BUILD
+#include "step_kernel_dev.h"   // timing probes (dev builds only)
+#else
+namespace qs_dev {
+constexpr bool kNoCompute = false, kNoResetDraw = false;
+}
+#define QS_STAMP(k) do { } while (0)
+#define QS_STAMP_SINK(x) do { } while (0)
+#endif
+
 namespace qs {
 
 // One wavefront per workgroup: a wave owns floor(64/D) whole envs, so every
@@ -279,10 +289,10 @@ template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T r
 template <class T>
 __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T pos[3], const T q[4], const T vel[3],
                                         const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
-#if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOPID)
-  rpm[0] = rpm[1] = rpm[2] = rpm[3] = T(cf2x::HOVER_RPM) + T(1e-3) * pos[2];
-  return;
-#endif
+  if constexpr (qs_dev::kNoCompute) {
+    rpm[0] = rpm[1] = rpm[2] = rpm[3] = T(cf2x::HOVER_RPM) + T(1e-3) * pos[2];
+    return;
+  }
   using F = M<T>;
   const T dt = ctrl_dt;
   T R[9];
@@ -654,14 +664,6 @@ __device__ __forceinline__ float downwash16(float px, float py, float pz) {
   return f;
 }
 
-#ifdef QS_STAMPS_BUILD
-#define QS_STAMP(k)                                                                         \
-  do {                                                                                      \
-    if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define QS_STAMP(k) do { } while (0)
-#endif
 
 // ---------------------------------------------------------------- the step
 // TASK (qs_task) and ACT (qs_action_type) are compile-time: each launch runs
@@ -688,11 +690,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const int tid = threadIdx.x;
   const int D = P.D, N = P.N;
   const int H = CF ? CF / 2 : P.H;
-#if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOSUB)
-  const int S = 0;   // dev probe: memory traffic of the launch without the substeps and PID
-#else
-  const int S = CF ? 240 / CF : P.S;
-#endif
+  const int S = qs_dev::kNoCompute ? 0 : (CF ? 240 / CF : P.S);
   const int O = CF ? 12 + (CF / 2) * A + (kSpiral ? 11 : 0) : P.O;
   const int lenv = tid / D, d = tid - lenv * D;
   const int e = blockIdx.x * P.EPB + lenv;
@@ -704,21 +702,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   SA.fstride = (unsigned)N * (unsigned)sizeof(T);
   SA.voff = (unsigned)a * (unsigned)sizeof(T);
   QS_STAMP(0);
-#ifdef QS_STAGGER
-  // dev experiment: the second half of the grid (the second wave on each SIMD)
-  // starts its loads later, so its memory phase overlaps the first half's VALU phase
-#ifndef QS_STAGGER_MODE
-#define QS_STAGGER_MODE 0
-#endif
-  bool late;
-  if constexpr (QS_STAGGER_MODE == 0) late = blockIdx.x >= gridDim.x / 2;
-  else if constexpr (QS_STAGGER_MODE == 1) late = __builtin_amdgcn_s_getreg((3 << 11) | 4) & 1;   // HW_ID wave slot
-  else if constexpr (QS_STAGGER_MODE == 2) late = (blockIdx.x >> 5) & 1;
-  else late = blockIdx.x & 1;
-  if (late) {
-    for (int i = 0; i < QS_STAGGER; i += 8) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
 
   // ---------------- loads
   // Every global read of the launch is issued here, unconditionally and
@@ -852,20 +835,14 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   float cur_act[A];            // this step's action (newest history entry)
 #pragma unroll
   for (int k = 0; k < A; ++k) cur_act[k] = 0.f;
-#ifdef QS_STAMPS_BUILD
-  if (P.stamps) { volatile T sink = pos[0] + q[3] + pid[0] + tgt[0] + (T)total; (void)sink; }
-#endif
+  QS_STAMP_SINK(pos[0] + q[3] + pid[0] + tgt[0] + (T)total);
   // ---------------- action (trainer-provided or synthetic random policy)
   if (P.mode == MODE_STEP) {
     if (P.act_in) {
 #pragma unroll
       for (int k = 0; k < A; ++k) cur_act[k] = act_in[k];
     } else {
-#ifdef QS_X_NOPHILOX
-      U4 r = U4{(uint32_t)total * 2654435761u, genv, 0u, 0u};
-#else
       U4 r = philox(U4{(uint32_t)total, genv, 0u, (uint32_t)((STREAM_ACT << 24) | d)}, P.k0, P.k1);
-#endif
       const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
       for (int k = 0; k < A; ++k) cur_act[k] = 2.0f * u01<float>(rr[k]) - 1.0f;
@@ -885,10 +862,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         T r = T(cf2x::HOVER_RPM) * (T(1) + T(0.05) * T(act[0]));
         rpm[0] = rpm[1] = rpm[2] = rpm[3] = r;
       } else {
-#if defined(QS_X_NOCOMPUTE) || defined(QS_X_NOPID)
-        if (false)
-#endif
-        quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
+        if (!qs_dev::kNoCompute) quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
         if constexpr (ACT == QS_ACT_ONE_D_PID) {
           T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
           dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
@@ -1141,11 +1115,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     } else {
     // One substep (BaseAviary.py:343-372).  kAux: ground effect / drag /
     // downwash enabled; the common force-free path is compiled separately.
-#ifdef QS_SUB_NOUNROLL
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
     for (int sub = 0; sub < S; ++sub) {
 #if QS_SUB_CONTRACT
       // a*b+c → fma inside the substep (≈25 % fewer instructions).  The one
@@ -1316,9 +1286,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       for (int m = 0; m < 4; ++m) lrpm[m] = rpm[m];   // last_clipped_action (BaseAviary.py:372)
     }
     }   // general substep path
-#ifndef QS_X_NORB
     quat_to_rpy(q, rpy);   // readback (BaseAviary.py:374, 518)
-#endif
     total += 1;
     // Kinematic state is final unless this env auto-resets (rewritten below):
     // store now so the writes drain under the reward / obs phases.
@@ -1417,11 +1385,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // each env appends to its own ring, slot = its logged count mod log_per_env —
     // no atomic (a returned global slot made the finishing waves wait ~µs for it
     // and for all their outstanding stores, and they set the launch's tail).
-#ifdef QS_X_NOLOG
-    if (false) {
-#else
     if (dn) {
-#endif
       qs_episode_rec rec;
       rec.ret = ret; rec.len = len; rec.env = (int32_t)genv; rec.seq = total;
       P.log[(size_t)e * P.log_per_env + (unsigned)log_n % (unsigned)P.log_per_env] = rec;
@@ -1500,9 +1464,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   };
 
   QS_STAMP(4);
-#ifndef QS_X_NOTOBS
   if (valid && done_env && P.mode == MODE_STEP && P.tobs) write_obs_row(P.tobs + (size_t)a * O, obs_sc);
-#endif
 
   // ---------------- auto-reset (worker.step_env → env.reset)
   s.any = 0;
@@ -1517,9 +1479,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       // Phase 1: every group tries index 0 for its own env.
       if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
       __syncthreads();
-#ifndef QS_X_NORESETDRAW
-      eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset, init);
-#endif
+      if (!qs_dev::kNoResetDraw) eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset, init);
       if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
       __syncthreads();
       // Phase 2: for each still-rejected env, all groups search in parallel,
@@ -1590,11 +1550,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
   QS_STAMP(5);
   // ---------------- obs output
-#ifdef QS_X_NOOBS
-  if (false) {
-#else
   if (P.obs) {
-#endif
     if (P.mode == MODE_RESET_MASK) {
       if (valid && do_reset) write_obs_row(P.obs + (size_t)a * O, obs_sc);
     } else {
@@ -1645,11 +1601,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   if (!valid) return;
 
   // ---------------- store state of the envs that (auto-)reset
-#ifdef QS_X_NORESETSTORE
-  if (false) {
-#else
   if (do_reset) {
-#endif
     store_kin();
     if constexpr (kHover) {
 #pragma unroll

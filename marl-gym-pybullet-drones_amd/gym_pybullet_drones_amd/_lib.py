@@ -63,7 +63,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_mlp_bias_tanh", "qs_mlp_bwd_blocks", "qs_mlp_tanh_bwd", "qs_mlp_sum_partials",
            "qs_mlp_sum_partials_multi", "qs_adam_step", "qs_mlp3_tiles", "qs_mlp3_pack_floats",
            "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_mlp_wgrad", "qs_mlp_wgrad_chunks", "qs_adam_multi",
-           "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
+           "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
            "qs_learner_last_error")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
@@ -147,6 +147,8 @@ def load():
     L.qs_mlp3_pack_floats.restype = i64
     L.qs_mlp3f_pack_floats.restype = i64
     L.qs_mlp3f_work_bytes.restype = i64
+    L.qs_mlp_sum_adam_work_bytes.restype = i64
+    L.qs_mlp_sum_adam_work_bytes.argtypes = []
     _lib = L
     return L
 

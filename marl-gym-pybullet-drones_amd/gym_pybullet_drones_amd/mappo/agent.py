@@ -369,7 +369,9 @@ class _F16Work(_M3Work):
         self.mean = None   # tests: set to a [K][A] tensor to receive the actor output
         # split-K GEMMs for both weight gradients (qs_mlp_wgrad_x measured slower for dW1:
         # 19 µs + a 256-row partial sum vs 15.5 µs at 32 768 rows)
-        m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 1024), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
+        # dW2: 2 048-row chunks (half the partials of 1 024 at equal GEMM time: the
+        # reduction reads 4 MB less per minibatch; measured -3 µs)
+        m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 2048), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
         self.C2 = self.C1 = 0
         self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
         self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
@@ -768,6 +770,9 @@ class MAPPOAgent:
         # the direct iteration's actor on qs_mlp3f_actor (forward + loss head + backward in one launch)
         self.fused_actor = kwargs.get('fused_actor', True)
         self.side_stream = kwargs.get('side_stream', True)   # critic backward beside the actor's (_iteration_direct)
+        # one rank, fused actor: the critic's sums + Adam on the side stream too (its own
+        # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
+        self.critic_adam_side = kwargs.get('critic_adam_side', False)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
                                    share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
@@ -796,7 +801,10 @@ class MAPPOAgent:
         self.actor_opt = FlatBuffers(self.ac.actor, self.actor_lr, grad=self._reduce_buf[nc:nc + na])
         self._kl = self._reduce_buf[nc + na:]
         self._critic_bucket, self._actor_bucket = self._reduce_buf[:nc], self._reduce_buf[nc:]
-        self._adam_work = torch.zeros(4, dtype=torch.int32, device=self.device)   # qs_adam_multi's block counters
+        # qs_adam_multi's block counters / qs_mlp_sum_adam's arrival counts (one area per stream)
+        nw = max(4, int(L.load().qs_mlp_sum_adam_work_bytes()) // 4) if self.device.type == 'cuda' else 4
+        self._adam_work = torch.zeros(nw, dtype=torch.int32, device=self.device)
+        self._adam_work_c = torch.zeros(nw, dtype=torch.int32, device=self.device)
         if _dist_world() > 1:   # identical initial weights on every rank
             tdist.broadcast(self.actor_opt.flat, 0)
             tdist.broadcast(self.critic_opt.flat, 0)
@@ -946,11 +954,19 @@ class MAPPOAgent:
                 self._exchange_bucket(self._critic_bucket, world)
 
         if fused:
-            def critic_all(exchange):
+            def critic_all(exchange, own_adam=False):
                 v = critic_fwd()
                 L.check(lib.qs_value_head(mb, D, L.ptr(idx), L.ptr(rollouts.ret_env), L.ptr(v), L.ptr(self._dv),
                                           L.ptr(acc), L.ptr(self._vh_work), _stream()), "qs_value_head")
                 critic_bwd(exchange)
+                if own_adam:
+                    # the critic's Adam is ungated: its sums and step run here, beside
+                    # the actor's weight-gradient GEMMs, not after the join
+                    tc.extend((1, g.numel(), g, g, g.numel(), None, 0, None) for g in wc)
+                    FlatBuffers.sum_adam(tc, [0] * len(tc), [(self.critic_opt, None, 0.0)],
+                                         [self._ws_critic.pack_segment(self.critic_opt)], self._adam_work_c)
+                    tc.clear()
+                    wc.clear()
 
             def actor_all(exchange):
                 self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
@@ -960,11 +976,19 @@ class MAPPOAgent:
                     self._exchange_bucket(self._actor_bucket, world)
 
             if self.side_stream:
+                own = not multi and self.critic_adam_side
                 self._side.wait_stream(cur)
                 with torch.cuda.stream(self._side):
-                    critic_all(multi)
+                    critic_all(multi, own)
                 actor_all(multi)
                 cur.wait_stream(self._side)
+                if own:
+                    for g in [logstd.grad] + wa:
+                        ta.append((1, g.numel(), g, g, g.numel(), None, 0, None))
+                    gate = self._kl if self.target_kl > 0 else None
+                    FlatBuffers.sum_adam(ta, [0] * len(ta), [(self.actor_opt, gate, 1.5 * self.target_kl)],
+                                         [self._ws_actor.pack_segment(self.actor_opt)], self._adam_work)
+                    return
             else:
                 actor_all(False)
                 critic_all(False)

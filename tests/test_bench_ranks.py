@@ -33,7 +33,8 @@ def test_bench_two_ranks_max_over_ranks():
     # window hold rank 1's work too, and the reported time is the MAX of the windows
     per_rank = line["rank_ms_per_step"]
     assert len(per_rank) == 2
-    assert min(per_rank) >= 2 * dry_ms
+    # (10 % for the barrier-exit skew between the ranks: rank 0's own step is 1 x dry_ms)
+    assert min(per_rank) >= 0.9 * 2 * dry_ms
     assert line["ms_per_step"] == max(per_rank)
     assert line["value"] == pytest.approx(2 / (line["ms_per_step"] * 1e-3), rel=1e-9)
     # rank 0 runs in a torchrun child of the launcher: its grandparent is the

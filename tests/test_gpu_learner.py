@@ -216,8 +216,8 @@ def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, **variant):
 @pytest.mark.parametrize("E,T", [(256, 16), (32, 8)])
 @pytest.mark.parametrize("graphs", [False, True])
 def test_direct_update_side_stream_bit_identical(graphs, E, T):
-    """The critic forward / backward on their own stream (side_stream) change no
-    bit of the update; the direct iteration agrees with the autograd-driven fused
+    """The critic forward / backward (and, opt-in with the fused actor, its sums +
+    Adam) on their own stream (side_stream) change no bit of the update; the direct iteration agrees with the autograd-driven fused
     one (E=256, T=16: the same kernels at 16 384 actor / 2 048 critic rows)."""
     a_side, r_side = _hidden256_update(graphs, E, T)
     assert a_side._direct_ok()
@@ -226,6 +226,12 @@ def test_direct_update_side_stream_bit_identical(graphs, E, T):
     assert torch.equal(a_side.critic_opt.flat, a_one.critic_opt.flat)
     assert torch.equal(a_side.actor_opt.exp_avg_sq, a_one.actor_opt.exp_avg_sq)
     assert r_side == r_one
+    # the critic's sums + Adam in their own launch on the side stream (opt-in)
+    a_join, r_join = _hidden256_update(graphs, E, T, critic_adam_side=True)
+    assert torch.equal(a_side.actor_opt.flat, a_join.actor_opt.flat)
+    assert torch.equal(a_side.critic_opt.flat, a_join.critic_opt.flat)
+    assert torch.equal(a_side.critic_opt.exp_avg, a_join.critic_opt.exp_avg)
+    assert r_side == r_join
     a_fused, r_fused = _hidden256_update(graphs, E, T, direct=False)
     # (the fused path's critic, at 128 rows, is plain torch: ulp-level gradient
     # differences, which Adam's normalised steps carry up to ~lr/60 per step; 4 steps)

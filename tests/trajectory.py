@@ -11,9 +11,16 @@ ties (flagged, not failed)"): an env whose terminated/truncated flags differ
 while its state was still inside the tolerance is a tie; it is counted and
 dropped from the comparison from then on (its two copies now live different
 episodes).  A MultiHover reward that differs by more than the reward bound in
-an env where some drone sits within `tie_eps` of a reward branch threshold
-(MultiHoverAviary.py:140-179: |e_z| < 0.2, e_xy < 0.03, |e_z| < 0.03,
-|v_z| < 0.03) is a reward tie, counted, and not a failure.
+an env where some drone sits within the tie window of a reward branch
+threshold (MultiHoverAviary.py:140-179: |e_z| < 0.2, e_xy < 0.03, |e_z| < 0.03,
+|v_z| < 0.03) is a reward tie, counted, and not a failure.  The window is 10x
+the step's own max |Δpos| / |Δvel| (tie_window): a threshold can only be
+straddled by as much as the state differs.
+
+diverge(subject="oracle") runs the oracle's fp32 instantiation in the kernel's
+place: the departure of an exact fp32 restatement from fp64 — the reference's
+own sensitivity to fp32 rounding, against which the kernel's fp32 horizons are
+measured (tests/test_gpu_tolerance.py, scripts/horizon_compare.py).
 """
 import numpy as np
 import torch
@@ -52,8 +59,48 @@ def _mh_reward_tie(state, target, D, env, eps):
     return bool(near.any())
 
 
-def diverge(cfg, E, precision, steps, seed=11, env_offset=0, rew_bound=1e-4, tie_eps=1e-3, full_E=None,
-            on_step=None, on_reset=None):
+class _OracleSubject:
+    """The oracle at `precision` behind the swarm interface diverge() reads: the
+    exact-arithmetic subject (IEEE fp32 division / sqrt, libm transcendentals,
+    no contraction) whose departure from the fp64 oracle is the reference's own
+    sensitivity to fp32 rounding (CPU only)."""
+
+    class _R:
+        pass
+
+    def __init__(self, cfg, E, precision, env_offset):
+        self.o = make_oracle(cfg, E, precision, env_offset)
+        self.num_drones = self.o.D
+
+    def reset(self, seed):
+        self.o.reset(seed)
+
+    def step(self, actions, want_terminal=True):
+        c = self.o.step(actions)
+        r = self._R()
+        for k in ("terminated", "truncated", "reward"):
+            setattr(r, k, torch.from_numpy(np.asarray(c[k])))
+        return r
+
+    def get_state(self, block):
+        return torch.from_numpy(self.o.get_state(block))
+
+    def close(self):
+        self.o.close()
+
+
+def tie_window(dpos, dvel, eps=None):
+    """Width of the reward-threshold tie window at one step: a fixed eps if
+    given, else 10x the step's own |Δpos| / |Δvel| (the MultiHover branches
+    compare position errors and |vz| with thresholds, MH:140-179), floored at
+    1e-7 so that a zero-deviation step excuses nothing."""
+    if eps is not None:
+        return eps
+    return max(10.0 * max(dpos, dvel), 1e-7)
+
+
+def diverge(cfg, E, precision, steps, seed=11, env_offset=0, rew_bound=1e-4, tie_eps=None, full_E=None,
+            on_step=None, on_reset=None, subject="kernel"):
     """Run the kernel (at `precision`) and the fp64 oracle side by side for
     `steps` control steps.  Returns a dict of per-step curves and tie counts.
 
@@ -61,8 +108,14 @@ def diverge(cfg, E, precision, steps, seed=11, env_offset=0, rew_bound=1e-4, tie
     compare its envs [env_offset, env_offset + E) with an E-env oracle built with
     the same env_offset (the Philox key holds the global env id, so the slice is
     the same computation).  on_step(t, sw, result) runs property checks over
-    every env of the kernel after each step (on_reset(sw) after the reset)."""
-    if full_E is None:
+    every env of the kernel after each step (on_reset(sw) after the reset).
+    tie_eps: reward-threshold tie window (None: tie_window's 10x the step's own
+    state deviation).  subject="oracle": the oracle at `precision` in place of
+    the kernel (the exact-fp32 sensitivity reference, CPU)."""
+    if subject == "oracle":
+        sw = _OracleSubject(cfg, E, precision, env_offset)
+        lo = 0
+    elif full_E is None:
         sw = make_swarm(cfg, E, precision, env_offset)
         lo = 0
     else:
@@ -86,7 +139,8 @@ def diverge(cfg, E, precision, steps, seed=11, env_offset=0, rew_bound=1e-4, tie
         c = truth.step(None, nthreads=1 if E * D < 4096 else 8)
         if on_step is not None:
             on_step(t, sw, r)
-        torch.cuda.synchronize()
+        if subject != "oracle":
+            torch.cuda.synchronize()
         term_g, trunc_g = r.terminated[esl].cpu().numpy().astype(bool), r.truncated[esl].cpu().numpy().astype(bool)
         term_c, trunc_c = c["terminated"].astype(bool), c["truncated"].astype(bool)
         mism = live & ((term_g != term_c) | (trunc_g != trunc_c))
@@ -103,6 +157,7 @@ def diverge(cfg, E, precision, steps, seed=11, env_offset=0, rew_bound=1e-4, tie
         drew[~live] = 0.0
         if mh:
             done_c = term_c | trunc_c
+            eps_t = tie_window(curves["pos"][t], curves["vel"][t], tie_eps)
             for e in np.flatnonzero(drew > rew_bound):
                 # reward is formed from the pre-reset state: for a done env the
                 # terminal obs carries pos/vel, the target is the previous step's
@@ -114,7 +169,7 @@ def diverge(cfg, E, precision, steps, seed=11, env_offset=0, rew_bound=1e-4, tie
                     tgt = st_prev[F_TARGET:F_TARGET + 3]
                 else:
                     view, tgt = o, o[F_TARGET:F_TARGET + 3]
-                if _mh_reward_tie(view, tgt, D, e, tie_eps):
+                if _mh_reward_tie(view, tgt, D, e, eps_t):
                     rew_ties += 1
                     drew[e] = 0.0
         curves["rew"][t] = drew.max() if live.any() else 0.0
