@@ -86,6 +86,8 @@ def parse():
     p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO legs")
     p.add_argument("--mappo-iters", type=int, default=2, help="timed train steps (after one warm-up)")
     p.add_argument("--mappo-t32", type=int, default=1, help="also time the T=32 MAPPO leg (0 = skip)")
+    p.add_argument("--mappo-configs", default="C4,C5,ref",
+                   help="also time these MAPPO_LEGS trainer configs at N=1 ('' = none)")
     p.add_argument("--wgrad", default="", help="learner weight gradients on the MFMA qs_mlp_wgrad kernel (w1,w2; '' = GEMMs)")
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
@@ -95,6 +97,11 @@ def parse():
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
     p.add_argument("--dry-ms", type=float, default=2.0, help="--dry-run: ms per stand-in step of rank 0 (rank r: (1+r)x)")
     return p.parse_args()
+
+
+def progress(msg):
+    """A progress line on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def free_port():
@@ -189,27 +196,40 @@ def _ppid(pid):
         return int(f.read().rsplit(")", 1)[1].split()[1])
 
 
-def cpu_baseline(args, seconds):
+def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dyn", aux=()):
+    """The oracle (C++ restatement of the reference step, fp64) timed on this host's
+    cores at the reference's 176 envs (README.md:38-39: 22 workers x 8 envs) on the
+    same task, D, action type and physics as a GPU leg (BASELINE.md:36): a bounded
+    sample of about `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import qs_oracle
+    D = D or args.drones
+    act = act or args.act
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 22, os.cpu_count() or 1))
-    E = 176   # README.md:38-39: 176 envs on 22 workers
-    sim = qs_oracle.OracleSim(task="multihover", num_envs=E, num_drones=args.drones, act=args.act, precision=8,
-                              initial_xyzs=grid_layout(args.drones) if args.drones >= 6 else None)
+    E = 176
+    ophys, oaux = ("pyb", ("dw",)) if physics == "pyb_dw" else (physics, tuple(aux))
+    kw = dict(initial_xyzs=grid_layout(D)) if task == "multihover" and D >= 6 else {}
+    sim = qs_oracle.OracleSim(task=task, num_envs=E, num_drones=D, act=act, precision=8, physics=ophys, aux=oaux,
+                              **kw)
     sim.reset(0)
-    t0 = time.perf_counter()
-    sim.run_random(5, threads)
-    dt = time.perf_counter() - t0
-    steps = max(10, int(seconds / max(dt / 5, 1e-6)))
-    t0 = time.perf_counter()
-    sim.run_random(steps, threads)
-    dt = time.perf_counter() - t0
+    sim.run_random(2, threads)   # warm the thread pool
+    # doubling chunks until the budget is spent: a step's cost changes over an
+    # episode (C2's resets run the rejection loop), so no calibration from the first steps
+    steps, chunk, dt = 0, 4, 0.0
+    while dt < seconds:
+        t0 = time.perf_counter()
+        sim.run_random(chunk, threads)
+        dc = time.perf_counter() - t0
+        dt += dc
+        steps += chunk
+        # next chunk: double, but no longer than the rest of the budget at the last chunk's rate
+        chunk = max(1, min(2 * chunk, int((seconds - dt) / max(dc / chunk, 1e-9)) + 1))
     sim.close()
-    return {"value": E * args.drones * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
-            "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {E} envs x "
-                      f"{args.drones} drones x {steps} random-policy ctrl steps, OpenMP {threads} threads, "
-                      f"{dt:.1f} s"}
+    return {"value": E * D * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {task} {E} envs x "
+                      f"{D} drones, {act}, {physics}{'+' + '+'.join(aux) if aux else ''}, {steps} random-policy "
+                      f"ctrl steps, OpenMP {threads} threads, {dt:.1f} s"}
 
 
 def pmc_traffic(E, D, act):
@@ -344,19 +364,48 @@ def mappo_flops(T, E, D, O, A, H=256, epochs=10):
     return update, rollout
 
 
-def mappo_leg(args, ranks, T):
-    """Full MAPPO train steps on the bench's C3 envs (learn_mappo.py:196-203 hyper-parameters,
-    hidden 256, opt_epochs 10; minibatch scaled to the ~100x larger env batch)."""
-    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+# MAPPO trainer configurations beside the headline leg (C3 envs, learn_mappo.py
+# hyper-parameters): the reference's other trainer script on the Spiral config,
+# the 16-drone PYB_DW config, and the reference's own learner shape (176 envs,
+# mini_batch_size 32).  Keys: MAPPO constructor overrides + the env.
+LEARN_MAPPO = dict(clip_param=0.2, entropy_coef=0.005, action_scale=0.25, clip_obs=100)   # learn_mappo.py:207-216
+MAPPO_LEGS = {
+    # env_select_learn_mappo.py:262-283: T=64, mini_batch_size 32 (here 4 096 env-timesteps, as the
+    # headline leg), clip 0.1, entropy 5e-4, action_scale 0.4, norm_obs (reference_compat off: the
+    # rollout graph; the compat quirk re-normalises done steps on the host)
+    "C4": dict(task="spiral", drones=5, envs=8192, act="vel", physics="dyn", T=64, mb=4096, norm_obs=True,
+               clip_param=0.1, entropy_coef=0.0005, action_scale=0.4, clip_obs=10, reference_compat=False,
+               label="Spiral 5-drone x 8192 envs, VEL, DYN; env_select_learn_mappo.py:262-283"),
+    "C5": dict(task="multihover", drones=16, envs=8192, act="one_d_pid", physics="pyb_dw", T=256, mb=4096,
+               **LEARN_MAPPO, label="MultiHover 16-drone x 8192 envs, ONE_D_PID, PYB_DW; learn_mappo.py:196-216"),
+    # learn_mappo.py:196-216 at the README's 176 envs: 1 408 minibatches of 32 env-timesteps per epoch
+    "ref": dict(task="multihover", drones=8, envs=176, act="one_d_pid", physics="dyn", T=256, mb=32,
+                **LEARN_MAPPO, label="MultiHover 8-drone x 176 envs, ONE_D_PID, DYN, mini_batch_size 32 (the reference's "
+                      "learner shape, README.md:38-39, learn_mappo.py:196-216)"),
+}
+
+
+def mappo_leg(args, ranks, T, cfg=None):
+    """Full MAPPO train steps: by default on the bench's C3 envs (learn_mappo.py:196-216
+    hyper-parameters, hidden 256, opt_epochs 10; minibatch scaled to the ~100x larger
+    env batch), or one of MAPPO_LEGS."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary, SpiralFormationAviary
     from gym_pybullet_drones_amd.mappo import MAPPO
     from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
-    D, E = args.drones, args.envs
-    act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[args.act]
-    env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act, physics=Physics.DYN,
-                                               initial_xyzs=grid_layout(D) if D >= 6 else None)
+    cfg = dict(cfg or dict(task="multihover", drones=args.drones, envs=args.envs, act=args.act, physics="dyn",
+                           T=T, mb=args.mappo_mb, **LEARN_MAPPO))
+    D, E, T, mb = cfg.pop("drones"), cfg.pop("envs"), cfg.pop("T"), cfg.pop("mb")
+    task, phys, label = cfg.pop("task"), cfg.pop("physics"), cfg.pop("label", None)
+    act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[cfg.pop("act")]
+    physics = {"dyn": Physics.DYN, "pyb": Physics.PYB, "pyb_dw": Physics.PYB_DW}[phys]
+    if task == "spiral":
+        env_func = lambda seed=0: SpiralFormationAviary(num_drones=D, act=act, physics=physics)
+    else:
+        env_func = lambda seed=0: MultiHoverAviary(num_drones=D, act=act, physics=physics,
+                                                   initial_xyzs=grid_layout(D) if D >= 6 else None)
     m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
               rollout_steps=T, rollout_batch_size=E, opt_epochs=10,
-              mini_batch_size=args.mappo_mb, output_dir="/tmp/qs_bench_mappo")
+              mini_batch_size=mb, output_dir="/tmp/qs_bench_mappo", **cfg)
     m.agent.side_stream = bool(args.side_stream)
     m.agent.critic_adam_side = bool(args.critic_adam_side)
     from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
@@ -367,6 +416,7 @@ def mappo_leg(args, ranks, T):
         k, mm = km.split("x")
         _SPLITK_MIN_ROWS[(int(k), int(mm))] = int(rows)
     m.reset()
+    progress(f"mappo leg {label or 'C3'}: T={T} E={E} D={D} mb={mb}, warm-up train step")
     m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
     m.time_phases = True
     ranks.fence()
@@ -374,11 +424,14 @@ def mappo_leg(args, ranks, T):
     t0 = time.perf_counter()
     for _ in range(args.mappo_iters):
         phases.append(m.train_step()['phase_ms'])
+        progress(f"  train step {len(phases)}: {phases[-1]}")
     ranks.fence()
     dt = ranks.max((time.perf_counter() - t0) / args.mappo_iters)
     O, A = m.obs_dim, m.agent.ac.act_dim
     world = ranks.world
     graphed = world == 1 or m.agent.graph_collectives
+    rollout_graph = m._rollout_graph is not None
+    fused_actor = type(getattr(m.agent, "_ws_actor", None)).__name__ == "_F16Work"
     m.close()
     ph = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     upd_flop, roll_flop = mappo_flops(T, E, D, O, A)
@@ -390,11 +443,12 @@ def mappo_leg(args, ranks, T):
                                  "flop_per_update": upd_flop, "rollout_actor_flop": roll_flop,
                                  "train_step_tflops": (upd_flop + roll_flop) / dt / 1e12,
                                  "what": "PPO update: MLP fwd+bwd FLOP / update device time, fp32"},
-            "config": {"rollout_steps": T, "envs_per_gpu": E, "drones": D, "hidden": 256, "opt_epochs": 10,
-                       "mini_batch_size": args.mappo_mb,
-                       "minibatches_per_epoch": T * E // args.mappo_mb,
+            "config": {"workload": label, "rollout_steps": T, "envs_per_gpu": E, "drones": D, "obs_dim": O,
+                       "act_dim": A, "hidden": 256, "opt_epochs": 10, "mini_batch_size": mb,
+                       "minibatches_per_epoch": T * E // mb, "fused_actor_kernel": fused_actor,
+                       "overrides": cfg or None,
                        "reference": "learn_mappo.py: T=256, 176 envs, mini_batch_size 32 (1408 minibatches/epoch)",
-                       "graphs": "rollout + update" if graphed else "rollout",
+                       "graphs": ("rollout + " if rollout_graph else "") + ("update" if graphed else ""),
                        "grad_allreduce": ("one fused all-reduce per minibatch" + (", captured in the update graph"
                                                                                    if graphed else ""))
                        if world > 1 else None}}
@@ -441,6 +495,7 @@ def main():
         ranks.close()
         return
     E, D = args.envs, args.drones
+    progress("headline rollout leg")
     value, elapsed, kern_ms, steps, eps_done = sim_leg(args, ranks, "dyn")
     nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
@@ -449,12 +504,19 @@ def main():
         pv, _, pk, _, _ = sim_leg(args, ranks, "pyb")
         pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
                "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        if rank == 0 and not args.no_cpu_baseline:
+            pyb["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, physics="pyb")
     mappo = mappo_leg(args, ranks, args.mappo_steps) if args.mappo else None
     mappo32 = mappo_leg(args, ranks, 32) if (args.mappo and args.mappo_t32) else None
+    mappo_cfgs = None
+    if args.mappo and args.mappo_configs and world == 1:   # the other trainer configs, one GPU each
+        mappo_cfgs = {k: mappo_leg(args, ranks, c["T"], c) for k, c in MAPPO_LEGS.items()
+                      if k in args.mappo_configs.split(",")}
     configs = None
     if args.configs and world == 1:   # the other BASELINE configs, one GPU each
         configs = {}
         for name, c in EXTRA_CONFIGS.items():
+            progress(f"config leg {name}")
             v, el, km, st, ne = sim_leg(args, ranks, c["physics"], c["task"], c["envs"], c["drones"],
                                         c["act"], c["aux"])
             nb = c["bytes"] * c["envs"] * c["drones"]
@@ -465,6 +527,9 @@ def main():
             vr = valu_roofline(name, km)
             if vr:
                 configs[name]["valu_roofline"] = vr
+            if not args.no_cpu_baseline:   # BASELINE.md:36: the CPU restatement of the same config
+                configs[name]["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, c["task"], c["drones"],
+                                                             c["act"], c["physics"], c["aux"])
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_src = pmc_traffic(E, D, args.act)
@@ -488,6 +553,7 @@ def main():
             "pyb": pyb,
             "mappo": mappo,
             "mappo_t32": mappo32,
+            "mappo_configs": mappo_cfgs,
             "configs": configs,
         }
         print(json.dumps(line), flush=True)

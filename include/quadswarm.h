@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 1
+#define QS_ABI_VERSION 2   /* 2: qs_episode_log reports the records it wrote */
 
 /* ---- status codes ------------------------------------------------------ */
 #define QS_OK 0
@@ -221,7 +221,11 @@ int qs_state_io(qs_handle* h, int block, void* buf, int dir, void* stream);
  * completed.  qs_episode_log merges the rings in (seq, env) order — the
  * order the reference's env loop logs them — copies up to `cap` most-recent
  * records to `dst` (device) and writes the total number of episodes ever
- * logged to *total (host, synchronous).  An env that completes more episodes
+ * logged to *total and the number of records written to dst to *written
+ * (host, synchronous; written may be NULL): fewer than min(total, cap) when
+ * rings dropped episodes.  The selection runs on the device
+ * (a seq-distance histogram, then a compaction): O(cap) records cross to the
+ * host, and cap = 0 reads back the total alone.  An env that completes more episodes
  * than its ring holds between two reads keeps only its latest ones. */
 typedef struct qs_episode_rec {
   double ret;
@@ -230,7 +234,7 @@ typedef struct qs_episode_rec {
   int64_t seq;
 } qs_episode_rec;
 int qs_episode_log(qs_handle* h, qs_episode_rec* dst, int64_t cap,
-                   int64_t* total, void* stream);
+                   int64_t* total, int64_t* written, void* stream);
 
 /* 1 if an in-kernel reset rejection search hit its try cap (2^24) since the
  * last qs_reset (synchronous). */

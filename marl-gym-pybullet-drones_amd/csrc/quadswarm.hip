@@ -23,6 +23,91 @@ __global__ void calib_copy_kernel(float* __restrict__ dst, const float* __restri
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
+// ------------------------------------------------------------ episode log query
+// qs_episode_log selects the newest `cap` records of the per-env rings on the
+// device, so that O(cap) records — not the E·R ring slots — cross to the host.
+// An env's ring holds its last min(n, R) episodes (n = its logged count) in
+// slots (n − min(n, R)) … (n − 1) mod R.
+constexpr int kLogBins = 4096;   // seq-distance bins below the newest seq (the last one: ≥ 4095)
+struct LogWork {
+  unsigned long long total;      // Σ_e n_e
+  long long maxseq;              // newest seq over every ring
+  unsigned int nsel;             // records compacted by log_select_kernel
+  unsigned int pad;
+  unsigned int hist[kLogBins];   // live ring slots per (maxseq − seq) bin
+};
+
+__device__ __forceinline__ long long env_logged(const int32_t* env, int e) {
+  return env[(size_t)e * kEnvRec + kEnvLogWord];
+}
+
+// total and newest seq: block sums / maxima, then one global atomic per block
+__global__ void __launch_bounds__(256) log_scan_kernel(const int32_t* __restrict__ env,
+                                                       const qs_episode_rec* __restrict__ log, int E, int R,
+                                                       LogWork* w) {
+  __shared__ unsigned long long ssum[4];
+  __shared__ long long smax[4];
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  unsigned long long n = 0;
+  long long mx = -1;
+  if (e < E) {
+    const long long c = env_logged(env, e);
+    n = (unsigned long long)c;
+    // every live slot (seq grows along a ring, but qs_state_io may rewrite the counters)
+    for (long long i = c > R ? c - R : 0; i < c; ++i) mx = max(mx, log[(size_t)e * R + (size_t)(i % R)].seq);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_xor(n, o, 64);
+    mx = max(mx, __shfl_xor(mx, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) { ssum[threadIdx.x >> 6] = n; smax[threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = ssum[0] + ssum[1] + ssum[2] + ssum[3];
+    const long long m = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+    if (t) atomicAdd(&w->total, t);
+    if (m >= 0) atomicMax(&w->maxseq, m);
+  }
+}
+
+// histogram of (maxseq − seq) over the live ring slots: LDS bins, only the
+// non-empty ones flushed
+__global__ void __launch_bounds__(256) log_hist_kernel(const int32_t* __restrict__ env,
+                                                       const qs_episode_rec* __restrict__ log, int E, int R,
+                                                       LogWork* w) {
+  __shared__ unsigned int h[kLogBins];
+  for (int b = threadIdx.x; b < kLogBins; b += 256) h[b] = 0;
+  __syncthreads();
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const long long top = w->maxseq;
+  if (e < E) {
+    const long long n = env_logged(env, e);
+    for (long long i = n > R ? n - R : 0; i < n; ++i) {
+      const long long d = max(0LL, top - log[(size_t)e * R + (size_t)(i % R)].seq);
+      atomicAdd(&h[d < kLogBins - 1 ? (int)d : kLogBins - 1], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kLogBins; b += 256)
+    if (h[b]) atomicAdd(&w->hist[b], h[b]);
+}
+
+// every live record with seq ≥ thr, in no particular order (the host orders them)
+__global__ void __launch_bounds__(256) log_select_kernel(const int32_t* __restrict__ env,
+                                                         const qs_episode_rec* __restrict__ log, int E, int R,
+                                                         long long thr, qs_episode_rec* __restrict__ out,
+                                                         unsigned int out_cap, LogWork* w) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  const long long n = env_logged(env, e);
+  for (long long i = n > R ? n - R : 0; i < n; ++i) {
+    const qs_episode_rec r = log[(size_t)e * R + (size_t)(i % R)];
+    if (r.seq < thr) continue;
+    const unsigned int k = atomicAdd(&w->nsel, 1u);
+    if (k < out_cap) out[k] = r;
+  }
+}
+
 }  // namespace qs
 
 // ===========================================================================
@@ -59,6 +144,9 @@ struct qs_handle {
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
   int* rq = nullptr;            // deferred reset-search queue (2 + E ints), MultiHover layouts that can reject
+  qs::LogWork* logw = nullptr;  // qs_episode_log's device scratch
+  qs_episode_rec* log_sel = nullptr;   // its compacted records (log_sel_cap slots, grown on demand)
+  size_t log_sel_cap = 0;
   uint64_t seed = 0;
   bool reset_done = false;
   std::vector<double> orig_host;
@@ -290,7 +378,7 @@ extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
   (void)hipSetDevice(h->device);   // teardown: best effort, nothing to report to
-  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->err, h->stamps, h->rq};
+  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->err, h->stamps, h->rq, h->logw, h->log_sel};
   for (void* p : ptrs) if (p) (void)hipFree(p);
   delete h;
   return QS_OK;
@@ -402,34 +490,68 @@ int qs_state_io(qs_handle* h, int block, void* buf, int dir, void* stream) {
   return QS_OK;
 }
 
-int qs_episode_log(qs_handle* h, qs_episode_rec* dst, int64_t cap, int64_t* total, void* stream) {
+int qs_episode_log(qs_handle* h, qs_episode_rec* dst, int64_t cap, int64_t* total, int64_t* written, void* stream) {
   if (!h || !total) return fail(QS_E_INVALID, "qs_episode_log: null argument");
+  if (written) *written = 0;
   hipStream_t st = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(h->device));
   const int E = h->dims.num_envs, R = h->log_per_env;
-  std::vector<int32_t> rec((size_t)E * qs::kEnvRec);
-  HIP_TRY(hipMemcpyAsync(rec.data(), h->env, rec.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  const unsigned grid = (unsigned)((E + 255) / 256);
+  if (!h->logw) HIP_TRY(hipMalloc((void**)&h->logw, sizeof(qs::LogWork)));
+  qs::LogWork* w = h->logw;
+  // 1. total and the newest seq (one 16-byte read back)
+  HIP_TRY(hipMemsetAsync(w, 0, sizeof(qs::LogWork), st));
+  HIP_TRY(hipMemsetAsync(&w->maxseq, 0xff, sizeof(long long), st));   // −1: nothing logged
+  hipLaunchKernelGGL(qs::log_scan_kernel, dim3(grid), dim3(256), 0, st, h->env, h->log, E, R, w);
+  HIP_TRY(hipGetLastError());
+  struct { unsigned long long total; long long maxseq; } head;
+  HIP_TRY(hipMemcpyAsync(&head, w, sizeof(head), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  int64_t cnt = 0;
-  for (int e = 0; e < E; ++e) cnt += rec[(size_t)e * qs::kEnvRec + qs::kEnvLogWord];
-  *total = cnt;
-  if (!dst || cap <= 0 || cnt == 0) return QS_OK;
-  // the per-env rings hold each env's last min(logged, R) episodes: merge them in
-  // (step, env) order — the order the reference's env loop logs them — and keep
-  // the most recent `cap`
-  std::vector<qs_episode_rec> ring((size_t)E * R), all;
-  HIP_TRY(hipMemcpyAsync(ring.data(), h->log, ring.size() * sizeof(qs_episode_rec), hipMemcpyDeviceToHost, st));
+  *total = (int64_t)head.total;
+  if (!dst || cap <= 0 || head.total == 0) return QS_OK;
+  // 2. how far below the newest seq the newest `cap` live records reach
+  hipLaunchKernelGGL(qs::log_hist_kernel, dim3(grid), dim3(256), 0, st, h->env, h->log, E, R, w);
+  HIP_TRY(hipGetLastError());
+  std::vector<unsigned int> hist(qs::kLogBins);
+  HIP_TRY(hipMemcpyAsync(hist.data(), w->hist, hist.size() * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  for (int e = 0; e < E; ++e) {
-    const int64_t n = rec[(size_t)e * qs::kEnvRec + qs::kEnvLogWord];
-    for (int64_t i = std::max<int64_t>(0, n - R); i < n; ++i) all.push_back(ring[(size_t)e * R + (size_t)(i % R)]);
+  uint64_t live = 0, cum = 0;
+  for (unsigned int c : hist) live += c;
+  long long thr = -1;   // every live record, unless the newest `cap` lie within the binned window
+  uint64_t want = live;
+  for (int b = 0; b < qs::kLogBins - 1; ++b) {
+    cum += hist[b];
+    if (cum >= (uint64_t)cap) {   // bin b = seq maxseq − b holds the cap-th newest
+      thr = head.maxseq - b;
+      want = cum;
+      break;
+    }
   }
-  std::sort(all.begin(), all.end(), [](const qs_episode_rec& a, const qs_episode_rec& b) {
-    return a.seq != b.seq ? a.seq < b.seq : a.env < b.env;
-  });
-  const size_t k = std::min<size_t>(all.size(), (size_t)cap);
-  HIP_TRY(hipMemcpyAsync(dst, all.data() + (all.size() - k), k * sizeof(qs_episode_rec), hipMemcpyHostToDevice, st));
+  // 3. compact the records at or above the threshold (the cap newest plus the rest
+  // of the threshold seq's ties) and order them on the host: (seq, env) is the
+  // order the reference's env loop logs them
+  if (h->log_sel_cap < want) {
+    if (h->log_sel) HIP_TRY(hipFree(h->log_sel));
+    h->log_sel = nullptr;
+    h->log_sel_cap = std::max<size_t>((size_t)want, 1024);
+    HIP_TRY(hipMalloc((void**)&h->log_sel, h->log_sel_cap * sizeof(qs_episode_rec)));
+  }
+  hipLaunchKernelGGL(qs::log_select_kernel, dim3(grid), dim3(256), 0, st, h->env, h->log, E, R, thr, h->log_sel,
+                     (unsigned)want, w);
+  HIP_TRY(hipGetLastError());
+  std::vector<qs_episode_rec> sel((size_t)want);
+  HIP_TRY(hipMemcpyAsync(sel.data(), h->log_sel, sel.size() * sizeof(qs_episode_rec), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  const size_t k = std::min<size_t>(sel.size(), (size_t)cap);
+  auto older = [](const qs_episode_rec& a, const qs_episode_rec& b) {
+    return a.seq != b.seq ? a.seq < b.seq : a.env < b.env;
+  };
+  // the k newest, oldest first
+  std::nth_element(sel.begin(), sel.begin() + (sel.size() - k), sel.end(), older);
+  std::sort(sel.begin() + (sel.size() - k), sel.end(), older);
+  HIP_TRY(hipMemcpyAsync(dst, sel.data() + (sel.size() - k), k * sizeof(qs_episode_rec), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (written) *written = (int64_t)k;
   return QS_OK;
 }
 

@@ -56,6 +56,7 @@ class QsStepOut(ctypes.Structure):
 EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq", "<i8")])
 
 # Every symbol include/quadswarm.h declares (tests check the .so exports them).
+ABI_VERSION = 2   # include/quadswarm.h QS_ABI_VERSION
 EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
            "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
            # include/qs_learner.h
@@ -92,6 +93,9 @@ def load():
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
     L.qs_last_error.restype = ctypes.c_char_p
     L.qs_abi_version.restype = i32
+    if L.qs_abi_version() != ABI_VERSION:   # a stale build: its signatures differ from the argtypes below
+        raise QuadSwarmError(f"{LIB_PATH} has ABI version {L.qs_abi_version()}, this package binds "
+                             f"{ABI_VERSION}: rebuild the HIP extension")
     L.qs_create.argtypes = [ctypes.POINTER(QsSpec), i32, ctypes.POINTER(vp)]
     L.qs_destroy.argtypes = [vp]
     L.qs_get_dims.argtypes = [vp, ctypes.POINTER(QsDims)]
@@ -99,7 +103,7 @@ def load():
     L.qs_reset_envs.argtypes = [vp, vp, vp, vp]
     L.qs_step.argtypes = [vp, vp, ctypes.POINTER(QsStepOut), vp]
     L.qs_state_io.argtypes = [vp, i32, vp, i32, vp]
-    L.qs_episode_log.argtypes = [vp, vp, i64, ctypes.POINTER(i64), vp]
+    L.qs_episode_log.argtypes = [vp, vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64), vp]
     L.qs_reset_error.argtypes = [vp, ctypes.POINTER(i32)]
     L.qs_calib_copy.argtypes = [vp, vp, i64, vp]
     L.qs_gae.argtypes = [ctypes.c_int32, i64, vp, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_int32,

@@ -226,11 +226,11 @@ class QuadSwarm:
 
     def episode_log(self, cap=1 << 16):
         """(records ndarray[EPISODE_DTYPE] of the most recent ≤cap completed episodes, total ever)."""
-        dst = torch.zeros(cap * L.EPISODE_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
-        total = ctypes.c_int64(0)
-        L.check(self.lib.qs_episode_log(self._h, L.ptr(dst), cap, ctypes.byref(total), self._stream()),
-                "qs_episode_log")
-        n = min(total.value, cap)
+        dst = torch.empty(max(cap, 1) * L.EPISODE_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        total, written = ctypes.c_int64(0), ctypes.c_int64(0)
+        L.check(self.lib.qs_episode_log(self._h, L.ptr(dst) if cap > 0 else None, cap, ctypes.byref(total),
+                                        ctypes.byref(written), self._stream()), "qs_episode_log")
+        n = written.value   # fewer than min(total, cap) when rings dropped episodes
         recs = dst[: n * L.EPISODE_DTYPE.itemsize].cpu().numpy().view(L.EPISODE_DTYPE)
         order = np.lexsort((recs["env"], recs["seq"]))   # the reference's env-loop order per step
         return recs[order], total.value

@@ -165,7 +165,7 @@ class _TanhMLP3(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, w3, b3):
         lib, st = L.load(), _stream()
         K, N1, N2, A = x.shape[0], w1.shape[0], w2.shape[0], w3.shape[0]
-        ctx.fused = N1 == N2 == 256 and A <= 4 and x.shape[1] <= 1024
+        ctx.fused = N1 == N2 == 256 and A <= 4 and x.shape[1] <= 1024 and _m3_shape_ok(K, x.shape[1])
         if ctx.fused:   # qs_mlp3_fwd: both layers and the head on MFMA, activations kept transposed [N][K]
             I = x.shape[1]
             pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device=x.device, dtype=torch.float32)
@@ -439,6 +439,12 @@ def _f16_ok(mlp):
     return f2.out_features == 1 and f0.in_features <= 128
 
 
+def _m3_shape_ok(K, I):
+    """The qs_mlp3_* launchers' row limits: at least one row, [256][K] activations
+    and the [K][I] input addressed in 32 bits (larger batches take the GEMM path)."""
+    return 0 < K and K * 1024 < 2 ** 31 and K * I * 4 < 2 ** 31
+
+
 def _m3_ok(mlp, max_in=1024):
     f0, f1, f2 = mlp.fcs
     return (mlp._tanh3 and f0.out_features == 256 and f1.out_features == 256 and f2.out_features <= 4
@@ -484,7 +490,8 @@ class MLP(nn.Module):
     def forward(self, x):
         if (not torch.is_grad_enabled() and self._tanh3 and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32
                 and x.shape[1] <= 1024 and self.fcs[0].out_features == 256
-                and self.fcs[1].out_features == 256 and self.fcs[2].out_features <= 4):
+                and self.fcs[1].out_features == 256 and self.fcs[2].out_features <= 4
+                and _m3_shape_ok(x.shape[0], x.shape[1])):
             return self._infer_fused(x.contiguous())
         if self._fused_ok(x):
             f0, f1, f2 = self.fcs

@@ -351,6 +351,8 @@ class MAPPO:
         # loads are not allowed while capturing); the simulator call is skipped and the
         # RNG state restored, so the warm-up has no effect on the run
         rng = torch.cuda.get_rng_state()
+        rms = getattr(self.obs_normalizer, 'rms', None)
+        snap = rms.snapshot() if rms is not None else None   # the warm-up's normaliser update is undone too
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -358,6 +360,8 @@ class MAPPO:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         torch.cuda.set_rng_state(rng)
+        if snap is not None:
+            rms.restore(snap)
         rollouts.next_obs_slots[0].copy_(self.obs)
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
@@ -381,8 +385,11 @@ class MAPPO:
         if ev:
             ev[0].record()
         rollouts.next_obs_slots[0].copy_(self.obs)
-        # the quirk path (norm_obs + double normalisation on done) needs a host branch per step
-        graph_ok = self.use_graphs and not self.norm_obs and not self.norm_reward   # no collective in a step
+        # the quirk path (norm_obs + double normalisation on done, reference_compat) needs a
+        # host branch per step; the plain norm_obs update is device-only (in-place
+        # statistics, with several ranks an all-reduce captured like the update's)
+        graph_ok = (self.use_graphs and not self.norm_reward
+                    and not (self.norm_obs and getattr(self, 'reference_compat', True)))
         if graph_ok:
             if self._rollout_graph is None:
                 # the capture records the T steps; the stream runs them only at replay

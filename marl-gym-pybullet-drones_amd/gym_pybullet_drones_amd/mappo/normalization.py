@@ -24,11 +24,11 @@ class RunningMeanStd:
 
     def update(self, arr):
         x = arr.to(torch.float64)
-        n = torch.tensor(float(x.shape[0]), dtype=torch.float64, device=x.device)
+        n = float(x.shape[0])   # a host constant: no host-to-device copy (the step is graph-captured)
         s1 = x.sum(0)
         s2 = (x * x).sum(0)
         if _dist_on():
-            buf = torch.cat([s1.reshape(-1), s2.reshape(-1), n.reshape(1)])
+            buf = torch.cat([s1.reshape(-1), s2.reshape(-1), torch.full((1,), n, dtype=torch.float64, device=x.device)])
             tdist.all_reduce(buf)
             k = s1.numel()
             s1, s2, n = buf[:k].view_as(s1), buf[k:2 * k].view_as(s2), buf[2 * k]
@@ -40,15 +40,25 @@ class RunningMeanStd:
         self.update_from_moments(batch_mean, batch_var, n)
 
     def update_from_moments(self, batch_mean, batch_var, batch_count):
+        """normalization.py:42-60.  The statistics are updated in place, so a
+        captured rollout graph reads and writes the same tensors on every replay."""
         delta = batch_mean - self.mean
         tot_count = self.count + batch_count
         new_mean = self.mean + delta * batch_count / tot_count
         m_a = self.var * self.count
         m_b = batch_var * batch_count
         m_2 = m_a + m_b + delta * delta * self.count * batch_count / (self.count + batch_count)
-        self.var = m_2 / (self.count + batch_count)
-        self.mean = new_mean
-        self.count = batch_count + self.count
+        new_var = m_2 / (self.count + batch_count)
+        self.var.copy_(new_var)
+        self.mean.copy_(new_mean)
+        self.count.copy_(batch_count + self.count)
+
+    def snapshot(self):
+        return self.mean.clone(), self.var.clone(), self.count.clone()
+
+    def restore(self, snap):
+        for dst, src in zip((self.mean, self.var, self.count), snap):
+            dst.copy_(src)
 
 
 class BaseNormalizer:
@@ -92,9 +102,10 @@ class MeanStdNormalizer(BaseNormalizer):
         return {'mean': self.rms.mean.cpu().numpy(), 'var': self.rms.var.cpu().numpy()}
 
     def load_state_dict(self, saved):
+        # in place: a captured rollout graph keeps reading these tensors
         dev = self.rms.mean.device
-        self.rms.mean = torch.as_tensor(np.asarray(saved['mean']), dtype=torch.float64, device=dev)
-        self.rms.var = torch.as_tensor(np.asarray(saved['var']), dtype=torch.float64, device=dev)
+        self.rms.mean.copy_(torch.as_tensor(np.asarray(saved['mean']), dtype=torch.float64, device=dev))
+        self.rms.var.copy_(torch.as_tensor(np.asarray(saved['var']), dtype=torch.float64, device=dev))
 
 
 class RewardStdNormalizer(MeanStdNormalizer):

@@ -229,6 +229,7 @@ class VecRecordEpisodeStatistics(VecEnvWrapper):
     def reset(self, **kwargs):
         self.episode_return = np.zeros(self.num_envs)
         self.episode_length = np.zeros(self.num_envs)
+        self._synced, self._synced_seq = 0, -1   # the reset restarts the device episode counters
         for key in self.episode_stats:
             for i in range(self.num_envs):
                 self.episode_stats[key][i] *= 0
@@ -272,11 +273,24 @@ class VecRecordEpisodeStatistics(VecEnvWrapper):
 
     def sync_from_device(self):
         """Fast-path equivalent for step_t users: pull the episodes the kernel
-        logged since the last sync (device ring, env-order per step)."""
-        recs, total = self.venv.swarm.episode_log(cap=max(1, self.deque_size or 1))
-        new = total - getattr(self, "_synced", 0)
+        logged since the last sync (device ring, env order per step).  Returns
+        how many episodes ended since then; queues the newest of them that the
+        rings still hold (at most deque_size), each exactly once: a record is
+        new iff its seq (the step it ended at) is past the last synced one."""
+        sw = self.venv.swarm
+        _, total = sw.episode_log(cap=0)
+        last = getattr(self, "_synced", 0)
+        if total < last:   # the swarm was reset: its counters restarted
+            last, self._synced_seq = 0, -1
+        new = total - last
         self._synced = total
-        for rec in recs[max(0, len(recs) - new):]:
+        if new <= 0:
+            return 0
+        recs, _ = sw.episode_log(cap=new if self.deque_size is None else min(new, self.deque_size))
+        recs = recs[recs["seq"] > getattr(self, "_synced_seq", -1)]
+        if len(recs):
+            self._synced_seq = int(recs["seq"].max())
+        for rec in recs:
             self.return_queue.append(float(rec["ret"]))
             self.length_queue.append(float(rec["len"]))
         return new

@@ -21,7 +21,7 @@ def test_quadswarm_exports_every_declared_symbol():
         assert hasattr(lib, n), n
     assert set(names) <= set(_lib.EXPORTS)
     lib.qs_abi_version.restype = ctypes.c_int
-    assert lib.qs_abi_version() == 1
+    assert lib.qs_abi_version() == 2
 
 
 def test_create_rejects_bad_spec_without_gpu_work():

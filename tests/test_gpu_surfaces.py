@@ -117,6 +117,45 @@ def test_vec_record_episode_statistics():
     env.close()
 
 
+@pytest.mark.parametrize("deque_size", [None, 7])
+def test_sync_from_device_queues_each_episode_once(deque_size):
+    """VecRecordEpisodeStatistics.sync_from_device (the trainer's per-train-step
+    pull of the device episode log): at 8 192 envs an env's ring holds 8
+    episodes, and between two syncs (200 random-RPM steps, an episode every ~16
+    steps) envs end more than that, so the rings drop records.  Each sync must
+    queue exactly the surviving records newer than the last sync (the newest
+    deque_size of them), in (seq, env) order, none twice; and return how many
+    episodes ended in between.  qs_episode_log's device selection is checked
+    against a full read of the rings (cap above every live record)."""
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    from gym_pybullet_drones_amd.vec_env import SwarmVecEnv, VecRecordEpisodeStatistics
+    E, D = 8192, 4
+    venv = SwarmVecEnv(task="multihover", num_envs=E, num_drones=D, act=ActionType.RPM, seed=5, precision=4)
+    env = VecRecordEpisodeStatistics(venv, deque_size=deque_size)
+    env.reset()
+    sw = venv.swarm
+    last_seq, last_total, queued = -1, 0, []
+    for _ in range(3):
+        for _ in range(200):
+            venv.step_t()
+        full, total = sw.episode_log(cap=1 << 22)
+        assert len(full) < total   # the rings dropped records
+        assert np.all(np.diff(full["seq"]) >= 0)
+        for k in (1, 5, 1000):     # the device selection = the newest k of the full read
+            part, t2 = sw.episode_log(cap=k)
+            assert t2 == total
+            np.testing.assert_array_equal(part, full[-k:])
+        assert env.sync_from_device() == total - last_total
+        fresh = full[full["seq"] > last_seq]
+        if deque_size is not None:
+            fresh = fresh[-deque_size:]
+        queued += fresh["ret"].tolist()
+        want = queued if deque_size is None else queued[-deque_size:]
+        assert list(env.return_queue) == want
+        last_seq, last_total = int(full["seq"].max()), total
+    env.close()
+
+
 class _NpRunningMeanStd:
     """normalization.py:13-60 (numpy, float64)."""
 
@@ -142,8 +181,10 @@ def test_norm_obs_and_double_normalisation(reference_compat, tmp_path):
     from gym_pybullet_drones_amd.utils.enums import ActionType
     env_func = lambda seed=None, **kw: MultiHoverAviary(num_drones=4, act=ActionType.RPM)
     T, E = 12, 16
+    # eager rollout: the recorder reads every call back to the host
     m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=64, rollout_batch_size=E,
-              rollout_steps=T, mini_batch_size=32, opt_epochs=1, norm_obs=True, reference_compat=reference_compat)
+              rollout_steps=T, mini_batch_size=32, opt_epochs=1, norm_obs=True, reference_compat=reference_compat,
+              use_graphs=False)
     calls = []
 
     class Recorder:   # every obs-normaliser call, its input and output
@@ -182,6 +223,37 @@ def test_norm_obs_and_double_normalisation(reference_compat, tmp_path):
     # the rollout buffer holds the last normalised obs of each step
     np.testing.assert_allclose(m._rollouts.next_obs_slots[T].cpu().numpy(), calls[-1][1], rtol=0, atol=1e-6)
     m.close()
+
+
+def test_norm_obs_rollout_graph_matches_eager(tmp_path):
+    """With norm_obs and reference_compat off the rollout is one graph replay per
+    train step (the normaliser's statistics updated in place on the device): two
+    train steps — the second replay must read the statistics the first one left —
+    give the same normaliser state, rollout buffer and weights as the eager
+    rollout (reference config C4: env_select_learn_mappo.py:265-279 runs
+    norm_obs)."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    env_func = lambda seed=None, **kw: MultiHoverAviary(num_drones=4, act=ActionType.RPM)
+    runs = []
+    for graphs in (True, False):
+        m = MAPPO(env_func, output_dir=str(tmp_path / str(graphs)), use_gpu=True, seed=0, hidden_dim=64,
+                  rollout_batch_size=16, rollout_steps=12, mini_batch_size=32, opt_epochs=1, norm_obs=True,
+                  reference_compat=False, use_graphs=graphs)
+        m.reset()
+        for _ in range(2):
+            m.train_step()
+        assert (m._rollout_graph is not None) == graphs
+        rms = m.obs_normalizer.rms
+        runs.append(dict(mean=rms.mean.cpu().numpy(), var=rms.var.cpu().numpy(), count=float(rms.count),
+                         obs=m._rollouts.next_obs_slots.cpu().numpy(), rew=m._rollouts.rew_env.cpu().numpy(),
+                         w=m.agent.actor_opt.flat.cpu().numpy()))
+        m.close()
+    g, e = runs
+    assert g["count"] == e["count"] == pytest.approx(1e-4 + 16 * (1 + 2 * 12))   # the reset + 2 x 12 steps, 16 rows each
+    for k in ("mean", "var", "obs", "rew", "w"):
+        np.testing.assert_allclose(g[k], e[k], rtol=1e-6, atol=1e-7, err_msg=k)
 
 
 class _RefMLP(nn.Module):

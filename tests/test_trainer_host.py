@@ -54,3 +54,15 @@ def test_mappo_utils_match_their_definitions():
     assert ev == pytest.approx(1 - np.var(y - yp, ddof=1) / np.var(y, ddof=1), rel=1e-12)
     with pytest.raises(AssertionError):
         explained_variance(torch.zeros(2, 2), torch.zeros(2, 2))
+
+
+def test_fused_mlp_row_limits():
+    """The fused MLP paths (MLP.forward inference, _TanhMLP3) take a batch only
+    within the qs_mlp3_* launchers' limits (csrc/learner.hip: K > 0, K·256·4 and
+    K·I·4 below 2^31); anything else falls back to the GEMM path instead of
+    raising QS_E_INVALID."""
+    from gym_pybullet_drones_amd.mappo.agent import _m3_shape_ok
+    assert not _m3_shape_ok(0, 27)
+    assert _m3_shape_ok(1, 27)
+    assert _m3_shape_ok(2 ** 21 - 1, 27) and not _m3_shape_ok(2 ** 21, 27)      # 262 144 envs x 8 drones
+    assert not _m3_shape_ok(2 ** 19, 1024) and _m3_shape_ok(2 ** 19 - 1, 1024)
