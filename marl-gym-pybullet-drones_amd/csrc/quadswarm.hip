@@ -144,6 +144,7 @@ struct qs_handle {
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
   int* rq = nullptr;            // deferred reset-search queue (2 + E ints), MultiHover layouts that can reject
+  int num_cu = 256;             // compute units of the device (LDS residency plan)
   qs::LogWork* logw = nullptr;  // qs_episode_log's device scratch
   qs_episode_rec* log_sel = nullptr;   // its compacted records (log_sel_cap slots, grown on demand)
   size_t log_sel_cap = 0;
@@ -172,14 +173,23 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.stamps = h->stamps;
 }
 
-// LDS per workgroup: the history prefetch image plus as many obs rows as fit.
-static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 8192, kStageBudget = 48 * 1024;
-static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
+// LDS per workgroup: the history prefetch image plus obs rows staged per pass.
+// The staging is sized so that the launch's workgroups are resident at once:
+// `resident` = ⌈grid / CUs⌉ of them must share a CU's 160 KB (else the grid runs
+// in rounds, each paying the whole per-wave latency again: Spiral C4's 683
+// one-wave workgroups at 61 KB each ran as 512 + 171, 17.5 µs → 12.0 µs).  When
+// the whole grid cannot be resident even with fewer staged rows (MultiHover VEL:
+// 15 KB of history per workgroup), full staging is kept — more passes of fewer
+// rows cost more than the partial residency returns (C3-VEL 22.3 → 26.0 µs).
+static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 8192, kLdsGrain = 512, kStageBudget = 48 * 1024;
+static int lds_plan(const qs_dims& d, int resident, int* stage_rows, size_t* bytes) {
   const size_t hist = (size_t)d.hist_len * qs::kBlock * d.act_dim * sizeof(float);
   const size_t row = (size_t)d.obs_dim * sizeof(float);
   if (hist + row + kLdsStatic > kLdsBytes) return QS_E_INVALID;
-  const size_t budget = std::min(kStageBudget, kLdsBytes - kLdsStatic - hist);
   const int rows = (qs::kBlock / d.num_drones) * d.num_drones;
+  size_t per = kLdsBytes / (size_t)std::max(1, std::min(resident, 32));   // a workgroup's share at full residency
+  if (per < kLdsStatic + kLdsGrain + hist + row) per = kLdsBytes;          // unreachable: plain staging
+  const size_t budget = std::min(kStageBudget, per - kLdsStatic - kLdsGrain - hist);
   *stage_rows = (int)std::max<size_t>(1, std::min<size_t>(rows, budget / row));
   *bytes = hist + (size_t)*stage_rows * row;
   return QS_OK;
@@ -188,7 +198,7 @@ static int lds_plan(const qs_dims& d, int* stage_rows, size_t* bytes) {
 template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t st) {
   const int grid = (P.E + P.EPB - 1) / P.EPB;
   size_t lds = 0;
-  if (lds_plan(h->dims, &P.stage_rows, &lds) != QS_OK)
+  if (lds_plan(h->dims, (grid + h->num_cu - 1) / h->num_cu, &P.stage_rows, &lds) != QS_OK)
     return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
   const qs_spec& s = h->spec;
   bool ok;
@@ -284,6 +294,11 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   h->spec = s;
   h->spec.initial_xyzs = nullptr;
   h->device = device;
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
+      h->num_cu = cu;
+  }
   qs_dims& d = h->dims;
   d.num_envs = s.num_envs; d.num_drones = s.num_drones; d.num_agents = s.num_envs * s.num_drones;
   d.act_dim = A; d.hist_len = s.ctrl_freq / 2; d.substeps = s.pyb_freq / s.ctrl_freq;
@@ -291,7 +306,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   d.precision = s.precision; d.agent_fields = QS_AGENT_FIELDS; d.env_fields = QS_ENV_FIELDS;
   {
     int rows; size_t bytes;
-    if (lds_plan(d, &rows, &bytes) != QS_OK) {
+    if (lds_plan(d, 1, &rows, &bytes) != QS_OK) {
       delete h;
       return fail(QS_E_INVALID, "qs_create: action history (ctrl_freq // 2 entries) does not fit in LDS");
     }

@@ -6,14 +6,22 @@ os.environ["QS_STAMPS"] = "1"
 import numpy as np, torch
 from gym_pybullet_drones_amd import _lib as L
 from gym_pybullet_drones_amd.envs import QuadSwarm, grid_layout
-E, D = 16384, 8
-sw = QuadSwarm("multihover", num_envs=E, num_drones=D, act="one_d_pid", precision=4, initial_xyzs=grid_layout(D))
-obs = torch.empty((E, D, sw.obs_dim), device="cuda"); act = torch.empty((E, D, 1), device="cuda")
+from gym_pybullet_drones_amd.utils.enums import Physics
+sys.path.insert(0, ROOT)
+from bench import stagger_episodes
+# config: C3 (default), C5, C4 — python scripts/stamps.py [NAME]  (needs a QS_STAMPS_BUILD library)
+CFG = {"C3": ("multihover", 16384, 8, "one_d_pid", Physics.DYN), "C5": ("multihover", 8192, 16, "one_d_pid", Physics.PYB_DW),
+       "C4": ("spiral", 8192, 5, "vel", Physics.DYN)}[sys.argv[1] if len(sys.argv) > 1 else "C3"]
+task, E, D, actn, phys = CFG
+kw = dict(initial_xyzs=grid_layout(D)) if task == "multihover" else {}
+sw = QuadSwarm(task, num_envs=E, num_drones=D, act=actn, precision=4, physics=phys, **kw)
+obs = torch.empty((E, D, sw.obs_dim), device="cuda"); act = torch.empty((E, D, sw.act_dim), device="cuda")
 sw.reset(0, obs=obs)
+stagger_episodes(sw, task)
 for t in range(20):
     sw.step(None, obs=obs, actions_out=act)
 torch.cuda.synchronize()
-G = E // (64 // D)
+G = -(-E // (64 // D))
 buf = np.zeros(G * 8, np.uint64)
 lib = L.load(); lib.qs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
 L.check(lib.qs_debug_stamps(sw._h, buf.ctypes.data_as(ctypes.c_void_p), G * 8), "stamps")
