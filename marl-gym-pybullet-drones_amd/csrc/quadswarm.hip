@@ -143,7 +143,8 @@ struct qs_handle {
   int log_per_env = 0;
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
-  int* rq = nullptr;            // deferred reset-search queue (2 + E ints), MultiHover layouts that can reject
+  int* rq = nullptr;            // deferred reset-search queue (header + one 128-B record per env), MultiHover layouts that can reject
+  bool reject_free = false;     // MultiHover layout whose reset draws can never be rejected
   int num_cu = 256;             // compute units of the device (LDS residency plan)
   qs::LogWork* logw = nullptr;  // qs_episode_log's device scratch
   qs_episode_rec* log_sel = nullptr;   // its compacted records (log_sel_cap slots, grown on demand)
@@ -164,6 +165,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
   P.env_offset = s.env_offset;
   P.reset_queue = h->rq;
+  P.reject_free = h->reject_free ? 1 : 0;
   const double dt = 1.0 / s.pyb_freq;
   P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq); P.ctrl_hz = T(s.ctrl_freq);
   P.sp_R = T(s.spiral_radius); P.sp_OMEGA = T(2 * M_PI / s.spiral_period); P.sp_VZ = T(s.height_rate);
@@ -210,9 +212,9 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
     ok = qs::launch_task<T, qs::kTaskMarl>(s.act_type, grid, lds, st, P, s.ctrl_freq, s.pyb_freq, s.physics);
   if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
-  if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none): one workgroup each
-    // Several workgroups per queued env when few are queued; the grid is sized
-    // from E so a small shard does not pay 1024 empty workgroups every step.
+  if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none)
+    // Workgroups claim chunks of the queued envs' tries dynamically; the grid is
+    // sized from E so a small shard does not pay 1024 empty workgroups every step.
     static const int cap = [] {   // dev knob QS_RESET_GRID: the search grid's workgroup cap
       const char* v = getenv("QS_RESET_GRID");
       const int c = v ? atoi(v) : 0;
@@ -220,6 +222,10 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
     }();
     const int rgrid = std::min(cap, std::max(64, P.E * 4));
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
+    HIP_TRY(hipGetLastError());
+    // one thread per queued drone; workgroups past the queue's end return at once
+    const int fgrid = (int)(((int64_t)P.E * P.D + qs::kResetBlock - 1) / qs::kResetBlock);
+    hipLaunchKernelGGL(qs::reset_finalize_kernel<T>, dim3(fgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }
   return QS_OK;
@@ -331,13 +337,15 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   // whose every pair is >= 1 m apart in x or y never rejects (the bench's grid);
   // otherwise (the reference's default diagonal layout) rejected envs are queued
   // for reset_search_kernel instead of being searched inside the step.
-  bool may_reject = false;
-  if (s.task == QS_TASK_MULTIHOVER && s.num_drones <= qs::kResetMaxD)
-    for (int i = 0; i < s.num_drones; ++i)
-      for (int j = i + 1; j < s.num_drones; ++j)
-        if (std::fabs(h->orig_host[i * 3] - h->orig_host[j * 3]) < 1.0 &&
-            std::fabs(h->orig_host[i * 3 + 1] - h->orig_host[j * 3 + 1]) < 1.0)
-          may_reject = true;
+  bool can_reject = false;
+  for (int i = 0; i < s.num_drones; ++i)
+    for (int j = i + 1; j < s.num_drones; ++j)
+      if (std::fabs(h->orig_host[i * 3] - h->orig_host[j * 3]) < 1.0 &&
+          std::fabs(h->orig_host[i * 3 + 1] - h->orig_host[j * 3 + 1]) < 1.0)
+        can_reject = true;
+  // (z is clipped to [0.1, 1], so MH:96's z < 0.1 test never rejects either)
+  h->reject_free = s.task == QS_TASK_MULTIHOVER && !can_reject;
+  const bool may_reject = s.task == QS_TASK_MULTIHOVER && s.num_drones <= qs::kResetMaxD && can_reject;
   const size_t rs = (size_t)s.precision;
   const size_t N = d.num_agents;
   // per-env episode rings: at least 8 slots each, 65 536 records in all for small batches
@@ -352,13 +360,11 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
   if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
   if (may_reject && getenv("QS_INKERNEL_RESET_SEARCH") == nullptr) {
-    const size_t qn = 2 + 3 * (size_t)s.num_envs;   // count, done, env ids, per-slot best try, stopped count
+    // header line {count, finalize arrivals}, then one 128-B record per slot
+    // (initialised when the step kernel queues an env; qs::reset_search_kernel)
+    const size_t qn = (size_t)qs::kRqLine * (1 + (size_t)s.num_envs);
     if (hipMalloc((void**)&h->rq, sizeof(int) * qn) != hipSuccess) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
-    if (hipMemset(h->rq, 0, sizeof(int) * (2 + (size_t)s.num_envs)) ||
-        hipMemset(h->rq + 2 + s.num_envs, 0x7f, sizeof(int) * (size_t)s.num_envs) ||   // qs::kResetNone
-        hipMemset(h->rq + 2 + 2 * (size_t)s.num_envs, 0, sizeof(int) * (size_t)s.num_envs)) {
-      cleanup(); return fail(QS_E_HIP, "qs_create: memset");
-    }
+    if (hipMemset(h->rq, 0, sizeof(int) * qn)) { cleanup(); return fail(QS_E_HIP, "qs_create: memset"); }
   }
   if (s.precision == 8) {
     if (hipMemcpy(h->orig, h->orig_host.data(), 8 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }

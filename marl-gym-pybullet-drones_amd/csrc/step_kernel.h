@@ -56,6 +56,10 @@ constexpr int kEnvRec = 8;
 constexpr int kEnvRetWord = 4;
 constexpr int kEnvLogWord = 6;
 constexpr uint32_t kMaxResetTries = 1u << 24;
+constexpr int kResetNoneDev = 0x7f7f7f7f;   // deferred reset search: "no accepted try yet"
+// deferred reset search queue: 128-B records (int32 words); kRqWin is the high
+// half of the u64 claim word at word 0
+constexpr int kRqLine = 32, kRqWin = 1, kRqGang = 2, kRqEnv = 3;
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
 enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
 
@@ -228,7 +232,8 @@ template <class T> struct Params {
   qs_episode_rec* log;    // [E][log_per_env] per-env rings of completed episodes
   int log_per_env;
   int* err;               // [1] reset search overflow flag
-  int* reset_queue;       // deferred MultiHover reset searches: [0] count, [1] envs done, [2..] env ids; or NULL
+  int* reset_queue;       // deferred MultiHover reset searches (reset_search_kernel's records); or NULL
+  int reject_free;        // MultiHover layout whose reset draws can never be rejected: try 0 is the reset
   int stage_rows;         // obs rows staged in LDS per pass
   unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
   // per-step I/O
@@ -420,6 +425,7 @@ template <class T> struct Shared {
   int win_group;
   int any;
   uint32_t ep_bcast;
+  int qcount, qbase;        // deferred reset search: this workgroup's queue slots
   int32_t rec[kBlock * kEnvRec];   // per-env records on their way out
 };
 
@@ -1476,61 +1482,75 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     if (P.mode != MODE_RESET_ALL && do_reset) episode += 1;
     T init[3] = {orig[0], orig[1], orig[2]};
     if constexpr (kHover) {
-      // Phase 1: every group tries index 0 for its own env.
-      if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
-      __syncthreads();
-      if (!qs_dev::kNoResetDraw) eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset, init);
-      if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
-      __syncthreads();
-      // Phase 2: for each still-rejected env, all groups search in parallel,
-      // tries base+g; the smallest accepted index wins (= sequential order).
-      for (int k = 0; k < P.EPB; ++k) {
-        if (!s.need[k]) continue;   // block-uniform (LDS)
-        const int ek = blockIdx.x * P.EPB + k;
+      if (P.reject_free) {   // workgroup-uniform: no pair test, no barriers
+        if (do_reset && !qs_dev::kNoResetDraw)
+          reset_candidate(P, orig, d, 0u, genv, (uint32_t)episode, init[0], init[1], init[2]);
+      } else {
+        // Phase 1: every group tries index 0 for its own env.
+        if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
+        __syncthreads();
+        if (!qs_dev::kNoResetDraw) eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset, init);
+        if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
+        if (tid == 0) s.qcount = 0;
+        __syncthreads();
         if (P.reset_queue) {
           // deferred: reset_search_kernel (next launch, same stream) finds the first
-          // accepted try with a whole workgroup per env and rewrites the env's
-          // position, target and obs; try 0 stands in until then
-          if (tid == 0) {
-            const int slot = atomicAdd(&P.reset_queue[0], 1);
-            P.reset_queue[2 + slot] = ek;
-            s.need[k] = 0;
+          // accepted try and reset_finalize_kernel rewrites the env's position,
+          // target and obs; try 0 stands in until then.  One returning atomic per
+          // workgroup reserves its slots (a per-env one serialised the rejected
+          // envs of a workgroup behind ~1 µs round trips each).
+          int local = -1;
+          if (d == 0 && lenv < P.EPB && s.need[lenv]) local = atomicAdd(&s.qcount, 1);
+          __syncthreads();
+          if (tid == 0 && s.qcount) s.qbase = atomicAdd(&P.reset_queue[0], s.qcount);
+          __syncthreads();
+          if (local >= 0) {
+            int* const r = P.reset_queue + kRqLine * (1 + s.qbase + local);
+            // one 16-B store: claim word {chunks claimed 0, best try none}, gang 0, env id
+            *reinterpret_cast<int4*>(r) = make_int4(0, kResetNoneDev, 0, (int)(blockIdx.x * P.EPB + lenv));
+            s.need[lenv] = 0;
           }
           __syncthreads();
-          continue;
         }
-        const uint32_t genv_k = (uint32_t)(P.env_offset + ek);
-        // episode number of env k lives in its drone-0 thread; broadcast via LDS
-        __syncthreads();
-        if (tid == k * D) s.ep_bcast = (uint32_t)episode;
-        __syncthreads();
-        const uint32_t epk = s.ep_bcast;
-        uint32_t base = 1;
-        for (;;) {
-          if (tid < P.EPB) s.reject[tid] = 0;
-          if (tid == 0) s.win_group = 1 << 30;
+        // Phase 2 (in-kernel search): for each still-rejected env, all groups
+        // search in parallel, tries base+g; the smallest accepted index wins
+        // (= sequential order).
+        for (int k = 0; k < P.EPB; ++k) {
+          if (!s.need[k]) continue;   // block-uniform (LDS)
+          const int ek = blockIdx.x * P.EPB + k;
+          const uint32_t genv_k = (uint32_t)(P.env_offset + ek);
+          // episode number of env k lives in its drone-0 thread; broadcast via LDS
           __syncthreads();
-          const bool act_ = lenv < P.EPB && base + (uint32_t)lenv < kMaxResetTries;   // tries [0, cap)
-          eval_candidate(P, s, orig, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
-          if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
+          if (tid == k * D) s.ep_bcast = (uint32_t)episode;
           __syncthreads();
-          if (s.win_group < (1 << 30) || base + P.EPB >= kMaxResetTries) {
-            if (tid == 0) {
-              if (s.win_group < (1 << 30)) s.win_try[k] = base + (uint32_t)s.win_group;
-              else { s.win_try[k] = 0; atomicExch(P.err, 1); }
-            }
+          const uint32_t epk = s.ep_bcast;
+          uint32_t base = 1;
+          for (;;) {
+            if (tid < P.EPB) s.reject[tid] = 0;
+            if (tid == 0) s.win_group = 1 << 30;
             __syncthreads();
-            break;
+            const bool act_ = lenv < P.EPB && base + (uint32_t)lenv < kMaxResetTries;   // tries [0, cap)
+            eval_candidate(P, s, orig, lenv, d, base + (uint32_t)lenv, genv_k, epk, act_);
+            if (act_ && d == 0 && s.reject[lenv] == 0) atomicMin(&s.win_group, lenv);
+            __syncthreads();
+            if (s.win_group < (1 << 30) || base + P.EPB >= kMaxResetTries) {
+              if (tid == 0) {
+                if (s.win_group < (1 << 30)) s.win_try[k] = base + (uint32_t)s.win_group;
+                else { s.win_try[k] = 0; atomicExch(P.err, 1); }
+              }
+              __syncthreads();
+              break;
+            }
+            base += (uint32_t)P.EPB;
           }
-          base += (uint32_t)P.EPB;
+          if (tid == 0) s.need[k] = 2;   // resolved by phase 2 (win_try holds the index)
+          __syncthreads();
         }
-        if (tid == 0) s.need[k] = 2;   // resolved by phase 2 (win_try holds the index)
-        __syncthreads();
+        // try 0 accepted (the usual case): its draw is already in init (one Philox
+        // per drone less on the reset path, which sets the launch's tail)
+        if (do_reset && s.need[lenv] == 2)
+          reset_candidate(P, orig, d, s.win_try[lenv], genv, (uint32_t)episode, init[0], init[1], init[2]);
       }
-      // try 0 accepted (the usual case): its draw is already in init (one Philox
-      // per drone less on the reset path, which sets the launch's tail)
-      if (do_reset && s.need[lenv] == 2)
-        reset_candidate(P, orig, d, s.win_try[lenv], genv, (uint32_t)episode, init[0], init[1], init[2]);
     } else {
       if (do_reset) { init[0] = orig[0]; init[1] = orig[1]; init[2] = orig[2]; }
     }
@@ -1613,133 +1633,197 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
 // ------------------------------------------------- deferred reset search
 // MultiHoverAviary.reset's rejection loop (MH:83-102) for the envs the step
-// kernel queued (try 0 rejected).  Queue (int32): [0] count, [1] envs written,
-// [2, 2+E) env ids, then per queue slot the best accepted try so far (win) and
-// the number of workgroups that stopped searching it.
-// B = gridDim / count workgroups share an env: workgroup j tests chunks
-// j, j+B, j+2B, … of kResetChunk tries (thread t: tries 1 + kResetChunk·chunk +
-// t + 256·q, q < kResetPer, whole candidates), publishes its smallest accepted try with atomicMin and stops, and
-// stops as well once the best try is below its next chunk.  When all B have
-// stopped every chunk below the best try has been tested, so it is the first
-// accepted try of the sequential loop; the last one to stop writes the env's
-// position, target and obs row.  The last env written empties the
-// queue.  D <= kResetMaxD.
+// kernel queued (try 0 rejected).  Queue (int32, one 128-B line per record):
+// line 0 = header {count, finalize arrivals}; line 1 + slot = the slot's
+// record {claim word (u64), workgroups searching it (gang), env id}.  The
+// claim word holds the best accepted try so far (win) in its high half and the
+// number of chunks claimed (next) in its low half, so one returning 64-bit
+// atomicAdd both claims a chunk and reads the best try.  One line per slot:
+// packed 32 to a line, the claims of ~1 000 workgroups queued on the same few
+// lines.  The step kernel initialises a slot when it queues an env.
+//
+// Work is distributed dynamically.  An env's tries are cut into chunks of
+// kResetChunk (chunk c holds tries 1 + kResetChunk·c + t, thread t); a
+// workgroup claims the env's next chunk (issued one chunk ahead, so the
+// atomic's round trip runs under the Philox work), tests it, and publishes
+// its smallest accepted try into the win half (compare-and-swap, rare).
+// A workgroup leaves an env once its claimed chunk starts above the best try
+// (every chunk below it is claimed, so the env needs no more workers) or
+// above the cap, and then joins the open env with the fewest workers (ties:
+// the nearest after its own index, so workgroups spread).  At most
+// kResetGang workgroups join one env: at acceptance ~7e-4 (four drones
+// around the reference's diagonal layout) 16 × 256 tries resolve an env per
+// round with probability 0.94, and more claimants only queue on its line.
+// When the launch ends every claimed chunk has been tested, so `win` is the
+// smallest accepted try below every unclaimed chunk: the first accepted try
+// of the sequential loop.  reset_finalize_kernel (next launch) writes it.
+// The scan's loads are heuristic (a stale value only moves work around); the
+// claims and the best-try reads are returning atomics, exact.  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
-// candidates per thread and chunk: 4 (1 024-try chunks, a quarter of the
-// barrier rounds) measured slower on C2 (search 31 vs 23 µs): the longer
-// chunk delays every workgroup's exit test
-constexpr int kResetPer = 1;
-constexpr int kResetChunk = kResetBlock * kResetPer;  // tries per chunk
+constexpr int kResetChunk = kResetBlock;   // tries per chunk, one per thread
 constexpr int kResetMaxD = 8;
-constexpr int kResetNone = 0x7f7f7f7f;   // "no accepted try yet" (the queue's memset byte 0x7f)
+constexpr int kResetGang = 16;
+constexpr int kResetNone = kResetNoneDev;  // "no accepted try yet"
+
+__device__ __forceinline__ unsigned long long rq_claim(unsigned long long* w) {
+  return atomicAdd(w, 1ull);   // low half: chunks claimed; high half: best try
+}
+__device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
+  unsigned long long old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if ((int)(old >> 32) <= t) return;
+    const unsigned long long nw = ((unsigned long long)(unsigned)t << 32) | (old & 0xffffffffull);
+    const unsigned long long seen = atomicCAS(w, old, nw);
+    if (seen == old) return;
+    old = seen;
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) {
-  __shared__ int s_win, s_best;
-  __shared__ bool s_last;
+  __shared__ unsigned long long s_pick, s_claim;
+  __shared__ int s_win;
   int* const rq = P.reset_queue;
   const int n = rq[0];
-  if (n == 0) return;   // nothing queued (the usual step): the queue is empty already
-  const int D = P.D, E = P.E;
-  int* const qwin = rq + 2 + E;
-  int* const qstop = qwin + E;
+  if (n == 0) return;   // nothing queued (the usual step)
+  const int D = P.D;
+  auto rec = [&](int slot) { return rq + kRqLine * (1 + slot); };
+  const int tid = threadIdx.x;
   T orig[kResetMaxD][3];
 #pragma unroll
   for (int d = 0; d < kResetMaxD; ++d)
 #pragma unroll
     for (int k = 0; k < 3; ++k) orig[d][k] = d < D ? P.orig_xyz[d * 3 + k] : T(0);
-  const int G = gridDim.x;
-  const int B = n > 0 && n <= G ? G / n : 1;            // workgroups per env
-  const int first = n <= G ? (int)blockIdx.x % (n > 0 ? n : 1) : (int)blockIdx.x;
-  const int j = n <= G ? (int)blockIdx.x / (n > 0 ? n : 1) : 0;
-  const bool active = n > 0 && (n > G || (int)blockIdx.x < n * B);
-  for (int idx = first; active && idx < n; idx += (n <= G ? n : G)) {
-    const int e = rq[2 + idx];
+  const int home = (int)(blockIdx.x % (unsigned)n);
+  // the open env with the fewest workers below the gang cap, or -1 (workgroup-uniform)
+  auto pick = [&]() -> int {
+    if (tid == 0) s_pick = ~0ull;
+    __syncthreads();
+    for (int i = tid; i < n; i += kResetBlock) {
+      int j = home + i;
+      if (j >= n) j -= n;
+      int* const r = rec(j);
+      const unsigned long long cw = __hip_atomic_load(reinterpret_cast<unsigned long long*>(r), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+      const int g = __hip_atomic_load(r + kRqGang, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const long long base = 1 + (long long)(cw & 0xffffffffull) * kResetChunk;
+      if (base < (long long)(int)(cw >> 32) && base < (long long)kMaxResetTries && g < kResetGang)
+        atomicMin(&s_pick, ((unsigned long long)(unsigned)g << 32) | (unsigned)i);
+    }
+    __syncthreads();
+    const unsigned long long p = s_pick;
+    __syncthreads();   // s_pick is rewritten by the next pick
+    if (p == ~0ull) return -1;
+    int j = home + (int)(p & 0xffffffffu);
+    return j >= n ? j - n : j;
+  };
+  // first assignment without a scan: n·kResetGang workgroups start on their home env
+  int idx = (int)blockIdx.x < n * kResetGang ? home : pick();
+#ifdef QS_X_RSTATS
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  int st_picks = 1, st_joins = 0, st_chunks = 0, st_futile = 0, st_found = 0;
+#endif
+  while (idx >= 0) {
+    int* const r = rec(idx);
+    unsigned long long* const cwp = reinterpret_cast<unsigned long long*>(r);
+    const int e = r[kRqEnv];
     const uint32_t genv = (uint32_t)(P.env_offset + e);
     const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
-    int best = kResetNone;   // the env's best try as of the previous chunk (workgroup-uniform)
-    for (uint32_t c = (uint32_t)j;; c += (uint32_t)B) {
-      const uint32_t base = 1u + c * kResetChunk;
-      // the exit must be workgroup-uniform (the body holds barriers); the best
-      // try is read one chunk ahead — its ~µs atomic round trip runs under this
-      // chunk's Philox work — and a stale value only delays the exit
-      if ((int)base > best) break;
-      if (base >= kMaxResetTries) break;   // cap: tries >= kMaxResetTries are never accepted (as in-kernel)
-      int next_best = 0;
-      if (threadIdx.x == 0) next_best = __hip_atomic_load(&qwin[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // kResetPer whole candidates per thread: tries base + threadIdx.x + 256·q
-      int mine = kResetNone;
+    if (tid == 0) {
+      atomicAdd(r + kRqGang, 1);
+      s_claim = rq_claim(cwp);
+    }
+    __syncthreads();
+    unsigned long long cw = s_claim;
+    __syncthreads();
+#ifdef QS_X_RSTATS
+    ++st_joins;
+    if (1 + (long long)(cw & 0xffffffffull) * kResetChunk > (long long)(int)(cw >> 32)) ++st_futile;
+#endif
+    int found = kResetNone;   // this workgroup's accepted try (workgroup-uniform)
+    for (;;) {
+      const long long base = 1 + (long long)(cw & 0xffffffffull) * kResetChunk;   // workgroup-uniform
+      if (base > (long long)min((int)(cw >> 32), found) || base >= (long long)kMaxResetTries) break;
+      unsigned long long cw_next = 0;
+      if (tid == 0) cw_next = rq_claim(cwp);   // one chunk ahead: used after this chunk's tries
+      const uint32_t t = (uint32_t)base + (uint32_t)tid;
+      bool ok = t < kMaxResetTries;
+      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
 #pragma unroll
-      for (int q = 0; q < kResetPer; ++q) {
-        const uint32_t t = base + threadIdx.x + (uint32_t)(kResetBlock * q);
-        bool ok = t < kMaxResetTries;
-        T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
+      for (int d = 0; d < kResetMaxD; ++d) {
+        if (d < D && ok) {
+          reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
+          if (pz[d] < T(0.1)) ok = false;
 #pragma unroll
-        for (int d = 0; d < kResetMaxD; ++d) {
-          if (d < D && ok) {
-            reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
-            if (pz[d] < T(0.1)) ok = false;
-#pragma unroll
-            for (int i = 0; i < d; ++i)
-              if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
-          }
+          for (int i = 0; i < d; ++i)
+            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
         }
-        if (ok && (int)t < mine) mine = (int)t;
       }
-      if (threadIdx.x == 0) s_win = kResetNone;
+      if (tid == 0) s_win = kResetNone;
       __syncthreads();
-      if (mine != kResetNone) atomicMin(&s_win, mine);
-      if (threadIdx.x == 0) s_best = next_best;
+      if (ok) atomicMin(&s_win, (int)t);
+      if (tid == 0) s_claim = cw_next;
       __syncthreads();
       const int w = s_win;
-      best = s_best;
-      __syncthreads();   // s_win / s_best are rewritten next chunk
+      cw = s_claim;
+      __syncthreads();   // s_win / s_claim are rewritten next chunk
       if (w != kResetNone) {
-        if (threadIdx.x == 0) atomicMin(&qwin[idx], w);
-        break;            // this workgroup's later chunks hold only larger tries
+        found = w;       // the claim ahead is above w: the loop test leaves
+        if (tid == 0) rq_publish(cwp, w);
       }
+#ifdef QS_X_RSTATS
+      ++st_chunks; st_found += w != kResetNone;
+#endif
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // the atomicMin above is performed before this workgroup counts itself
-      // stopped; both are atomics, so no fence (≈3.5 µs each, MI355X_MICROARCH.md)
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      s_last = atomicAdd(&qstop[idx], 1) == B - 1;
-      // the last to stop reads the best try with an atomic read-modify-write,
-      // which returns the coherent value (a cached load may be stale)
-      if (s_last) s_best = atomicOr(&qwin[idx], 0);
-    }
-    __syncthreads();
-    if (s_last) {   // every workgroup of this env has stopped: s_best is the first accepted try
-      const int wv = s_best;
-      // no try below the cap accepted (every workgroup has stopped): flag the
-      // error and keep try 0, as the in-kernel search does
-      if (wv == kResetNone && threadIdx.x == 0) atomicExch(P.err, 1);
-      const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;
-      if ((int)threadIdx.x < D) {
-        const int d = threadIdx.x;
-        T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};
-        T ix, iy, iz;
-        reset_candidate(P, od, d, win, genv, episode, ix, iy, iz);
-        const size_t a = (size_t)e * D + d, N = (size_t)P.N;
-        P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
-        P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
-        P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(d + 1));   // MH:106
-        if (P.obs) {
-          float* o = P.obs + a * (size_t)P.O;
-          o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
-        }
-      }
-      if (threadIdx.x == 0) {
-        qwin[idx] = kResetNone; qstop[idx] = 0;   // ready for the next launch
-        // the last env to be written empties the queue: one same-address atomic
-        // per queued env, not per workgroup (1 024 of them serialise at L2 for
-        // ~16 µs).  Every workgroup with work read n before its env could finish;
-        // one that reads n after the reset had nothing to do.
-        if (atomicAdd(&rq[1], 1) == n - 1) { rq[0] = 0; rq[1] = 0; }
-      }
-    }
-    __syncthreads();
+    if (tid == 0) atomicSub(r + kRqGang, 1);
+    idx = pick();
+#ifdef QS_X_RSTATS
+    ++st_picks;
+#endif
   }
+#ifdef QS_X_RSTATS
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0 && (blockIdx.x % 32 == 0 || t_end - t_start > 5000))
+    printf("RS n=%d wg=%d us=%.2f picks=%d joins=%d futile=%d chunks=%d found=%d\n", n, (int)blockIdx.x,
+           (double)(t_end - t_start) * 0.01, st_picks, st_joins, st_futile, st_chunks, st_found);
+#endif
+}
+
+// Writes the first accepted try of every queued env (reset_search_kernel's
+// result): position, target (MH:106) and obs row, one thread per drone; the
+// last workgroup to arrive empties the queue.  No accepted try below the cap
+// flags the error and keeps try 0, as the in-kernel search does.
+template <class T>
+__global__ void __launch_bounds__(kResetBlock) reset_finalize_kernel(Params<T> P) {
+  int* const rq = P.reset_queue;
+  const int n = rq[0];
+  const int D = P.D;
+  const int active = (n * D + kResetBlock - 1) / kResetBlock;   // workgroups with drones to write
+  if ((int)blockIdx.x >= active) return;
+  const int g = (int)blockIdx.x * kResetBlock + (int)threadIdx.x;
+  if (g < n * D) {
+    const int idx = g / D, d = g - idx * D;
+    const int* const r = rq + kRqLine * (1 + idx);
+    const int e = r[kRqEnv];
+    const int wv = r[kRqWin];
+    if (wv == kResetNone) atomicExch(P.err, 1);
+    const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;
+    const uint32_t genv = (uint32_t)(P.env_offset + e);
+    const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
+    T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};
+    T ix, iy, iz;
+    reset_candidate(P, od, d, win, genv, episode, ix, iy, iz);
+    const size_t a = (size_t)e * D + d, N = (size_t)P.N;
+    P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
+    P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
+    P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(d + 1));   // MH:106
+    if (P.obs) {
+      float* o = P.obs + a * (size_t)P.O;
+      o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(&rq[1], 1) == active - 1) { rq[0] = 0; rq[1] = 0; }
 }
 
 }  // namespace qs

@@ -5,6 +5,7 @@
 // and DESIGN.md §4.
 //   QS_X_NOCOMPUTE    no PID and no substeps: the launch's memory floor
 //   QS_X_NORESETDRAW  no try-0 reset draw / pair test (the reset path's share)
+//   QS_X_RSTATS       per-workgroup counters of reset_search_kernel (printf)
 //   QS_STAMPS_BUILD   per-wave phase timestamps (QS_STAMPS=1 at run time,
 //                     scripts/stamps.py)
 #pragma once
