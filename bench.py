@@ -92,6 +92,7 @@ def parse():
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
     p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
+    p.add_argument("--wgrad-rm", type=int, default=1, help="learner: actor dW2 on qs_wgrad_rm (0 = torch.bmm GEMMs)")
     p.add_argument("--critic-adam-side", type=int, default=0,
                    help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
@@ -410,6 +411,7 @@ def mappo_leg(args, ranks, T, cfg=None):
     m.agent.critic_adam_side = bool(args.critic_adam_side)
     from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
     _F16Work.w1_stream = bool(args.w1_stream)
+    _F16Work.wgrad_rm = bool(args.wgrad_rm)
     _M3Work.wgrad = tuple(w for w in args.wgrad.split(",") if w)
     for item in filter(None, args.splitk.split(",")):   # "KxM=rows": split-K chunk rows of a weight gradient
         km, rows = item.split("=")

@@ -208,6 +208,15 @@ int qs_adam_step(int64_t n, float* params, const float* grads, float* exp_avg, f
  * [K/8][N][8].  (Measured slower than split-K GEMMs at the learner's shapes:
  * opt-in)  Sum with qs_mlp_sum_partials /
  * qs_mlp_sum_adam (G = chunks, P = N·M). */
+/* Split-K weight gradient of a 256-wide layer from row-major operands:
+ * partial[c][N][M] = Σ_{b in chunk c} A[b][N]·B[b][M] over C chunks of K/C
+ * rows (nn.Linear's dW = dYᵀ·X, AG:733 / AG:759, with A = dY [K][N] and B = X
+ * [K][M] as qs_mlp3f_actor writes them).  N, M multiples of 128, K a multiple
+ * of 8·C, pointers 16-byte aligned.  Sum with qs_mlp_sum_adam (G = C,
+ * P = N·M).  Replaces the C batched row-chunk GEMMs of torch.bmm. */
+int qs_wgrad_rm(int64_t K, int32_t N, int32_t M, const float* A, const float* B, int32_t C, float* partial,
+                void* stream);
+
 int32_t qs_mlp_wgrad_x_chunks(int64_t K, int32_t M);
 int qs_mlp_wgrad_x(int64_t K, int32_t N, int32_t M, const float* AT, int32_t at_blocked, const float* X,
                    float* partial, void* stream);

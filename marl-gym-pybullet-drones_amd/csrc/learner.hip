@@ -2045,6 +2045,101 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_bwd_kernel(long long K, const
 }
 }  // namespace
 
+
+// ------------------------------------------------- row-major weight gradient
+// nn.Linear's dW = dYᵀ·X for the 256-wide layers of a PPO minibatch (dW2 =
+// dZ2ᵀ·H1, AG:733 / AG:759) straight from the row-major [K][N] / [K][M]
+// activations the fused actor kernel writes, as chunk partials
+// partial[c][N][M] (c < C, K/C rows each) summed by qs_mlp_sum_adam.
+//
+// A workgroup = 8 waves owns one 128×128 output tile of one chunk; waves 0-3
+// take the chunk's first half of rows and waves 4-7 the second (a 64×64
+// sub-tile each), and the halves are added through LDS at the end, so the
+// chip holds two waves per SIMD without doubling the partials.  One k-step =
+// 4 rows: lane (g, i) loads A[k + g][n0 + 4i .. +3] and B[k + g][m0 + 4i .. +3]
+// as two 16-byte loads (four full 256-B row segments per wave instruction) and
+// issues 16 v_mfma_f32_16x16x4_f32: element e of its A float4 is the A operand
+// for output rows n0 + 4i' + e, element f of the B float4 the B operand for
+// columns m0 + 4j + f, so no operand is shuffled.  Loads run four k-steps
+// ahead.  blockIdx → (chunk, tile) keeps the four tiles of a chunk, which read
+// the same rows, on one XCD (shared L2).
+constexpr int kWrWaves = 8;
+constexpr int kWrAhead = 4;
+__global__ void __launch_bounds__(64 * kWrWaves) wgrad_rm_kernel(int N, int M, int Kc, int C,
+                                                                const float* __restrict__ A,
+                                                                const float* __restrict__ B,
+                                                                float* __restrict__ partial) {
+  __shared__ float4 red[4][16][64];   // the second half's accumulators, [sub-tile][acc][lane]
+  const int TN = N / 128, TM = M / 128, T = TN * TM, total = T * C;
+  int flat = (int)blockIdx.x;
+  if (total % 8 == 0) flat = (flat & 7) * (total / 8) + (flat >> 3);   // XCD = blockIdx % 8
+  const int chunk = flat / T, tile = flat - chunk * T;
+  const int tn = tile / TM, tm = tile - tn * TM;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, i = l & 15;
+  const int wq = w & 3, kh = w >> 2;
+  const int nb = 128 * tn + 64 * (wq >> 1), mb = 128 * tm + 64 * (wq & 1);
+  const int half = Kc / 2, steps = half / 4;
+  const long long k0 = (long long)chunk * Kc + (long long)kh * half + g;
+  const float4* pa = reinterpret_cast<const float4*>(A + k0 * N + nb + 4 * i);
+  const float4* pb = reinterpret_cast<const float4*>(B + k0 * M + mb + 4 * i);
+  const long long sa = (long long)N, sb = (long long)M;   // float4 stride of 4 rows
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[e][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 ra[kWrAhead], rb[kWrAhead];
+#pragma unroll
+  for (int u = 0; u < kWrAhead; ++u) {
+    ra[u] = u < steps ? pa[u * sa] : make_float4(0.f, 0.f, 0.f, 0.f);
+    rb[u] = u < steps ? pb[u * sb] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int s0 = 0; s0 < steps; s0 += kWrAhead) {
+#pragma unroll
+    for (int u = 0; u < kWrAhead; ++u) {
+      const int st = s0 + u;
+      if (st < steps) {   // uniform
+        const float4 a = ra[u], b = rb[u];
+        if (st + kWrAhead < steps) {
+          ra[u] = pa[(long long)(st + kWrAhead) * sa];
+          rb[u] = pb[(long long)(st + kWrAhead) * sb];
+        }
+        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int f = 0; f < 4; ++f) acc[e][f] = mfma16(av[e], bv[f], acc[e][f]);
+      }
+    }
+  }
+  if (kh == 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        red[wq][4 * e + f][l] = make_float4(acc[e][f][0], acc[e][f][1], acc[e][f][2], acc[e][f][3]);
+  __syncthreads();
+  if (kh == 1) return;
+  // output (n, m) of acc[e][f][r]: n = nb + 4·(4g + r) + e, m = mb + 4i + f; the
+  // four f of one (e, r) are one float4 of a partial row
+  float* const out = partial + (size_t)chunk * N * M;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float v[4][4];   // [r][f]
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float4 o = red[wq][4 * e + f][l];
+      v[0][f] = acc[e][f][0] + o.x; v[1][f] = acc[e][f][1] + o.y;
+      v[2][f] = acc[e][f][2] + o.z; v[3][f] = acc[e][f][3] + o.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + 4 * (4 * g + r) + e;
+      *reinterpret_cast<float4*>(out + (size_t)n * M + mb + 4 * i) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+    }
+  }
+}
+
 extern "C" {
 
 const char* qs_learner_last_error(void) { return g_err.c_str(); }
@@ -2543,6 +2638,20 @@ int qs_mlp_wgrad(int64_t K, int32_t N, int32_t M, const float* AT, const float* 
                        (int)M, R, AT, B, partial);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_mlp_wgrad: ") + hipGetErrorString(e));
+}
+
+
+int qs_wgrad_rm(int64_t K, int32_t N, int32_t M, const float* A, const float* B, int32_t C, float* partial,
+                void* stream) {
+  if (K <= 0 || N <= 0 || M <= 0 || N % 128 || M % 128 || C <= 0 || K % (8 * (int64_t)C) || !A || !B || !partial ||
+      ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)partial & 15) || K / C > (int64_t)1 << 30 ||
+      (int64_t)(N / 128) * (M / 128) * C > (int64_t)1 << 30)
+    return fail(QS_E_INVALID, "qs_wgrad_rm: bad argument (N, M multiples of 128, K a multiple of 8·C, 16-B aligned)");
+  const int grid = (N / 128) * (M / 128) * C;
+  hipLaunchKernelGGL(wgrad_rm_kernel, dim3(grid), dim3(64 * kWrWaves), 0, (hipStream_t)stream, (int)N, (int)M,
+                     (int)(K / C), (int)C, A, B, partial);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : fail(QS_E_HIP, std::string("qs_wgrad_rm: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

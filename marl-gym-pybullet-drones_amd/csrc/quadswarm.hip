@@ -144,6 +144,7 @@ struct qs_handle {
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
   int* rq = nullptr;            // deferred reset-search queue (header + one 128-B record per env), MultiHover layouts that can reject
+  int* rqs = nullptr;           // its per-slot {gang, closed} words (uncached)
   bool reject_free = false;     // MultiHover layout whose reset draws can never be rejected
   int num_cu = 256;             // compute units of the device (LDS residency plan)
   qs::LogWork* logw = nullptr;  // qs_episode_log's device scratch
@@ -165,6 +166,7 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
   P.env_offset = s.env_offset;
   P.reset_queue = h->rq;
+  P.reset_status = h->rqs;
   P.reject_free = h->reject_free ? 1 : 0;
   const double dt = 1.0 / s.pyb_freq;
   P.dt = T(dt); P.hdt = T(dt / 2); P.hdt2 = T((dt / 2) * (dt / 2)); P.ctrl_dt = T(1.0 / s.ctrl_freq); P.ctrl_hz = T(s.ctrl_freq);
@@ -222,10 +224,6 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
     }();
     const int rgrid = std::min(cap, std::max(64, P.E * 4));
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
-    HIP_TRY(hipGetLastError());
-    // one thread per queued drone; workgroups past the queue's end return at once
-    const int fgrid = (int)(((int64_t)P.E * P.D + qs::kResetBlock - 1) / qs::kResetBlock);
-    hipLaunchKernelGGL(qs::reset_finalize_kernel<T>, dim3(fgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }
   return QS_OK;
@@ -360,11 +358,19 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
   if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
   if (may_reject && getenv("QS_INKERNEL_RESET_SEARCH") == nullptr) {
-    // header line {count, finalize arrivals}, then one 128-B record per slot
+    // header line {count, envs written}, then one 128-B record per slot
     // (initialised when the step kernel queues an env; qs::reset_search_kernel)
     const size_t qn = (size_t)qs::kRqLine * (1 + (size_t)s.num_envs);
     if (hipMalloc((void**)&h->rq, sizeof(int) * qn) != hipSuccess) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
-    if (hipMemset(h->rq, 0, sizeof(int) * qn)) { cleanup(); return fail(QS_E_HIP, "qs_create: memset"); }
+    // the per-slot {gang, closed} words, uncached: reset_search_kernel's scan must
+    // see other XCDs' atomics
+    const size_t sn = 2 * (size_t)s.num_envs;
+    if (hipExtMallocWithFlags((void**)&h->rqs, sizeof(int) * sn, hipDeviceMallocUncached) != hipSuccess) {
+      cleanup(); return fail(QS_E_NOMEM, "qs_create: hipExtMallocWithFlags failed");
+    }
+    if (hipMemset(h->rq, 0, sizeof(int) * qn) || hipMemset(h->rqs, 0, sizeof(int) * sn)) {
+      cleanup(); return fail(QS_E_HIP, "qs_create: memset");
+    }
   }
   if (s.precision == 8) {
     if (hipMemcpy(h->orig, h->orig_host.data(), 8 * 3 * s.num_drones, hipMemcpyHostToDevice)) { cleanup(); return fail(QS_E_HIP, "qs_create: copy"); }
@@ -399,7 +405,7 @@ extern "C" int qs_debug_stamps(qs_handle* h, unsigned long long* host, int64_t n
 int qs_destroy(qs_handle* h) {
   if (!h) return QS_OK;
   (void)hipSetDevice(h->device);   // teardown: best effort, nothing to report to
-  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->err, h->stamps, h->rq, h->logw, h->log_sel};
+  void* ptrs[] = {h->st, h->env, h->hist, h->orig, h->log, h->err, h->stamps, h->rq, h->rqs, h->logw, h->log_sel};
   for (void* p : ptrs) if (p) (void)hipFree(p);
   delete h;
   return QS_OK;

@@ -57,9 +57,12 @@ constexpr int kEnvRetWord = 4;
 constexpr int kEnvLogWord = 6;
 constexpr uint32_t kMaxResetTries = 1u << 24;
 constexpr int kResetNoneDev = 0x7f7f7f7f;   // deferred reset search: "no accepted try yet"
-// deferred reset search queue: 128-B records (int32 words); kRqWin is the high
-// half of the u64 claim word at word 0
-constexpr int kRqLine = 32, kRqWin = 1, kRqGang = 2, kRqEnv = 3;
+// deferred reset search queue (reset_search_kernel): 128-B lines of int32
+// words in `reset_queue` — line 0 {count, envs written}, line 1 + slot {claim
+// word (u64: chunks claimed | best try << 32), env id, gang} — and two words per
+// slot {gang hint, closed} in the uncached `reset_status`
+constexpr int kRqLine = 32, kRqWin = 1, kRqEnv = 2, kRqGang = 3;
+constexpr int kRqDone = 1 << 24;   // gang value of a slot whose env has been written
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
 enum { MODE_STEP = 0, MODE_RESET_ALL = 1, MODE_RESET_MASK = 2 };
 
@@ -233,6 +236,7 @@ template <class T> struct Params {
   int log_per_env;
   int* err;               // [1] reset search overflow flag
   int* reset_queue;       // deferred MultiHover reset searches (reset_search_kernel's records); or NULL
+  int* reset_status;      // their per-slot {gang, closed} words (uncached memory)
   int reject_free;        // MultiHover layout whose reset draws can never be rejected: try 0 is the reset
   int stage_rows;         // obs rows staged in LDS per pass
   unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
@@ -1495,8 +1499,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         __syncthreads();
         if (P.reset_queue) {
           // deferred: reset_search_kernel (next launch, same stream) finds the first
-          // accepted try and reset_finalize_kernel rewrites the env's position,
-          // target and obs; try 0 stands in until then.  One returning atomic per
+          // accepted try and rewrites the env's position, target and obs; try 0
+          // stands in until then.  One returning atomic per
           // workgroup reserves its slots (a per-env one serialised the rejected
           // envs of a workgroup behind ~1 µs round trips each).
           int local = -1;
@@ -1505,9 +1509,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           if (tid == 0 && s.qcount) s.qbase = atomicAdd(&P.reset_queue[0], s.qcount);
           __syncthreads();
           if (local >= 0) {
-            int* const r = P.reset_queue + kRqLine * (1 + s.qbase + local);
-            // one 16-B store: claim word {chunks claimed 0, best try none}, gang 0, env id
-            *reinterpret_cast<int4*>(r) = make_int4(0, kResetNoneDev, 0, (int)(blockIdx.x * P.EPB + lenv));
+            const int slot = s.qbase + local;
+            // claim word {chunks claimed 0, best try none}, env id, gang 0; status {0, open}
+            *reinterpret_cast<int4*>(P.reset_queue + kRqLine * (1 + slot)) =
+                make_int4(0, kResetNoneDev, (int)(blockIdx.x * P.EPB + lenv), 0);
+            *reinterpret_cast<int2*>(P.reset_status + 2 * slot) = make_int2(0, 0);
             s.need[lenv] = 0;
           }
           __syncthreads();
@@ -1633,32 +1639,39 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
 // ------------------------------------------------- deferred reset search
 // MultiHoverAviary.reset's rejection loop (MH:83-102) for the envs the step
-// kernel queued (try 0 rejected).  Queue (int32, one 128-B line per record):
-// line 0 = header {count, finalize arrivals}; line 1 + slot = the slot's
-// record {claim word (u64), workgroups searching it (gang), env id}.  The
-// claim word holds the best accepted try so far (win) in its high half and the
-// number of chunks claimed (next) in its low half, so one returning 64-bit
-// atomicAdd both claims a chunk and reads the best try.  One line per slot:
-// packed 32 to a line, the claims of ~1 000 workgroups queued on the same few
-// lines.  The step kernel initialises a slot when it queues an env.
+// kernel queued (try 0 rejected).  Per queue slot (kRq* above): a claim word
+// holding the number of chunks claimed (low half) and the best accepted try
+// so far (high half) on a 128-B line of its own, so one returning 64-bit
+// atomicAdd both claims a chunk and reads the best try, and the number of
+// workgroups searching the slot (gang); in uncached memory, a copy of the gang
+// count and a closed flag for the scan, written without waiting.
+// The step kernel initialises a slot when it queues an env.
 //
 // Work is distributed dynamically.  An env's tries are cut into chunks of
 // kResetChunk (chunk c holds tries 1 + kResetChunk·c + t, thread t); a
 // workgroup claims the env's next chunk (issued one chunk ahead, so the
 // atomic's round trip runs under the Philox work), tests it, and publishes
-// its smallest accepted try into the win half (compare-and-swap, rare).
-// A workgroup leaves an env once its claimed chunk starts above the best try
-// (every chunk below it is claimed, so the env needs no more workers) or
-// above the cap, and then joins the open env with the fewest workers (ties:
-// the nearest after its own index, so workgroups spread).  At most
-// kResetGang workgroups join one env: at acceptance ~7e-4 (four drones
-// around the reference's diagonal layout) 16 × 256 tries resolve an env per
-// round with probability 0.94, and more claimants only queue on its line.
-// When the launch ends every claimed chunk has been tested, so `win` is the
-// smallest accepted try below every unclaimed chunk: the first accepted try
-// of the sequential loop.  reset_finalize_kernel (next launch) writes it.
-// The scan's loads are heuristic (a stale value only moves work around); the
-// claims and the best-try reads are returning atomics, exact.  D <= kResetMaxD.
+// its smallest accepted try (rq_publish) and the closed flag.  A workgroup
+// leaves an env once its claimed chunk starts above the best try (every chunk
+// below it is claimed, so the env needs no more workers) or above the cap,
+// and then joins the open env with the fewest workers (ties: the nearest after
+// its own index, so workgroups spread); with more envs than workgroups it
+// first takes envs b, b + G, b + 2G, … in turn.  At most kResetGang
+// workgroups join one env: at acceptance ~7e-4 (four drones around the
+// reference's diagonal layout) 16 × 256 tries resolve an env per round with
+// probability 0.94, and more claimants only queue on its line.
+//
+// The last workgroup to leave an env writes it (position, target, obs row):
+// by then every chunk below the best try has been tested, so the best try is
+// the first accepted try of the sequential loop.
+//
+// The scan reads only the uncached status words: an XCD's L2 keeps a stale
+// copy of a line other XCDs' atomics have changed (scanning the claim words
+// through L2, a closed env kept being joined: a 4 094-env reset took 250 ms of
+// futile joins).  Every returning atomic stays in cached memory, where it is
+// fast (uncached claims ran the C2 search at 62 µs per step, uncached gang
+// counts at 47).  The scan is a heuristic; the claims, gang counts and
+// best-try reads are returning atomics, exact.  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
 constexpr int kResetChunk = kResetBlock;   // tries per chunk, one per thread
 constexpr int kResetMaxD = 8;
@@ -1668,26 +1681,27 @@ constexpr int kResetNone = kResetNoneDev;  // "no accepted try yet"
 __device__ __forceinline__ unsigned long long rq_claim(unsigned long long* w) {
   return atomicAdd(w, 1ull);   // low half: chunks claimed; high half: best try
 }
+// Publishes accepted try t: one 64-bit atomicMin.  The word becomes {win t,
+// chunks claimed 0x7fffffff} when t is the best so far: every chunk below t's
+// chunk was claimed before t's, so no chunk needs claiming any more, and every
+// later claim returns a base far above t (a compare-and-swap that kept the
+// count lost to the ~16 claimants' traffic on the word and starved).
 __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
-  unsigned long long old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (;;) {
-    if ((int)(old >> 32) <= t) return;
-    const unsigned long long nw = ((unsigned long long)(unsigned)t << 32) | (old & 0xffffffffull);
-    const unsigned long long seen = atomicCAS(w, old, nw);
-    if (seen == old) return;
-    old = seen;
-  }
+  atomicMin(w, ((unsigned long long)(unsigned)t << 32) | 0x7fffffffull);
+}
+__device__ __forceinline__ int qs_load_agent(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <class T>
 __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) {
   __shared__ unsigned long long s_pick, s_claim;
-  __shared__ int s_win;
+  __shared__ int s_win, s_fin;
   int* const rq = P.reset_queue;
+  int* const rs = P.reset_status;
   const int n = rq[0];
   if (n == 0) return;   // nothing queued (the usual step)
   const int D = P.D;
-  auto rec = [&](int slot) { return rq + kRqLine * (1 + slot); };
   const int tid = threadIdx.x;
   T orig[kResetMaxD][3];
 #pragma unroll
@@ -1702,13 +1716,8 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     for (int i = tid; i < n; i += kResetBlock) {
       int j = home + i;
       if (j >= n) j -= n;
-      int* const r = rec(j);
-      const unsigned long long cw = __hip_atomic_load(reinterpret_cast<unsigned long long*>(r), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-      const int g = __hip_atomic_load(r + kRqGang, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const long long base = 1 + (long long)(cw & 0xffffffffull) * kResetChunk;
-      if (base < (long long)(int)(cw >> 32) && base < (long long)kMaxResetTries && g < kResetGang)
-        atomicMin(&s_pick, ((unsigned long long)(unsigned)g << 32) | (unsigned)i);
+      const int g = qs_load_agent(rs + 2 * j), closed = qs_load_agent(rs + 2 * j + 1);
+      if (!closed && g < kResetGang) atomicMin(&s_pick, ((unsigned long long)(unsigned)g << 32) | (unsigned)i);
     }
     __syncthreads();
     const unsigned long long p = s_pick;
@@ -1717,21 +1726,31 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     int j = home + (int)(p & 0xffffffffu);
     return j >= n ? j - n : j;
   };
-  // first assignment without a scan: n·kResetGang workgroups start on their home env
-  int idx = (int)blockIdx.x < n * kResetGang ? home : pick();
+  // More envs than workgroups (a reset of every env): workgroup b first takes
+  // envs b, b + G, b + 2G, … in turn, then scans.
+  const int G = (int)gridDim.x;
+  int own = (int)blockIdx.x < n * kResetGang ? home : -1;
+  int idx = own >= 0 ? own : pick();
 #ifdef QS_X_RSTATS
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   int st_picks = 1, st_joins = 0, st_chunks = 0, st_futile = 0, st_found = 0;
 #endif
   while (idx >= 0) {
-    int* const r = rec(idx);
+    int* const r = rq + kRqLine * (1 + idx);
+    int* const gang = r + kRqGang;
+    int* const hint = rs + 2 * idx;
     unsigned long long* const cwp = reinterpret_cast<unsigned long long*>(r);
     const int e = r[kRqEnv];
     const uint32_t genv = (uint32_t)(P.env_offset + e);
     const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
     if (tid == 0) {
-      atomicAdd(r + kRqGang, 1);
-      s_claim = rq_claim(cwp);
+      // returning: the gang count is raised before the claim is made.  A slot
+      // already written (gang >= kRqDone) is left at once: a claim that cannot
+      // be below its best try stands in
+      const int g0 = atomicAdd(gang, 1);
+      const unsigned long long c0 = rq_claim(cwp);   // in flight with the gang add (a claim
+      s_claim = g0 >= kRqDone ? 0x7fffffffull : c0;  // after the env closed is above its best try)
+      atomicAdd(hint, 1);
     }
     __syncthreads();
     unsigned long long cw = s_claim;
@@ -1743,7 +1762,11 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     int found = kResetNone;   // this workgroup's accepted try (workgroup-uniform)
     for (;;) {
       const long long base = 1 + (long long)(cw & 0xffffffffull) * kResetChunk;   // workgroup-uniform
-      if (base > (long long)min((int)(cw >> 32), found) || base >= (long long)kMaxResetTries) break;
+      if (base > (long long)min((int)(cw >> 32), found)) break;
+      if (base >= (long long)kMaxResetTries) {
+        if (tid == 0) __hip_atomic_store(hint + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // closed
+        break;
+      }
       unsigned long long cw_next = 0;
       if (tid == 0) cw_next = rq_claim(cwp);   // one chunk ahead: used after this chunk's tries
       const uint32_t t = (uint32_t)base + (uint32_t)tid;
@@ -1769,14 +1792,64 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       __syncthreads();   // s_win / s_claim are rewritten next chunk
       if (w != kResetNone) {
         found = w;       // the claim ahead is above w: the loop test leaves
-        if (tid == 0) rq_publish(cwp, w);
+        if (tid == 0) {
+          rq_publish(cwp, w);
+          __hip_atomic_store(hint + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // closed
+        }
       }
 #ifdef QS_X_RSTATS
       ++st_chunks; st_found += w != kResetNone;
 #endif
     }
-    if (tid == 0) atomicSub(r + kRqGang, 1);
-    idx = pick();
+    // The last workgroup to leave writes the env: every leave happens once the
+    // env's claims have passed its best try (or the cap), and a workgroup leaves
+    // only after testing its chunks and publishing its accepted try, so at gang
+    // 0 every chunk below the best try has been tested.  The compare-and-swap to
+    // kRqDone makes the write exclusive (a late joiner, raising gang again after
+    // 1 -> 0, leaves and takes the turn instead).
+    if (tid == 0) {
+      s_fin = 0;
+      // the publish above is performed before the leave (returning atomics below)
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      atomicSub(hint, 1);
+      if (atomicSub(gang, 1) == 1 && atomicCAS(gang, 0, kRqDone) == 0) {
+        s_fin = 1;
+        s_claim = atomicAdd(cwp, 0ull);   // read-modify-write: the coherent best try
+      }
+    }
+    __syncthreads();
+    if (s_fin) {
+      const int wv = (int)(s_claim >> 32);
+      // no accepted try below the cap: flag the error and keep try 0, as the
+      // in-kernel search does
+      const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;
+      if (tid < D) {
+        T od[3] = {P.orig_xyz[tid * 3 + 0], P.orig_xyz[tid * 3 + 1], P.orig_xyz[tid * 3 + 2]};
+        T ix, iy, iz;
+        reset_candidate(P, od, tid, win, genv, episode, ix, iy, iz);
+        const size_t a = (size_t)e * D + tid, N = (size_t)P.N;
+        P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
+        P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
+        P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(tid + 1));   // MH:106
+        if (P.obs) {
+          float* o = P.obs + a * (size_t)P.O;
+          o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
+        }
+      }
+      if (tid == 0) {
+        if (wv == kResetNone) atomicExch(P.err, 1);
+        // the last env written empties the queue (one same-address atomic per
+        // queued env); a workgroup that reads the count after that has nothing to do
+        if (atomicAdd(&rq[1], 1) == n - 1) { rq[0] = 0; rq[1] = 0; }
+      }
+    }
+    if (own >= 0 && own + G < n) {
+      own += G;
+      idx = own;
+    } else {
+      own = -1;
+      idx = pick();
+    }
 #ifdef QS_X_RSTATS
     ++st_picks;
 #endif
@@ -1787,43 +1860,6 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     printf("RS n=%d wg=%d us=%.2f picks=%d joins=%d futile=%d chunks=%d found=%d\n", n, (int)blockIdx.x,
            (double)(t_end - t_start) * 0.01, st_picks, st_joins, st_futile, st_chunks, st_found);
 #endif
-}
-
-// Writes the first accepted try of every queued env (reset_search_kernel's
-// result): position, target (MH:106) and obs row, one thread per drone; the
-// last workgroup to arrive empties the queue.  No accepted try below the cap
-// flags the error and keeps try 0, as the in-kernel search does.
-template <class T>
-__global__ void __launch_bounds__(kResetBlock) reset_finalize_kernel(Params<T> P) {
-  int* const rq = P.reset_queue;
-  const int n = rq[0];
-  const int D = P.D;
-  const int active = (n * D + kResetBlock - 1) / kResetBlock;   // workgroups with drones to write
-  if ((int)blockIdx.x >= active) return;
-  const int g = (int)blockIdx.x * kResetBlock + (int)threadIdx.x;
-  if (g < n * D) {
-    const int idx = g / D, d = g - idx * D;
-    const int* const r = rq + kRqLine * (1 + idx);
-    const int e = r[kRqEnv];
-    const int wv = r[kRqWin];
-    if (wv == kResetNone) atomicExch(P.err, 1);
-    const uint32_t win = wv == kResetNone ? 0u : (uint32_t)wv;
-    const uint32_t genv = (uint32_t)(P.env_offset + e);
-    const uint32_t episode = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE];
-    T od[3] = {P.orig_xyz[d * 3 + 0], P.orig_xyz[d * 3 + 1], P.orig_xyz[d * 3 + 2]};
-    T ix, iy, iz;
-    reset_candidate(P, od, d, win, genv, episode, ix, iy, iz);
-    const size_t a = (size_t)e * D + d, N = (size_t)P.N;
-    P.st[(QS_F_POS + 0) * N + a] = ix; P.st[(QS_F_POS + 1) * N + a] = iy; P.st[(QS_F_POS + 2) * N + a] = iz;
-    P.st[(QS_F_TARGET + 0) * N + a] = ix; P.st[(QS_F_TARGET + 1) * N + a] = iy;
-    P.st[(QS_F_TARGET + 2) * N + a] = iz + T(1.0 / (double)(d + 1));   // MH:106
-    if (P.obs) {
-      float* o = P.obs + a * (size_t)P.O;
-      o[0] = (float)ix; o[1] = (float)iy; o[2] = (float)iz;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(&rq[1], 1) == active - 1) { rq[0] = 0; rq[1] = 0; }
 }
 
 }  // namespace qs

@@ -66,7 +66,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_mlp_wgrad", "qs_mlp_wgrad_chunks", "qs_adam_multi",
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
-           "qs_learner_last_error")
+           "qs_wgrad_rm", "qs_learner_last_error")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
 
 _lib = None
@@ -143,6 +143,7 @@ def load():
     L.qs_value_head.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 7
     L.qs_mlp_wgrad_x_chunks.argtypes = [i64, ctypes.c_int32]
     L.qs_mlp_wgrad_x.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32, vp, vp, vp]
+    L.qs_wgrad_rm.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_learner_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         if name not in ("qs_last_error", "qs_learner_last_error"):

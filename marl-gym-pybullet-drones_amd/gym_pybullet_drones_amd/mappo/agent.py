@@ -35,6 +35,18 @@ def get_activation(name):
     return getattr(torch, name) if name in ("tanh", "relu", "sigmoid") else (getattr(F, name) if name else (lambda x: x))
 
 
+def _wgrad_rm_chunks(rows, tiles=4):
+    """Row chunks of qs_wgrad_rm for a 256×256 weight gradient: about one
+    workgroup per CU (tiles × chunks <= 256), every chunk a multiple of 8 rows
+    and at least 64 (0: the shape is not taken)."""
+    if rows % 8:
+        return 0
+    c = 1
+    while c * 2 * tiles <= 256 and rows % (16 * c) == 0 and rows // (2 * c) >= 64:
+        c *= 2
+    return c
+
+
 def _splitk_chunks(rows, min_rows=1024):
     """Row chunks of the split-K weight gradient: the largest power of two S with
     rows / S >= min_rows that divides rows (1 = plain GEMM)."""
@@ -353,6 +365,7 @@ class _F16Work(_M3Work):
     rows and reduction tasks as _M3Work.backward."""
 
     w1_stream = True   # dW1 on a third stream beside dW2 (False: after it, one stream)
+    wgrad_rm = True    # dW2 on qs_wgrad_rm (False: torch.bmm row-chunk GEMMs)
 
     def __init__(self, mlp, K, device):
         f0, f1, f2 = mlp.fcs
@@ -374,7 +387,12 @@ class _F16Work(_M3Work):
         m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 2048), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
         self.C2 = self.C1 = 0
         self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
-        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
+        # dW2 on qs_wgrad_rm: 64 chunks of 512 rows at 32 768 rows (hipBLASLt ran the
+        # 16 batched 2 048-row GEMMs at 63 µs, 0.43 of the fp32 MFMA peak)
+        self.R2 = _wgrad_rm_chunks(K) if self.wgrad_rm else 0
+        if self.R2:
+            self.S2 = self.R2
+        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 or self.R2 else None
         self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 else None
 
     def repack(self):
@@ -386,10 +404,15 @@ class _F16Work(_M3Work):
         pk, w1, w2, I = super().pack_segment(fb)
         return pk, w1, w2, I | L.QS_PACK_F16
 
-    def _splitk_rm(self, dst, dy, x, part, S):
+    def _splitk_rm(self, dst, dy, x, part, S, rm=False):
         """dst = dyᵀ·x over K rows (dy [K][N], x [K][M], both row-major) as S row-chunk
-        GEMMs into the preallocated partials (S = 1: one GEMM straight into dst)."""
+        GEMMs into the preallocated partials (S = 1: one GEMM straight into dst);
+        rm: S chunk partials of qs_wgrad_rm instead."""
         K = dy.shape[0]
+        if rm:
+            L.check(L.load().qs_wgrad_rm(K, dy.shape[1], x.shape[1], L.ptr(dy), L.ptr(x), S, L.ptr(part), _stream()),
+                    "qs_wgrad_rm")
+            return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
         if S == 1:
             torch.mm(dy.t(), x, out=dst)
             return None
@@ -420,10 +443,10 @@ class _F16Work(_M3Work):
             self._s3.wait_stream(cur)
             with torch.cuda.stream(self._s3):
                 w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)       # dW2 = dZ2ᵀ·H1
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
             cur.wait_stream(self._s3)
         else:
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)    # dW2 = dZ2ᵀ·H1
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
             w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)    # dW1 = dZ1ᵀ·Xa
         for dst, t in ((f1.weight.grad, w2), (f0.weight.grad, w1)):
             if t is not None:

@@ -93,3 +93,28 @@ def test_fused_actor_matches_autograd(mb, D, I, A):
         for got, want in ((dZ2.double().t() @ H1.double(), net[2].weight.grad), (dZ1.double().t() @ xa.double(), net[0].weight.grad)):
             sc = float(want.abs().max())
             torch.testing.assert_close(got.float(), want, rtol=1e-3, atol=1e-4 * sc)
+
+
+@pytest.mark.parametrize("K,N,M,C", [(32768, 256, 256, 64), (4096, 256, 256, 64), (2048, 128, 256, 4), (1024, 256, 128, 1)])
+def test_wgrad_rm_matches_fp64(K, N, M, C):
+    """qs_wgrad_rm chunk partials (the actor's dW2 = dZ2ᵀ·H1 from the fused
+    kernel's row-major activations) against an fp64 matmul per chunk."""
+    import ctypes
+    from gym_pybullet_drones_amd import _lib as L
+    lib = L.load()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn(K, N, device="cuda", generator=g)
+    B = torch.tanh(torch.randn(K, M, device="cuda", generator=g))
+    part = torch.full((C, N, M), np.nan, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L.check(lib.qs_wgrad_rm(K, N, M, L.ptr(A), L.ptr(B), C, L.ptr(part), stream), "qs_wgrad_rm")
+    torch.cuda.synchronize()
+    want = torch.bmm(A.double().view(C, K // C, N).transpose(1, 2), B.double().view(C, K // C, M))
+    torch.testing.assert_close(part.double(), want, rtol=0, atol=2e-6 * (K // C) ** 0.5 * 4)
+    # a replay is bit-identical (fixed summation order)
+    again = torch.empty_like(part)
+    L.check(lib.qs_wgrad_rm(K, N, M, L.ptr(A), L.ptr(B), C, L.ptr(again), stream), "qs_wgrad_rm")
+    torch.cuda.synchronize()
+    assert torch.equal(part, again)
+    # shapes the kernel does not take are refused
+    assert lib.qs_wgrad_rm(K, 96, M, L.ptr(A), L.ptr(B), C, L.ptr(part), stream) != 0
