@@ -39,6 +39,11 @@ constexpr bool kNoCompute = false, kNoResetDraw = false;
 }
 #define QS_STAMP(k) do { } while (0)
 #define QS_STAMP_SINK(x) do { } while (0)
+#define QS_RS_BEGIN() do { } while (0)
+#define QS_RS_JOIN(futile) do { } while (0)
+#define QS_RS_CHUNK(found) do { } while (0)
+#define QS_RS_PICK() do { } while (0)
+#define QS_RS_END(n) do { } while (0)
 #endif
 
 namespace qs {
@@ -49,18 +54,20 @@ namespace qs {
 constexpr int kBlock = 64;
 // Per-env record, kEnvRec int32 words: the QS_ENV_FIELDS counters (words 0-3,
 // QS_E_* order), the episode return as f64 (words 4-5), the number of episodes
-// this env has logged (word 6, kEnvLogWord), padding.  32 B per env
+// this env has logged (word 6, kEnvLogWord), the precomputed reset of its next
+// episode (word 7, kEnvPreWord: bit 31 set, episode & 0x7f in bits 24-30, the
+// first accepted MultiHover reset try in bits 0-23; reset_search_kernel).  32 B per env
 // make a wave's envs (D = 8) one 256-B span, loaded and stored whole: written
 // field by field, [field][E] arrays took partial-line writes.
 constexpr int kEnvRec = 8;
 constexpr int kEnvRetWord = 4;
 constexpr int kEnvLogWord = 6;
+constexpr int kEnvPreWord = 7;
 constexpr uint32_t kMaxResetTries = 1u << 24;
 constexpr int kResetNoneDev = 0x7f7f7f7f;   // deferred reset search: "no accepted try yet"
 // deferred reset search queue (reset_search_kernel): 128-B lines of int32
 // words in `reset_queue` — line 0 {count, envs written}, line 1 + slot {claim
-// word (u64: chunks claimed | best try << 32), env id, gang} — and two words per
-// slot {gang hint, closed} in the uncached `reset_status`
+// word (u64: chunks claimed | best try << 32), env id, gang}
 constexpr int kRqLine = 32, kRqWin = 1, kRqEnv = 2, kRqGang = 3;
 constexpr int kRqDone = 1 << 24;   // gang value of a slot whose env has been written
 enum { STREAM_ACT = 1, STREAM_RESET = 2 };
@@ -236,8 +243,8 @@ template <class T> struct Params {
   int log_per_env;
   int* err;               // [1] reset search overflow flag
   int* reset_queue;       // deferred MultiHover reset searches (reset_search_kernel's records); or NULL
-  int* reset_status;      // their per-slot {gang, closed} words (uncached memory)
   int reject_free;        // MultiHover layout whose reset draws can never be rejected: try 0 is the reset
+  int32_t* reset_pre;     // [E] next chunk of each env's precomputed next-episode reset search; or NULL
   int stage_rows;         // obs rows staged in LDS per pass
   unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
   // per-step I/O
@@ -736,7 +743,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   int32_t step_counter = (int32_t)c01.x, episode = (int32_t)c01.y;
   int32_t total = (int32_t)c23.x, ep_len = (int32_t)c23.y;
   const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvRetWord * 4, 0));
-  const int32_t log_n0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(env_r, (int)ev, kEnvLogWord * 4, 0);
+  const v2u_t c67 = __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvLogWord * 4, 0);
+  const int32_t log_n0 = (int32_t)c67.x, pre0 = (int32_t)c67.y;
   issue_fence();
   T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
 #pragma unroll
@@ -1490,10 +1498,16 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         if (do_reset && !qs_dev::kNoResetDraw)
           reset_candidate(P, orig, d, 0u, genv, (uint32_t)episode, init[0], init[1], init[2]);
       } else {
-        // Phase 1: every group tries index 0 for its own env.
+        // The next episode's first accepted try, when reset_search_kernel has
+        // found it ahead of time (word 7 of the env record, for this episode)
+        const bool pre_ok = P.reset_pre && P.mode != MODE_RESET_ALL && do_reset && pre0 < 0 &&
+                            ((pre0 >> 24) & 0x7f) == (episode & 0x7f);
+        if (pre_ok) reset_candidate(P, orig, d, (uint32_t)pre0 & 0xffffffu, genv, (uint32_t)episode, init[0], init[1], init[2]);
+        // Phase 1: every other group tries index 0 for its own env.
         if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
         __syncthreads();
-        if (!qs_dev::kNoResetDraw) eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset, init);
+        if (!qs_dev::kNoResetDraw)
+          eval_candidate(P, s, orig, lenv, d, 0u, genv, (uint32_t)episode, do_reset && !pre_ok, pre_ok ? nullptr : init);
         if (d == 0 && do_reset && s.reject[lenv] == 0) s.need[lenv] = 0;
         if (tid == 0) s.qcount = 0;
         __syncthreads();
@@ -1510,10 +1524,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           __syncthreads();
           if (local >= 0) {
             const int slot = s.qbase + local;
-            // claim word {chunks claimed 0, best try none}, env id, gang 0; status {0, open}
+            // claim word {chunks claimed 0, best try none}, env id, gang 0
             *reinterpret_cast<int4*>(P.reset_queue + kRqLine * (1 + slot)) =
                 make_int4(0, kResetNoneDev, (int)(blockIdx.x * P.EPB + lenv), 0);
-            *reinterpret_cast<int2*>(P.reset_status + 2 * slot) = make_int2(0, 0);
             s.need[lenv] = 0;
           }
           __syncthreads();
@@ -1616,7 +1629,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     r[QS_E_STEP_COUNTER] = step_counter; r[QS_E_EPISODE] = episode; r[QS_E_TOTAL_STEPS] = total;
     r[QS_E_EP_LEN] = ep_len_out;
     r[kEnvRetWord] = (int32_t)(unsigned)rb; r[kEnvRetWord + 1] = (int32_t)(unsigned)(rb >> 32);
-    r[kEnvLogWord] = log_n; r[7] = 0;
+    // a reset consumes the precomputed try (the next search starts over)
+    r[kEnvLogWord] = log_n; r[kEnvPreWord] = do_reset ? 0 : pre0;
+    if (P.reset_pre && do_reset) P.reset_pre[e] = 0;
   }
   __syncthreads();
   {
@@ -1639,39 +1654,28 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 
 // ------------------------------------------------- deferred reset search
 // MultiHoverAviary.reset's rejection loop (MH:83-102) for the envs the step
-// kernel queued (try 0 rejected).  Per queue slot (kRq* above): a claim word
+// kernel queued (no precomputed try, and try 0 rejected; rare once the
+// precomputed resets below run).  Per queue slot (kRq* above): a claim word
 // holding the number of chunks claimed (low half) and the best accepted try
-// so far (high half) on a 128-B line of its own, so one returning 64-bit
-// atomicAdd both claims a chunk and reads the best try, and the number of
-// workgroups searching the slot (gang); in uncached memory, a copy of the gang
-// count and a closed flag for the scan, written without waiting.
-// The step kernel initialises a slot when it queues an env.
+// so far (high half), the env id and the number of workgroups searching the
+// slot (gang), on a 128-B line of its own, so one returning 64-bit atomicAdd
+// both claims a chunk and reads the best try.  The step kernel initialises a
+// slot when it queues an env.
 //
-// Work is distributed dynamically.  An env's tries are cut into chunks of
-// kResetChunk (chunk c holds tries 1 + kResetChunk·c + t, thread t); a
-// workgroup claims the env's next chunk (issued one chunk ahead, so the
-// atomic's round trip runs under the Philox work), tests it, and publishes
-// its smallest accepted try (rq_publish) and the closed flag.  A workgroup
-// leaves an env once its claimed chunk starts above the best try (every chunk
-// below it is claimed, so the env needs no more workers) or above the cap,
-// and then joins the open env with the fewest workers (ties: the nearest after
-// its own index, so workgroups spread); with more envs than workgroups it
-// first takes envs b, b + G, b + 2G, … in turn.  At most kResetGang
-// workgroups join one env: at acceptance ~7e-4 (four drones around the
-// reference's diagonal layout) 16 × 256 tries resolve an env per round with
-// probability 0.94, and more claimants only queue on its line.
-//
-// The last workgroup to leave an env writes it (position, target, obs row):
-// by then every chunk below the best try has been tested, so the best try is
-// the first accepted try of the sequential loop.
-//
-// The scan reads only the uncached status words: an XCD's L2 keeps a stale
-// copy of a line other XCDs' atomics have changed (scanning the claim words
-// through L2, a closed env kept being joined: a 4 094-env reset took 250 ms of
-// futile joins).  Every returning atomic stays in cached memory, where it is
-// fast (uncached claims ran the C2 search at 62 µs per step, uncached gang
-// counts at 47).  The scan is a heuristic; the claims, gang counts and
-// best-try reads are returning atomics, exact.  D <= kResetMaxD.
+// An env's tries are cut into chunks of kResetChunk (chunk c holds tries
+// 1 + kResetChunk·c + t, thread t).  Workgroup b works on slot b mod n (so up
+// to kResetGang workgroups share an env; with more envs than workgroups, slots
+// b, b + G, … in turn): it claims the slot's next chunk (issued one chunk
+// ahead, so the atomic's round trip runs under the Philox work), tests it,
+// publishes its smallest accepted try (rq_publish), and leaves once its
+// claimed chunk starts above the best try (every chunk below it is claimed)
+// or above the cap.  The last workgroup to leave writes the env (position,
+// target, obs row): by then every chunk below the best try has been tested,
+// so the best try is the first accepted try of the sequential loop.
+// (Workgroups that scanned for open envs to help needed coherent reads of
+// other XCDs' atomics — uncached memory — and piled onto single envs: 1 000
+// claimants on one line cost ~50 µs; the precomputed resets made the queue
+// small instead.)  D <= kResetMaxD.
 constexpr int kResetBlock = 256;
 constexpr int kResetChunk = kResetBlock;   // tries per chunk, one per thread
 constexpr int kResetMaxD = 8;
@@ -1689,18 +1693,64 @@ __device__ __forceinline__ unsigned long long rq_claim(unsigned long long* w) {
 __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
   atomicMin(w, ((unsigned long long)(unsigned)t << 32) | 0x7fffffffull);
 }
-__device__ __forceinline__ int qs_load_agent(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+// The precomputed resets: an env's next-episode reset draw depends only on
+// (seed, env, episode), so the search for it need not wait for the reset.
+// After the queue, workgroup b tests kPreChunks chunks (tries c·256 + t, try 0
+// included) of each env b, b + G, … whose word 7 holds no try for its next
+// episode, continuing at chunk reset_pre[e]; the first accepted try goes into
+// word 7 and the step kernel that resets the env into that episode uses it
+// instead of testing try 0 (the first accepted try of MH:83-102, as the queue
+// search finds it).  One workgroup per env: no atomics.  An env that resets
+// before its search ends takes the step kernel's own path (try 0, then the
+// queue).
+constexpr int kPreChunks = 2;
+template <class T>
+__device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD][3]) {
+  __shared__ int s_pw;
+  const int D = P.D, tid = threadIdx.x;
+  for (int e = (int)blockIdx.x; e < P.E; e += (int)gridDim.x) {   // workgroup-uniform
+    int32_t* const rec = P.env + (size_t)e * kEnvRec;
+    if (rec[kEnvPreWord] < 0) continue;   // found already
+    const uint32_t ep = (uint32_t)rec[QS_E_EPISODE] + 1u, genv = (uint32_t)(P.env_offset + e);
+    int c = P.reset_pre[e];
+    for (int k = 0; k < kPreChunks; ++k, ++c) {
+      const uint32_t t = (uint32_t)c * kResetChunk + (uint32_t)tid;
+      if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
+      bool ok = true;
+      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
+#pragma unroll
+      for (int d = 0; d < kResetMaxD; ++d) {
+        if (d < D && ok) {
+          reset_candidate(P, orig[d], d, t, genv, ep, px[d], py[d], pz[d]);
+          if (pz[d] < T(0.1)) ok = false;
+#pragma unroll
+          for (int i = 0; i < d; ++i)
+            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
+        }
+      }
+      if (tid == 0) s_pw = kResetNone;
+      __syncthreads();
+      if (ok) atomicMin(&s_pw, (int)t);
+      __syncthreads();
+      const int w = s_pw;
+      __syncthreads();
+      if (w != kResetNone) {
+        if (tid == 0) rec[kEnvPreWord] = (int32_t)(0x80000000u | ((ep & 0x7fu) << 24) | (uint32_t)w);
+        c = -1;
+        break;
+      }
+    }
+    if (tid == 0 && c >= 0) P.reset_pre[e] = c;
+  }
 }
 
 template <class T>
 __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) {
-  __shared__ unsigned long long s_pick, s_claim;
+  __shared__ unsigned long long s_claim;
   __shared__ int s_win, s_fin;
   int* const rq = P.reset_queue;
-  int* const rs = P.reset_status;
   const int n = rq[0];
-  if (n == 0) return;   // nothing queued (the usual step)
   const int D = P.D;
   const int tid = threadIdx.x;
   T orig[kResetMaxD][3];
@@ -1708,37 +1758,15 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
   for (int d = 0; d < kResetMaxD; ++d)
 #pragma unroll
     for (int k = 0; k < 3; ++k) orig[d][k] = d < D ? P.orig_xyz[d * 3 + k] : T(0);
-  const int home = (int)(blockIdx.x % (unsigned)n);
-  // the open env with the fewest workers below the gang cap, or -1 (workgroup-uniform)
-  auto pick = [&]() -> int {
-    if (tid == 0) s_pick = ~0ull;
-    __syncthreads();
-    for (int i = tid; i < n; i += kResetBlock) {
-      int j = home + i;
-      if (j >= n) j -= n;
-      const int g = qs_load_agent(rs + 2 * j), closed = qs_load_agent(rs + 2 * j + 1);
-      if (!closed && g < kResetGang) atomicMin(&s_pick, ((unsigned long long)(unsigned)g << 32) | (unsigned)i);
-    }
-    __syncthreads();
-    const unsigned long long p = s_pick;
-    __syncthreads();   // s_pick is rewritten by the next pick
-    if (p == ~0ull) return -1;
-    int j = home + (int)(p & 0xffffffffu);
-    return j >= n ? j - n : j;
-  };
-  // More envs than workgroups (a reset of every env): workgroup b first takes
-  // envs b, b + G, b + 2G, … in turn, then scans.
+  const int home = n > 0 ? (int)(blockIdx.x % (unsigned)n) : 0;
+  // More envs than workgroups (a reset of every env): workgroup b takes envs
+  // b, b + G, b + 2G, … in turn.
   const int G = (int)gridDim.x;
-  int own = (int)blockIdx.x < n * kResetGang ? home : -1;
-  int idx = own >= 0 ? own : pick();
-#ifdef QS_X_RSTATS
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  int st_picks = 1, st_joins = 0, st_chunks = 0, st_futile = 0, st_found = 0;
-#endif
+  int idx = n > 0 && (int)blockIdx.x < n * kResetGang ? home : -1;   // nothing queued: the usual step
+  QS_RS_BEGIN();
   while (idx >= 0) {
     int* const r = rq + kRqLine * (1 + idx);
     int* const gang = r + kRqGang;
-    int* const hint = rs + 2 * idx;
     unsigned long long* const cwp = reinterpret_cast<unsigned long long*>(r);
     const int e = r[kRqEnv];
     const uint32_t genv = (uint32_t)(P.env_offset + e);
@@ -1750,23 +1778,16 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       const int g0 = atomicAdd(gang, 1);
       const unsigned long long c0 = rq_claim(cwp);   // in flight with the gang add (a claim
       s_claim = g0 >= kRqDone ? 0x7fffffffull : c0;  // after the env closed is above its best try)
-      atomicAdd(hint, 1);
     }
     __syncthreads();
     unsigned long long cw = s_claim;
     __syncthreads();
-#ifdef QS_X_RSTATS
-    ++st_joins;
-    if (1 + (long long)(cw & 0xffffffffull) * kResetChunk > (long long)(int)(cw >> 32)) ++st_futile;
-#endif
+    QS_RS_JOIN(1 + (long long)(cw & 0xffffffffull) * kResetChunk > (long long)(int)(cw >> 32));
     int found = kResetNone;   // this workgroup's accepted try (workgroup-uniform)
     for (;;) {
       const long long base = 1 + (long long)(cw & 0xffffffffull) * kResetChunk;   // workgroup-uniform
       if (base > (long long)min((int)(cw >> 32), found)) break;
-      if (base >= (long long)kMaxResetTries) {
-        if (tid == 0) __hip_atomic_store(hint + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // closed
-        break;
-      }
+      if (base >= (long long)kMaxResetTries) break;
       unsigned long long cw_next = 0;
       if (tid == 0) cw_next = rq_claim(cwp);   // one chunk ahead: used after this chunk's tries
       const uint32_t t = (uint32_t)base + (uint32_t)tid;
@@ -1792,14 +1813,9 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       __syncthreads();   // s_win / s_claim are rewritten next chunk
       if (w != kResetNone) {
         found = w;       // the claim ahead is above w: the loop test leaves
-        if (tid == 0) {
-          rq_publish(cwp, w);
-          __hip_atomic_store(hint + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // closed
-        }
+        if (tid == 0) rq_publish(cwp, w);
       }
-#ifdef QS_X_RSTATS
-      ++st_chunks; st_found += w != kResetNone;
-#endif
+      QS_RS_CHUNK(w != kResetNone);
     }
     // The last workgroup to leave writes the env: every leave happens once the
     // env's claims have passed its best try (or the cap), and a workgroup leaves
@@ -1811,7 +1827,6 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       s_fin = 0;
       // the publish above is performed before the leave (returning atomics below)
       __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      atomicSub(hint, 1);
       if (atomicSub(gang, 1) == 1 && atomicCAS(gang, 0, kRqDone) == 0) {
         s_fin = 1;
         s_claim = atomicAdd(cwp, 0ull);   // read-modify-write: the coherent best try
@@ -1843,23 +1858,11 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
         if (atomicAdd(&rq[1], 1) == n - 1) { rq[0] = 0; rq[1] = 0; }
       }
     }
-    if (own >= 0 && own + G < n) {
-      own += G;
-      idx = own;
-    } else {
-      own = -1;
-      idx = pick();
-    }
-#ifdef QS_X_RSTATS
-    ++st_picks;
-#endif
+    idx = idx + G < n ? idx + G : -1;
+    QS_RS_PICK();
   }
-#ifdef QS_X_RSTATS
-  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-  if (tid == 0 && (blockIdx.x % 32 == 0 || t_end - t_start > 5000))
-    printf("RS n=%d wg=%d us=%.2f picks=%d joins=%d futile=%d chunks=%d found=%d\n", n, (int)blockIdx.x,
-           (double)(t_end - t_start) * 0.01, st_picks, st_joins, st_futile, st_chunks, st_found);
-#endif
+  QS_RS_END(n);
+  if (P.reset_pre) reset_precompute(P, orig);
 }
 
 }  // namespace qs

@@ -40,3 +40,27 @@ constexpr bool kNoResetDraw = false;
 #define QS_STAMP(k) do { } while (0)
 #define QS_STAMP_SINK(x) do { } while (0)
 #endif
+
+// reset_search_kernel's per-workgroup counters (QS_X_RSTATS): time in the
+// launch, picks, joins (futile: the env had closed), chunks tested, finds
+#ifdef QS_X_RSTATS
+#define QS_RS_BEGIN()                                               \
+  const uint64_t rs_t0_ = __builtin_amdgcn_s_memrealtime();         \
+  int rs_picks_ = 1, rs_joins_ = 0, rs_futile_ = 0, rs_chunks_ = 0, rs_found_ = 0
+#define QS_RS_JOIN(futile) do { ++rs_joins_; rs_futile_ += (futile) ? 1 : 0; } while (0)
+#define QS_RS_CHUNK(found) do { ++rs_chunks_; rs_found_ += (found) ? 1 : 0; } while (0)
+#define QS_RS_PICK() do { ++rs_picks_; } while (0)
+#define QS_RS_END(n)                                                                                        \
+  do {                                                                                                      \
+    const uint64_t rs_t1_ = __builtin_amdgcn_s_memrealtime();                                               \
+    if (threadIdx.x == 0 && (blockIdx.x % 32 == 0 || rs_t1_ - rs_t0_ > 5000))                                \
+      printf("RS n=%d wg=%d us=%.2f picks=%d joins=%d futile=%d chunks=%d found=%d\n", (n), (int)blockIdx.x, \
+             (double)(rs_t1_ - rs_t0_) * 0.01, rs_picks_, rs_joins_, rs_futile_, rs_chunks_, rs_found_);     \
+  } while (0)
+#else
+#define QS_RS_BEGIN() do { } while (0)
+#define QS_RS_JOIN(futile) do { } while (0)
+#define QS_RS_CHUNK(found) do { } while (0)
+#define QS_RS_PICK() do { } while (0)
+#define QS_RS_END(n) do { } while (0)
+#endif

@@ -21,6 +21,7 @@ MI355X-specific structure:
 """
 import ctypes
 import math
+import os
 from collections import defaultdict
 
 import torch
@@ -390,6 +391,9 @@ class _F16Work(_M3Work):
         # dW2 on qs_wgrad_rm: 64 chunks of 512 rows at 32 768 rows (hipBLASLt ran the
         # 16 batched 2 048-row GEMMs at 63 µs, 0.43 of the fp32 MFMA peak)
         self.R2 = _wgrad_rm_chunks(K) if self.wgrad_rm else 0
+        if os.environ.get("QS_DEBUG_SHAPES"):
+            print(f"_F16Work: K={K} I={self.I} dW2 chunks={self.R2 or self.S2} ({'qs_wgrad_rm' if self.R2 else 'bmm'})",
+                  flush=True)
         if self.R2:
             self.S2 = self.R2
         self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 or self.R2 else None
@@ -419,9 +423,11 @@ class _F16Work(_M3Work):
         torch.bmm(dy.view(S, K // S, -1).transpose(1, 2), x.view(S, K // S, -1), out=part)
         return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
 
-    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole):
+    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole, defer_w1=False):
         """qs_mlp3f_actor over the minibatch's agent rows (env-timesteps idx, D rows
-        each, straight from the rollout table), then the weight gradients."""
+        each, straight from the rollout table), then the weight gradients.
+        defer_w1: dW1 is left to the caller — returns a function that launches it
+        on the current stream (after an event recorded behind the actor kernel)."""
         f0, f1, f2 = self.mlp.fcs
         logstd = actor.logstd
         L.check(L.load().qs_mlp3f_actor(
@@ -434,6 +440,24 @@ class _F16Work(_M3Work):
         N, A = 256, self.A
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
+        if defer_w1:
+            cur = torch.cuda.current_stream()
+            ev = torch.cuda.Event()
+            ev.record(cur)   # the actor kernel's outputs
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
+            if w2 is not None:
+                tasks.append(w2)
+            elif whole is not None:
+                whole.append(f1.weight.grad)
+
+            def launch_w1():
+                torch.cuda.current_stream().wait_event(ev)
+                w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
+                if w1 is not None:
+                    tasks.append(w1)
+                elif whole is not None:
+                    whole.append(f0.weight.grad)
+            return launch_w1
         if self.w1_stream:
             # dW1's small GEMMs (a few dozen workgroups each) beside dW2's on a third
             # stream; joined before the caller's reductions
@@ -441,9 +465,10 @@ class _F16Work(_M3Work):
             if getattr(self, '_s3', None) is None or self._s3.device != cur.device:
                 self._s3 = torch.cuda.Stream(device=cur.device)
             self._s3.wait_stream(cur)
+            # dW2 first: it stays on the actor's queue (the critical path)
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
             with torch.cuda.stream(self._s3):
                 w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
             cur.wait_stream(self._s3)
         else:
             w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
@@ -998,19 +1023,33 @@ class MAPPOAgent:
                     tc.clear()
                     wc.clear()
 
-            def actor_all(exchange):
-                self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
-                                    self.clip_param, self.entropy_coef, self._kl, acc, ta, wa)
+            def actor_all(exchange, defer_w1=False):
+                w1 = self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
+                                         self.clip_param, self.entropy_coef, self._kl, acc, ta, wa, defer_w1=defer_w1)
                 if exchange:
                     _flush_sums(ta)
                     self._exchange_bucket(self._actor_bucket, world)
+                return w1
 
             if self.side_stream:
                 own = not multi and self.critic_adam_side
                 self._side.wait_stream(cur)
-                with torch.cuda.stream(self._side):
-                    critic_all(multi, own)
-                actor_all(multi)
+                if multi or own:
+                    with torch.cuda.stream(self._side):
+                        critic_all(multi, own)
+                    actor_all(multi)
+                else:
+                    # Graph replay puts the first branch of a fork on the parent's
+                    # hardware queue and runs each queue's nodes in capture order;
+                    # every cross-queue edge costs ~5-13 µs.  So the critical chain
+                    # (actor kernel → dW2 → the reductions) is captured first on the
+                    # launch stream, the critic on the side stream beside it, and
+                    # the actor's small dW1 GEMM after the critic on the side stream
+                    # (on its own queue it would hold the critic back in order).
+                    launch_w1 = actor_all(False, defer_w1=True)
+                    with torch.cuda.stream(self._side):
+                        critic_all(False, False)
+                        launch_w1()
                 cur.wait_stream(self._side)
                 if own:
                     for g in [logstd.grad] + wa:
