@@ -1696,27 +1696,31 @@ __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
 
 // The precomputed resets: an env's next-episode reset draw depends only on
 // (seed, env, episode), so the search for it need not wait for the reset.
-// After the queue, workgroup b tests kPreChunks chunks (tries c·256 + t, try 0
-// included) of each env b, b + G, … whose word 7 holds no try for its next
-// episode, continuing at chunk reset_pre[e]; the first accepted try goes into
-// word 7 and the step kernel that resets the env into that episode uses it
-// instead of testing try 0 (the first accepted try of MH:83-102, as the queue
-// search finds it).  One workgroup per env: no atomics.  An env that resets
-// before its search ends takes the step kernel's own path (try 0, then the
-// queue).
-constexpr int kPreChunks = 2;
+// One wave per env (the launch's workgroups past the first kQueueWG): each
+// launch it tests kPreSteps × 64 tries (tries 64·c + lane, try 0 included) of
+// its env when word 7 of the env record holds no try for the next episode,
+// continuing at step reset_pre[e]; the first accepted try (the lowest lane of
+// the first step whose ballot is not empty) goes into word 7, and the step
+// kernel that resets the env into that episode uses it instead of testing
+// try 0 — the first accepted try of MH:83-102, as the queue search finds it.
+// No atomics, no barriers.  An env that resets before its search ends takes the
+// step kernel's own path (try 0, then the queue).  (A workgroup per env with
+// 256-try chunks ran 17 workgroups per CU in three residency rounds: 12 µs.)
+constexpr int kPreSteps = 8;
+constexpr int kQueueWG = 256;   // workgroups of the search launch that serve the queue (the rest precompute)
 template <class T>
-__device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD][3]) {
-  __shared__ int s_pw;
-  const int D = P.D, tid = threadIdx.x;
-  for (int e = (int)blockIdx.x; e < P.E; e += (int)gridDim.x) {   // workgroup-uniform
+__device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD][3], int first, int stride) {
+  const int D = P.D, lane = threadIdx.x & 63;
+  for (int e = first; e < P.E; e += stride) {   // wave-uniform
     int32_t* const rec = P.env + (size_t)e * kEnvRec;
-    if (rec[kEnvPreWord] < 0) continue;   // found already
-    const uint32_t ep = (uint32_t)rec[QS_E_EPISODE] + 1u, genv = (uint32_t)(P.env_offset + e);
+    // the record's two halves and the step counter in one round trip
+    const int4 r0 = *reinterpret_cast<const int4*>(rec), r1 = *reinterpret_cast<const int4*>(rec + 4);
     int c = P.reset_pre[e];
-    for (int k = 0; k < kPreChunks; ++k, ++c) {
-      const uint32_t t = (uint32_t)c * kResetChunk + (uint32_t)tid;
-      if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
+    if (r1.w < 0) continue;   // word 7: found already
+    const uint32_t ep = (uint32_t)r0.y + 1u, genv = (uint32_t)(P.env_offset + e);   // r0.y: QS_E_EPISODE
+    for (int k = 0; k < kPreSteps; ++k, ++c) {
+      if ((uint32_t)c * 64u >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
+      const uint32_t t = (uint32_t)c * 64u + (uint32_t)lane;
       bool ok = true;
       T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
 #pragma unroll
@@ -1729,19 +1733,15 @@ __device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD]
             if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
         }
       }
-      if (tid == 0) s_pw = kResetNone;
-      __syncthreads();
-      if (ok) atomicMin(&s_pw, (int)t);
-      __syncthreads();
-      const int w = s_pw;
-      __syncthreads();
-      if (w != kResetNone) {
-        if (tid == 0) rec[kEnvPreWord] = (int32_t)(0x80000000u | ((ep & 0x7fu) << 24) | (uint32_t)w);
+      const unsigned long long m = __ballot(ok);
+      if (m) {
+        const uint32_t w = (uint32_t)c * 64u + (uint32_t)(__ffsll((long long)m) - 1);
+        if (lane == 0) rec[kEnvPreWord] = (int32_t)(0x80000000u | ((ep & 0x7fu) << 24) | w);
         c = -1;
         break;
       }
     }
-    if (tid == 0 && c >= 0) P.reset_pre[e] = c;
+    if (lane == 0 && c >= 0) P.reset_pre[e] = c;
   }
 }
 
@@ -1759,10 +1759,12 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
 #pragma unroll
     for (int k = 0; k < 3; ++k) orig[d][k] = d < D ? P.orig_xyz[d * 3 + k] : T(0);
   const int home = n > 0 ? (int)(blockIdx.x % (unsigned)n) : 0;
-  // More envs than workgroups (a reset of every env): workgroup b takes envs
-  // b, b + G, b + 2G, … in turn.
-  const int G = (int)gridDim.x;
-  int idx = n > 0 && (int)blockIdx.x < n * kResetGang ? home : -1;   // nothing queued: the usual step
+  // With the precomputed resets the first kQueueWG workgroups serve the queue
+  // and the others precompute (so neither waits for the other).  More envs than
+  // queue workgroups (a reset of every env): workgroup b takes envs b, b + G,
+  // b + 2G, … in turn.
+  const int G = P.reset_pre ? min((int)gridDim.x, kQueueWG) : (int)gridDim.x;
+  int idx = n > 0 && (int)blockIdx.x < min(G, n * kResetGang) ? home : -1;   // nothing queued: the usual step
   QS_RS_BEGIN();
   while (idx >= 0) {
     int* const r = rq + kRqLine * (1 + idx);
@@ -1862,7 +1864,9 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     QS_RS_PICK();
   }
   QS_RS_END(n);
-  if (P.reset_pre) reset_precompute(P, orig);
+  if (P.reset_pre && (int)blockIdx.x >= G)
+    reset_precompute(P, orig, ((int)blockIdx.x - G) * (kResetBlock / 64) + (int)(threadIdx.x >> 6),
+                     ((int)gridDim.x - G) * (kResetBlock / 64));
 }
 
 }  // namespace qs

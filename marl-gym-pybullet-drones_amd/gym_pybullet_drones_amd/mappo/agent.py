@@ -1041,15 +1041,15 @@ class MAPPOAgent:
                 else:
                     # Graph replay puts the first branch of a fork on the parent's
                     # hardware queue and runs each queue's nodes in capture order;
-                    # every cross-queue edge costs ~5-13 µs.  So the critical chain
-                    # (actor kernel → dW2 → the reductions) is captured first on the
-                    # launch stream, the critic on the side stream beside it, and
-                    # the actor's small dW1 GEMM after the critic on the side stream
-                    # (on its own queue it would hold the critic back in order).
+                    # every cross-queue edge costs ~5-13 µs.  So the actor chain
+                    # (actor kernel → dW2 → dW1 → the reductions) is captured first
+                    # on the launch stream and the critic on the side stream beside
+                    # it (dW1 on a third queue held the critic back behind its wait
+                    # for the actor; after the critic it put a join on the path).
                     launch_w1 = actor_all(False, defer_w1=True)
                     with torch.cuda.stream(self._side):
                         critic_all(False, False)
-                        launch_w1()
+                    launch_w1()
                 cur.wait_stream(self._side)
                 if own:
                     for g in [logstd.grad] + wa:
