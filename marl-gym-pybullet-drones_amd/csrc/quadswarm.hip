@@ -222,9 +222,9 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
       const int c = v ? atoi(v) : 0;
       return c >= 64 && c <= 16384 ? c : 1024;
     }();
-    // kQueueWG workgroups for the queue, then one wave per env for the
-    // precomputed resets
-    const int rgrid = P.reset_pre ? qs::kQueueWG + std::min(4 * cap, (P.E + 3) / 4)
+    // kQueueWG workgroups for the queue, then one per env for the precomputed
+    // resets
+    const int rgrid = P.reset_pre ? qs::kQueueWG + std::min(4 * cap, P.E)
                                   : std::min(cap, std::max(64, P.E * 4));
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());

@@ -745,6 +745,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvRetWord * 4, 0));
   const v2u_t c67 = __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvLogWord * 4, 0);
   const int32_t log_n0 = (int32_t)c67.x, pre0 = (int32_t)c67.y;
+  // the precomputed search's progress (256-try chunks all rejected), so a queued
+  // env's search starts past them; a null buffer reads 0 (num_records 0)
+  const int32_t pre_c = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
+      rsrc(P.reset_pre, P.reset_pre ? E * 4u : 0u), valid ? (int)(e * 4u) : (int)kOOB, 0, 0);
   issue_fence();
   T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
 #pragma unroll
@@ -1524,9 +1528,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           __syncthreads();
           if (local >= 0) {
             const int slot = s.qbase + local;
-            // claim word {chunks claimed 0, best try none}, env id, gang 0
+            // claim word {chunks claimed, best try none}, env id, gang 0.  The
+            // precomputed search rejected tries [0, 256·pre_c): the claims start at
+            // the chunk (tries 1 + 256k … 256k + 256) that holds try 256·pre_c
+            const int k0 = pre_c > 0 ? pre_c - 1 : 0;
             *reinterpret_cast<int4*>(P.reset_queue + kRqLine * (1 + slot)) =
-                make_int4(0, kResetNoneDev, (int)(blockIdx.x * P.EPB + lenv), 0);
+                make_int4(k0, kResetNoneDev, (int)(blockIdx.x * P.EPB + lenv), 0);
             s.need[lenv] = 0;
           }
           __syncthreads();
@@ -1663,7 +1670,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 // slot when it queues an env.
 //
 // An env's tries are cut into chunks of kResetChunk (chunk c holds tries
-// 1 + kResetChunk·c + t, thread t).  Workgroup b works on slot b mod n (so up
+// 1 + kResetChunk·c + t, thread t; the claims start past the tries the
+// precomputed search already rejected).  Workgroup b works on slot b mod n (so up
 // to kResetGang workgroups share an env; with more envs than workgroups, slots
 // b, b + G, … in turn): it claims the slot's next chunk (issued one chunk
 // ahead, so the atomic's round trip runs under the Philox work), tests it,
@@ -1679,7 +1687,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 constexpr int kResetBlock = 256;
 constexpr int kResetChunk = kResetBlock;   // tries per chunk, one per thread
 constexpr int kResetMaxD = 8;
-constexpr int kResetGang = 16;
+constexpr int kResetGang = 32;
 constexpr int kResetNone = kResetNoneDev;  // "no accepted try yet"
 
 __device__ __forceinline__ unsigned long long rq_claim(unsigned long long* w) {
@@ -1696,31 +1704,32 @@ __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
 
 // The precomputed resets: an env's next-episode reset draw depends only on
 // (seed, env, episode), so the search for it need not wait for the reset.
-// One wave per env (the launch's workgroups past the first kQueueWG): each
-// launch it tests kPreSteps × 64 tries (tries 64·c + lane, try 0 included) of
-// its env when word 7 of the env record holds no try for the next episode,
-// continuing at step reset_pre[e]; the first accepted try (the lowest lane of
-// the first step whose ballot is not empty) goes into word 7, and the step
-// kernel that resets the env into that episode uses it instead of testing
-// try 0 — the first accepted try of MH:83-102, as the queue search finds it.
-// No atomics, no barriers.  An env that resets before its search ends takes the
-// step kernel's own path (try 0, then the queue).  (A workgroup per env with
-// 256-try chunks ran 17 workgroups per CU in three residency rounds: 12 µs.)
-constexpr int kPreSteps = 8;
+// One workgroup per env (the launch's workgroups past the first kQueueWG):
+// each launch it tests kPreChunks chunks of 256 tries (tries 256·c + t, try 0
+// included) of its env when word 7 of the env record holds no try for the
+// next episode, continuing at chunk reset_pre[e]; the first accepted try goes
+// into word 7, and the step kernel that resets the env into that episode uses
+// it instead of testing try 0 — the first accepted try of MH:83-102, as the
+// queue search finds it.  No atomics.  An env that resets before its search
+// ends takes the step kernel's own path (try 0, then the queue, whose claims
+// start past the chunks tested here).  (One wave per env, 64 tries a step:
+// the serial Philox chain of a lone wave made 8 steps cost 25 µs a launch.)
+constexpr int kPreChunks = 2;
 constexpr int kQueueWG = 256;   // workgroups of the search launch that serve the queue (the rest precompute)
 template <class T>
 __device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD][3], int first, int stride) {
-  const int D = P.D, lane = threadIdx.x & 63;
-  for (int e = first; e < P.E; e += stride) {   // wave-uniform
+  __shared__ int s_pw;
+  const int D = P.D, tid = threadIdx.x;
+  for (int e = first; e < P.E; e += stride) {   // workgroup-uniform
     int32_t* const rec = P.env + (size_t)e * kEnvRec;
-    // the record's two halves and the step counter in one round trip
+    // the record's two halves and the chunk counter in one round trip
     const int4 r0 = *reinterpret_cast<const int4*>(rec), r1 = *reinterpret_cast<const int4*>(rec + 4);
     int c = P.reset_pre[e];
     if (r1.w < 0) continue;   // word 7: found already
     const uint32_t ep = (uint32_t)r0.y + 1u, genv = (uint32_t)(P.env_offset + e);   // r0.y: QS_E_EPISODE
-    for (int k = 0; k < kPreSteps; ++k, ++c) {
-      if ((uint32_t)c * 64u >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
-      const uint32_t t = (uint32_t)c * 64u + (uint32_t)lane;
+    for (int k = 0; k < kPreChunks; ++k, ++c) {
+      if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
+      const uint32_t t = (uint32_t)c * kResetChunk + (uint32_t)tid;
       bool ok = true;
       T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
 #pragma unroll
@@ -1733,15 +1742,19 @@ __device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD]
             if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
         }
       }
-      const unsigned long long m = __ballot(ok);
-      if (m) {
-        const uint32_t w = (uint32_t)c * 64u + (uint32_t)(__ffsll((long long)m) - 1);
-        if (lane == 0) rec[kEnvPreWord] = (int32_t)(0x80000000u | ((ep & 0x7fu) << 24) | w);
+      if (tid == 0) s_pw = kResetNone;
+      __syncthreads();
+      if (ok) atomicMin(&s_pw, (int)t);
+      __syncthreads();
+      const int w = s_pw;
+      __syncthreads();
+      if (w != kResetNone) {
+        if (tid == 0) rec[kEnvPreWord] = (int32_t)(0x80000000u | ((ep & 0x7fu) << 24) | (uint32_t)w);
         c = -1;
         break;
       }
     }
-    if (lane == 0 && c >= 0) P.reset_pre[e] = c;
+    if (tid == 0 && c >= 0) P.reset_pre[e] = c;
   }
 }
 
@@ -1864,9 +1877,7 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
     QS_RS_PICK();
   }
   QS_RS_END(n);
-  if (P.reset_pre && (int)blockIdx.x >= G)
-    reset_precompute(P, orig, ((int)blockIdx.x - G) * (kResetBlock / 64) + (int)(threadIdx.x >> 6),
-                     ((int)gridDim.x - G) * (kResetBlock / 64));
+  if (P.reset_pre && (int)blockIdx.x >= G) reset_precompute(P, orig, (int)blockIdx.x - G, (int)gridDim.x - G);
 }
 
 }  // namespace qs
