@@ -92,7 +92,8 @@ def parse():
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
     p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
-    p.add_argument("--wgrad-rm", type=int, default=1, help="learner: actor dW2 on qs_wgrad_rm (0 = torch.bmm GEMMs)")
+    p.add_argument("--wgrad-rm", type=int, default=0, help="learner: actor dW2 on qs_wgrad_rm (0 = torch.bmm GEMMs)")
+    p.add_argument("--actor-first", type=int, default=0, help="learner: capture the actor chain first (dW1 after dW2)")
     p.add_argument("--critic-adam-side", type=int, default=0,
                    help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
@@ -409,6 +410,7 @@ def mappo_leg(args, ranks, T, cfg=None):
               mini_batch_size=mb, output_dir="/tmp/qs_bench_mappo", **cfg)
     m.agent.side_stream = bool(args.side_stream)
     m.agent.critic_adam_side = bool(args.critic_adam_side)
+    m.agent.actor_first = bool(args.actor_first)
     from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
     _F16Work.w1_stream = bool(args.w1_stream)
     _F16Work.wgrad_rm = bool(args.wgrad_rm)

@@ -366,7 +366,7 @@ class _F16Work(_M3Work):
     rows and reduction tasks as _M3Work.backward."""
 
     w1_stream = True   # dW1 on a third stream beside dW2 (False: after it, one stream)
-    wgrad_rm = True    # dW2 on qs_wgrad_rm (False: torch.bmm row-chunk GEMMs)
+    wgrad_rm = False   # dW2 on qs_wgrad_rm (opt-in: 47 µs vs 41 µs for the torch.bmm row-chunk GEMMs)
 
     def __init__(self, mlp, K, device):
         f0, f1, f2 = mlp.fcs
@@ -388,8 +388,7 @@ class _F16Work(_M3Work):
         m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 2048), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
         self.C2 = self.C1 = 0
         self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
-        # dW2 on qs_wgrad_rm: 64 chunks of 512 rows at 32 768 rows (hipBLASLt ran the
-        # 16 batched 2 048-row GEMMs at 63 µs, 0.43 of the fp32 MFMA peak)
+        # dW2 on qs_wgrad_rm (opt-in): 64 chunks of 512 rows at 32 768 rows
         self.R2 = _wgrad_rm_chunks(K) if self.wgrad_rm else 0
         if os.environ.get("QS_DEBUG_SHAPES"):
             print(f"_F16Work: K={K} I={self.I} dW2 chunks={self.R2 or self.S2} ({'qs_wgrad_rm' if self.R2 else 'bmm'})",
@@ -465,10 +464,9 @@ class _F16Work(_M3Work):
             if getattr(self, '_s3', None) is None or self._s3.device != cur.device:
                 self._s3 = torch.cuda.Stream(device=cur.device)
             self._s3.wait_stream(cur)
-            # dW2 first: it stays on the actor's queue (the critical path)
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
             with torch.cuda.stream(self._s3):
                 w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
             cur.wait_stream(self._s3)
         else:
             w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
@@ -828,6 +826,7 @@ class MAPPOAgent:
         # one rank, fused actor: the critic's sums + Adam on the side stream too (its own
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
+        self.actor_first = kwargs.get('actor_first', False)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
                                    share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
@@ -1034,22 +1033,20 @@ class MAPPOAgent:
             if self.side_stream:
                 own = not multi and self.critic_adam_side
                 self._side.wait_stream(cur)
-                if multi or own:
-                    with torch.cuda.stream(self._side):
-                        critic_all(multi, own)
-                    actor_all(multi)
-                else:
-                    # Graph replay puts the first branch of a fork on the parent's
-                    # hardware queue and runs each queue's nodes in capture order;
-                    # every cross-queue edge costs ~5-13 µs.  So the actor chain
-                    # (actor kernel → dW2 → dW1 → the reductions) is captured first
-                    # on the launch stream and the critic on the side stream beside
-                    # it (dW1 on a third queue held the critic back behind its wait
-                    # for the actor; after the critic it put a join on the path).
+                if self.actor_first and not (multi or own):
+                    # (opt-in) the actor chain captured first on the launch stream,
+                    # dW1 after dW2 on it, the critic beside it: graph replay keeps
+                    # the first branch of a fork on the parent's hardware queue.  It
+                    # read faster under rocprofv3's kernel trace and measured slower
+                    # in the bench
                     launch_w1 = actor_all(False, defer_w1=True)
                     with torch.cuda.stream(self._side):
                         critic_all(False, False)
                     launch_w1()
+                else:
+                    with torch.cuda.stream(self._side):
+                        critic_all(multi, own)
+                    actor_all(multi)
                 cur.wait_stream(self._side)
                 if own:
                     for g in [logstd.grad] + wa:
