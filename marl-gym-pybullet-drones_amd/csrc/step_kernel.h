@@ -1687,7 +1687,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
 constexpr int kResetBlock = 256;
 constexpr int kResetChunk = kResetBlock;   // tries per chunk, one per thread
 constexpr int kResetMaxD = 8;
-constexpr int kResetGang = 32;
+#ifndef QS_RESET_GANG   // (dev builds may override the three search sizes)
+#define QS_RESET_GANG 32
+#endif
+constexpr int kResetGang = QS_RESET_GANG;
 constexpr int kResetNone = kResetNoneDev;  // "no accepted try yet"
 
 __device__ __forceinline__ unsigned long long rq_claim(unsigned long long* w) {
@@ -1714,8 +1717,14 @@ __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
 // ends takes the step kernel's own path (try 0, then the queue, whose claims
 // start past the chunks tested here).  (One wave per env, 64 tries a step:
 // the serial Philox chain of a lone wave made 8 steps cost 25 µs a launch.)
-constexpr int kPreChunks = 2;
-constexpr int kQueueWG = 256;   // workgroups of the search launch that serve the queue (the rest precompute)
+#ifndef QS_PRE_CHUNKS
+#define QS_PRE_CHUNKS 2
+#endif
+#ifndef QS_QUEUE_WG
+#define QS_QUEUE_WG 256
+#endif
+constexpr int kPreChunks = QS_PRE_CHUNKS;
+constexpr int kQueueWG = QS_QUEUE_WG;   // workgroups of the search launch that serve the queue (the rest precompute)
 template <class T>
 __device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD][3], int first, int stride) {
   __shared__ int s_pw;
