@@ -355,11 +355,11 @@ def test_update_graph_captures_the_allreduce():
             port = sk.getsockname()[1]
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                 device_id=torch.device("cuda", torch.cuda.current_device()))
+    agents, res = [], []
     try:
         E, D, O, A, T = 64, 3, 27, 1, 8
         obs_space = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O)))
         act_space = Box(-np.ones((D, A)), np.ones((D, A)))
-        agents = []
         for graphs in (False, True):
             torch.manual_seed(5)
             ag = MAPPOAgent(obs_space, act_space, hidden_dim=64, opt_epochs=2, mini_batch_size=128,
@@ -374,7 +374,6 @@ def test_update_graph_captures_the_allreduce():
         buf.ret_env.normal_()
         buf.adv_env.normal_()
         buf.t, buf.full = 0, True
-        res = []
         for ag in agents:
             gen = torch.Generator(device="cuda")
             gen.manual_seed(0)
@@ -386,8 +385,20 @@ def test_update_graph_captures_the_allreduce():
         for k in ('policy_loss', 'value_loss', 'approx_kl'):
             assert res[0][k] == res[1][k]
     finally:
+        agents.clear()
+        res.clear()
+        _release_graphs()
         if own:
             dist.destroy_process_group()
+
+
+def _release_graphs():
+    """Frees the agents' HIP graphs (and the RCCL all-reduces captured in them)
+    before the process group is destroyed: tearing the communicator down under a
+    live graph that holds its kernels aborted the process once (exit 134)."""
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("graphs", [False, True])
@@ -408,14 +419,18 @@ def test_direct_update_allreduce_path_bit_identical(graphs):
             port = sk.getsockname()[1]
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                 device_id=torch.device("cuda", torch.cuda.current_device()))
+    def case(E, T, side):
+        a_one, r_one = _hidden256_update(graphs, E, T)
+        a_ar, r_ar = _hidden256_update(graphs, E, T, force_allreduce=True, side_stream=side)
+        assert torch.equal(a_one.actor_opt.flat, a_ar.actor_opt.flat)
+        assert torch.equal(a_one.critic_opt.flat, a_ar.critic_opt.flat)
+        assert torch.equal(a_one.critic_opt.exp_avg_sq, a_ar.critic_opt.exp_avg_sq)
+        assert r_one == r_ar
+
     try:
         for E, T, side in ((256, 16, True), (32, 8, True), (256, 16, False)):
-            a_one, r_one = _hidden256_update(graphs, E, T)
-            a_ar, r_ar = _hidden256_update(graphs, E, T, force_allreduce=True, side_stream=side)
-            assert torch.equal(a_one.actor_opt.flat, a_ar.actor_opt.flat)
-            assert torch.equal(a_one.critic_opt.flat, a_ar.critic_opt.flat)
-            assert torch.equal(a_one.critic_opt.exp_avg_sq, a_ar.critic_opt.exp_avg_sq)
-            assert r_one == r_ar
+            case(E, T, side)
     finally:
+        _release_graphs()
         if own:
             dist.destroy_process_group()
