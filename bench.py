@@ -164,6 +164,11 @@ class Ranks:
 
     def close(self):
         if self.dist:
+            # the MAPPO legs' HIP graphs hold captured RCCL all-reduces: free them
+            # before the communicator goes (a teardown under a live graph aborted once)
+            import gc
+            gc.collect()
+            self.sync()
             self.dist.destroy_process_group()
 
 
