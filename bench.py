@@ -96,6 +96,8 @@ def parse():
     p.add_argument("--actor-first", type=int, default=0, help="learner: capture the actor chain first (dW1 after dW2)")
     p.add_argument("--critic-adam-side", type=int, default=0,
                    help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
+    p.add_argument("--strong", type=int, default=1,
+                   help="with N > 1 ranks: also time SURVEY §8(e)'s strong partitions of configs 3-5 (0 = skip)")
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
     p.add_argument("--dry-ms", type=float, default=2.0, help="--dry-run: ms per stand-in step of rank 0 (rank r: (1+r)x)")
     return p.parse_args()
@@ -164,10 +166,9 @@ class Ranks:
 
     def close(self):
         if self.dist:
-            # the MAPPO legs' HIP graphs hold captured RCCL all-reduces: free them
-            # before the communicator goes (a teardown under a live graph aborted once)
-            import gc
-            gc.collect()
+            # every MAPPO leg released its HIP graphs (MAPPO.close -> release_graphs:
+            # they hold captured RCCL all-reduces, which must not outlive the
+            # communicator); drain the device before it goes
             self.sync()
             self.dist.destroy_process_group()
 
@@ -392,6 +393,60 @@ MAPPO_LEGS = {
 }
 
 
+# SURVEY §8(e)'s partitions of BASELINE.json configs 3-5 over the ranks of a run
+# (strong scaling: the global env batch and the global minibatch are fixed, each
+# rank holds 1/G of both and the gradients are all-reduced per minibatch).  At
+# G = 8 the C3 and C5 legs are exactly configs[2] and configs[4]; at G = 4 the
+# C4 leg is configs[3].
+STRONG_LEGS = {
+    "C3": dict(task="multihover", drones=8, global_envs=16384, act="one_d_pid", physics="dyn", T=256,
+               global_mb=4096, **LEARN_MAPPO,
+               label="MultiHover 8-drone x 16384 envs (BASELINE configs[2]); learn_mappo.py:196-216"),
+    "C4": dict(task="spiral", drones=5, global_envs=8192, act="vel", physics="dyn", T=64, global_mb=4096,
+               norm_obs=True, clip_param=0.1, entropy_coef=0.0005, action_scale=0.4, clip_obs=10,
+               reference_compat=False,
+               label="Spiral 5-drone x 8192 envs (BASELINE configs[3]); env_select_learn_mappo.py:262-283"),
+    "C5": dict(task="multihover", drones=16, global_envs=8192, act="one_d_pid", physics="pyb_dw", T=256,
+               global_mb=4096, **LEARN_MAPPO,
+               label="MultiHover 16-drone x 8192 envs, PYB_DW (BASELINE configs[4]); learn_mappo.py:196-216"),
+}
+STRONG_SIM = {"C3": ("one_d_pid", "dyn", "multihover", 8, 16384, 418.0),
+              "C4": ("vel", "dyn", "spiral", 5, 8192, 1111.0),
+              "C5": ("one_d_pid", "pyb_dw", "multihover", 16, 8192, 418.0)}
+
+
+def leg_plan(args, world):
+    """The legs a run of `world` ranks times, in order: (kind, name, scaling, per-rank
+    envs, per-rank mini_batch_size or None).  world 1: the headline, PYB, the MAPPO
+    legs (C3 at T = 256 and 32, the C4 / C5 / reference-shape trainer configs) and
+    the other BASELINE configs' rollouts.  world > 1: the headline and the MAPPO C3
+    leg weak-scaled (16 384 envs per rank, as at world 1), the C4 / C5 trainer and
+    rollout legs weak-scaled beside them, and §8(e)'s strong partitions of
+    configs 3-5 (STRONG_LEGS / STRONG_SIM)."""
+    plan = [("sim", "headline", "weak", args.envs, None)]
+    if args.pyb:
+        plan.append(("sim", "pyb", "weak", args.envs, None))
+    if args.mappo:
+        plan.append(("mappo", "C3", "weak", args.envs, args.mappo_mb))
+        if args.mappo_t32 and world == 1:
+            plan.append(("mappo", "C3_t32", "weak", args.envs, args.mappo_mb))
+        for k in filter(None, args.mappo_configs.split(",")):
+            if k in MAPPO_LEGS and (world == 1 or k != "ref"):   # ref: the 1-GPU reference shape
+                plan.append(("mappo", k, "weak", MAPPO_LEGS[k]["envs"], MAPPO_LEGS[k]["mb"]))
+        if world > 1 and args.strong:
+            for k, c in STRONG_LEGS.items():
+                if c["global_envs"] % world == 0 and c["global_mb"] % world == 0:
+                    plan.append(("mappo", k, "strong", c["global_envs"] // world, c["global_mb"] // world))
+    if args.configs:
+        for k, c in EXTRA_CONFIGS.items():
+            plan.append(("sim", k, "weak", c["envs"], None))
+        if world > 1 and args.strong:
+            for k, c in STRONG_SIM.items():
+                if c[4] % world == 0:
+                    plan.append(("sim", k, "strong", c[4] // world, None))
+    return plan
+
+
 def mappo_leg(args, ranks, T, cfg=None):
     """Full MAPPO train steps: by default on the bench's C3 envs (learn_mappo.py:196-216
     hyper-parameters, hidden 256, opt_epochs 10; minibatch scaled to the ~100x larger
@@ -401,6 +456,10 @@ def mappo_leg(args, ranks, T, cfg=None):
     from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
     cfg = dict(cfg or dict(task="multihover", drones=args.drones, envs=args.envs, act=args.act, physics="dyn",
                            T=T, mb=args.mappo_mb, **LEARN_MAPPO))
+    scaling = "weak"
+    if "global_envs" in cfg:   # a strong partition (STRONG_LEGS): 1/G of the envs and of the minibatch per rank
+        cfg["envs"], cfg["mb"] = cfg.pop("global_envs") // ranks.world, cfg.pop("global_mb") // ranks.world
+        scaling = "strong"
     D, E, T, mb = cfg.pop("drones"), cfg.pop("envs"), cfg.pop("T"), cfg.pop("mb")
     task, phys, label = cfg.pop("task"), cfg.pop("physics"), cfg.pop("label", None)
     act = {"one_d_pid": ActionType.ONE_D_PID, "vel": ActionType.VEL, "rpm": ActionType.RPM}[cfg.pop("act")]
@@ -452,7 +511,9 @@ def mappo_leg(args, ranks, T, cfg=None):
                                  "flop_per_update": upd_flop, "rollout_actor_flop": roll_flop,
                                  "train_step_tflops": (upd_flop + roll_flop) / dt / 1e12,
                                  "what": "PPO update: MLP fwd+bwd FLOP / update device time, fp32"},
-            "config": {"workload": label, "rollout_steps": T, "envs_per_gpu": E, "drones": D, "obs_dim": O,
+            "config": {"workload": label, "scaling": scaling, "global_envs": E * world,
+                       "global_mini_batch_size": mb * world, "rollout_steps": T, "envs_per_gpu": E, "drones": D,
+                       "obs_dim": O,
                        "act_dim": A, "hidden": 256, "opt_epochs": 10, "mini_batch_size": mb,
                        "minibatches_per_epoch": T * E // mb, "fused_actor_kernel": fused_actor,
                        "overrides": cfg or None,
@@ -500,7 +561,9 @@ def main():
                 "unit": "stand-in steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": elapsed / args.steps * 1e3, "rank_ms_per_step": [e / args.steps * 1e3 for e in every],
                 "dry_run": {"pid": os.getpid(), "ppid": os.getppid(), "pppid": _ppid(os.getppid()),
-                            "backend": "gloo" if world > 1 else None}}), flush=True)
+                            "backend": "gloo" if world > 1 else None},
+                "legs": [{"kind": k, "name": n, "scaling": sc, "envs_per_rank": e, "mini_batch_per_rank": m}
+                         for k, n, sc, e, m in leg_plan(args, world)]}), flush=True)
         ranks.close()
         return
     E, D = args.envs, args.drones
@@ -508,39 +571,54 @@ def main():
     value, elapsed, kern_ms, steps, eps_done = sim_leg(args, ranks, "dyn")
     nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
-    pyb = None
-    if args.pyb:   # the same rollout under Physics.PYB (the reference's training default)
-        pv, _, pk, _, _ = sim_leg(args, ranks, "pyb")
-        pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
-               "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        if rank == 0 and not args.no_cpu_baseline:
-            pyb["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, physics="pyb")
-    mappo = mappo_leg(args, ranks, args.mappo_steps) if args.mappo else None
-    mappo32 = mappo_leg(args, ranks, 32) if (args.mappo and args.mappo_t32) else None
-    mappo_cfgs = None
-    if args.mappo and args.mappo_configs and world == 1:   # the other trainer configs, one GPU each
-        mappo_cfgs = {k: mappo_leg(args, ranks, c["T"], c) for k, c in MAPPO_LEGS.items()
-                      if k in args.mappo_configs.split(",")}
-    configs = None
-    if args.configs and world == 1:   # the other BASELINE configs, one GPU each
-        configs = {}
-        for name, c in EXTRA_CONFIGS.items():
+    pyb = mappo = mappo32 = mappo_cfgs = configs = None
+    mappo_strong, configs_strong = {}, {}
+    for kind, name, scaling, e_rank, mb_rank in leg_plan(args, world)[1:]:
+        if kind == "sim" and name == "pyb":   # the same rollout under Physics.PYB (the reference's training default)
+            pv, _, pk, _, _ = sim_leg(args, ranks, "pyb")
+            pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
+                   "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                pyb["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, physics="pyb")
+        elif kind == "mappo" and scaling == "strong":
+            mappo_strong[name] = mappo_leg(args, ranks, STRONG_LEGS[name]["T"], STRONG_LEGS[name])
+        elif kind == "mappo" and name == "C3":
+            mappo = mappo_leg(args, ranks, args.mappo_steps)
+        elif kind == "mappo" and name == "C3_t32":
+            mappo32 = mappo_leg(args, ranks, 32)
+        elif kind == "mappo":   # the other trainer configs, per-GPU sizes
+            mappo_cfgs = mappo_cfgs or {}
+            mappo_cfgs[name] = mappo_leg(args, ranks, MAPPO_LEGS[name]["T"], MAPPO_LEGS[name])
+        elif kind == "sim" and scaling == "strong":
+            act, phys, task, D_, glob, byts = STRONG_SIM[name]
+            progress(f"config leg {name} (strong: {glob} envs over {world} ranks)")
+            v, el, km, st, ne = sim_leg(args, ranks, phys, task, e_rank, D_, act, ())
+            nb = byts * e_rank * D_
+            configs_strong[name] = {"workload": f"{task} {D_}-drone x {glob} envs over {world} ranks "
+                                                f"({e_rank} per rank), {act}, {phys}", "scaling": "strong",
+                                    "value": v, "unit": "agent-steps/s", "kernel_ms": km,
+                                    "bytes_per_agent_step": byts, "roofline_frac": nb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "episodes_ended_in_timed_window_rank0": ne}
+        elif kind == "sim":   # the other BASELINE configs, per-GPU sizes
+            c = EXTRA_CONFIGS[name]
             progress(f"config leg {name}")
             v, el, km, st, ne = sim_leg(args, ranks, c["physics"], c["task"], c["envs"], c["drones"],
                                         c["act"], c["aux"])
             nb = c["bytes"] * c["envs"] * c["drones"]
-            configs[name] = {"workload": c["label"], "value": v, "unit": "agent-steps/s", "kernel_ms": km,
-                             "bytes_per_agent_step": c["bytes"],
+            configs = configs or {}
+            configs[name] = {"workload": c["label"], "scaling": "weak", "value": v, "unit": "agent-steps/s",
+                             "kernel_ms": km, "bytes_per_agent_step": c["bytes"],
                              "roofline_frac": nb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "episodes_ended_in_timed_window": ne}
             vr = valu_roofline(name, km)
             if vr:
                 configs[name]["valu_roofline"] = vr
-            if not args.no_cpu_baseline:   # BASELINE.md:36: the CPU restatement of the same config
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                # BASELINE.md:36: the CPU restatement of the same config (rank 0 at N=1 only)
                 configs[name]["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, c["task"], c["drones"],
                                                              c["act"], c["physics"], c["aux"])
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_src = pmc_traffic(E, D, args.act)
         line = {
             "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": steps,
@@ -565,6 +643,9 @@ def main():
             "mappo_configs": mappo_cfgs,
             "configs": configs,
         }
+        if world > 1:
+            line["mappo_strong"] = mappo_strong or None
+            line["configs_strong"] = configs_strong or None
         print(json.dumps(line), flush=True)
     ranks.close()
 

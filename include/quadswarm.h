@@ -93,6 +93,11 @@ typedef enum {            /* Physics (enums.py:13-21)                      */
 /* qs_spec.flags */
 #define QS_FLAG_NO_AUTORESET 1u  /* single-env facade: BaseAviary.step never
                                     resets by itself (BaseAviary.py:259-383) */
+#define QS_FLAG_INKERNEL_RESET_SEARCH 2u  /* MultiHover layouts that can reject:
+                                    run the whole reset rejection loop
+                                    (MultiHoverAviary.py:83-102) inside the
+                                    step kernel, no deferred search launch
+                                    (the validation form of the deferred one) */
 
 typedef struct qs_spec {
   int32_t task;          /* qs_task                                        */

@@ -217,11 +217,15 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none)
     // Workgroups claim chunks of the queued envs' tries dynamically; the grid is
     // sized from E so a small shard does not pay 1024 empty workgroups every step.
+#ifdef QS_DEV_BUILD
     static const int cap = [] {   // dev knob QS_RESET_GRID: the search grid's workgroup cap
       const char* v = getenv("QS_RESET_GRID");
       const int c = v ? atoi(v) : 0;
       return c >= 64 && c <= 16384 ? c : 1024;
     }();
+#else
+    constexpr int cap = 1024;
+#endif
     // kQueueWG workgroups for the queue, then one per env for the precomputed
     // resets
     const int rgrid = P.reset_pre ? qs::kQueueWG + std::min(4 * cap, P.E)
@@ -265,7 +269,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   if (s.num_envs < 1) return fail(QS_E_INVALID, "qs_create: num_envs must be >= 1");
   if (s.physics != QS_PHYS_DYN && s.physics != QS_PHYS_PYB) return fail(QS_E_INVALID, "qs_create: bad physics");
   if (s.aux_forces & ~7u) return fail(QS_E_INVALID, "qs_create: bad aux_forces");
-  if (s.flags & ~QS_FLAG_NO_AUTORESET) return fail(QS_E_INVALID, "qs_create: bad flags");
+  if (s.flags & ~(QS_FLAG_NO_AUTORESET | QS_FLAG_INKERNEL_RESET_SEARCH)) return fail(QS_E_INVALID, "qs_create: bad flags");
   if (s.pyb_freq <= 0 || s.ctrl_freq <= 0 || s.pyb_freq % s.ctrl_freq)
     return fail(QS_E_INVALID, "qs_create: pyb_freq is not divisible by env_freq");  // BaseAviary.py:79-80
   if (s.ctrl_freq < 2) return fail(QS_E_INVALID, "qs_create: ctrl_freq must be >= 2 (action history length ctrl_freq//2)");
@@ -360,7 +364,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   hipError_t e7 = hipSuccess;
   hipError_t e8 = hipMalloc((void**)&h->err, sizeof(int));
   if (e1 || e2 || e3 || e5 || e6 || e7 || e8) { cleanup(); return fail(QS_E_NOMEM, "qs_create: hipMalloc failed"); }
-  if (may_reject && getenv("QS_INKERNEL_RESET_SEARCH") == nullptr) {
+  if (may_reject && !(s.flags & QS_FLAG_INKERNEL_RESET_SEARCH)) {
     // header line {count, envs written}, then one 128-B record per slot
     // (initialised when the step kernel queues an env; qs::reset_search_kernel)
     const size_t qn = (size_t)qs::kRqLine * (1 + (size_t)s.num_envs);
@@ -428,6 +432,10 @@ int qs_reset(qs_handle* h, uint64_t seed, float* obs, void* stream) {
   HIP_TRY(hipMemsetAsync(h->env, 0, sizeof(int32_t) * qs::kEnvRec * d.num_envs, st));
   HIP_TRY(hipMemsetAsync(h->hist, 0, sizeof(float) * d.hist_len * N * d.act_dim, st));
   HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(int), st));
+  // the precomputed reset searches belong to the old (seed, episode) tags: restart
+  // them, or a queued search would skip the new episode's first chunks (MH:83-102
+  // takes the FIRST accepted try)
+  if (h->rpre) HIP_TRY(hipMemsetAsync(h->rpre, 0, sizeof(int32_t) * d.num_envs, st));
   h->seed = seed;
   int rc;
   if (d.precision == 8) {

@@ -21,6 +21,7 @@ AUX_GND, AUX_DRAG, AUX_DW = 1, 2, 4
 AGENT_FIELDS, ENV_FIELDS = 29, 4
 STATE_AGENT, STATE_ENV, STATE_HISTORY, STATE_EP_RETURN = 0, 1, 2, 3
 FLAG_NO_AUTORESET = 1
+FLAG_INKERNEL_RESET_SEARCH = 2
 REASON_CRASH, REASON_FLIP, REASON_OOB, REASON_ZRANGE = 1, 2, 4, 8
 
 # agent field offsets (include/quadswarm.h)

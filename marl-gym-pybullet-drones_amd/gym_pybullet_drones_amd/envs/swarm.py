@@ -71,8 +71,10 @@ class QuadSwarm:
                  pyb_freq=240, ctrl_freq=None, precision=4, device=None, env_offset=0, initial_xyzs=None,
                  episode_len_sec=None, autoreset=True, drone_model=DroneModel.CF2X,
                  spiral_radius=0.4, spiral_period=10.0, height_rate=0.05, target_center=(0.0, 0.0, 0.0),
-                 aux=()):
-        """aux: extra force models ("gnd", "drag", "dw") added on top of `physics`;
+                 aux=(), inkernel_reset_search=False):
+        """inkernel_reset_search: run MultiHover's whole reset rejection loop inside
+        the step kernel instead of the deferred search launch (validation form).
+        aux: extra force models ("gnd", "drag", "dw") added on top of `physics`;
         with Physics.DYN this is the build-defined DYN + aux combination (SURVEY §8
         physics-mode note), e.g. C5's DYN + downwash."""
         if task not in TASKS:
@@ -106,7 +108,7 @@ class QuadSwarm:
         spec.pyb_freq = int(pyb_freq)
         spec.ctrl_freq = int(ctrl_freq)
         spec.precision = int(precision)
-        spec.flags = 0 if autoreset else L.FLAG_NO_AUTORESET
+        spec.flags = (0 if autoreset else L.FLAG_NO_AUTORESET) | (L.FLAG_INKERNEL_RESET_SEARCH if inkernel_reset_search else 0)
         spec.env_offset = int(env_offset)
         spec.episode_len_sec = float(episode_len_sec)
         self._xyz_keep = None
@@ -144,6 +146,7 @@ class QuadSwarm:
         self.terminal_obs = torch.zeros((E, D, O), dtype=torch.float32, **kw)
         self.reasons = torch.zeros((E, D), dtype=torch.uint8, **kw)
         self.seed = 0
+        self.reset_generation = 0   # qs_reset count: the device episode counters restart at each
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
@@ -167,6 +170,7 @@ class QuadSwarm:
         self.seed = int(seed)
         out = self.obs if obs is None else obs
         L.check(self.lib.qs_reset(self._h, ctypes.c_uint64(self.seed), L.ptr(out), self._stream()), "qs_reset")
+        self.reset_generation += 1
         return out
 
     def reset_envs(self, mask: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None):

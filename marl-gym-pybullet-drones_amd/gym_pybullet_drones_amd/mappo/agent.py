@@ -865,6 +865,20 @@ class MAPPOAgent:
         self._opt_ready = True
         self._graph = None
 
+    def release_graphs(self):
+        """Free the captured update graph — with several ranks it holds the RCCL
+        all-reduces of every minibatch — and its static index / accumulator
+        buffers.  Call before the process group is destroyed: tearing the
+        communicator down under a live graph that holds its kernels aborted a
+        process once (exit 134).  The next update captures again."""
+        g, self._graph = self._graph, None
+        if g is not None:
+            if self.device.type == 'cuda':
+                torch.cuda.synchronize(self.device)
+            g.reset()
+        self._g_perm = self._g_idx = self._g_acc = self._g_rollouts = None
+        self._g_k = 0
+
     def train(self):
         self.ac.train()
 
@@ -952,7 +966,8 @@ class MAPPOAgent:
         lib = L.load()
         if getattr(self, '_ws_key', None) == (mb, D, O, A):
             return
-        f16 = self.fused_actor and _f16_ok(self.ac.actor.pi_net)
+        # the fused actor's own row limit (K·1024 < 2^31, qs_mlp3f_actor) as well as the widths
+        f16 = self.fused_actor and _f16_ok(self.ac.actor.pi_net) and _m3_shape_ok(mb * D, O)
         self._ws_actor = (_F16Work if f16 else _M3Work)(self.ac.actor.pi_net, mb * D, self.device)
         self._ws_critic = _M3Work(self.ac.critic.v_net, mb, self.device)
         self._vh_work = torch.zeros(int(lib.qs_ppo_heads_work_bytes(mb, D)), dtype=torch.uint8, device=self.device)

@@ -251,7 +251,19 @@ class MAPPO:
             self.env.add_tracker('constraint_values', 0, mode='queue')
             self.env.add_tracker('mse', 0, mode='queue')
 
+    def release_graphs(self):
+        """Free the rollout graph and the agent's update graph (and the RCCL
+        collectives captured in them); the next train_step captures again."""
+        g, self._rollout_graph = getattr(self, '_rollout_graph', None), None
+        if g is not None:
+            torch.cuda.synchronize()
+            g.reset()
+        agent = getattr(self, 'agent', None)
+        if agent is not None:
+            agent.release_graphs()
+
     def close(self):
+        self.release_graphs()
         for env in (getattr(self, 'env', None), getattr(self, 'eval_env', None)):
             try:
                 if env is not None:

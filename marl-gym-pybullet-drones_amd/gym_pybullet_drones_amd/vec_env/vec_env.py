@@ -280,8 +280,12 @@ class VecRecordEpisodeStatistics(VecEnvWrapper):
         sw = self.venv.swarm
         _, total = sw.episode_log(cap=0)
         last = getattr(self, "_synced", 0)
-        if total < last:   # the swarm was reset: its counters restarted
+        gen = getattr(sw, "reset_generation", 0)
+        if gen != getattr(self, "_synced_gen", gen) or total < last:
+            # the swarm was reset (by any path) since the last sync: its episode
+            # counters and record seqs restarted at 0
             last, self._synced_seq = 0, -1
+        self._synced_gen = gen
         new = total - last
         self._synced = total
         if new <= 0:

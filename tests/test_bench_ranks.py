@@ -48,3 +48,21 @@ def test_bench_two_ranks_max_over_ranks():
 def test_bench_one_rank_dry_run():
     launcher, line = _run_bench("--dry-run", "--dry-ms", "1", "--steps", "3", "--warmup", "0")
     assert line["n_gpus"] == 1 and line["dry_run"]["pid"] == launcher and line["dry_run"]["backend"] is None
+
+
+def test_bench_two_ranks_lists_strong_legs():
+    """At N > 1 the bench also times SURVEY §8(e)'s strong partitions of BASELINE
+    configs 3-5 (global envs and global minibatch fixed, 1/G per rank), beside the
+    weak-scaled legs; the dry run lists the plan a GPU run of that size executes."""
+    _, line = _run_bench("--gpus", "2", "--dry-run", "--dry-ms", "1", "--steps", "2", "--warmup", "0")
+    legs = {(g["kind"], g["name"], g["scaling"]): g for g in line["legs"]}
+    for name, envs in (("C3", 16384), ("C4", 8192), ("C5", 8192)):
+        m = legs[("mappo", name, "strong")]
+        assert m["envs_per_rank"] == envs // 2 and m["mini_batch_per_rank"] == 4096 // 2
+        assert legs[("sim", name, "strong")]["envs_per_rank"] == envs // 2
+    assert legs[("mappo", "C3", "weak")]["envs_per_rank"] == 16384   # the weak legs stay, labelled
+    assert ("mappo", "C4", "weak") in legs and ("mappo", "C5", "weak") in legs
+    assert ("mappo", "ref", "weak") not in legs   # the 1-GPU reference learner shape
+    _, one = _run_bench("--dry-run", "--dry-ms", "1", "--steps", "2", "--warmup", "0")
+    assert not any(g["scaling"] == "strong" for g in one["legs"])
+    assert ("mappo", "ref", "weak") in {(g["kind"], g["name"], g["scaling"]) for g in one["legs"]}

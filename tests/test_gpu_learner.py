@@ -267,6 +267,28 @@ def test_mappo_train_step_and_checkpoint(graphs, tmp_path):
     m.close()
 
 
+def test_close_releases_graphs(tmp_path):
+    """MAPPO.close() frees the rollout graph and the agent's update graph (with
+    several ranks they hold captured RCCL all-reduces, which must not outlive the
+    process group): no CUDAGraph of the trainer is alive after close()."""
+    import gc
+    import weakref
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    env_func = lambda seed=None, **kw: MultiHoverAviary(num_drones=2, act=ActionType.ONE_D_PID)
+    m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=64, rollout_batch_size=16,
+              rollout_steps=8, mini_batch_size=32, opt_epochs=1, eval_interval=0, log_interval=0, use_graphs=True)
+    m.reset()
+    m.train_step()
+    assert m._rollout_graph is not None and m.agent._graph is not None
+    refs = [weakref.ref(m._rollout_graph), weakref.ref(m.agent._graph)]
+    m.close()
+    gc.collect()   # only to rule out reference cycles: close() itself dropped the graphs
+    assert m._rollout_graph is None and m.agent._graph is None
+    assert all(r() is None for r in refs)
+
+
 @pytest.mark.parametrize("A", [1, 4])
 def test_ppo_heads_kernel_matches_autograd(A):
     """qs_ppo_heads (one launch) against autograd through compute_policy_loss +
@@ -385,20 +407,12 @@ def test_update_graph_captures_the_allreduce():
         for k in ('policy_loss', 'value_loss', 'approx_kl'):
             assert res[0][k] == res[1][k]
     finally:
+        for ag in agents:
+            ag.release_graphs()
         agents.clear()
         res.clear()
-        _release_graphs()
         if own:
             dist.destroy_process_group()
-
-
-def _release_graphs():
-    """Frees the agents' HIP graphs (and the RCCL all-reduces captured in them)
-    before the process group is destroyed: tearing the communicator down under a
-    live graph that holds its kernels aborted the process once (exit 134)."""
-    import gc
-    gc.collect()
-    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("graphs", [False, True])
@@ -422,15 +436,20 @@ def test_direct_update_allreduce_path_bit_identical(graphs):
     def case(E, T, side):
         a_one, r_one = _hidden256_update(graphs, E, T)
         a_ar, r_ar = _hidden256_update(graphs, E, T, force_allreduce=True, side_stream=side)
-        assert torch.equal(a_one.actor_opt.flat, a_ar.actor_opt.flat)
-        assert torch.equal(a_one.critic_opt.flat, a_ar.critic_opt.flat)
-        assert torch.equal(a_one.critic_opt.exp_avg_sq, a_ar.critic_opt.exp_avg_sq)
-        assert r_one == r_ar
+        try:
+            assert torch.equal(a_one.actor_opt.flat, a_ar.actor_opt.flat)
+            assert torch.equal(a_one.critic_opt.flat, a_ar.critic_opt.flat)
+            assert torch.equal(a_one.critic_opt.exp_avg_sq, a_ar.critic_opt.exp_avg_sq)
+            assert r_one == r_ar
+        finally:
+            # the graph holding the captured all-reduces goes before the communicator
+            a_one.release_graphs()
+            a_ar.release_graphs()
 
     try:
         for E, T, side in ((256, 16, True), (32, 8, True), (256, 16, False)):
             case(E, T, side)
     finally:
-        _release_graphs()
+        torch.cuda.synchronize()
         if own:
             dist.destroy_process_group()

@@ -278,20 +278,19 @@ def test_no_autoreset_facade():
 
 
 @pytest.mark.parametrize("precision,num_envs,steps", [(8, 96, 60), (4, 96, 60), (4, 2304, 30)])
-def test_deferred_reset_search_matches_inkernel(precision, num_envs, steps, monkeypatch):
+def test_deferred_reset_search_matches_inkernel(precision, num_envs, steps):
     """The MultiHover reset rejection search queued to reset_search_kernel (layouts
     that can reject, e.g. the reference's default diagonal layout) draws exactly
-    what the in-kernel sequential search draws: state and obs bit-identical over a
-    rollout with many resets (random RPM actions end episodes every ~20 steps).
-    96 envs: several workgroups share each queued env; 2304 envs: the reset queues
-    more envs than the search launch has workgroups (one workgroup walks several)."""
+    what the in-kernel sequential search (QS_FLAG_INKERNEL_RESET_SEARCH) draws:
+    state and obs bit-identical over a rollout with many resets (random RPM
+    actions end episodes every ~20 steps).  96 envs: several workgroups share each
+    queued env; 2304 envs: the reset queues more envs than the search launch has
+    workgroups (one workgroup walks several)."""
     from gym_pybullet_drones_amd.envs import QuadSwarm
     cfg = dict(task="multihover", num_drones=4, act="rpm")
     runs = []
     for inkernel in (False, True):
-        if inkernel:
-            monkeypatch.setenv("QS_INKERNEL_RESET_SEARCH", "1")
-        sw = QuadSwarm(num_envs=num_envs, precision=precision, **cfg)
+        sw = QuadSwarm(num_envs=num_envs, precision=precision, inkernel_reset_search=inkernel, **cfg)
         obs = [sw.reset(9).cpu().numpy()]
         n_done = 0
         for _ in range(steps):
@@ -302,10 +301,43 @@ def test_deferred_reset_search_matches_inkernel(precision, num_envs, steps, monk
         runs.append((np.stack(obs), sw.get_state(0).cpu().numpy(), sw.get_state(1).cpu().numpy(), n_done))
         assert sw.reset_error() == 0
         sw.close()
-        monkeypatch.delenv("QS_INKERNEL_RESET_SEARCH", raising=False)
     assert runs[0][3] > (50 if num_envs < 1024 else 0)   # resets happened
     for a, b in zip(runs[0][:3], runs[1][:3]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("precision", [8, 4])
+def test_reseed_restarts_precomputed_search(precision):
+    """A second qs_reset with a new seed on a rejecting layout (the reference's
+    default diagonal one) while precomputed reset searches of the old seed are
+    part-way done: the next resets draw the new seed's FIRST accepted try
+    (MH:83-102), as the oracle's sequential loop does (qs_reset must
+    restart reset_pre)."""
+    cfg = dict(task="multihover", num_drones=4, act="rpm")
+    sw, orc = make_pair(cfg, E=64, precision=precision)
+    sw.reset(3)
+    orc.reset(3)
+    for _ in range(12):   # searches for the next episodes start and progress (no state writes:
+        # qs_state_io would restart them)
+        sw.step(None)
+        orc.step(None)
+    og = sw.reset(17).cpu().numpy()
+    oc = orc.reset(17)
+    np.testing.assert_array_equal(og[..., :3], oc[..., :3])
+    n_done = 0
+    for t in range(60):
+        r = sw.step(None)
+        c = orc.step(None)
+        torch.cuda.synchronize()
+        done = (c["terminated"] | c["truncated"]).astype(bool)
+        n_done += int(done.sum())
+        np.testing.assert_array_equal(sw.get_state(1).cpu().numpy(), orc.get_state(1), err_msg=f"env t={t}")
+        if done.any():   # the auto-reset draws: positions exact in fp64, same draw in fp32
+            tol = (0.0, 0.0) if precision == 8 else (1e-6, 1e-6)
+            assert_close(f"reset pos t={t}", r.obs.cpu().numpy()[done][..., :3], c["obs"][done][..., :3], tol)
+    assert n_done > 20
+    assert sw.reset_error() == 0
+    sw.close()
 
 
 def _collision_course_state(orc, rng, frac=0.5):

@@ -156,6 +156,32 @@ def test_sync_from_device_queues_each_episode_once(deque_size):
     env.close()
 
 
+def test_sync_from_device_after_outside_reset():
+    """A swarm reset that bypasses VecRecordEpisodeStatistics.reset (e.g. the
+    swarm's own reset), followed by MORE episodes than the last sync counted:
+    the record seqs restarted at 0, so the new run's episodes must still be
+    queued (total < last alone misses this)."""
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    from gym_pybullet_drones_amd.vec_env import SwarmVecEnv, VecRecordEpisodeStatistics
+    E, D = 64, 4
+    venv = SwarmVecEnv(task="multihover", num_envs=E, num_drones=D, act=ActionType.RPM, seed=5, precision=4)
+    env = VecRecordEpisodeStatistics(venv, deque_size=None)
+    env.reset()
+    sw = venv.swarm
+    for _ in range(60):
+        venv.step_t()
+    first = env.sync_from_device()
+    assert first > 0 and len(env.return_queue) == first
+    sw.reset(6)   # outside the wrapper
+    for _ in range(200):   # far more episodes than `first`
+        venv.step_t()
+    full, total = sw.episode_log(cap=1 << 20)
+    assert total > first
+    assert env.sync_from_device() == total
+    assert list(env.return_queue)[first:] == full["ret"].tolist()
+    env.close()
+
+
 class _NpRunningMeanStd:
     """normalization.py:13-60 (numpy, float64)."""
 
