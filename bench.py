@@ -94,6 +94,8 @@ def parse():
     p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
     p.add_argument("--wgrad-rm", type=int, default=0, help="learner: actor dW2 on qs_wgrad_rm (0 = torch.bmm GEMMs)")
     p.add_argument("--actor-first", type=int, default=0, help="learner: capture the actor chain first (dW1 after dW2)")
+    p.add_argument("--fused-max-a", type=int, default=None,
+                   help="learner: widest actor output on the fused actor kernel (default: the agent's _F16_MAX_A)")
     p.add_argument("--critic-adam-side", type=int, default=0,
                    help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
     p.add_argument("--strong", type=int, default=1,
@@ -475,7 +477,10 @@ def mappo_leg(args, ranks, T, cfg=None):
     m.agent.side_stream = bool(args.side_stream)
     m.agent.critic_adam_side = bool(args.critic_adam_side)
     m.agent.actor_first = bool(args.actor_first)
+    from gym_pybullet_drones_amd.mappo import agent as agent_mod
     from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
+    if args.fused_max_a is not None:
+        agent_mod._F16_MAX_A = int(args.fused_max_a)
     _F16Work.w1_stream = bool(args.w1_stream)
     _F16Work.wgrad_rm = bool(args.wgrad_rm)
     _M3Work.wgrad = tuple(w for w in args.wgrad.split(",") if w)

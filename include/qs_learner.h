@@ -19,6 +19,9 @@
  *     MFMA (nn.Linear + torch.tanh autograd in the reference)      qs_mlp3_bwd
  *   the actor's forward, policy loss and backward of a minibatch  qs_mlp3f_actor,
  *     (agent.py:602-640, 728-734)                                  qs_value_head
+ *   MeanStdNormalizer.__call__ / RunningMeanStd.update            qs_rms_update,
+ *     (safe_control_gym normalization.py:13-120): torch float64      qs_rms_normalize
+ *     column reductions per rollout step
  *
  * All pointers are device pointers; every call is asynchronous on `stream`
  * (hipStream_t as void*) and contains no host synchronisation, so it can be
@@ -265,6 +268,25 @@ int qs_mlp_sum_adam(int32_t n, const int32_t* G, const int64_t* P, const float* 
                     const int32_t* pack_I, void* work, void* stream);
 
 const char* qs_learner_last_error(void);
+
+/* The observation normaliser of the rollout (MeanStdNormalizer,
+ * safe_control_gym/math_and_models/normalization.py:13-120; torch float64
+ * column reductions in the reference's GPU-less loop).  x float32 [R][C]
+ * (R rows = envs, C = D·O columns), statistics float64 on the device.
+ * qs_rms_update: the batch's per-column mean and variance (np.mean / np.var
+ * over axis 0), merged into mean[C] / var[C] / *count in place in
+ * normalization.py:42-60's operation order (RunningMeanStd.update); with
+ * sums != NULL nothing is updated and this rank's [Σx (C) | Σx² (C) | R] are
+ * written to sums[2C + 1] instead (the multi-rank path all-reduces them).
+ * work: qs_rms_work_bytes(R, C) bytes, zeroed once (the launch leaves it zero).
+ * qs_rms_normalize: out[R][C] = float32(clip((x − mean)/sqrt(var + eps),
+ * −clip, clip)) in float64 (normalization.py:110-113). */
+int64_t qs_rms_work_bytes(int64_t R, int32_t C);
+int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* var, double* count, double* sums,
+                  void* work, void* stream);
+int qs_rms_normalize(int64_t R, int32_t C, const float* x, const double* mean, const double* var, double eps,
+                     double clip, float* out, void* stream);
+const char* qs_rms_last_error(void);
 
 #ifdef __cplusplus
 }

@@ -67,7 +67,8 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_mlp_wgrad", "qs_mlp_wgrad_chunks", "qs_adam_multi",
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
-           "qs_wgrad_rm", "qs_learner_last_error")
+           "qs_wgrad_rm", "qs_learner_last_error", "qs_rms_work_bytes", "qs_rms_update", "qs_rms_normalize",
+           "qs_rms_last_error")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
 
 _lib = None
@@ -146,14 +147,19 @@ def load():
     L.qs_mlp_wgrad_x.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32, vp, vp, vp]
     L.qs_wgrad_rm.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_learner_last_error.restype = ctypes.c_char_p
+    L.qs_rms_last_error.restype = ctypes.c_char_p
+    L.qs_rms_work_bytes.argtypes = [i64, ctypes.c_int32]
+    L.qs_rms_update.argtypes = [i64, ctypes.c_int32] + [vp] * 7
+    L.qs_rms_normalize.argtypes = [i64, ctypes.c_int32, vp, vp, vp, ctypes.c_double, ctypes.c_double, vp, vp]
     for name in EXPORTS:
-        if name not in ("qs_last_error", "qs_learner_last_error"):
+        if name not in ("qs_last_error", "qs_learner_last_error", "qs_rms_last_error"):
             getattr(L, name).restype = i32
     L.qs_ppo_heads_work_bytes.restype = i64
     L.qs_mlp3_pack_floats.restype = i64
     L.qs_mlp3f_pack_floats.restype = i64
     L.qs_mlp3f_work_bytes.restype = i64
     L.qs_mlp_sum_adam_work_bytes.restype = i64
+    L.qs_rms_work_bytes.restype = i64
     L.qs_mlp_sum_adam_work_bytes.argtypes = []
     _lib = L
     return L
@@ -162,7 +168,12 @@ def load():
 def check(rc, what=""):
     if rc != QS_OK:
         lib = load()
-        msg = lib.qs_learner_last_error() if what.startswith(("qs_gae", "qs_adam", "qs_ppo", "qs_mlp")) else lib.qs_last_error()
+        if what.startswith("qs_rms"):
+            msg = lib.qs_rms_last_error()
+        elif what.startswith(("qs_gae", "qs_adam", "qs_ppo", "qs_mlp", "qs_wgrad", "qs_value")):
+            msg = lib.qs_learner_last_error()
+        else:
+            msg = lib.qs_last_error()
         raise QuadSwarmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
 
 

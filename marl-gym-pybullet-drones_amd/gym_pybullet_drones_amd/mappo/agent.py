@@ -478,11 +478,17 @@ class _F16Work(_M3Work):
                 whole.append(dst)
 
 
+# widest actor output the fused actor step takes (qs_mlp3f_actor: A <= 4;
+# bench.py --fused-max-a)
+_F16_MAX_A = 1
+
+
 def _f16_ok(mlp):
     """The fused actor step takes the one-action-output actor with inputs <= 128
-    wide (the bench's ONE_D_* actors); other widths keep the two-kernel path."""
+    wide (the bench's ONE_D_* actors), up to _F16_MAX_A outputs; other widths
+    keep the two-kernel path."""
     f0, _, f2 = mlp.fcs
-    return f2.out_features == 1 and f0.in_features <= 128
+    return 1 <= f2.out_features <= _F16_MAX_A and f0.in_features <= 128
 
 
 def _m3_shape_ok(K, I):

@@ -2,14 +2,22 @@
 
 Same semantics as safe_control_gym/math_and_models/normalization.py:13-160
 (RunningMeanStd parallel-moment merge in float64, MeanStdNormalizer, and the
-return-based RewardStdNormalizer), computed with torch on the GPU so the rollout
-never leaves HBM.  With torch.distributed initialised, batch moments are merged
-across ranks (sum / sum-of-squares all-reduce) so every shard normalises with
-the global statistics.
+return-based RewardStdNormalizer), on the device so the rollout never leaves
+HBM.  A float32 batch on the GPU takes the HIP kernels qs_rms_update (column
+moments and the running merge in one launch) and qs_rms_normalize
+(csrc/normalizer.hip); other inputs (CPU tensors of the gloo tests, the
+float64 returns of RewardStdNormalizer) use the same formulas as torch ops.
+With torch.distributed initialised, batch moments are merged across ranks
+(sum / sum-of-squares all-reduce) so every shard normalises with the global
+statistics.
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.distributed as tdist
+
+from .. import _lib as L
 
 
 def _dist_on():
@@ -22,7 +30,21 @@ class RunningMeanStd:
         self.var = torch.ones(shape, dtype=torch.float64, device=device)
         self.count = torch.full((), epsilon, dtype=torch.float64, device=device)
 
+    def _hip_ok(self, arr):
+        return arr.is_cuda and arr.dtype == torch.float32 and arr.dim() >= 1 and arr.shape[0] > 0
+
+    def _work(self, R, C):
+        key = (R, C)
+        if getattr(self, '_wkey', None) != key:
+            n = int(L.load().qs_rms_work_bytes(R, C))
+            self._wbuf = torch.zeros(n, dtype=torch.uint8, device=self.mean.device)
+            self._wkey = key
+        return self._wbuf
+
     def update(self, arr):
+        if self._hip_ok(arr):
+            self._update_hip(arr)
+            return
         x = arr.to(torch.float64)
         n = float(x.shape[0])   # a host constant: no host-to-device copy (the step is graph-captured)
         s1 = x.sum(0)
@@ -38,6 +60,28 @@ class RunningMeanStd:
             batch_mean = x.mean(0)
             batch_var = x.var(0, unbiased=False)     # np.var
         self.update_from_moments(batch_mean, batch_var, n)
+
+    def _update_hip(self, arr):
+        """qs_rms_update: the batch's column moments merged into the statistics in
+        one launch (one rank); with several ranks the kernel writes this rank's
+        [Σx | Σx² | n], which are all-reduced and merged as in update()."""
+        x = arr.contiguous()
+        R = int(x.shape[0])
+        C = x.numel() // R
+        lib = L.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        work = self._work(R, C)
+        if not _dist_on():
+            L.check(lib.qs_rms_update(R, C, L.ptr(x), L.ptr(self.mean), L.ptr(self.var), L.ptr(self.count), None,
+                                      L.ptr(work), st), "qs_rms_update")
+            return
+        buf = torch.empty(2 * C + 1, dtype=torch.float64, device=x.device)
+        L.check(lib.qs_rms_update(R, C, L.ptr(x), None, None, None, L.ptr(buf), L.ptr(work), st), "qs_rms_update")
+        tdist.all_reduce(buf)
+        shape = self.mean.shape
+        s1, s2, n = buf[:C].view(shape), buf[C:2 * C].view(shape), buf[2 * C]
+        batch_mean = s1 / n
+        self.update_from_moments(batch_mean, s2 / n - batch_mean * batch_mean, n)
 
     def update_from_moments(self, batch_mean, batch_var, batch_count):
         """normalization.py:42-60.  The statistics are updated in place, so a
@@ -91,6 +135,16 @@ class MeanStdNormalizer(BaseNormalizer):
     def __call__(self, x, out=None):
         if not self.read_only:
             self.rms.update(x)
+        if self.rms._hip_ok(x) and (out is None or (out.dtype == torch.float32 and out.is_contiguous()
+                                                      and out.numel() == x.numel())):
+            # qs_rms_normalize: the same float64 expression, float32 out, one launch
+            xc = x.contiguous()
+            R = int(xc.shape[0])
+            y = torch.empty_like(xc) if out is None else out
+            st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            L.check(L.load().qs_rms_normalize(R, xc.numel() // R, L.ptr(xc), L.ptr(self.rms.mean), L.ptr(self.rms.var),
+                                              float(self.epsilon), float(self.clip), L.ptr(y), st), "qs_rms_normalize")
+            return y
         y = torch.clamp((x.to(torch.float64) - self.rms.mean) / torch.sqrt(self.rms.var + self.epsilon),
                         -self.clip, self.clip)
         if out is not None:
@@ -115,11 +169,14 @@ class RewardStdNormalizer(MeanStdNormalizer):
         self.ret = None
 
     def __call__(self, x, dones):
-        x64 = x.to(torch.float64)
+        """normalization.py:147-160: the discounted return is tracked in the
+        reward's own dtype (np.zeros_like(x); float32 · γ stays float32, NEP 50),
+        its moments feed the running statistics, and the reward is only scaled."""
         if not self.read_only:
             if self.ret is None:
-                self.ret = torch.zeros_like(x64)
-            self.ret = self.ret * self.gamma + x64
+                self.ret = torch.zeros_like(x)
+            self.ret = self.ret * self.gamma + x
             self.rms.update(self.ret.reshape(-1))
             self.ret = torch.where(dones.bool(), torch.zeros_like(self.ret), self.ret)
+        x64 = x.to(torch.float64)
         return torch.clamp(x64 / torch.sqrt(self.rms.var + self.epsilon), -self.clip, self.clip).to(x.dtype)

@@ -66,3 +66,40 @@ def test_fused_mlp_row_limits():
     assert _m3_shape_ok(1, 27)
     assert _m3_shape_ok(2 ** 21 - 1, 27) and not _m3_shape_ok(2 ** 21, 27)      # 262 144 envs x 8 drones
     assert not _m3_shape_ok(2 ** 19, 1024) and _m3_shape_ok(2 ** 19 - 1, 1024)
+
+
+def test_reward_std_normalizer_matches_reference_restatement():
+    """RewardStdNormalizer (normalization.py:123-160) against a numpy restatement
+    of the reference: the return tracked in float32 (np.zeros_like of the float32
+    reward), its float64 running moments, the reward scaled (not centred) and
+    clipped, the return cleared on done.  Off in both reference trainer configs
+    (learn_mappo.py / env_select_learn_mappo.py: norm_reward False), kept for
+    the MAPPO constructor's norm_reward switch."""
+    import numpy as np
+    import torch
+    from gym_pybullet_drones_amd.mappo.normalization import RewardStdNormalizer
+    rng = np.random.default_rng(4)
+    E, gamma = 64, 0.99
+    norm = RewardStdNormalizer(gamma=gamma, clip=10.0, epsilon=1e-8, device="cpu")
+    mean, var, count, ret = 0.0, 1.0, 1e-4, None
+    for t in range(40):
+        x = (rng.normal(size=E) * 0.3 - 1.0).astype(np.float32)
+        dones = rng.random(E) < 0.05
+        got = norm(torch.as_tensor(x), torch.as_tensor(dones)).numpy()
+        # the reference (numpy, with float64 batch moments as this port computes them)
+        ret = np.zeros_like(x) if ret is None else ret
+        ret = ret * np.float32(gamma) + x
+        assert ret.dtype == np.float32
+        r64 = ret.astype(np.float64)
+        bm, bv, bc = r64.mean(0), r64.var(0), E
+        delta = bm - mean
+        tot = count + bc
+        mean, var, count = (mean + delta * bc / tot,
+                            (var * count + bv * bc + delta * delta * count * bc / (count + bc)) / (count + bc),
+                            bc + count)
+        ret[dones] = 0
+        want = np.clip(x / np.sqrt(var + 1e-8), -10.0, 10.0).astype(np.float32)
+        np.testing.assert_array_equal(norm.ret.numpy(), ret)
+        np.testing.assert_allclose(float(norm.rms.var), var, rtol=1e-12)
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=0)
+    assert got.dtype == np.float32
