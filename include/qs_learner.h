@@ -19,6 +19,8 @@
  *     MFMA (nn.Linear + torch.tanh autograd in the reference)      qs_mlp3_bwd
  *   the actor's forward, policy loss and backward of a minibatch  qs_mlp3f_actor,
  *     (agent.py:602-640, 728-734)                                  qs_value_head
+ *   one PPO minibatch at the reference's learner shape            qs_ppo_small_step
+ *     (agent.py:702-772 with mini_batch_size 32, learn_mappo.py:199)
  *   MeanStdNormalizer.__call__ / RunningMeanStd.update            qs_rms_update,
  *     (safe_control_gym normalization.py:13-120): torch float64      qs_rms_normalize
  *     column reductions per rollout step
@@ -287,6 +289,41 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
 int qs_rms_normalize(int64_t R, int32_t C, const float* x, const double* mean, const double* var, double eps,
                      double clip, float* out, void* stream);
 const char* qs_rms_last_error(void);
+
+/* One PPO minibatch at small batch sizes (the reference's own learner shape,
+ * learn_mappo.py:196-216: mini_batch_size 32 → 256 actor rows) in two
+ * launches, replacing qs_mlp3f_actor / qs_mlp3w_* / qs_value_head / the
+ * weight-gradient GEMMs / qs_mlp_sum_adam there: the actor's forward, policy
+ * loss head (AG:602-640) and backward and the critic's forward, value head
+ * (AG:642-683) and backward in 16-row tiles, then every weight gradient
+ * summed over the whole minibatch and applied by Adam in place (the actor's
+ * step gated on approx_kl <= kl_thr when gate != 0, AG:731-734; the critic's
+ * always, AG:757-760).  Both nets are 256-wide tanh MLPs (nn.Linear layout,
+ * row-major [out][in]) inside flat parameter / Adam buffers; w2t is a
+ * [256][256] transposed copy of W2, formed by the caller once and kept current
+ * by the step.  obs is the rollout's obs table [T·E·D][O] (actor rows) =
+ * [T·E][D·O] (critic rows), idx[mb] int64 env-timesteps; act [T·E·D][A],
+ * logp_old [T·E·D], adv / ret [T·E] (float64).  Writes kl_out[0] = approx_kl
+ * and acc[0..3] += policy, value, entropy loss, approx_kl, as qs_ppo_heads.
+ * work: qs_ppo_small_work_bytes(mb, D, actor in, critic in, A) bytes, zeroed
+ * once (the launches leave their counters zero). */
+#define QS_PPO_SMALL_MAX_ROWS 8192   /* mb·D at most */
+typedef struct qs_mlp256 {
+  float* params;       /* flat parameter buffer of the net (FlatBuffers)     */
+  float* exp_avg;      /* Adam moments, same layout                           */
+  float* exp_avg_sq;
+  float* step;         /* Adam step count (float32, device)                  */
+  float* w2t;          /* [256][256] = W2ᵀ                                    */
+  int64_t w1, b1, w2, b2, w3, b3, logstd;   /* element offsets in params (logstd -1: none) */
+  int32_t in, out;     /* input width (<= 256), outputs (actor <= 4, critic 1) */
+  float lr, beta1, beta2, eps;
+} qs_mlp256;
+int64_t qs_ppo_small_work_bytes(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A);
+int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
+                      const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
+                      float ent_coef, int32_t gate, float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic,
+                      float* kl_out, double* acc, void* work, void* stream);
+const char* qs_ppo_small_last_error(void);
 
 #ifdef __cplusplus
 }

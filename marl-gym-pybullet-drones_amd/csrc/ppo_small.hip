@@ -1,0 +1,664 @@
+// ppo_small.hip — one PPO minibatch at small batch sizes in two launches
+// (include/qs_learner.h: qs_ppo_small_step).
+//
+// The reference's own learner shape (learn_mappo.py:196-216 at README.md:38-39's
+// 176 envs: mini_batch_size 32 env-timesteps = 256 actor rows of 27 and 32
+// critic rows of 216, hidden 256, 14 080 minibatches per update) is pure
+// latency: the large-batch path (qs_mlp3f_actor + split-K GEMMs + qs_mlp_sum_adam,
+// built for 32 768 rows) streams every weight through two CUs and chains ~10
+// dependent launches per minibatch.  Here a minibatch is two launches:
+//
+//  1. ppo_small_fb_kernel: one workgroup per 16-row tile (actor tiles first,
+//     then critic tiles), the hidden width split over its 8 waves (wave w owns
+//     hidden blocks 2w, 2w+1): layer 1, layer 2, the head (a fixed-order sum of
+//     the waves' partial dots through LDS), the PPO policy / value head
+//     (AG:602-683), dZ2, dH1 = dZ2·W2 and dZ1, with the activations exchanged
+//     between the waves through LDS.  v_mfma_f32_16x16x4_f32: lane (g, j)
+//     supplies A[j][κ] and B[κ][j] with κ = 16t + 4g + e for the four steps e of
+//     quad t, so each operand is one float4 (weights row-major from L2, the
+//     activations from LDS rows padded to 4 mod 32 floats: a 16-lane float4
+//     read is conflict-free).  Writes the transposed activations [h][K] (the
+//     weight gradients' float4 operands), per-tile bias / head partial rows,
+//     and from the last tile of each net the loss sums (ppo_heads_kernel's tail).
+//  2. ppo_small_adam_kernel: one wave per 16×16 weight tile computes its
+//     gradient over the whole minibatch (fixed order: no partials, no atomics)
+//     and applies Adam to it in place (actor gated by approx_kl, AG:731-734), W2
+//     also written transposed for the next minibatch's dH1; the vector
+//     parameters (biases, head, logstd) from the tile partials.  The last
+//     workgroup commits the step counts.
+//
+// MFMA-bound per CU: a 16-row actor tile is 16·(32·256 + 2·256²) MACs =
+// 272 MFMAs a wave, two waves a SIMD (~7 µs); the whole minibatch is 0.13 GFLOP.
+
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <string>
+
+#include "qs_learner.h"
+#include "quadswarm.h"
+
+namespace {
+thread_local std::string g_serr;
+int sfail(int code, const std::string& m) { g_serr = m; return code; }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSW = 8;                 // waves per workgroup of the forward/backward kernel
+constexpr int kSBlock = 64 * kSW;
+constexpr int kSH = 256;               // hidden width
+constexpr int kSHS = kSH + 4;          // LDS row stride of the hidden exchange (4 mod 32 floats)
+constexpr int kSMaxI = 256;            // widest input
+constexpr int kSMaxA = 4;
+constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of the Adam kernel
+constexpr int kSVecWG = 4;             // Adam workgroups for the vector parameters
+
+__host__ __device__ constexpr int s_ip(int I) { return (I + 15) & ~15; }       // input padded to whole quads
+__host__ __device__ constexpr int s_xs(int I) { return ((I + 31) & ~31) + 4; } // LDS row stride of the X tile
+
+struct SNet {   // one 256-wide tanh MLP inside its flat Adam buffers (qs_mlp256)
+  float* p;
+  float* m;
+  float* v;
+  float* step;
+  float* w2t;
+  long long w1, b1, w2, b2, w3, b3, logstd;
+  int I, A;
+  float lr, beta1, beta2, eps;
+};
+
+struct SWork {   // workspace views (qs_ppo_small_work_bytes)
+  float *xaT, *h1aT, *dz2aT, *dz1aT, *xcT, *h1cT, *dz2cT, *dz1cT;
+  float *partAa, *partBa, *partAc, *partBc, *dlogstd;
+  double *lossa, *lossc;
+  unsigned* cnt;   // [0] actor tiles, [64] critic tiles, [128] Adam workgroups
+};
+
+struct SArgs {
+  int mb, D, nA, nC, KaP, KcP;
+  const float* X;          // the rollout's obs table [T·E·D][O] (critic rows: [T·E][D·O])
+  const long long* idx;    // the minibatch's env-timesteps [mb]
+  const float* act;        // [T·E·D][A]
+  const float* logp_old;   // [T·E·D]
+  const double* adv;       // [T·E]
+  const double* ret;       // [T·E]
+  float scale, clip, ent_coef, kl_thr;
+  int gate;
+  float* kl_out;
+  double* acc;
+  SNet a, c;
+  SWork w;
+};
+
+__device__ __forceinline__ float s_tanh(float x) {   // learner.hip's m3_tanh
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+  return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+__device__ __forceinline__ f32x4 s_mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// elements k0 .. k0+3 of a row of I floats (zero past I); one float4 when the
+// row is 16-byte aligned and whole
+__device__ __forceinline__ float4 s_ld4(const float* row, int k0, int I) {
+  if ((I & 3) == 0) return k0 < I ? *reinterpret_cast<const float4*>(row + k0) : float4{0.f, 0.f, 0.f, 0.f};
+  float4 r;
+  r.x = k0 < I ? row[k0] : 0.f;
+  r.y = k0 + 1 < I ? row[k0 + 1] : 0.f;
+  r.z = k0 + 2 < I ? row[k0 + 2] : 0.f;
+  r.w = k0 + 3 < I ? row[k0 + 3] : 0.f;
+  return r;
+}
+template <int CTRL>
+__device__ __forceinline__ float s_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Σ over the 16 lanes of a DPP row (every lane gets a sum; lane 0's order is fixed)
+__device__ __forceinline__ float s_row_sum(float t) {
+  t += s_dpp<0x128>(t);   // row_ror:8
+  t += s_dpp<0x124>(t);   // row_ror:4
+  t += s_dpp<0x4E>(t);    // quad_perm [2,3,0,1]
+  return t + s_dpp<0xB1>(t);   // quad_perm [1,0,3,2]
+}
+
+__device__ __forceinline__ double s_powi(double b, unsigned t) {
+  double r = 1.0;
+  while (t) {
+    if (t & 1u) r *= b;
+    b *= b;
+    t >>= 1;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- launch 1
+// One 16-row tile of one net: POL = the actor (policy head over A outputs),
+// otherwise the critic (value head).
+template <int A, bool POL>
+__device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, float* xs, float* h1s, float* dz2s,
+                                       float (*hp)[16], double (*ls_w)[2 + kSMaxA]) {
+  constexpr int NL = POL ? 2 + A : 1;   // loss sums: policy, approx_kl, d logstd[A] | value
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const int I = N.I, XS = s_xs(I), Ip = s_ip(I);
+  const int K = POL ? P.mb * P.D : P.mb;
+  const int KP = POL ? P.KaP : P.KcP;
+  const int r0 = tile * 16;
+  const SWork& W = P.w;
+  float* xT = POL ? W.xaT : W.xcT;
+  float* h1T = POL ? W.h1aT : W.h1cT;
+  float* dz2T = POL ? W.dz2aT : W.dz2cT;
+  float* dz1T = POL ? W.dz1aT : W.dz1cT;
+  // ---- the X tile: LDS rows (zero-padded) and the transposed copy the weight
+  // gradients read (rows past K are zeros)
+  for (int e = tid; e < 16 * Ip; e += kSBlock) {
+    const int rr = e & 15, k = e >> 4, R = r0 + rr;
+    float v = 0.f;
+    if (R < K && k < I) {
+      const long long src = POL ? (P.idx[R / P.D] * P.D + R % P.D) : P.idx[R];
+      v = P.X[src * I + k];
+    }
+    xs[rr * XS + k] = v;
+    if (k < I) xT[(size_t)k * KP + R] = v;
+  }
+  __syncthreads();
+  const int b0 = 2 * w;   // the wave's hidden blocks b0, b0 + 1
+  // ---- layer 1: Z1ᵀ[16b + 4g + r][row j] in register r of lane (g, j)
+  f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  {
+    const float* w1 = N.p + N.w1;
+    for (int t = 0; t < Ip / 16; ++t) {
+      const float4 xb = *reinterpret_cast<const float4*>(xs + j * XS + 16 * t + 4 * g);
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        const float4 wa = s_ld4(w1 + (size_t)(16 * (b0 + bb) + j) * I, 16 * t + 4 * g, I);
+        z[bb] = s_mfma(wa.x, xb.x, z[bb]);
+        z[bb] = s_mfma(wa.y, xb.y, z[bb]);
+        z[bb] = s_mfma(wa.z, xb.z, z[bb]);
+        z[bb] = s_mfma(wa.w, xb.w, z[bb]);
+      }
+    }
+  }
+  float h1[2][4];
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int h0 = 16 * (b0 + bb) + 4 * g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      h1[bb][r] = s_tanh(z[bb][r] + N.p[N.b1 + h0 + r]);
+      h1T[(size_t)(h0 + r) * KP + r0 + j] = h1[bb][r];
+    }
+    *reinterpret_cast<float4*>(h1s + j * kSHS + h0) = float4{h1[bb][0], h1[bb][1], h1[bb][2], h1[bb][3]};
+  }
+  __syncthreads();
+  // ---- layer 2: Z2ᵀ = W2·H1ᵀ (W2 rows straight from L2, four quads ahead)
+  const float* w2 = N.p + N.w2;
+  auto contract = [&](const float* wrow0, const float* wrow1, const float* brow) {
+    f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+    float4 ra[4], rb[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      ra[t] = *reinterpret_cast<const float4*>(wrow0 + 16 * t + 4 * g);
+      rb[t] = *reinterpret_cast<const float4*>(wrow1 + 16 * t + 4 * g);
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float4 a0 = ra[t & 3], a1 = rb[t & 3];
+      if (t + 4 < 16) {
+        ra[t & 3] = *reinterpret_cast<const float4*>(wrow0 + 16 * (t + 4) + 4 * g);
+        rb[t & 3] = *reinterpret_cast<const float4*>(wrow1 + 16 * (t + 4) + 4 * g);
+      }
+      const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+      c0 = s_mfma(a0.x, bv.x, c0);
+      c1 = s_mfma(a1.x, bv.x, c1);
+      c0 = s_mfma(a0.y, bv.y, c0);
+      c1 = s_mfma(a1.y, bv.y, c1);
+      c0 = s_mfma(a0.z, bv.z, c0);
+      c1 = s_mfma(a1.z, bv.z, c1);
+      c0 = s_mfma(a0.w, bv.w, c0);
+      c1 = s_mfma(a1.w, bv.w, c1);
+    }
+    z[0] = c0;
+    z[1] = c1;
+  };
+  contract(w2 + (size_t)(16 * b0 + j) * kSH, w2 + (size_t)(16 * b0 + 16 + j) * kSH, h1s + j * kSHS);
+  float h2[2][4], hs[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) hs[a] = 0.f;
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * (b0 + bb) + 4 * g + r;
+      h2[bb][r] = s_tanh(z[bb][r] + N.p[N.b2 + h]);
+#pragma unroll
+      for (int a = 0; a < A; ++a) hs[a] += h2[bb][r] * N.p[N.w3 + a * kSH + h];
+    }
+  // the head: the wave's partial dot of row j (lane groups g added), then the 8 waves in order
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    float t = hs[a] + __shfl_xor(hs[a], 16, 64);
+    t = t + __shfl_xor(t, 32, 64);
+    if (g == 0) hp[w * A + a][j] = t;
+  }
+  __syncthreads();
+  const int R = r0 + j;
+  const bool rv = R < K;
+  float mu[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    float t = hp[a][j];
+#pragma unroll
+    for (int v = 1; v < kSW; ++v) t += hp[v * A + a][j];
+    mu[a] = t + N.p[N.b3 + a];
+  }
+  // ---- the loss head of row j (every wave forms it; wave 0, lane group 0 counts it)
+  float dout[A];
+  double ls[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) ls[k] = 0.0;
+  if constexpr (POL) {
+    // compute_policy_loss (AG:602-640) and its gradient: ppo_heads_kernel's arithmetic
+    float sd[A], lsd[A], var2[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      sd[a] = expf(N.p[N.logstd + a]);
+      lsd[a] = logf(sd[a]);
+      var2[a] = 2.0f * (sd[a] * sd[a]);
+    }
+    const float lc = (float)log(sqrt(2.0 * M_PI));
+    const float lo = 1.0f - P.clip, hi = 1.0f + P.clip;
+    const double G = -1.0 / (double)K;
+    const long long ei = rv ? R / P.D : 0;
+    const long long gi = rv ? P.idx[ei] * P.D + (R - ei * P.D) : 0;
+    float t1[A], logp = 0.0f;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float m = mu[a] * P.scale;
+      t1[a] = (rv ? P.act[gi * A + a] : 0.f) - m;
+      const float t4 = (float)((double)(-(t1[a] * t1[a])) / (double)var2[a]);
+      const float lp = (t4 - lsd[a]) - lc;
+      logp = a == 0 ? lp : logp + lp;
+    }
+    const float lpo = rv ? P.logp_old[gi] : 0.f;
+    const float ratio = expf(logp - lpo);
+    const double ad = rv ? P.adv[P.idx[ei]] : 0.0;
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
+    const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
+    const double g2 = s2 < s1 ? G : (s1 == s2 ? G / 2 : 0.0);
+    float gr = (float)(g1 * ad);
+    if (ratio >= lo && ratio <= hi) gr = gr + (float)(g2 * ad);
+    const float gl = gr * ratio;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float gt3 = (float)((double)gl / (double)var2[a]);
+      const float gt1 = -gt3 * 2.0f * t1[a];
+      dout[a] = rv ? -gt1 * P.scale : 0.f;
+      if (rv) ls[2 + a] = (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
+    }
+    if (rv) {
+      ls[0] = -(s1 < s2 ? s1 : s2);
+      ls[1] = (double)(lpo - logp);
+    }
+  } else {
+    // compute_value_loss (AG:642-683, centralized, unclipped): qs_value_head's arithmetic
+    if (rv) {
+      const double rt = P.ret[P.idx[R]];
+      double rs = 0;
+      for (int d = 0; d < P.D; ++d) rs += rt;
+      const double diff = (double)mu[0] - rs / (double)P.D;
+      ls[0] = diff * diff;
+      dout[0] = (float)(diff / (double)P.mb);
+    } else {
+      dout[0] = 0.f;
+    }
+  }
+  // ---- dZ2 = (dout·W3) ⊙ (1 − H2²); the tile's b2 / W3 / b3 partial rows (row sums over j)
+  float* pa = (POL ? W.partAa : W.partAc) + (size_t)tile * (kSH + A * kSH + A);
+  float* pb = (POL ? W.partBa : W.partBc) + (size_t)tile * kSH;
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int h0 = 16 * (b0 + bb) + 4 * g;
+    float d4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = h0 + r;
+      float gg = 0.f;
+#pragma unroll
+      for (int a = 0; a < A; ++a) gg += dout[a] * N.p[N.w3 + a * kSH + h];
+      const float hv = h2[bb][r];
+      d4[r] = gg * (1.f - hv * hv);
+      dz2T[(size_t)h * KP + R] = d4[r];
+      const float sb = s_row_sum(d4[r]);
+      if (j == 0) pa[h] = sb;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const float sw = s_row_sum(dout[a] * hv);
+        if (j == 0) pa[kSH + a * kSH + h] = sw;
+      }
+    }
+    *reinterpret_cast<float4*>(dz2s + j * kSHS + h0) = float4{d4[0], d4[1], d4[2], d4[3]};
+  }
+  if (w == 0)
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float t = s_row_sum(dout[a]);
+      if (l == 0) pa[kSH + A * kSH + a] = t;
+    }
+  __syncthreads();
+  // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (rows of the transposed copy), dZ1 = dH1 ⊙ (1 − H1²)
+  contract(N.w2t + (size_t)(16 * b0 + j) * kSH, N.w2t + (size_t)(16 * b0 + 16 + j) * kSH, dz2s + j * kSHS);
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int h0 = 16 * (b0 + bb) + 4 * g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float u = h1[bb][r];
+      const float d = z[bb][r] * (1.f - u * u);
+      dz1T[(size_t)(h0 + r) * KP + R] = d;
+      const float sb = s_row_sum(d);
+      if (j == 0) pb[h0 + r] = sb;
+    }
+  }
+  // ---- the tile's loss sums (wave 0, rows in order), then the net's last tile
+  if (w == 0 && g == 0)
+#pragma unroll
+    for (int k = 0; k < NL; ++k) ls_w[j][k] = ls[k];
+  __syncthreads();
+  __shared__ bool last;
+  if (tid == 0) {
+    double* lp = POL ? W.lossa + (size_t)tile * NL : W.lossc + tile;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      double s = 0.0;
+      for (int q = 0; q < 16; ++q) s += ls_w[q][k];
+      lp[k] = s;
+    }
+    __threadfence();
+    const int ntiles = POL ? P.nA : P.nC;
+    last = atomicAdd(W.cnt + (POL ? 0 : 64), 1u) == (unsigned)ntiles - 1;
+  }
+  __syncthreads();
+  if (!last || tid != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  W.cnt[POL ? 0 : 64] = 0u;
+  const int ntiles = POL ? P.nA : P.nC;
+  double tot[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) tot[k] = 0.0;
+  for (int t = 0; t < ntiles; ++t)
+#pragma unroll
+    for (int k = 0; k < NL; ++k) tot[k] += (POL ? W.lossa[(size_t)t * NL + k] : W.lossc[t]);
+  if constexpr (!POL) {
+    P.acc[1] += 0.5 * (tot[0] / (double)P.mb);
+  } else {
+    const float lc = (float)log(sqrt(2.0 * M_PI));
+    float ent = 0.0f;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float lsd = logf(expf(N.p[N.logstd + a]));
+      ent = a == 0 ? (0.5f + lc) + lsd : ent + ((0.5f + lc) + lsd);
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) W.dlogstd[a] = (float)tot[2 + a] - P.ent_coef;
+    const float akl = (float)(tot[1] / (double)K);
+    *P.kl_out = akl;
+    P.acc[0] += tot[0] / (double)K;
+    P.acc[2] += (double)(-ent);
+    P.acc[3] += (double)akl;
+  }
+}
+
+template <int A>
+__global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
+  __shared__ float xs[16 * s_xs(kSMaxI)];
+  __shared__ float h1s[16 * kSHS];
+  __shared__ float dz2s[16 * kSHS];
+  __shared__ float hp[kSW * kSMaxA][16];
+  __shared__ double ls_w[16][2 + kSMaxA];
+  if ((int)blockIdx.x < P.nA) s_tile<A, true>(P, P.a, blockIdx.x, xs, h1s, dz2s, hp, ls_w);
+  else s_tile<1, false>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, hp, ls_w);
+}
+
+// ---------------------------------------------------------------- launch 2
+struct STile {
+  const SNet* n;
+  bool actor;
+  int which, nb, kb;   // W1 / W2, output block, input block
+};
+
+__device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, float bc1, float bc2s, float* w2t,
+                                       int n, int k) {
+  // torch.optim.Adam (amsgrad=False, weight_decay=0): learner.hip's adam_elem
+  const float p = N.p[i], m = N.m[i], v = N.v[i];
+  const float m1 = m + (1.0f - N.beta1) * (g - m);
+  const float v1 = v * N.beta2 + (1.0f - N.beta2) * g * g;
+  N.m[i] = m1;
+  N.v[i] = v1;
+  const float denom = sqrtf(v1) / bc2s + N.eps;
+  const float p1 = p - (N.lr / bc1) * (m1 / denom);
+  N.p[i] = p1;
+  if (w2t) w2t[(size_t)k * kSH + n] = p1;
+}
+
+__global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int nTiles) {
+  __shared__ float sc[2][2];
+  __shared__ bool last;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  if (tid < 2) {
+    const SNet& N = tid == 0 ? P.a : P.c;
+    const unsigned t = (unsigned)(*N.step) + 1u;
+    sc[tid][0] = (float)(1.0 - s_powi((double)N.beta1, t));
+    sc[tid][1] = (float)sqrt(1.0 - s_powi((double)N.beta2, t));
+  }
+  const bool open_a = !P.gate || *P.kl_out <= P.kl_thr;
+  __syncthreads();
+  const int nwg_tiles = (nTiles + kSAW - 1) / kSAW;
+  if ((int)blockIdx.x < nwg_tiles) {
+    const int T = blockIdx.x * kSAW + w;
+    if (T < nTiles) {
+      // tile T → (net, layer, output block, input block); the actor's first
+      const int a1 = 16 * (s_ip(P.a.I) / 16), c1 = 16 * (s_ip(P.c.I) / 16);
+      int u = T;
+      bool actor = true;
+      int which = 1;
+      if (u < a1) { which = 1; }
+      else if ((u -= a1) < 256) { which = 2; }
+      else if ((u -= 256) < c1) { actor = false; which = 1; }
+      else { u -= c1; actor = false; which = 2; }
+      const SNet& N = actor ? P.a : P.c;
+      if (!actor || open_a) {
+        const int nin = which == 1 ? s_ip(N.I) / 16 : 16;
+        const int nb = u / nin, kb = u - nb * nin;
+        const int KP = actor ? P.KaP : P.KcP;
+        const float* dzT = actor ? (which == 1 ? P.w.dz1aT : P.w.dz2aT) : (which == 1 ? P.w.dz1cT : P.w.dz2cT);
+        const float* xT = actor ? (which == 1 ? P.w.xaT : P.w.h1aT) : (which == 1 ? P.w.xcT : P.w.h1cT);
+        const int Kin = which == 1 ? N.I : kSH;
+        const int kcol = 16 * kb + j;
+        const float* arow = dzT + (size_t)(16 * nb + j) * KP;
+        const float* brow = kcol < Kin ? xT + (size_t)kcol * KP : nullptr;
+        // dW[16nb + 4g + r][16kb + j] = Σ_rows dZ[row][n]·X[row][k], rows in MFMA order
+        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < KP / 16; ++q) {
+          const float4 av = *reinterpret_cast<const float4*>(arow + 16 * q + 4 * g);
+          const float4 bv = brow ? *reinterpret_cast<const float4*>(brow + 16 * q + 4 * g) : float4{0.f, 0.f, 0.f, 0.f};
+          c = s_mfma(av.x, bv.x, c);
+          c = s_mfma(av.y, bv.y, c);
+          c = s_mfma(av.z, bv.z, c);
+          c = s_mfma(av.w, bv.w, c);
+        }
+        if (kcol < Kin) {
+          const int si = actor ? 0 : 1;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = 16 * nb + 4 * g + r;
+            const long long i = (which == 1 ? N.w1 : N.w2) + (long long)n * Kin + kcol;
+            s_adam(N, i, c[r], sc[si][0], sc[si][1], which == 2 ? N.w2t : nullptr, n, kcol);
+          }
+        }
+      }
+    }
+  } else {
+    // the vector parameters: b1, b2, W3, b3 (and the actor's logstd) from the tile partials
+    const int A = P.a.A;
+    const int na = 2 * kSH + A * kSH + 2 * A, nc = 2 * kSH + kSH + 1;
+    for (int e = (blockIdx.x - nwg_tiles) * blockDim.x + tid; e < na + nc; e += kSVecWG * blockDim.x) {
+      const bool actor = e < na;
+      if (actor && !open_a) continue;
+      const SNet& N = actor ? P.a : P.c;
+      const int AA = actor ? A : 1, nt = actor ? P.nA : P.nC;
+      const float* pA = actor ? P.w.partAa : P.w.partAc;
+      const float* pB = actor ? P.w.partBa : P.w.partBc;
+      const int PA = kSH + AA * kSH + AA;
+      int u = actor ? e : e - na;
+      float gsum = 0.f;
+      long long i;
+      if (u < kSH) {                       // b1: Σ dZ1
+        for (int t = 0; t < nt; ++t) gsum += pB[(size_t)t * kSH + u];
+        i = N.b1 + u;
+      } else if ((u -= kSH) < kSH) {       // b2: Σ dZ2
+        for (int t = 0; t < nt; ++t) gsum += pA[(size_t)t * PA + u];
+        i = N.b2 + u;
+      } else if ((u -= kSH) < AA * kSH) {  // W3: Σ dout·H2
+        for (int t = 0; t < nt; ++t) gsum += pA[(size_t)t * PA + kSH + u];
+        i = N.w3 + u;
+      } else if ((u -= AA * kSH) < AA) {   // b3: Σ dout
+        for (int t = 0; t < nt; ++t) gsum += pA[(size_t)t * PA + kSH + AA * kSH + u];
+        i = N.b3 + u;
+      } else {                             // logstd (the actor's loss tail)
+        u -= AA;
+        gsum = P.w.dlogstd[u];
+        i = N.logstd + u;
+      }
+      const int si = actor ? 0 : 1;
+      s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(P.w.cnt + 128, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last && tid == 0) {   // every workgroup read the step counts before arriving
+    P.w.cnt[128] = 0u;
+    if (open_a) *P.a.step = *P.a.step + 1.0f;
+    *P.c.step = *P.c.step + 1.0f;
+  }
+}
+
+struct SLayout {
+  int nA, nC, KaP, KcP;
+  long long off[16];
+  long long bytes;
+};
+SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
+  SLayout L;
+  const long long Ka = (long long)mb * D, Kc = mb;
+  L.nA = (int)((Ka + 15) / 16);
+  L.nC = (int)((Kc + 15) / 16);
+  L.KaP = 16 * L.nA;
+  L.KcP = 16 * L.nC;
+  const long long sz[16] = {
+      4LL * Ia * L.KaP, 4LL * kSH * L.KaP, 4LL * kSH * L.KaP, 4LL * kSH * L.KaP,   // xaT h1aT dz2aT dz1aT
+      4LL * Ic * L.KcP, 4LL * kSH * L.KcP, 4LL * kSH * L.KcP, 4LL * kSH * L.KcP,   // xcT h1cT dz2cT dz1cT
+      4LL * L.nA * (kSH + A * kSH + A), 4LL * L.nA * kSH,                           // partAa partBa
+      4LL * L.nC * (2 * kSH + 1), 4LL * L.nC * kSH,                                 // partAc partBc
+      4LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192};                   // dlogstd lossa lossc cnt
+  long long o = 0;
+  for (int i = 0; i < 16; ++i) {
+    L.off[i] = o;
+    o += (sz[i] + 255) & ~255LL;
+  }
+  L.bytes = o;
+  return L;
+}
+}  // namespace
+
+extern "C" {
+
+const char* qs_ppo_small_last_error(void) { return g_serr.c_str(); }
+
+int64_t qs_ppo_small_work_bytes(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A) {
+  if (mb <= 0 || D <= 0 || Ia <= 0 || Ic <= 0 || A < 1 || A > kSMaxA) return 0;
+  return s_layout(mb, D, Ia, Ic, A).bytes;
+}
+
+int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
+                      const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
+                      float ent_coef, int32_t gate, float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic,
+                      float* kl_out, double* acc, void* work, void* stream) {
+  if (mb <= 0 || D <= 0 || !obs || !idx || !act || !logp_old || !adv || !ret || !actor || !critic || !kl_out || !acc ||
+      !work)
+    return sfail(QS_E_INVALID, "qs_ppo_small_step: bad argument");
+  const int A = actor->out;
+  if (A < 1 || A > kSMaxA || critic->out != 1 || actor->in < 1 || actor->in > kSMaxI || critic->in < 1 ||
+      critic->in > kSMaxI || actor->logstd < 0 || !actor->w2t || !critic->w2t)
+    return sfail(QS_E_INVALID, "qs_ppo_small_step: nets must be 256-wide with <= 256 inputs, A <= 4 actor outputs "
+                               "(with logstd) and one critic output, W2ᵀ copies given");
+  if ((actor->w2 & 3) || (critic->w2 & 3) || ((actor->in & 3) == 0 && (actor->w1 & 3)) ||
+      ((critic->in & 3) == 0 && (critic->w1 & 3)))
+    return sfail(QS_E_INVALID, "qs_ppo_small_step: W1 / W2 must start 16-byte aligned in the flat buffers");
+  if ((long long)mb * D > QS_PPO_SMALL_MAX_ROWS)
+    return sfail(QS_E_INVALID, "qs_ppo_small_step: minibatch above QS_PPO_SMALL_MAX_ROWS actor rows");
+  const SLayout L = s_layout(mb, D, actor->in, critic->in, A);
+  SArgs P;
+  P.mb = mb;
+  P.D = D;
+  P.nA = L.nA;
+  P.nC = L.nC;
+  P.KaP = L.KaP;
+  P.KcP = L.KcP;
+  P.X = obs;
+  P.idx = (const long long*)idx;
+  P.act = act;
+  P.logp_old = logp_old;
+  P.adv = adv;
+  P.ret = ret;
+  P.scale = action_scale;
+  P.clip = clip;
+  P.ent_coef = ent_coef;
+  P.kl_thr = kl_thr;
+  P.gate = gate;
+  P.kl_out = kl_out;
+  P.acc = acc;
+  auto net = [](const qs_mlp256* q) {
+    SNet n;
+    n.p = q->params;
+    n.m = q->exp_avg;
+    n.v = q->exp_avg_sq;
+    n.step = q->step;
+    n.w2t = q->w2t;
+    n.w1 = q->w1;
+    n.b1 = q->b1;
+    n.w2 = q->w2;
+    n.b2 = q->b2;
+    n.w3 = q->w3;
+    n.b3 = q->b3;
+    n.logstd = q->logstd;
+    n.I = q->in;
+    n.A = q->out;
+    n.lr = q->lr;
+    n.beta1 = q->beta1;
+    n.beta2 = q->beta2;
+    n.eps = q->eps;
+    return n;
+  };
+  P.a = net(actor);
+  P.c = net(critic);
+  char* wb = (char*)work;
+  float** fv[13] = {&P.w.xaT, &P.w.h1aT, &P.w.dz2aT, &P.w.dz1aT, &P.w.xcT, &P.w.h1cT, &P.w.dz2cT,
+                    &P.w.dz1cT, &P.w.partAa, &P.w.partBa, &P.w.partAc, &P.w.partBc, &P.w.dlogstd};
+  for (int i = 0; i < 13; ++i) *fv[i] = (float*)(wb + L.off[i]);
+  P.w.lossa = (double*)(wb + L.off[13]);
+  P.w.lossc = (double*)(wb + L.off[14]);
+  P.w.cnt = (unsigned*)(wb + L.off[15]);
+  hipStream_t st = (hipStream_t)stream;
+  switch (A) {
+    case 1: hipLaunchKernelGGL(ppo_small_fb_kernel<1>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
+    case 2: hipLaunchKernelGGL(ppo_small_fb_kernel<2>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
+    case 3: hipLaunchKernelGGL(ppo_small_fb_kernel<3>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
+    default: hipLaunchKernelGGL(ppo_small_fb_kernel<4>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
+  }
+  const int nTiles = 16 * (s_ip(actor->in) / 16) + 256 + 16 * (s_ip(critic->in) / 16) + 256;
+  const int grid = (nTiles + kSAW - 1) / kSAW + kSVecWG;
+  hipLaunchKernelGGL(ppo_small_adam_kernel, dim3(grid), dim3(64 * kSAW), 0, st, P, nTiles);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_small_step: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

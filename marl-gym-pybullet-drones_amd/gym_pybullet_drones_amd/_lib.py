@@ -68,10 +68,20 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
            "qs_wgrad_rm", "qs_learner_last_error", "qs_rms_work_bytes", "qs_rms_update", "qs_rms_normalize",
-           "qs_rms_last_error")
+           "qs_rms_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
 
 _lib = None
+
+
+class QsMlp256(ctypes.Structure):
+    """include/qs_learner.h qs_mlp256: one 256-wide tanh MLP inside its flat Adam buffers."""
+    _fields_ = [("params", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+                ("step", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
+                ("w1", ctypes.c_int64), ("b1", ctypes.c_int64), ("w2", ctypes.c_int64), ("b2", ctypes.c_int64),
+                ("w3", ctypes.c_int64), ("b3", ctypes.c_int64), ("logstd", ctypes.c_int64),
+                ("in_", ctypes.c_int32), ("out", ctypes.c_int32),
+                ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
 
 
 class QuadSwarmError(RuntimeError):
@@ -148,11 +158,15 @@ def load():
     L.qs_wgrad_rm.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_learner_last_error.restype = ctypes.c_char_p
     L.qs_rms_last_error.restype = ctypes.c_char_p
+    L.qs_ppo_small_last_error.restype = ctypes.c_char_p
+    L.qs_ppo_small_work_bytes.argtypes = [ctypes.c_int32] * 5
+    L.qs_ppo_small_step.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [f32, f32, f32, ctypes.c_int32, f32]
+                                    + [ctypes.POINTER(QsMlp256)] * 2 + [vp] * 4)
     L.qs_rms_work_bytes.argtypes = [i64, ctypes.c_int32]
     L.qs_rms_update.argtypes = [i64, ctypes.c_int32] + [vp] * 7
     L.qs_rms_normalize.argtypes = [i64, ctypes.c_int32, vp, vp, vp, ctypes.c_double, ctypes.c_double, vp, vp]
     for name in EXPORTS:
-        if name not in ("qs_last_error", "qs_learner_last_error", "qs_rms_last_error"):
+        if name not in ("qs_last_error", "qs_learner_last_error", "qs_rms_last_error", "qs_ppo_small_last_error"):
             getattr(L, name).restype = i32
     L.qs_ppo_heads_work_bytes.restype = i64
     L.qs_mlp3_pack_floats.restype = i64
@@ -160,6 +174,7 @@ def load():
     L.qs_mlp3f_work_bytes.restype = i64
     L.qs_mlp_sum_adam_work_bytes.restype = i64
     L.qs_rms_work_bytes.restype = i64
+    L.qs_ppo_small_work_bytes.restype = i64
     L.qs_mlp_sum_adam_work_bytes.argtypes = []
     _lib = L
     return L
@@ -170,6 +185,8 @@ def check(rc, what=""):
         lib = load()
         if what.startswith("qs_rms"):
             msg = lib.qs_rms_last_error()
+        elif what.startswith("qs_ppo_small"):
+            msg = lib.qs_ppo_small_last_error()
         elif what.startswith(("qs_gae", "qs_adam", "qs_ppo", "qs_mlp", "qs_wgrad", "qs_value")):
             msg = lib.qs_learner_last_error()
         else:

@@ -478,6 +478,29 @@ class _F16Work(_M3Work):
                 whole.append(dst)
 
 
+# the small-minibatch path (qs_ppo_small_step: both nets' forward / backward
+# and the Adam steps in two launches) takes minibatches of at most this many
+# actor rows (mb·D); larger ones run the split-K path (_iteration_direct)
+_SMALL_MAX_ROWS = 2048
+
+
+def _mlp256(fb, mlp, logstd, w2t, lib_struct):
+    """qs_mlp256 of a 256-wide tanh MLP (and the actor's logstd) inside FlatBuffers fb."""
+    ids = [id(p) for p in fb.params]
+    off = lambda t: fb.offsets[ids.index(id(t))][0] if t is not None else -1
+    f0, f1, f2 = mlp.fcs
+    q = lib_struct()
+    q.params, q.exp_avg, q.exp_avg_sq, q.step = (fb.flat.data_ptr(), fb.exp_avg.data_ptr(), fb.exp_avg_sq.data_ptr(),
+                                                 fb.step.data_ptr())
+    q.w2t = w2t.data_ptr()
+    q.w1, q.b1, q.w2, q.b2, q.w3, q.b3 = (off(f0.weight), off(f0.bias), off(f1.weight), off(f1.bias), off(f2.weight),
+                                          off(f2.bias))
+    q.logstd = off(logstd)
+    q.in_, q.out = f0.in_features, f2.out_features
+    q.lr, q.beta1, q.beta2, q.eps = fb.lr, fb.betas[0], fb.betas[1], fb.eps
+    return q
+
+
 # widest actor output the fused actor step takes (qs_mlp3f_actor: A <= 4;
 # bench.py --fused-max-a)
 _F16_MAX_A = 1
@@ -833,6 +856,9 @@ class MAPPOAgent:
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
         self.actor_first = kwargs.get('actor_first', False)
+        # minibatches of at most _SMALL_MAX_ROWS actor rows on qs_ppo_small_step (one
+        # rank); False: always the split-K direct iteration
+        self.small = kwargs.get('small', True)
         self.device = torch.device(device)
         self.ac = MAPPOActorCritic(obs_space, act_space, hidden_dims=[hidden_dim] * 2, activation=activation,
                                    share_actor_weights=share_actor_weights, centralized_critic=centralized_critic,
@@ -901,6 +927,7 @@ class MAPPOAgent:
         self.critic_opt.load_state_dict(state_dict['critic_opt'])
         # a captured update graph has lr / betas / eps baked in as kernel arguments
         self._graph = None
+        self._sm_key = None
 
     # ------------------------------------------------------------- losses
     def compute_policy_loss(self, batch, agent_idx=None):
@@ -991,6 +1018,9 @@ class MAPPOAgent:
         if getattr(self, '_ws_key', None) is not None:
             self._ws_actor.repack()
             self._ws_critic.repack()
+        if getattr(self, '_sm_key', None) is not None:
+            for w2t, mlp in zip(self._sm_w2t, (self.ac.actor.pi_net, self.ac.critic.v_net)):
+                w2t.copy_(mlp.fcs[1].weight.t())
         self._reduce_buf.zero_()
 
     def _iteration_direct(self, rollouts, idx, acc):
@@ -1138,6 +1168,46 @@ class MAPPOAgent:
             return
         FlatBuffers.adam_multi(segs, self._adam_work, packs=packs, zero_grads=True)
 
+    def _small_ok(self, rollouts, mb):
+        """qs_ppo_small_step takes the minibatch: one rank, both nets 256-wide tanh
+        MLPs with <= 256 inputs, <= 4 actor outputs, mb·D <= _SMALL_MAX_ROWS."""
+        if not (self.small and self.device.type == 'cuda' and _dist_world() == 1 and not self._force_allreduce):
+            return False
+        pa, pc = self.ac.actor.pi_net, self.ac.critic.v_net
+        if not (_m3_ok(pa, 256) and _m3_ok(pc, 256) and pc.fcs[2].out_features == 1):
+            return False
+        return 0 < mb * rollouts.num_agents <= _SMALL_MAX_ROWS and rollouts.obs.is_contiguous()
+
+    def _small_setup(self, mb, D):
+        if getattr(self, '_sm_key', None) == (mb, D):
+            return
+        lib = L.load()
+        pa, pc = self.ac.actor.pi_net, self.ac.critic.v_net
+        n = int(lib.qs_ppo_small_work_bytes(mb, D, pa.fcs[0].in_features, pc.fcs[0].in_features,
+                                            pa.fcs[2].out_features))
+        self._sm_work = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        self._sm_w2t = [torch.empty((256, 256), device=self.device) for _ in range(2)]
+        self._sm_nets = (_mlp256(self.actor_opt, pa, self.ac.actor.logstd, self._sm_w2t[0], L.QsMlp256),
+                         _mlp256(self.critic_opt, pc, None, self._sm_w2t[1], L.QsMlp256))
+        self._sm_key = (mb, D)
+        for w2t, mlp in zip(self._sm_w2t, (pa, pc)):
+            w2t.copy_(mlp.fcs[1].weight.t())
+
+    def _iteration_small(self, rollouts, idx, acc):
+        """One minibatch in two launches (qs_ppo_small_step): the actor's forward,
+        policy loss head and backward and the critic's forward, value head and
+        backward in 16-row tiles, then every gradient summed over the minibatch
+        and applied by the KL-gated Adam (actor) / Adam (critic) in place."""
+        D, mb = rollouts.num_agents, idx.shape[0]
+        self._small_setup(mb, D)
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        na, nc = self._sm_nets
+        L.check(L.load().qs_ppo_small_step(
+            mb, D, L.ptr(rollouts.obs), L.ptr(idx), L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
+            L.ptr(rollouts.ret_env), float(self.action_scale), float(self.clip_param), float(self.entropy_coef),
+            int(self.target_kl > 0), float(1.5 * self.target_kl), ctypes.byref(na), ctypes.byref(nc), L.ptr(self._kl),
+            L.ptr(acc), L.ptr(self._sm_work), st), "qs_ppo_small_step")
+
     def _iteration(self, batch, acc):
         """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.
 
@@ -1197,7 +1267,9 @@ class MAPPOAgent:
 
     def _step_minibatch(self, rollouts, idx, acc):
         if self.fused_heads and self._fused_heads_ok(rollouts):
-            if self._direct_ok():
+            if self._small_ok(rollouts, idx.shape[0]):
+                self._iteration_small(rollouts, idx, acc)
+            elif self._direct_ok():
                 self._iteration_direct(rollouts, idx, acc)
             else:
                 self._iteration_fused(rollouts, idx, acc)

@@ -182,13 +182,15 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
-def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, **variant):
+def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, **variant):
     """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
-    iteration's configuration) from fixed weights, data and permutations."""
+    iteration's configuration) from fixed weights, data and permutations
+    (small=False unless given: the split-K direct iteration at every size)."""
     from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
     from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
     from gym_pybullet_drones_amd.utils.spaces import Box
-    D, O, A = 8, 27, 1
+    O = 27
+    variant.setdefault('small', False)
     obs_space = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O)))
     act_space = Box(-np.ones((D, A)), np.ones((D, A)))
     torch.manual_seed(1)
@@ -239,6 +241,42 @@ def test_direct_update_side_stream_bit_identical(graphs, E, T):
     torch.testing.assert_close(a_side.critic_opt.flat, a_fused.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
     for k in r_side:
         assert r_side[k] == pytest.approx(r_fused[k], rel=1e-5, abs=1e-7)
+
+
+@pytest.mark.parametrize("E,T,D,A", [(8, 8, 8, 1), (32, 8, 8, 1), (5, 6, 8, 1), (16, 4, 5, 4), (3, 2, 16, 1)])
+@pytest.mark.parametrize("graphs", [False, True])
+def test_small_update_matches_autograd(graphs, E, T, D, A):
+    """qs_ppo_small_step (the small-minibatch path: two launches per minibatch)
+    against the autograd-driven fused iteration over 2 epochs x 2 minibatches:
+    (8, 8, 8): the reference's mini_batch_size 32 (256 actor rows, 32 critic
+    rows); (5, 6, 8): 15 env-timesteps, rows not a multiple of the 16-row tile;
+    (16, 4, 5, 4): Spiral's 4-wide VEL actor; (3, 2, 16): 3 critic rows of 432 inputs
+    — past the 256-input limit, so the split-K path must take it."""
+    a_small, r_small = _hidden256_update(graphs, E, T, D=D, A=A, small=True)
+    mb = T * E // 2
+    took_small = getattr(a_small, '_sm_key', None) is not None
+    assert took_small == (D * 27 <= 256), (D, took_small)
+    a_ref, r_ref = _hidden256_update(graphs, E, T, D=D, A=A, direct=False)
+    # Adam's normalised steps carry ulp-level gradient differences up to ~lr/60 per step; 4 steps
+    torch.testing.assert_close(a_small.actor_opt.flat, a_ref.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
+    torch.testing.assert_close(a_small.critic_opt.flat, a_ref.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
+    assert float(a_small.actor_opt.step) == float(a_ref.actor_opt.step)
+    assert float(a_small.critic_opt.step) == float(a_ref.critic_opt.step) == 4.0
+    for k in r_small:
+        assert r_small[k] == pytest.approx(r_ref[k], rel=1e-5, abs=1e-7), k
+    if took_small:
+        # the transposed W2 copies stayed current through the Adam steps
+        for w2t, mlp in zip(a_small._sm_w2t, (a_small.ac.actor.pi_net, a_small.ac.critic.v_net)):
+            assert torch.equal(w2t, mlp.fcs[1].weight.t())
+    assert mb > 0
+
+
+def test_small_update_replay_deterministic():
+    """Fixed reduction orders: two runs of the small path give the same bits."""
+    a1, r1 = _hidden256_update(True, 8, 8, small=True)
+    a2, r2 = _hidden256_update(True, 8, 8, small=True)
+    assert torch.equal(a1.actor_opt.flat, a2.actor_opt.flat) and torch.equal(a1.critic_opt.flat, a2.critic_opt.flat)
+    assert r1 == r2
 
 
 @pytest.mark.parametrize("graphs", [True, False])
