@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, cons
   if (!last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // the batch moments: the ranges merged in order (parallel variance)
-  const double cnt = *count;
+  const double cnt = sums ? 0.0 : *count;   // (the multi-rank form has no statistics)
   for (int c = t; c < s.C; c += kRmsBlock) {
     double na = n_b[0], ma = mean_b[c], qa = m2_b[c];
     for (int b = 1; b < s.GR; ++b) {
