@@ -155,12 +155,30 @@ struct qs_handle {
   std::vector<double> orig_host;
 };
 
+// Envs per one-wave workgroup: ⌊64/D⌋, halved while the grid holds fewer than
+// kEpbWaves waves per SIMD (at most QS_EPB_HALVINGS times).  The step is
+// latency-bound per wave (loads → PID → substeps → reward → stores in one
+// dependent chain), so a grid under two waves per SIMD leaves the SIMDs idle
+// between its waves' phases; more, emptier waves overlap them (Spiral C4:
+// 683 waves of 12 envs for 1 024 SIMDs).  Results do not depend on it: every
+// per-env quantity is formed inside the env's own lanes.
+#ifndef QS_EPB_HALVINGS
+#define QS_EPB_HALVINGS 1
+#endif
+static constexpr int kEpbWaves = 2;
+static int envs_per_wave(const qs_handle* h) {
+  const int E = h->spec.num_envs, simds = 4 * h->num_cu;
+  int epb = qs::kBlock / h->spec.num_drones;
+  for (int k = 0; k < QS_EPB_HALVINGS && epb > 1 && (E + epb - 1) / epb < kEpbWaves * simds; ++k) epb = (epb + 1) / 2;
+  return epb;
+}
+
 template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P) {
   const qs_spec& s = h->spec;
   std::memset(&P, 0, sizeof(P));
   P.E = s.num_envs; P.D = s.num_drones; P.N = h->dims.num_agents; P.O = h->dims.obs_dim;
   P.H = h->dims.hist_len; P.S = h->dims.substeps;
-  P.EPB = qs::kBlock / s.num_drones;
+  P.EPB = envs_per_wave(h);
   P.aux = s.aux_forces; P.flags = s.flags; P.pyb_freq = s.pyb_freq; P.task = s.task;
   P.ep_len_sec = s.episode_len_sec;
   P.k0 = (uint32_t)h->seed; P.k1 = (uint32_t)(h->seed >> 32);
@@ -186,11 +204,11 @@ template <class T> static void fill_params(const qs_handle* h, qs::Params<T>& P)
 // 15 KB of history per workgroup), full staging is kept — more passes of fewer
 // rows cost more than the partial residency returns (C3-VEL 22.3 → 26.0 µs).
 static constexpr size_t kLdsBytes = 160 * 1024, kLdsStatic = 8192, kLdsGrain = 512, kStageBudget = 48 * 1024;
-static int lds_plan(const qs_dims& d, int resident, int* stage_rows, size_t* bytes) {
+static int lds_plan(const qs_dims& d, int epb, int resident, int* stage_rows, size_t* bytes) {
   const size_t hist = (size_t)d.hist_len * qs::kBlock * d.act_dim * sizeof(float);
   const size_t row = (size_t)d.obs_dim * sizeof(float);
   if (hist + row + kLdsStatic > kLdsBytes) return QS_E_INVALID;
-  const int rows = (qs::kBlock / d.num_drones) * d.num_drones;
+  const int rows = epb * d.num_drones;
   size_t per = kLdsBytes / (size_t)std::max(1, std::min(resident, 32));   // a workgroup's share at full residency
   if (per < kLdsStatic + kLdsGrain + hist + row) per = kLdsBytes;          // unreachable: plain staging
   const size_t budget = std::min(kStageBudget, per - kLdsStatic - kLdsGrain - hist);
@@ -202,7 +220,7 @@ static int lds_plan(const qs_dims& d, int resident, int* stage_rows, size_t* byt
 template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t st) {
   const int grid = (P.E + P.EPB - 1) / P.EPB;
   size_t lds = 0;
-  if (lds_plan(h->dims, (grid + h->num_cu - 1) / h->num_cu, &P.stage_rows, &lds) != QS_OK)
+  if (lds_plan(h->dims, P.EPB, (grid + h->num_cu - 1) / h->num_cu, &P.stage_rows, &lds) != QS_OK)
     return fail(QS_E_INVALID, "launch: action history does not fit in LDS (ctrl_freq too high)");
   const qs_spec& s = h->spec;
   bool ok;
@@ -317,7 +335,7 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   d.precision = s.precision; d.agent_fields = QS_AGENT_FIELDS; d.env_fields = QS_ENV_FIELDS;
   {
     int rows; size_t bytes;
-    if (lds_plan(d, 1, &rows, &bytes) != QS_OK) {
+    if (lds_plan(d, qs::kBlock / s.num_drones, 1, &rows, &bytes) != QS_OK) {
       delete h;
       return fail(QS_E_INVALID, "qs_create: action history (ctrl_freq // 2 entries) does not fit in LDS");
     }
