@@ -183,6 +183,7 @@ int qs_mlp_wgrad(int64_t K, int32_t N, int32_t M, const float* AT, const float* 
  *   qs_value_head's).  mean_out [K][A] (may be NULL): the actor output.
  * work: qs_mlp3f_work_bytes(K) bytes, zeroed once before the first call. */
 #define QS_PACK_F16 (1 << 16)
+#define QS_PACK_W2T (1 << 17)   /* pack_I flag: `pack` is a [256][256] W2ᵀ copy (qs_ppo_critic_tiles) */
 int32_t qs_mlp3f_tiles(int64_t K);
 int64_t qs_mlp3f_pack_floats(int32_t I);
 int64_t qs_mlp3f_work_bytes(int64_t K);
@@ -324,6 +325,28 @@ int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* id
                       float ent_coef, int32_t gate, float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic,
                       float* kl_out, double* acc, void* work, void* stream);
 const char* qs_ppo_small_last_error(void);
+/* The workspace's parts: off[0..15] byte offsets of xaT, h1aT, dz2aT, dz1aT,
+ * xcT, h1cT, dz2cT, dz1cT (transposed [width][rows padded to 16]), partAa,
+ * partBa, partAc, partBc (per-tile partial rows [tile][256 + 256·A + A] =
+ * Σ dZ2 | Σ dout·H2 | Σ dout, and [tile][256] = Σ dZ1), dlogstd, the loss
+ * partials, the counters; off[16..19] = actor tiles, critic tiles, padded
+ * actor rows, padded critic rows; off[20] = bytes.  Ia = 0: the critic-only
+ * layout of qs_ppo_critic_tiles. */
+int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off);
+/* The critic half of qs_ppo_small_step's first launch at any minibatch size:
+ * the critic's forward, value head (AG:642-683, acc[1] += value loss) and
+ * backward in 16-row tiles over every CU, writing the transposed activations
+ * and the per-tile partial rows of the Ia = 0 layout (no Adam step: the
+ * caller forms the weight gradients with qs_wgrad_t and reduces everything
+ * with qs_mlp_sum_adam).  critic->w2t must hold W2ᵀ (qs_mlp_sum_adam keeps a
+ * QS_PACK_W2T segment's copy current). */
+int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const double* ret,
+                        const qs_mlp256* critic, double* acc, void* work, void* stream);
+/* Split-K weight gradient from transposed operands: partial[s][n][m] =
+ * Σ_{rows r of chunk s} AT[n][r]·XT[m][r] (AT [N][KP], XT [M][KP], S chunks of
+ * KP/S rows; N a multiple of 16, KP of 16·S).  nn.Linear's dW = dYᵀ·X. */
+int qs_wgrad_t(int64_t KP, int32_t N, int32_t M, const float* AT, const float* XT, int32_t S, float* partial,
+               void* stream);
 
 #ifdef __cplusplus
 }

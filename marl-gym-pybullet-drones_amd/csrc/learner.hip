@@ -1508,7 +1508,7 @@ struct AdamSeg {
   long long n, w1, w2;    // elements; offsets of W1 [256][I] and W2 [256][256] in p
   float lr, b1, b2, eps, thr;
   int I, zero;
-  int kind;               // pack layout: 0 qs_mlp3_pack (32x32 tiles), 1 qs_mlp3f_pack (16x16 tiles)
+  int kind;               // pack layout: 0 qs_mlp3_pack (32x32 tiles), 1 qs_mlp3f_pack (16x16 tiles), 2 W2ᵀ
 };
 struct AdamSegs {
   AdamSeg s[kAdamMaxSeg];
@@ -1548,6 +1548,11 @@ __device__ __forceinline__ void adam_elem(const AdamSeg& A, long long i, float g
       const int mm = (int)((i - A.w2) >> 8), n = (int)((i - A.w2) & 255);
       A.pack[w2f0 + f16_pos_w2f(mm, n)] = p1;
       A.pack[w2b0 + f16_pos_w2b(mm, n)] = p1;
+    }
+  } else if (A.pack && A.kind == 2) {   // a W2ᵀ copy (QS_PACK_W2T)
+    if (i >= A.w2 && i < A.w2 + (long long)kM3N * kM3N) {
+      const int mm = (int)((i - A.w2) >> 8), n = (int)((i - A.w2) & 255);
+      A.pack[(size_t)n * kM3N + mm] = p1;
     }
   } else if (A.pack) {
     const int Ip = (A.I + 31) & ~31;
@@ -2434,7 +2439,8 @@ static int build_adam_segs(int32_t nseg, float* const* params, float* const* gra
       return fail(QS_E_INVALID, std::string(name) + ": bad segment");
     float* pk = pack ? pack[i] : nullptr;
     // pack_I: the MLP's input width, | QS_PACK_F16 for a qs_mlp3f_pack image
-    const int I = pk ? (pack_I[i] & ~QS_PACK_F16) : 0, kind = pk && (pack_I[i] & QS_PACK_F16) ? 1 : 0;
+    const int I = pk ? (pack_I[i] & ~(QS_PACK_F16 | QS_PACK_W2T)) : 0;
+    const int kind = !pk ? 0 : (pack_I[i] & QS_PACK_F16) ? 1 : (pack_I[i] & QS_PACK_W2T) ? 2 : 0;
     if (pk && (I <= 0 || I > 1024 || w1_off[i] < 0 || w2_off[i] < 0 || w1_off[i] + (int64_t)kM3N * I > n[i] ||
                w2_off[i] + (int64_t)kM3N * kM3N > n[i]))
       return fail(QS_E_INVALID, std::string(name) + ": bad pack segment");

@@ -541,14 +541,45 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
   }
 }
 
+// Split-K weight gradient from transposed activations: partial[s][n][m] =
+// Σ_{rows of chunk s} AT[n][row]·XT[m][row] (AT = dZᵀ [N][KP], XT = Xᵀ [M][KP],
+// rows past K zero), one wave per 16×16 output tile and chunk, the A / B
+// operands one float4 each per MFMA quad (rows 16q + 4g .. +3).  The chunk
+// partials are summed in chunk order by qs_mlp_sum_adam.
+__global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP, int S, const float* __restrict__ AT,
+                                                            const float* __restrict__ XT, float* __restrict__ partial) {
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const int nm = (M + 15) / 16, tiles = (N / 16) * nm;
+  const int T = blockIdx.x * kSAW + w;   // (chunk, tile): the chunks of a tile in consecutive waves
+  if (T >= tiles * S) return;
+  const int s = T % S, u = T / S, nb = u / nm, mb = u - nb * nm;
+  const int rows = KP / S, r0 = s * rows;
+  const int m = 16 * mb + j;
+  const float* arow = AT + (size_t)(16 * nb + j) * KP + r0;
+  const float* brow = m < M ? XT + (size_t)m * KP + r0 : nullptr;
+  f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < rows / 16; ++q) {
+    const float4 av = *reinterpret_cast<const float4*>(arow + 16 * q + 4 * g);
+    const float4 bv = brow ? *reinterpret_cast<const float4*>(brow + 16 * q + 4 * g) : float4{0.f, 0.f, 0.f, 0.f};
+    c = s_mfma(av.x, bv.x, c);
+    c = s_mfma(av.y, bv.y, c);
+    c = s_mfma(av.z, bv.z, c);
+    c = s_mfma(av.w, bv.w, c);
+  }
+  if (m < M)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) partial[((size_t)s * N + 16 * nb + 4 * g + r) * M + m] = c[r];
+}
+
 struct SLayout {
   int nA, nC, KaP, KcP;
   long long off[16];
   long long bytes;
 };
+// Ia = 0: the critic's tiles only (qs_ppo_critic_tiles), no actor buffers
 SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   SLayout L;
-  const long long Ka = (long long)mb * D, Kc = mb;
+  const long long Ka = Ia > 0 ? (long long)mb * D : 0, Kc = mb;
   L.nA = (int)((Ka + 15) / 16);
   L.nC = (int)((Kc + 15) / 16);
   L.KaP = 16 * L.nA;
@@ -574,29 +605,55 @@ extern "C" {
 const char* qs_ppo_small_last_error(void) { return g_serr.c_str(); }
 
 int64_t qs_ppo_small_work_bytes(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A) {
-  if (mb <= 0 || D <= 0 || Ia <= 0 || Ic <= 0 || A < 1 || A > kSMaxA) return 0;
+  if (mb <= 0 || D <= 0 || Ia < 0 || Ic <= 0 || A < 1 || A > kSMaxA) return 0;
   return s_layout(mb, D, Ia, Ic, A).bytes;
 }
 
-int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
-                      const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
-                      float ent_coef, int32_t gate, float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic,
-                      float* kl_out, double* acc, void* work, void* stream) {
-  if (mb <= 0 || D <= 0 || !obs || !idx || !act || !logp_old || !adv || !ret || !actor || !critic || !kl_out || !acc ||
-      !work)
-    return sfail(QS_E_INVALID, "qs_ppo_small_step: bad argument");
+int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off) {
+  if (mb <= 0 || D <= 0 || Ia < 0 || Ic <= 0 || A < 1 || A > kSMaxA || !off)
+    return sfail(QS_E_INVALID, "qs_ppo_small_layout: bad argument");
+  const SLayout L = s_layout(mb, D, Ia, Ic, A);
+  for (int i = 0; i < 16; ++i) off[i] = L.off[i];
+  off[16] = L.nA;
+  off[17] = L.nC;
+  off[18] = L.KaP;
+  off[19] = L.KcP;
+  off[20] = L.bytes;
+  return QS_OK;
+}
+
+int qs_wgrad_t(int64_t KP, int32_t N, int32_t M, const float* AT, const float* XT, int32_t S, float* partial,
+               void* stream) {
+  if (KP <= 0 || N <= 0 || N % 16 || M <= 0 || M > 4096 || S <= 0 || KP % (16LL * S) || !AT || !XT || !partial ||
+      KP * (int64_t)(N > M ? N : M) >= (int64_t(1) << 31))
+    return sfail(QS_E_INVALID, "qs_wgrad_t: bad argument (N a multiple of 16, KP a multiple of 16·S)");
+  const long long waves = (long long)(N / 16) * ((M + 15) / 16) * S;
+  hipLaunchKernelGGL(wgrad_t_kernel, dim3((unsigned)((waves + kSAW - 1) / kSAW)), dim3(64 * kSAW), 0,
+                     (hipStream_t)stream, (int)N, (int)M, (int)KP, (int)S, AT, XT, partial);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_wgrad_t: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"
+
+static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act, const float* logp_old,
+                  const double* adv, const double* ret, float action_scale, float clip, float ent_coef, int32_t gate,
+                  float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic, float* kl_out, double* acc, void* work,
+                  bool need_actor, SArgs& P, SLayout& L, const char* name) {
+  if (mb <= 0 || D <= 0 || !obs || !idx || !ret || !actor || !critic || !acc || !work ||
+      (need_actor && (!act || !logp_old || !adv || !kl_out)))
+    return sfail(QS_E_INVALID, std::string(name) + ": bad argument");
   const int A = actor->out;
   if (A < 1 || A > kSMaxA || critic->out != 1 || actor->in < 1 || actor->in > kSMaxI || critic->in < 1 ||
-      critic->in > kSMaxI || actor->logstd < 0 || !actor->w2t || !critic->w2t)
-    return sfail(QS_E_INVALID, "qs_ppo_small_step: nets must be 256-wide with <= 256 inputs, A <= 4 actor outputs "
-                               "(with logstd) and one critic output, W2ᵀ copies given");
+      critic->in > kSMaxI || (need_actor && (actor->logstd < 0 || !actor->w2t)) || !critic->w2t)
+    return sfail(QS_E_INVALID, std::string(name) + ": nets must be 256-wide with <= 256 inputs, A <= 4 actor outputs "
+                                                   "(with logstd) and one critic output, W2ᵀ copies given");
   if ((actor->w2 & 3) || (critic->w2 & 3) || ((actor->in & 3) == 0 && (actor->w1 & 3)) ||
       ((critic->in & 3) == 0 && (critic->w1 & 3)))
-    return sfail(QS_E_INVALID, "qs_ppo_small_step: W1 / W2 must start 16-byte aligned in the flat buffers");
-  if ((long long)mb * D > QS_PPO_SMALL_MAX_ROWS)
-    return sfail(QS_E_INVALID, "qs_ppo_small_step: minibatch above QS_PPO_SMALL_MAX_ROWS actor rows");
-  const SLayout L = s_layout(mb, D, actor->in, critic->in, A);
-  SArgs P;
+    return sfail(QS_E_INVALID, std::string(name) + ": W1 / W2 must start 16-byte aligned in the flat buffers");
+  if ((long long)mb * D * kSH >= (1LL << 31))
+    return sfail(QS_E_INVALID, std::string(name) + ": minibatch too large for 32-bit activation offsets");
+  L = s_layout(mb, D, actor->in, critic->in, A);
   P.mb = mb;
   P.D = D;
   P.nA = L.nA;
@@ -647,18 +704,63 @@ int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* id
   P.w.lossa = (double*)(wb + L.off[13]);
   P.w.lossc = (double*)(wb + L.off[14]);
   P.w.cnt = (unsigned*)(wb + L.off[15]);
-  hipStream_t st = (hipStream_t)stream;
-  switch (A) {
-    case 1: hipLaunchKernelGGL(ppo_small_fb_kernel<1>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
-    case 2: hipLaunchKernelGGL(ppo_small_fb_kernel<2>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
-    case 3: hipLaunchKernelGGL(ppo_small_fb_kernel<3>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
-    default: hipLaunchKernelGGL(ppo_small_fb_kernel<4>, dim3(L.nA + L.nC), dim3(kSBlock), 0, st, P); break;
+  return QS_OK;
+}
+
+static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
+  switch (P.a.A) {
+    case 1: hipLaunchKernelGGL(ppo_small_fb_kernel<1>, dim3(grid), dim3(kSBlock), 0, st, P); break;
+    case 2: hipLaunchKernelGGL(ppo_small_fb_kernel<2>, dim3(grid), dim3(kSBlock), 0, st, P); break;
+    case 3: hipLaunchKernelGGL(ppo_small_fb_kernel<3>, dim3(grid), dim3(kSBlock), 0, st, P); break;
+    default: hipLaunchKernelGGL(ppo_small_fb_kernel<4>, dim3(grid), dim3(kSBlock), 0, st, P); break;
   }
+}
+
+extern "C" {
+
+int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
+                      const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
+                      float ent_coef, int32_t gate, float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic,
+                      float* kl_out, double* acc, void* work, void* stream) {
+  SArgs P;
+  SLayout L;
+  int rc = s_args(mb, D, obs, idx, act, logp_old, adv, ret, action_scale, clip, ent_coef, gate, kl_thr, actor, critic,
+                  kl_out, acc, work, true, P, L, "qs_ppo_small_step");
+  if (rc != QS_OK) return rc;
+  if ((long long)mb * D > QS_PPO_SMALL_MAX_ROWS)
+    return sfail(QS_E_INVALID, "qs_ppo_small_step: minibatch above QS_PPO_SMALL_MAX_ROWS actor rows");
+  hipStream_t st = (hipStream_t)stream;
+  s_launch_fb(P, L.nA + L.nC, st);
   const int nTiles = 16 * (s_ip(actor->in) / 16) + 256 + 16 * (s_ip(critic->in) / 16) + 256;
   const int grid = (nTiles + kSAW - 1) / kSAW + kSVecWG;
   hipLaunchKernelGGL(ppo_small_adam_kernel, dim3(grid), dim3(64 * kSAW), 0, st, P, nTiles);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_small_step: ") + hipGetErrorString(e));
+}
+
+int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const double* ret,
+                        const qs_mlp256* critic, double* acc, void* work, void* stream) {
+  if (!critic) return sfail(QS_E_INVALID, "qs_ppo_critic_tiles: bad argument");
+  // the workspace layout of qs_ppo_small_layout(mb, D, 0, critic->in, 1): no actor tiles or buffers
+  qs_mlp256 dummy = *critic;
+  SArgs P;
+  SLayout L;
+  int rc = s_args(mb, D, obs, idx, nullptr, nullptr, nullptr, ret, 1.f, 0.f, 0.f, 0, 0.f, &dummy, critic, nullptr, acc,
+                  work, false, P, L, "qs_ppo_critic_tiles");
+  if (rc != QS_OK) return rc;
+  L = s_layout(mb, D, 0, critic->in, 1);
+  char* wb = (char*)work;
+  float** fv[13] = {&P.w.xaT, &P.w.h1aT, &P.w.dz2aT, &P.w.dz1aT, &P.w.xcT, &P.w.h1cT, &P.w.dz2cT,
+                    &P.w.dz1cT, &P.w.partAa, &P.w.partBa, &P.w.partAc, &P.w.partBc, &P.w.dlogstd};
+  for (int i = 0; i < 13; ++i) *fv[i] = (float*)(wb + L.off[i]);
+  P.w.lossa = (double*)(wb + L.off[13]);
+  P.w.lossc = (double*)(wb + L.off[14]);
+  P.w.cnt = (unsigned*)(wb + L.off[15]);
+  P.nA = 0;   // critic tiles only
+  P.KaP = 0;
+  s_launch_fb(P, L.nC, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_critic_tiles: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -68,8 +68,10 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
            "qs_wgrad_rm", "qs_learner_last_error", "qs_rms_work_bytes", "qs_rms_update", "qs_rms_normalize",
-           "qs_rms_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error")
+           "qs_rms_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error",
+           "qs_ppo_small_layout", "qs_ppo_critic_tiles", "qs_wgrad_t")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
+QS_PACK_W2T = 1 << 17   # pack_I flag: a [256][256] W2ᵀ copy (include/qs_learner.h)
 
 _lib = None
 
@@ -160,6 +162,9 @@ def load():
     L.qs_rms_last_error.restype = ctypes.c_char_p
     L.qs_ppo_small_last_error.restype = ctypes.c_char_p
     L.qs_ppo_small_work_bytes.argtypes = [ctypes.c_int32] * 5
+    L.qs_ppo_small_layout.argtypes = [ctypes.c_int32] * 5 + [vp]
+    L.qs_ppo_critic_tiles.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp, vp, ctypes.POINTER(QsMlp256), vp, vp, vp]
+    L.qs_wgrad_t.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_ppo_small_step.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [f32, f32, f32, ctypes.c_int32, f32]
                                     + [ctypes.POINTER(QsMlp256)] * 2 + [vp] * 4)
     L.qs_rms_work_bytes.argtypes = [i64, ctypes.c_int32]
@@ -185,7 +190,7 @@ def check(rc, what=""):
         lib = load()
         if what.startswith("qs_rms"):
             msg = lib.qs_rms_last_error()
-        elif what.startswith("qs_ppo_small"):
+        elif what.startswith(("qs_ppo_small", "qs_ppo_critic", "qs_wgrad_t")):
             msg = lib.qs_ppo_small_last_error()
         elif what.startswith(("qs_gae", "qs_adam", "qs_ppo", "qs_mlp", "qs_wgrad", "qs_value")):
             msg = lib.qs_learner_last_error()

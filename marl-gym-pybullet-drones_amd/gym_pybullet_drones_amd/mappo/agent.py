@@ -506,6 +506,60 @@ def _mlp256(fb, mlp, logstd, w2t, lib_struct):
 _F16_MAX_A = 1
 
 
+class _CriticTiles:
+    """The centralized critic's minibatch step for the direct iteration at any
+    size: qs_ppo_critic_tiles (forward, value head, backward in 16-row tiles
+    over every CU; the value loss into acc[1]) and the split-K weight gradients
+    qs_wgrad_t from its transposed activations.  The partial rows are the
+    _M3Work critic's (qs_mlp_sum_adam tasks); the step's W2ᵀ copy is the
+    segment's pack (QS_PACK_W2T), so Adam keeps it current."""
+
+    def __init__(self, agent, mb, D):
+        lib = L.load()
+        mlp = agent.ac.critic.v_net
+        f0, f1, f2 = mlp.fcs
+        self.mlp, self.mb, self.D, self.I = mlp, mb, D, f0.in_features
+        off = (ctypes.c_int64 * 21)()
+        L.check(lib.qs_ppo_small_layout(mb, D, 0, self.I, 1, off), "qs_ppo_small_layout")
+        self.nC, KcP = int(off[17]), int(off[19])
+        dev = agent.device
+        self.work = torch.zeros(int(off[20]), dtype=torch.uint8, device=dev)
+        view = lambda i, *shape: self.work[off[i]:off[i] + 4 * math.prod(shape)].view(torch.float32).view(*shape)
+        self.xT, self.h1T, self.dz2T, self.dz1T = (view(4, self.I, KcP), view(5, 256, KcP), view(6, 256, KcP),
+                                                   view(7, 256, KcP))
+        self.part_a, self.part_b = view(10, self.nC, 513), view(11, self.nC, 256)
+        self.S = next(d for d in (8, 4, 2, 1) if self.nC % d == 0)
+        self.pw1 = torch.empty((self.S, 256, self.I), device=dev)
+        self.pw2 = torch.empty((self.S, 256, 256), device=dev)
+        self.w2t = torch.empty((256, 256), device=dev)
+        self.net = _mlp256(agent.critic_opt, mlp, None, self.w2t, L.QsMlp256)
+        self.KcP = KcP
+        self.repack()
+
+    def repack(self):
+        self.w2t.copy_(self.mlp.fcs[1].weight.t())
+
+    def pack_segment(self, fb):
+        ids = [id(p) for p in fb.params]
+        f0, f1, _ = self.mlp.fcs
+        return (self.w2t, fb.offsets[ids.index(id(f0.weight))][0], fb.offsets[ids.index(id(f1.weight))][0],
+                self.I | L.QS_PACK_W2T)
+
+    def step(self, rollouts, idx, acc, tasks):
+        lib, st = L.load(), _stream()
+        f0, f1, f2 = self.mlp.fcs
+        L.check(lib.qs_ppo_critic_tiles(self.mb, self.D, L.ptr(rollouts.obs), L.ptr(idx), L.ptr(rollouts.ret_env),
+                                        ctypes.byref(self.net), L.ptr(acc), L.ptr(self.work), st), "qs_ppo_critic_tiles")
+        L.check(lib.qs_wgrad_t(self.KcP, 256, self.I, L.ptr(self.dz1T), L.ptr(self.xT), self.S, L.ptr(self.pw1), st),
+                "qs_wgrad_t")
+        L.check(lib.qs_wgrad_t(self.KcP, 256, 256, L.ptr(self.dz2T), L.ptr(self.h1T), self.S, L.ptr(self.pw2), st),
+                "qs_wgrad_t")
+        tasks.append((self.nC, 513, self.part_a, f1.bias.grad, 256, f2.weight.grad, 256, f2.bias.grad))
+        tasks.append((self.nC, 256, self.part_b, f0.bias.grad, 256, None, 0, None))
+        tasks.append((self.S, self.pw1[0].numel(), self.pw1, f0.weight.grad, f0.weight.numel(), None, 0, None))
+        tasks.append((self.S, self.pw2[0].numel(), self.pw2, f1.weight.grad, f1.weight.numel(), None, 0, None))
+
+
 def _f16_ok(mlp):
     """The fused actor step takes the one-action-output actor with inputs <= 128
     wide (the bench's ONE_D_* actors), up to _F16_MAX_A outputs; other widths
@@ -856,6 +910,9 @@ class MAPPOAgent:
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
         self.actor_first = kwargs.get('actor_first', False)
+        # with the fused actor, the critic's step on qs_ppo_critic_tiles + qs_wgrad_t
+        # (False: the qs_mlp3w kernels and hipBLASLt weight-gradient GEMMs)
+        self.critic_tiles = kwargs.get('critic_tiles', True)
         # minibatches of at most _SMALL_MAX_ROWS actor rows on qs_ppo_small_step (one
         # rank); False: always the split-K direct iteration
         self.small = kwargs.get('small', True)
@@ -1002,7 +1059,11 @@ class MAPPOAgent:
         # the fused actor's own row limit (K·1024 < 2^31, qs_mlp3f_actor) as well as the widths
         f16 = self.fused_actor and _f16_ok(self.ac.actor.pi_net) and _m3_shape_ok(mb * D, O)
         self._ws_actor = (_F16Work if f16 else _M3Work)(self.ac.actor.pi_net, mb * D, self.device)
-        self._ws_critic = _M3Work(self.ac.critic.v_net, mb, self.device)
+        pc = self.ac.critic.v_net
+        # with the fused actor the critic runs in 16-row tiles over every CU (qs_ppo_critic_tiles);
+        # the two-kernel actor path shares qs_ppo_heads' value head with the _M3Work critic
+        tiles = f16 and self.critic_tiles and pc.fcs[0].in_features <= 256 and pc.fcs[2].out_features == 1
+        self._ws_critic = _CriticTiles(self, mb, D) if tiles else _M3Work(pc, mb, self.device)
         self._vh_work = torch.zeros(int(lib.qs_ppo_heads_work_bytes(mb, D)), dtype=torch.uint8, device=self.device)
         self._xg = torch.empty((mb, D * O), device=self.device)
         self._dmean = torch.empty(mb * D, A, device=self.device)
@@ -1060,10 +1121,16 @@ class MAPPOAgent:
 
         if fused:
             def critic_all(exchange, own_adam=False):
-                v = critic_fwd()
-                L.check(lib.qs_value_head(mb, D, L.ptr(idx), L.ptr(rollouts.ret_env), L.ptr(v), L.ptr(self._dv),
-                                          L.ptr(acc), L.ptr(self._vh_work), _stream()), "qs_value_head")
-                critic_bwd(exchange)
+                if isinstance(self._ws_critic, _CriticTiles):
+                    self._ws_critic.step(rollouts, idx, acc, tc)
+                    if exchange:
+                        _flush_sums(tc)
+                        self._exchange_bucket(self._critic_bucket, world)
+                else:
+                    v = critic_fwd()
+                    L.check(lib.qs_value_head(mb, D, L.ptr(idx), L.ptr(rollouts.ret_env), L.ptr(v), L.ptr(self._dv),
+                                              L.ptr(acc), L.ptr(self._vh_work), _stream()), "qs_value_head")
+                    critic_bwd(exchange)
                 if own_adam:
                     # the critic's Adam is ungated: its sums and step run here, beside
                     # the actor's weight-gradient GEMMs, not after the join
