@@ -81,6 +81,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--mappo", type=int, default=1, help="also time full MAPPO train steps (0 = skip)")
     p.add_argument("--pyb", type=int, default=1, help="also time the rollout under Physics.PYB (0 = skip)")
+    p.add_argument("--fp64", type=int, default=1,
+                   help="also time the headline rollout in float64, the reference's own precision (0 = skip)")
     p.add_argument("--configs", type=int, default=1, help="also time BASELINE configs C2, C3-VEL, C4, C5 (N=1 only)")
     p.add_argument("--mappo-steps", type=int, default=256, help="rollout_steps T of the MAPPO leg (learn_mappo.py:665)")
     p.add_argument("--mappo-mb", type=int, default=4096, help="mini_batch_size (env-timesteps) of the MAPPO legs")
@@ -237,9 +239,27 @@ def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dy
         chunk = max(1, min(2 * chunk, int((seconds - dt) / max(dc / chunk, 1e-9)) + 1))
     sim.close()
     return {"value": E * D * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "host": host_cpu(),
             "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {task} {E} envs x "
                       f"{D} drones, {act}, {physics}{'+' + '+'.join(aux) if aux else ''}, {steps} random-policy "
                       f"ctrl steps, OpenMP {threads} threads, {dt:.1f} s"}
+
+
+def host_cpu():
+    """The CPU the baseline ran on (BASELINE.md:37): model name and the logical
+    CPUs this process may use (os.cpu_count() reports the whole machine's)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def pmc_traffic(E, D, act):
@@ -287,7 +307,7 @@ def stagger_episodes(sw, task):
     sw.set_state(L.STATE_ENV, env)
 
 
-def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=None, aux=()):
+def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=None, aux=(), precision=4):
     """The timed random-policy rollout: exactly `args.steps` control steps of E envs
     per rank, as replays of HIP graphs of step launches (one per rollout-buffer slot).
     Returns (agent-steps/s over all ranks, max-over-ranks seconds, mean step-kernel
@@ -299,13 +319,13 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
     act = args.act if act is None else act
     phys = {"dyn": Physics.DYN, "pyb": Physics.PYB, "pyb_dw": Physics.PYB_DW}[physics]
     layout = grid_layout(D) if (D >= 6 and task == "multihover") else None
-    sw = QuadSwarm(task, num_envs=E, num_drones=D, act=act, precision=4, physics=phys, aux=aux,
+    sw = QuadSwarm(task, num_envs=E, num_drones=D, act=act, precision=precision, physics=phys, aux=aux,
                    initial_xyzs=layout, env_offset=ranks.rank * E)
     O, A = sw.obs_dim, sw.act_dim
     slots = max(1, min(args.slots, args.steps))
     obs_buf = torch.empty((slots, E, D, O), dtype=torch.float32, device=sw.device)
     act_buf = torch.empty((slots, E, D, A), dtype=torch.float32, device=sw.device)
-    rew_buf = torch.empty((slots, E), dtype=torch.float32, device=sw.device)
+    rew_buf = torch.empty((slots, E), dtype=sw.reward.dtype, device=sw.device)   # the kernel's `real`
     te_buf = torch.zeros((slots, E), dtype=torch.uint8, device=sw.device)
     tr_buf = torch.zeros((slots, E), dtype=torch.uint8, device=sw.device)
     sw.reset(0, obs=obs_buf[0])
@@ -426,6 +446,8 @@ def leg_plan(args, world):
     rollout legs weak-scaled beside them, and §8(e)'s strong partitions of
     configs 3-5 (STRONG_LEGS / STRONG_SIM)."""
     plan = [("sim", "headline", "weak", args.envs, None)]
+    if args.fp64:
+        plan.append(("sim", "fp64", "weak", args.envs, None))
     if args.pyb:
         plan.append(("sim", "pyb", "weak", args.envs, None))
     if args.mappo:
@@ -576,10 +598,19 @@ def main():
     value, elapsed, kern_ms, steps, eps_done = sim_leg(args, ranks, "dyn")
     nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
-    pyb = mappo = mappo32 = mappo_cfgs = configs = None
+    pyb = fp64 = mappo = mappo32 = mappo_cfgs = configs = None
     mappo_strong, configs_strong = {}, {}
     for kind, name, scaling, e_rank, mb_rank in leg_plan(args, world)[1:]:
-        if kind == "sim" and name == "pyb":   # the same rollout under Physics.PYB (the reference's training default)
+        if kind == "sim" and name == "fp64":   # the headline rollout in the reference's float64
+            progress("headline rollout leg, float64")
+            fv, fel, fk, _, _ = sim_leg(args, ranks, "dyn", precision=8)
+            fp64 = {"value": fv, "unit": "agent-steps/s", "kernel_ms": fk, "ms_per_step": fel / args.steps * 1e3,
+                    "dtype": "f64", "roofline_frac": nbytes * 2 / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act, 418.0) * 2,
+                    "what": "the same C3 rollout with every state field, reward and the physics in float64 (the "
+                            "reference's numpy precision); obs float32 as the reference emits them; bytes: the "
+                            "float32 figure doubled (state, history and reward in f64)"}
+        elif kind == "sim" and name == "pyb":   # the same rollout under Physics.PYB (the reference's training default)
             pv, _, pk, _, _ = sim_leg(args, ranks, "pyb")
             pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
                    "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
@@ -641,7 +672,12 @@ def main():
                          "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": nbytes,
                          "kernel_ms": kern_ms, "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act)},
+            "timing": {"wall_ms_per_step": elapsed / steps * 1e3, "event_ms_per_step": kern_ms,
+                       "fixed_wall_us_per_window": (elapsed / steps * 1e3 - kern_ms) * steps * 1e3,
+                       "what": "wall: barrier + device sync on both sides of the K steps (the value); event: HIP "
+                               "events around the graph replays on the launch stream (the roofline's kernel time)"},
             "cpu_baseline": cpu,
+            "fp64": fp64,
             "pyb": pyb,
             "mappo": mappo,
             "mappo_t32": mappo32,

@@ -195,6 +195,13 @@ class QuadSwarm:
         reward = self.reward if reward is None else reward
         terminated = self.terminated if terminated is None else terminated
         truncated = self.truncated if truncated is None else truncated
+        # the kernel writes whole rows through these pointers: refuse a buffer it would overrun
+        for t, dt, n, what in ((obs, torch.float32, self.num_agents * self.obs_dim, "obs"),
+                               (reward, self.rdtype, self.num_envs, "reward"),
+                               (terminated, torch.uint8, self.num_envs, "terminated"),
+                               (truncated, torch.uint8, self.num_envs, "truncated")):
+            if t.dtype != dt or not t.is_contiguous() or t.numel() < n or t.device != self.device:
+                raise ValueError(f"{what} must be a contiguous {dt} tensor of >= {n} elements on {self.device}")
         if want_terminal and terminal_obs is None:
             terminal_obs = self.terminal_obs
         if want_reasons and reasons is None:
