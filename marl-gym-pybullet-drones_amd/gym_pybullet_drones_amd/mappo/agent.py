@@ -751,15 +751,23 @@ class MAPPOActorCritic(nn.Module):
         return self.actor(obs)[0].entropy()
 
 
+def _flat_len(module):
+    """Elements of a module's FlatBuffers: every parameter starts on a 16-byte
+    boundary (the MFMA kernels read weight rows as float4), the pads are zeros
+    that Adam leaves at zero."""
+    return sum((p.numel() + 3) & ~3 for p in module.parameters())
+
+
 class FlatBuffers:
-    """Parameters, gradients and Adam moments of one module in flat fp32 buffers."""
+    """Parameters, gradients and Adam moments of one module in flat fp32 buffers
+    (each parameter 16-byte aligned: _flat_len)."""
 
     def __init__(self, module, lr, betas=(0.9, 0.999), eps=1e-8, grad=None):
         """grad: optional external flat gradient view (MAPPOAgent packs the actor and
         critic gradients plus approx_kl into one buffer, so one all-reduce serves all)."""
         self.params = [p for p in module.parameters()]
         dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
+        n = _flat_len(module)
         self.n = n
         self.flat = torch.zeros(n, device=dev)
         self.grad = torch.zeros(n, device=dev) if grad is None else grad
@@ -775,7 +783,7 @@ class FlatBuffers:
             p.data = self.flat[off:off + k].view_as(p)
             p.grad = self.grad[off:off + k].view_as(p)
             self.offsets.append((off, k))
-            off += k
+            off += (k + 3) & ~3
         self.lr, self.betas, self.eps = lr, betas, eps
 
     def adam(self, gate_val=None, gate_thr=0.0):
@@ -933,8 +941,7 @@ class MAPPOAgent:
         self.ac.to(self.device)
         # The flat buffers exist on any device (the gloo tests drive the multi-rank
         # update on CPU tensors); the optimizer step itself is the HIP kernel.
-        na = sum(p.numel() for p in self.ac.actor.parameters())
-        nc = sum(p.numel() for p in self.ac.critic.parameters())
+        na, nc = _flat_len(self.ac.actor), _flat_len(self.ac.critic)
         # [critic grads | actor grads | approx_kl]: the buffer the ranks all-reduce, in
         # one piece (autograd paths) or as two buckets (the direct iteration): the
         # critic's [:nc], reduced while the actor backward still runs, then the
