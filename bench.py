@@ -94,10 +94,12 @@ def parse():
     p.add_argument("--splitk", default="", help="learner split-K chunk rows per weight-gradient shape, 'KxM=rows,...'")
     p.add_argument("--side-stream", type=int, default=1, help="learner: critic kernels on a second stream (0 = one stream)")
     p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
-    p.add_argument("--wgrad-rm", type=int, default=0, help="learner: actor dW2 on qs_wgrad_rm (0 = torch.bmm GEMMs)")
-    p.add_argument("--actor-first", type=int, default=0, help="learner: capture the actor chain first (dW1 after dW2)")
     p.add_argument("--fused-max-a", type=int, default=None,
                    help="learner: widest actor output on the fused actor kernel (default: the agent's _F16_MAX_A)")
+    p.add_argument("--critic-tiles", type=int, default=1,
+                   help="learner: the critic on qs_ppo_critic_tiles + qs_wgrad_t (0 = qs_mlp3w kernels + GEMMs)")
+    p.add_argument("--small-rows", type=int, default=None,
+                   help="learner: minibatches of at most this many actor rows on qs_ppo_small_step (0 = never)")
     p.add_argument("--critic-adam-side", type=int, default=0,
                    help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
     p.add_argument("--strong", type=int, default=1,
@@ -498,13 +500,14 @@ def mappo_leg(args, ranks, T, cfg=None):
               mini_batch_size=mb, output_dir="/tmp/qs_bench_mappo", **cfg)
     m.agent.side_stream = bool(args.side_stream)
     m.agent.critic_adam_side = bool(args.critic_adam_side)
-    m.agent.actor_first = bool(args.actor_first)
+    m.agent.critic_tiles = bool(args.critic_tiles)
     from gym_pybullet_drones_amd.mappo import agent as agent_mod
     from gym_pybullet_drones_amd.mappo.agent import _F16Work, _M3Work, _SPLITK_MIN_ROWS
+    if args.small_rows is not None:
+        agent_mod._SMALL_MAX_ROWS = int(args.small_rows)
     if args.fused_max_a is not None:
         agent_mod._F16_MAX_A = int(args.fused_max_a)
     _F16Work.w1_stream = bool(args.w1_stream)
-    _F16Work.wgrad_rm = bool(args.wgrad_rm)
     _M3Work.wgrad = tuple(w for w in args.wgrad.split(",") if w)
     for item in filter(None, args.splitk.split(",")):   # "KxM=rows": split-K chunk rows of a weight gradient
         km, rows = item.split("=")
@@ -527,6 +530,12 @@ def mappo_leg(args, ranks, T, cfg=None):
     graphed = world == 1 or m.agent.graph_collectives
     rollout_graph = m._rollout_graph is not None
     fused_actor = type(getattr(m.agent, "_ws_actor", None)).__name__ == "_F16Work"
+    if getattr(m.agent, "_sm_key", None) is not None:
+        learner_path = "qs_ppo_small_step (two launches per minibatch)"
+    else:
+        learner_path = ("qs_mlp3f_actor + bmm dW2" if fused_actor else "qs_mlp3 actor") + (
+            " | critic qs_ppo_critic_tiles + qs_wgrad_t" if type(getattr(m.agent, "_ws_critic", None)).__name__
+            == "_CriticTiles" else " | critic qs_mlp3w + GEMMs")
     m.close()
     ph = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     upd_flop, roll_flop = mappo_flops(T, E, D, O, A)
@@ -543,6 +552,7 @@ def mappo_leg(args, ranks, T, cfg=None):
                        "obs_dim": O,
                        "act_dim": A, "hidden": 256, "opt_epochs": 10, "mini_batch_size": mb,
                        "minibatches_per_epoch": T * E // mb, "fused_actor_kernel": fused_actor,
+                       "learner_path": learner_path,
                        "overrides": cfg or None,
                        "reference": "learn_mappo.py: T=256, 176 envs, mini_batch_size 32 (1408 minibatches/epoch)",
                        "graphs": ("rollout + " if rollout_graph else "") + ("update" if graphed else ""),

@@ -36,18 +36,6 @@ def get_activation(name):
     return getattr(torch, name) if name in ("tanh", "relu", "sigmoid") else (getattr(F, name) if name else (lambda x: x))
 
 
-def _wgrad_rm_chunks(rows, tiles=4):
-    """Row chunks of qs_wgrad_rm for a 256×256 weight gradient: about one
-    workgroup per CU (tiles × chunks <= 256), every chunk a multiple of 8 rows
-    and at least 64 (0: the shape is not taken)."""
-    if rows % 8:
-        return 0
-    c = 1
-    while c * 2 * tiles <= 256 and rows % (16 * c) == 0 and rows // (2 * c) >= 64:
-        c *= 2
-    return c
-
-
 def _splitk_chunks(rows, min_rows=1024):
     """Row chunks of the split-K weight gradient: the largest power of two S with
     rows / S >= min_rows that divides rows (1 = plain GEMM)."""
@@ -366,7 +354,6 @@ class _F16Work(_M3Work):
     rows and reduction tasks as _M3Work.backward."""
 
     w1_stream = True   # dW1 on a third stream beside dW2 (False: after it, one stream)
-    wgrad_rm = False   # dW2 on qs_wgrad_rm (opt-in: 47 µs vs 41 µs for the torch.bmm row-chunk GEMMs)
 
     def __init__(self, mlp, K, device):
         f0, f1, f2 = mlp.fcs
@@ -388,14 +375,7 @@ class _F16Work(_M3Work):
         m2, m1 = _SPLITK_MIN_ROWS.get((K, 256), 2048), _SPLITK_MIN_ROWS.get((K, self.I), 1024)
         self.C2 = self.C1 = 0
         self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
-        # dW2 on qs_wgrad_rm (opt-in): 64 chunks of 512 rows at 32 768 rows
-        self.R2 = _wgrad_rm_chunks(K) if self.wgrad_rm else 0
-        if os.environ.get("QS_DEBUG_SHAPES"):
-            print(f"_F16Work: K={K} I={self.I} dW2 chunks={self.R2 or self.S2} ({'qs_wgrad_rm' if self.R2 else 'bmm'})",
-                  flush=True)
-        if self.R2:
-            self.S2 = self.R2
-        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 or self.R2 else None
+        self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
         self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 else None
 
     def repack(self):
@@ -407,26 +387,19 @@ class _F16Work(_M3Work):
         pk, w1, w2, I = super().pack_segment(fb)
         return pk, w1, w2, I | L.QS_PACK_F16
 
-    def _splitk_rm(self, dst, dy, x, part, S, rm=False):
+    def _splitk_rm(self, dst, dy, x, part, S):
         """dst = dyᵀ·x over K rows (dy [K][N], x [K][M], both row-major) as S row-chunk
-        GEMMs into the preallocated partials (S = 1: one GEMM straight into dst);
-        rm: S chunk partials of qs_wgrad_rm instead."""
+        GEMMs into the preallocated partials (S = 1: one GEMM straight into dst)."""
         K = dy.shape[0]
-        if rm:
-            L.check(L.load().qs_wgrad_rm(K, dy.shape[1], x.shape[1], L.ptr(dy), L.ptr(x), S, L.ptr(part), _stream()),
-                    "qs_wgrad_rm")
-            return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
         if S == 1:
             torch.mm(dy.t(), x, out=dst)
             return None
         torch.bmm(dy.view(S, K // S, -1).transpose(1, 2), x.view(S, K // S, -1), out=part)
         return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
 
-    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole, defer_w1=False):
+    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole):
         """qs_mlp3f_actor over the minibatch's agent rows (env-timesteps idx, D rows
-        each, straight from the rollout table), then the weight gradients.
-        defer_w1: dW1 is left to the caller — returns a function that launches it
-        on the current stream (after an event recorded behind the actor kernel)."""
+        each, straight from the rollout table), then the weight gradients."""
         f0, f1, f2 = self.mlp.fcs
         logstd = actor.logstd
         L.check(L.load().qs_mlp3f_actor(
@@ -439,24 +412,6 @@ class _F16Work(_M3Work):
         N, A = 256, self.A
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
-        if defer_w1:
-            cur = torch.cuda.current_stream()
-            ev = torch.cuda.Event()
-            ev.record(cur)   # the actor kernel's outputs
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
-            if w2 is not None:
-                tasks.append(w2)
-            elif whole is not None:
-                whole.append(f1.weight.grad)
-
-            def launch_w1():
-                torch.cuda.current_stream().wait_event(ev)
-                w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
-                if w1 is not None:
-                    tasks.append(w1)
-                elif whole is not None:
-                    whole.append(f0.weight.grad)
-            return launch_w1
         if self.w1_stream:
             # dW1's small GEMMs (a few dozen workgroups each) beside dW2's on a third
             # stream; joined before the caller's reductions
@@ -466,10 +421,10 @@ class _F16Work(_M3Work):
             self._s3.wait_stream(cur)
             with torch.cuda.stream(self._s3):
                 w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)   # dW1 = dZ1ᵀ·Xa
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)   # dW2 = dZ2ᵀ·H1
             cur.wait_stream(self._s3)
         else:
-            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2, self.R2 > 0)   # dW2 = dZ2ᵀ·H1
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)   # dW2 = dZ2ᵀ·H1
             w1 = self._splitk_rm(f0.weight.grad, self.dz1, self.xa, self.pw1, self.S1)    # dW1 = dZ1ᵀ·Xa
         for dst, t in ((f1.weight.grad, w2), (f0.weight.grad, w1)):
             if t is not None:
@@ -917,7 +872,6 @@ class MAPPOAgent:
         # one rank, fused actor: the critic's sums + Adam on the side stream too (its own
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
-        self.actor_first = kwargs.get('actor_first', False)
         # with the fused actor, the critic's step on qs_ppo_critic_tiles + qs_wgrad_t
         # (False: the qs_mlp3w kernels and hipBLASLt weight-gradient GEMMs)
         self.critic_tiles = kwargs.get('critic_tiles', True)
@@ -1147,31 +1101,19 @@ class MAPPOAgent:
                     tc.clear()
                     wc.clear()
 
-            def actor_all(exchange, defer_w1=False):
-                w1 = self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
-                                         self.clip_param, self.entropy_coef, self._kl, acc, ta, wa, defer_w1=defer_w1)
+            def actor_all(exchange):
+                self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
+                                    self.clip_param, self.entropy_coef, self._kl, acc, ta, wa)
                 if exchange:
                     _flush_sums(ta)
                     self._exchange_bucket(self._actor_bucket, world)
-                return w1
 
             if self.side_stream:
                 own = not multi and self.critic_adam_side
                 self._side.wait_stream(cur)
-                if self.actor_first and not (multi or own):
-                    # (opt-in) the actor chain captured first on the launch stream,
-                    # dW1 after dW2 on it, the critic beside it: graph replay keeps
-                    # the first branch of a fork on the parent's hardware queue.  It
-                    # read faster under rocprofv3's kernel trace and measured slower
-                    # in the bench
-                    launch_w1 = actor_all(False, defer_w1=True)
-                    with torch.cuda.stream(self._side):
-                        critic_all(False, False)
-                    launch_w1()
-                else:
-                    with torch.cuda.stream(self._side):
-                        critic_all(multi, own)
-                    actor_all(multi)
+                with torch.cuda.stream(self._side):
+                    critic_all(multi, own)
+                actor_all(multi)
                 cur.wait_stream(self._side)
                 if own:
                     for g in [logstd.grad] + wa:
