@@ -354,7 +354,9 @@ def test_load_reference_layout_checkpoint(tmp_path):
         for p, gi in zip(mod.parameters(), g):
             p.grad = gi.clone()
         opt.step()
-        fb.grad.copy_(torch.cat([gi.reshape(-1) for gi in g]))
+        fb.grad.zero_()
+        for q, gi in zip(fb.params, g):   # each parameter's .grad is its view of the flat gradient
+            q.grad.copy_(gi)
         fb.adam()
         for p, q in zip(mod.parameters(), fb.params):
             torch.testing.assert_close(q.detach(), p.detach(), rtol=1e-6, atol=1e-7)
