@@ -128,6 +128,74 @@ __device__ __forceinline__ double s_powi(double b, unsigned t) {
   return r;
 }
 
+// c0 / c1 += Σ over nq quads of A_b[j][κ]·B[κ][j] (κ = 16t + 4g + e): the A
+// rows of the wave's two hidden blocks from L2 (elements past I zero), eight
+// quads of loads in flight ahead of the MFMAs; the B row (an activation row)
+// from LDS.  Latency-bound otherwise: one L2 round trip per quad.
+constexpr int kSRing = 8;
+__device__ __forceinline__ void s_contract2(const float* wrow0, const float* wrow1, int I, const float* brow, int nq,
+                                            int g, f32x4& c0, f32x4& c1) {
+  float4 ra[kSRing], rb[kSRing];
+#pragma unroll
+  for (int t = 0; t < kSRing; ++t)
+    if (t < nq) {
+      ra[t] = s_ld4(wrow0, 16 * t + 4 * g, I);
+      rb[t] = s_ld4(wrow1, 16 * t + 4 * g, I);
+    }
+  for (int t0 = 0; t0 < nq; t0 += kSRing) {
+#pragma unroll
+    for (int u = 0; u < kSRing; ++u) {
+      const int t = t0 + u;
+      if (t < nq) {
+        const float4 a0 = ra[u], a1 = rb[u];
+        if (t + kSRing < nq) {
+          ra[u] = s_ld4(wrow0, 16 * (t + kSRing) + 4 * g, I);
+          rb[u] = s_ld4(wrow1, 16 * (t + kSRing) + 4 * g, I);
+        }
+        const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+        c0 = s_mfma(a0.x, bv.x, c0);
+        c1 = s_mfma(a1.x, bv.x, c1);
+        c0 = s_mfma(a0.y, bv.y, c0);
+        c1 = s_mfma(a1.y, bv.y, c1);
+        c0 = s_mfma(a0.z, bv.z, c0);
+        c1 = s_mfma(a1.z, bv.z, c1);
+        c0 = s_mfma(a0.w, bv.w, c0);
+        c1 = s_mfma(a1.w, bv.w, c1);
+      }
+    }
+  }
+}
+
+// c += Σ over nq quads of A[j][rows]·B[rows][j] with both operands transposed
+// rows in global memory (brow NULL: zeros), eight quads of loads ahead
+__device__ __forceinline__ void s_wgrad_acc(const float* arow, const float* brow, int nq, int g, f32x4& c) {
+  float4 ra[kSRing], rb[kSRing];
+  const float4 zero = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < kSRing; ++t)
+    if (t < nq) {
+      ra[t] = *reinterpret_cast<const float4*>(arow + 16 * t + 4 * g);
+      rb[t] = brow ? *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g) : zero;
+    }
+  for (int t0 = 0; t0 < nq; t0 += kSRing) {
+#pragma unroll
+    for (int u = 0; u < kSRing; ++u) {
+      const int t = t0 + u;
+      if (t < nq) {
+        const float4 av = ra[u], bv = rb[u];
+        if (t + kSRing < nq) {
+          ra[u] = *reinterpret_cast<const float4*>(arow + 16 * (t + kSRing) + 4 * g);
+          rb[u] = brow ? *reinterpret_cast<const float4*>(brow + 16 * (t + kSRing) + 4 * g) : zero;
+        }
+        c = s_mfma(av.x, bv.x, c);
+        c = s_mfma(av.y, bv.y, c);
+        c = s_mfma(av.z, bv.z, c);
+        c = s_mfma(av.w, bv.w, c);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- launch 1
 // One 16-row tile of one net: POL = the actor (policy head over A outputs),
 // otherwise the critic (value head).
@@ -147,15 +215,23 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   float* dz1T = POL ? W.dz1aT : W.dz1cT;
   // ---- the X tile: LDS rows (zero-padded) and the transposed copy the weight
   // gradients read (rows past K are zeros)
-  for (int e = tid; e < 16 * Ip; e += kSBlock) {
-    const int rr = e & 15, k = e >> 4, R = r0 + rr;
-    float v = 0.f;
-    if (R < K && k < I) {
-      const long long src = POL ? (P.idx[R / P.D] * P.D + R % P.D) : P.idx[R];
-      v = P.X[src * I + k];
+  {
+    // every load of the tile first (one gather latency), then the LDS / global writes
+    constexpr int kXU = (16 * kSMaxI + kSBlock - 1) / kSBlock;
+    float v[kXU];
+    const int rr = tid & 15, R = r0 + rr;
+    const long long src = R < K ? (POL ? (P.idx[R / P.D] * P.D + R % P.D) : P.idx[R]) * I : -1;
+#pragma unroll
+    for (int u = 0; u < kXU; ++u) {
+      const int k = (tid >> 4) + u * (kSBlock / 16);
+      v[u] = src >= 0 && k < I ? P.X[src + k] : 0.f;
     }
-    xs[rr * XS + k] = v;
-    if (k < I) xT[(size_t)k * KP + R] = v;
+#pragma unroll
+    for (int u = 0; u < kXU; ++u) {
+      const int k = (tid >> 4) + u * (kSBlock / 16);
+      if (k < Ip) xs[rr * XS + k] = v[u];
+      if (k < I) xT[(size_t)k * KP + R] = v[u];
+    }
   }
   __syncthreads();
   const int b0 = 2 * w;   // the wave's hidden blocks b0, b0 + 1
@@ -163,17 +239,8 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   {
     const float* w1 = N.p + N.w1;
-    for (int t = 0; t < Ip / 16; ++t) {
-      const float4 xb = *reinterpret_cast<const float4*>(xs + j * XS + 16 * t + 4 * g);
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        const float4 wa = s_ld4(w1 + (size_t)(16 * (b0 + bb) + j) * I, 16 * t + 4 * g, I);
-        z[bb] = s_mfma(wa.x, xb.x, z[bb]);
-        z[bb] = s_mfma(wa.y, xb.y, z[bb]);
-        z[bb] = s_mfma(wa.z, xb.z, z[bb]);
-        z[bb] = s_mfma(wa.w, xb.w, z[bb]);
-      }
-    }
+    s_contract2(w1 + (size_t)(16 * b0 + j) * I, w1 + (size_t)(16 * b0 + 16 + j) * I, I, xs + j * XS, Ip / 16, g, z[0],
+                z[1]);
   }
   float h1[2][4];
 #pragma unroll
@@ -191,29 +258,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   const float* w2 = N.p + N.w2;
   auto contract = [&](const float* wrow0, const float* wrow1, const float* brow) {
     f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
-    float4 ra[4], rb[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      ra[t] = *reinterpret_cast<const float4*>(wrow0 + 16 * t + 4 * g);
-      rb[t] = *reinterpret_cast<const float4*>(wrow1 + 16 * t + 4 * g);
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const float4 a0 = ra[t & 3], a1 = rb[t & 3];
-      if (t + 4 < 16) {
-        ra[t & 3] = *reinterpret_cast<const float4*>(wrow0 + 16 * (t + 4) + 4 * g);
-        rb[t & 3] = *reinterpret_cast<const float4*>(wrow1 + 16 * (t + 4) + 4 * g);
-      }
-      const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
-      c0 = s_mfma(a0.x, bv.x, c0);
-      c1 = s_mfma(a1.x, bv.x, c1);
-      c0 = s_mfma(a0.y, bv.y, c0);
-      c1 = s_mfma(a1.y, bv.y, c1);
-      c0 = s_mfma(a0.z, bv.z, c0);
-      c1 = s_mfma(a1.z, bv.z, c1);
-      c0 = s_mfma(a0.w, bv.w, c0);
-      c1 = s_mfma(a1.w, bv.w, c1);
-    }
+    s_contract2(wrow0, wrow1, kSH, brow, kSH / 16, g, c0, c1);
     z[0] = c0;
     z[1] = c1;
   };
@@ -476,14 +521,7 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
         const float* brow = kcol < Kin ? xT + (size_t)kcol * KP : nullptr;
         // dW[16nb + 4g + r][16kb + j] = Σ_rows dZ[row][n]·X[row][k], rows in MFMA order
         f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int q = 0; q < KP / 16; ++q) {
-          const float4 av = *reinterpret_cast<const float4*>(arow + 16 * q + 4 * g);
-          const float4 bv = brow ? *reinterpret_cast<const float4*>(brow + 16 * q + 4 * g) : float4{0.f, 0.f, 0.f, 0.f};
-          c = s_mfma(av.x, bv.x, c);
-          c = s_mfma(av.y, bv.y, c);
-          c = s_mfma(av.z, bv.z, c);
-          c = s_mfma(av.w, bv.w, c);
-        }
+        s_wgrad_acc(arow, brow, KP / 16, g, c);
         if (kcol < Kin) {
           const int si = actor ? 0 : 1;
 #pragma unroll
@@ -558,14 +596,7 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
   const float* arow = AT + (size_t)(16 * nb + j) * KP + r0;
   const float* brow = m < M ? XT + (size_t)m * KP + r0 : nullptr;
   f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int q = 0; q < rows / 16; ++q) {
-    const float4 av = *reinterpret_cast<const float4*>(arow + 16 * q + 4 * g);
-    const float4 bv = brow ? *reinterpret_cast<const float4*>(brow + 16 * q + 4 * g) : float4{0.f, 0.f, 0.f, 0.f};
-    c = s_mfma(av.x, bv.x, c);
-    c = s_mfma(av.y, bv.y, c);
-    c = s_mfma(av.z, bv.z, c);
-    c = s_mfma(av.w, bv.w, c);
-  }
+  s_wgrad_acc(arow, brow, rows / 16, g, c);
   if (m < M)
 #pragma unroll
     for (int r = 0; r < 4; ++r) partial[((size_t)s * N + 16 * nb + 4 * g + r) * M + m] = c[r];

@@ -1,0 +1,126 @@
+"""Dev: device time per PPO minibatch of MAPPOAgent.update (graph replays, HIP
+events) for learner variants at the bench's shapes, in one process so the
+variants are compared on the same box:
+  C3   D=8,  O=27,  A=1, mini_batch_size 4096 (32 768 actor rows, 4 096 critic rows)
+  ref  D=8,  O=27,  A=1, mini_batch_size 32   (learn_mappo.py:199: 256 actor rows)
+  C4   D=5,  O=119, A=4, mini_batch_size 4096 (Spiral VEL)
+plus the critic-tile kernels alone at the C3 shape.
+  python scripts/learner_mb.py [C3|ref|C4|kernels ...]"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "marl-gym-pybullet-drones_amd"))
+from gym_pybullet_drones_amd import _lib as L  # noqa: E402
+from gym_pybullet_drones_amd.mappo import agent as agent_mod  # noqa: E402
+from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent  # noqa: E402
+from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer  # noqa: E402
+from gym_pybullet_drones_amd.utils.spaces import Box  # noqa: E402
+
+dev = "cuda"
+SHAPES = {"C3": (8, 27, 1, 4096, 16, 4096), "ref": (8, 27, 1, 32, 16, 256), "C4": (5, 119, 4, 4096, 16, 4096)}
+
+
+def per_minibatch_us(shape, reps=3, **variant):
+    D, O, A, mb, T, E = SHAPES[shape]
+    osp, asp = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O))), Box(-np.ones((D, A)), np.ones((D, A)))
+    torch.manual_seed(0)
+    agent = MAPPOAgent(osp, asp, hidden_dim=256, opt_epochs=1, mini_batch_size=mb, entropy_coef=0.005,
+                       target_kl=1e9, use_graphs=True, device=dev, **variant)
+    buf = MAPPOBuffer(osp, asp, T, E, include_global_state=True, device=dev)
+    buf.next_obs_slots.normal_()
+    buf.act.normal_()
+    buf.logp.normal_()
+    buf.ret_env.normal_()
+    buf.adv_env.normal_()
+    buf.t, buf.full = 0, True
+    agent.update(buf)   # capture + warm
+    torch.cuda.synchronize()
+    nmb = T * E // mb
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        agent.update(buf)
+    e1.record()
+    torch.cuda.synchronize()
+    path = ("small" if getattr(agent, "_sm_key", None) else
+            type(getattr(agent, "_ws_actor", None)).__name__ + "+" + type(getattr(agent, "_ws_critic", None)).__name__)
+    agent.release_graphs()
+    return e0.elapsed_time(e1) * 1e3 / (reps * nmb), path
+
+
+def timed(fn, reps=40):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(10):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps / 10 * 1e3
+
+
+def kernels():
+    """The critic-tile launch and its split-K weight gradients at the C3 shape."""
+    D, O, A, mb, T, E = SHAPES["C3"]
+    osp, asp = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O))), Box(-np.ones((D, A)), np.ones((D, A)))
+    agent = MAPPOAgent(osp, asp, hidden_dim=256, opt_epochs=1, mini_batch_size=mb, use_graphs=False, device=dev)
+    buf = MAPPOBuffer(osp, asp, T, E, include_global_state=True, device=dev)
+    buf.next_obs_slots.normal_()
+    buf.ret_env.normal_()
+    ct = agent_mod._CriticTiles(agent, mb, D)
+    idx = torch.randperm(T * E, device=dev)[:mb]
+    acc = torch.zeros(4, dtype=torch.float64, device=dev)
+    lib = L.load()
+    st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    fl = 2 * mb * (D * O * 256 + 2 * 256 * 256 + 256)
+    us = timed(lambda: L.check(lib.qs_ppo_critic_tiles(mb, D, L.ptr(buf.obs), L.ptr(idx), L.ptr(buf.ret_env),
+                                                       ctypes.byref(ct.net), L.ptr(acc), L.ptr(ct.work), st()), "t"))
+    print(f"qs_ppo_critic_tiles (4096 x 216)          {us:8.2f} us  {fl / us / 1e6:6.1f} TFLOP/s", flush=True)
+    for name, a, b, M, part in (("W1", ct.dz1T, ct.xT, ct.I, ct.pw1), ("W2", ct.dz2T, ct.h1T, 256, ct.pw2)):
+        us = timed(lambda: L.check(lib.qs_wgrad_t(ct.KcP, 256, M, L.ptr(a), L.ptr(b), ct.S, L.ptr(part), st()), "w"))
+        print(f"qs_wgrad_t critic {name} S={ct.S}                  {us:8.2f} us  "
+              f"{2 * mb * 256 * M / us / 1e6:6.1f} TFLOP/s", flush=True)
+
+
+def main():
+    which = sys.argv[1:] or ["kernels", "C3", "ref", "C4"]
+    if "kernels" in which:
+        kernels()
+    if "C3" in which:
+        for v in (dict(critic_tiles=True), dict(critic_tiles=False), dict(critic_tiles=True, side_stream=False),
+                  dict(critic_tiles=False, side_stream=False)):
+            us, path = per_minibatch_us("C3", **v)
+            print(f"C3  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "ref" in which:
+        for v in (dict(small=True), dict(small=False)):
+            us, path = per_minibatch_us("ref", reps=2, **v)
+            print(f"ref {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "C4" in which:
+        for a in (1, 4):
+            agent_mod._F16_MAX_A = a
+            us, path = per_minibatch_us("C4")
+            print(f"C4  fused_max_a={a:<43d} {us:8.1f} us/minibatch  [{path}]", flush=True)
+        agent_mod._F16_MAX_A = 1
+
+
+if __name__ == "__main__":
+    t0 = time.time()
+    main()
+    print(f"({time.time() - t0:.0f} s)")
