@@ -330,7 +330,8 @@ const char* qs_ppo_small_last_error(void);
  * partBa, partAc, partBc (per-tile partial rows [tile][256 + 256·A + A] =
  * Σ dZ2 | Σ dout·H2 | Σ dout, and [tile][256] = Σ dZ1), dlogstd, the loss
  * partials, the counters; off[16..19] = actor tiles, critic tiles, padded
- * actor rows, padded critic rows; off[20] = bytes.  Ia = 0: the critic-only
+ * actor rows, padded critic rows; off[20] = bytes; off[21..22] = the row
+ * strides of the actor's / critic's transposed buffers.  Ia = 0: the critic-only
  * layout of qs_ppo_critic_tiles. */
 int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off);
 /* The critic half of qs_ppo_small_step's first launch at any minibatch size:
@@ -343,10 +344,11 @@ int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A
 int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const double* ret,
                         const qs_mlp256* critic, double* acc, void* work, void* stream);
 /* Split-K weight gradient from transposed operands: partial[s][n][m] =
- * Σ_{rows r of chunk s} AT[n][r]·XT[m][r] (AT [N][KP], XT [M][KP], S chunks of
- * KP/S rows; N a multiple of 16, KP of 16·S).  nn.Linear's dW = dYᵀ·X. */
-int qs_wgrad_t(int64_t KP, int32_t N, int32_t M, const float* AT, const float* XT, int32_t S, float* partial,
-               void* stream);
+ * Σ_{rows r of chunk s} AT[n][r]·XT[m][r] (AT [N][ld], XT [M][ld], rows r < KP in
+ * S chunks of KP/S; N a multiple of 16, KP of 16·S, ld >= KP a multiple of 4).
+ * nn.Linear's dW = dYᵀ·X. */
+int qs_wgrad_t(int64_t KP, int64_t ld, int32_t N, int32_t M, const float* AT, const float* XT, int32_t S,
+               float* partial, void* stream);
 
 #ifdef __cplusplus
 }

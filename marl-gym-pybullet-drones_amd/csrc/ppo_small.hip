@@ -50,6 +50,7 @@ constexpr int kSMaxI = 256;            // widest input
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of the Adam kernel
 constexpr int kSVecWG = 4;             // Adam workgroups for the vector parameters
+constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
 
 __host__ __device__ constexpr int s_ip(int I) { return (I + 15) & ~15; }       // input padded to whole quads
 __host__ __device__ constexpr int s_xs(int I) { return ((I + 31) & ~31) + 4; } // LDS row stride of the X tile
@@ -74,6 +75,7 @@ struct SWork {   // workspace views (qs_ppo_small_work_bytes)
 
 struct SArgs {
   int mb, D, nA, nC, KaP, KcP;
+  int KaS, KcS;            // row strides of the transposed activations (KaP / KcP + kSPad)
   const float* X;          // the rollout's obs table [T·E·D][O] (critic rows: [T·E][D·O])
   const long long* idx;    // the minibatch's env-timesteps [mb]
   const float* act;        // [T·E·D][A]
@@ -206,7 +208,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const int I = N.I, XS = s_xs(I), Ip = s_ip(I);
   const int K = POL ? P.mb * P.D : P.mb;
-  const int KP = POL ? P.KaP : P.KcP;
+  const int KP = POL ? P.KaS : P.KcS;   // the transposed rows' stride
   const int r0 = tile * 16;
   const SWork& W = P.w;
   float* xT = POL ? W.xaT : W.xcT;
@@ -512,13 +514,13 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
       if (!actor || open_a) {
         const int nin = which == 1 ? s_ip(N.I) / 16 : 16;
         const int nb = u / nin, kb = u - nb * nin;
-        const int KP = actor ? P.KaP : P.KcP;
+        const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
         const float* dzT = actor ? (which == 1 ? P.w.dz1aT : P.w.dz2aT) : (which == 1 ? P.w.dz1cT : P.w.dz2cT);
         const float* xT = actor ? (which == 1 ? P.w.xaT : P.w.h1aT) : (which == 1 ? P.w.xcT : P.w.h1cT);
         const int Kin = which == 1 ? N.I : kSH;
         const int kcol = 16 * kb + j;
-        const float* arow = dzT + (size_t)(16 * nb + j) * KP;
-        const float* brow = kcol < Kin ? xT + (size_t)kcol * KP : nullptr;
+        const float* arow = dzT + (size_t)(16 * nb + j) * KS;
+        const float* brow = kcol < Kin ? xT + (size_t)kcol * KS : nullptr;
         // dW[16nb + 4g + r][16kb + j] = Σ_rows dZ[row][n]·X[row][k], rows in MFMA order
         f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
         s_wgrad_acc(arow, brow, KP / 16, g, c);
@@ -584,7 +586,7 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
 // rows past K zero), one wave per 16×16 output tile and chunk, the A / B
 // operands one float4 each per MFMA quad (rows 16q + 4g .. +3).  The chunk
 // partials are summed in chunk order by qs_mlp_sum_adam.
-__global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP, int S, const float* __restrict__ AT,
+__global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP, int ld, int S, const float* __restrict__ AT,
                                                             const float* __restrict__ XT, float* __restrict__ partial) {
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const int nm = (M + 15) / 16, tiles = (N / 16) * nm;
@@ -593,8 +595,8 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
   const int s = T % S, u = T / S, nb = u / nm, mb = u - nb * nm;
   const int rows = KP / S, r0 = s * rows;
   const int m = 16 * mb + j;
-  const float* arow = AT + (size_t)(16 * nb + j) * KP + r0;
-  const float* brow = m < M ? XT + (size_t)m * KP + r0 : nullptr;
+  const float* arow = AT + (size_t)(16 * nb + j) * ld + r0;
+  const float* brow = m < M ? XT + (size_t)m * ld + r0 : nullptr;
   f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
   s_wgrad_acc(arow, brow, rows / 16, g, c);
   if (m < M)
@@ -603,7 +605,7 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
 }
 
 struct SLayout {
-  int nA, nC, KaP, KcP;
+  int nA, nC, KaP, KcP, KaS, KcS;
   long long off[16];
   long long bytes;
 };
@@ -615,9 +617,13 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   L.nC = (int)((Kc + 15) / 16);
   L.KaP = 16 * L.nA;
   L.KcP = 16 * L.nC;
+  // row strides off a power of two: rows 16 KB apart all mapped to one memory
+  // channel (the critic's weight gradients ran 10x slower at 4 096 rows)
+  L.KaS = L.KaP ? L.KaP + kSPad : 0;
+  L.KcS = L.KcP + kSPad;
   const long long sz[16] = {
-      4LL * Ia * L.KaP, 4LL * kSH * L.KaP, 4LL * kSH * L.KaP, 4LL * kSH * L.KaP,   // xaT h1aT dz2aT dz1aT
-      4LL * Ic * L.KcP, 4LL * kSH * L.KcP, 4LL * kSH * L.KcP, 4LL * kSH * L.KcP,   // xcT h1cT dz2cT dz1cT
+      4LL * Ia * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS,   // xaT h1aT dz2aT dz1aT
+      4LL * Ic * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS,   // xcT h1cT dz2cT dz1cT
       4LL * L.nA * (kSH + A * kSH + A), 4LL * L.nA * kSH,                           // partAa partBa
       4LL * L.nC * (2 * kSH + 1), 4LL * L.nC * kSH,                                 // partAc partBc
       4LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192};                   // dlogstd lossa lossc cnt
@@ -650,17 +656,20 @@ int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A
   off[18] = L.KaP;
   off[19] = L.KcP;
   off[20] = L.bytes;
+  off[21] = L.KaS;
+  off[22] = L.KcS;
   return QS_OK;
 }
 
-int qs_wgrad_t(int64_t KP, int32_t N, int32_t M, const float* AT, const float* XT, int32_t S, float* partial,
-               void* stream) {
-  if (KP <= 0 || N <= 0 || N % 16 || M <= 0 || M > 4096 || S <= 0 || KP % (16LL * S) || !AT || !XT || !partial ||
-      KP * (int64_t)(N > M ? N : M) >= (int64_t(1) << 31))
-    return sfail(QS_E_INVALID, "qs_wgrad_t: bad argument (N a multiple of 16, KP a multiple of 16·S)");
+int qs_wgrad_t(int64_t KP, int64_t ld, int32_t N, int32_t M, const float* AT, const float* XT, int32_t S,
+               float* partial, void* stream) {
+  if (KP <= 0 || N <= 0 || N % 16 || M <= 0 || M > 4096 || S <= 0 || KP % (16LL * S) || ld < KP || ld % 4 || !AT ||
+      !XT || !partial || ld * (int64_t)(N > M ? N : M) >= (int64_t(1) << 31))
+    return sfail(QS_E_INVALID, "qs_wgrad_t: bad argument (N a multiple of 16, KP a multiple of 16·S, ld >= KP "
+                               "a multiple of 4)");
   const long long waves = (long long)(N / 16) * ((M + 15) / 16) * S;
   hipLaunchKernelGGL(wgrad_t_kernel, dim3((unsigned)((waves + kSAW - 1) / kSAW)), dim3(64 * kSAW), 0,
-                     (hipStream_t)stream, (int)N, (int)M, (int)KP, (int)S, AT, XT, partial);
+                     (hipStream_t)stream, (int)N, (int)M, (int)KP, (int)ld, (int)S, AT, XT, partial);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_wgrad_t: ") + hipGetErrorString(e));
 }
@@ -691,6 +700,8 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   P.nC = L.nC;
   P.KaP = L.KaP;
   P.KcP = L.KcP;
+  P.KaS = L.KaS;
+  P.KcS = L.KcS;
   P.X = obs;
   P.idx = (const long long*)idx;
   P.act = act;
@@ -788,7 +799,8 @@ int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* 
   P.w.lossc = (double*)(wb + L.off[14]);
   P.w.cnt = (unsigned*)(wb + L.off[15]);
   P.nA = 0;   // critic tiles only
-  P.KaP = 0;
+  P.KaP = P.KaS = 0;
+  P.KcS = L.KcS;
   s_launch_fb(P, L.nC, (hipStream_t)stream);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_critic_tiles: ") + hipGetErrorString(e));

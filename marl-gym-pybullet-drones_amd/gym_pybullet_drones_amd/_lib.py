@@ -164,7 +164,7 @@ def load():
     L.qs_ppo_small_work_bytes.argtypes = [ctypes.c_int32] * 5
     L.qs_ppo_small_layout.argtypes = [ctypes.c_int32] * 5 + [vp]
     L.qs_ppo_critic_tiles.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp, vp, ctypes.POINTER(QsMlp256), vp, vp, vp]
-    L.qs_wgrad_t.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
+    L.qs_wgrad_t.argtypes = [i64, i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_ppo_small_step.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [f32, f32, f32, ctypes.c_int32, f32]
                                     + [ctypes.POINTER(QsMlp256)] * 2 + [vp] * 4)
     L.qs_rms_work_bytes.argtypes = [i64, ctypes.c_int32]

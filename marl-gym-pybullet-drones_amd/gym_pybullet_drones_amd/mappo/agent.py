@@ -397,9 +397,11 @@ class _F16Work(_M3Work):
         torch.bmm(dy.view(S, K // S, -1).transpose(1, 2), x.view(S, K // S, -1), out=part)
         return (S, part[0].numel(), part, dst, dst.numel(), None, 0, None)
 
-    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole):
+    def step(self, table, idx, D, actor, rollouts, clip, ent_coef, kl, acc, tasks, whole, after_actor=None):
         """qs_mlp3f_actor over the minibatch's agent rows (env-timesteps idx, D rows
-        each, straight from the rollout table), then the weight gradients."""
+        each, straight from the rollout table), then the weight gradients.
+        after_actor(): called right after the fused launch is issued (the caller
+        forks work onto another stream behind it)."""
         f0, f1, f2 = self.mlp.fcs
         logstd = actor.logstd
         L.check(L.load().qs_mlp3f_actor(
@@ -412,6 +414,8 @@ class _F16Work(_M3Work):
         N, A = 256, self.A
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
+        if after_actor is not None:
+            after_actor()
         if self.w1_stream:
             # dW1's small GEMMs (a few dozen workgroups each) beside dW2's on a third
             # stream; joined before the caller's reductions
@@ -474,14 +478,15 @@ class _CriticTiles:
         mlp = agent.ac.critic.v_net
         f0, f1, f2 = mlp.fcs
         self.mlp, self.mb, self.D, self.I = mlp, mb, D, f0.in_features
-        off = (ctypes.c_int64 * 21)()
+        off = (ctypes.c_int64 * 23)()
         L.check(lib.qs_ppo_small_layout(mb, D, 0, self.I, 1, off), "qs_ppo_small_layout")
-        self.nC, KcP = int(off[17]), int(off[19])
+        self.nC, KcP, ld = int(off[17]), int(off[19]), int(off[22])
         dev = agent.device
         self.work = torch.zeros(int(off[20]), dtype=torch.uint8, device=dev)
         view = lambda i, *shape: self.work[off[i]:off[i] + 4 * math.prod(shape)].view(torch.float32).view(*shape)
-        self.xT, self.h1T, self.dz2T, self.dz1T = (view(4, self.I, KcP), view(5, 256, KcP), view(6, 256, KcP),
-                                                   view(7, 256, KcP))
+        self.xT, self.h1T, self.dz2T, self.dz1T = (view(4, self.I, ld), view(5, 256, ld), view(6, 256, ld),
+                                                   view(7, 256, ld))
+        self.ld = ld
         self.part_a, self.part_b = view(10, self.nC, 513), view(11, self.nC, 256)
         self.S = next(d for d in (8, 4, 2, 1) if self.nC % d == 0)
         self.pw1 = torch.empty((self.S, 256, self.I), device=dev)
@@ -505,10 +510,10 @@ class _CriticTiles:
         f0, f1, f2 = self.mlp.fcs
         L.check(lib.qs_ppo_critic_tiles(self.mb, self.D, L.ptr(rollouts.obs), L.ptr(idx), L.ptr(rollouts.ret_env),
                                         ctypes.byref(self.net), L.ptr(acc), L.ptr(self.work), st), "qs_ppo_critic_tiles")
-        L.check(lib.qs_wgrad_t(self.KcP, 256, self.I, L.ptr(self.dz1T), L.ptr(self.xT), self.S, L.ptr(self.pw1), st),
-                "qs_wgrad_t")
-        L.check(lib.qs_wgrad_t(self.KcP, 256, 256, L.ptr(self.dz2T), L.ptr(self.h1T), self.S, L.ptr(self.pw2), st),
-                "qs_wgrad_t")
+        L.check(lib.qs_wgrad_t(self.KcP, self.ld, 256, self.I, L.ptr(self.dz1T), L.ptr(self.xT), self.S,
+                               L.ptr(self.pw1), st), "qs_wgrad_t")
+        L.check(lib.qs_wgrad_t(self.KcP, self.ld, 256, 256, L.ptr(self.dz2T), L.ptr(self.h1T), self.S,
+                               L.ptr(self.pw2), st), "qs_wgrad_t")
         tasks.append((self.nC, 513, self.part_a, f1.bias.grad, 256, f2.weight.grad, 256, f2.bias.grad))
         tasks.append((self.nC, 256, self.part_b, f0.bias.grad, 256, None, 0, None))
         tasks.append((self.S, self.pw1[0].numel(), self.pw1, f0.weight.grad, f0.weight.numel(), None, 0, None))
@@ -875,6 +880,8 @@ class MAPPOAgent:
         # with the fused actor, the critic's step on qs_ppo_critic_tiles + qs_wgrad_t
         # (False: the qs_mlp3w kernels and hipBLASLt weight-gradient GEMMs)
         self.critic_tiles = kwargs.get('critic_tiles', True)
+        # ... after the fused actor kernel, beside its weight gradients (False: beside the actor kernel)
+        self.critic_after_actor = kwargs.get('critic_after_actor', True)
         # minibatches of at most _SMALL_MAX_ROWS actor rows on qs_ppo_small_step (one
         # rank); False: always the split-K direct iteration
         self.small = kwargs.get('small', True)
@@ -1101,9 +1108,9 @@ class MAPPOAgent:
                     tc.clear()
                     wc.clear()
 
-            def actor_all(exchange):
+            def actor_all(exchange, after_actor=None):
                 self._ws_actor.step(rollouts.obs.reshape(T * E * D, O), idx, D, self.ac.actor, rollouts,
-                                    self.clip_param, self.entropy_coef, self._kl, acc, ta, wa)
+                                    self.clip_param, self.entropy_coef, self._kl, acc, ta, wa, after_actor=after_actor)
                 if exchange:
                     _flush_sums(ta)
                     self._exchange_bucket(self._actor_bucket, world)
@@ -1111,9 +1118,19 @@ class MAPPOAgent:
             if self.side_stream:
                 own = not multi and self.critic_adam_side
                 self._side.wait_stream(cur)
-                with torch.cuda.stream(self._side):
-                    critic_all(multi, own)
-                actor_all(multi)
+                if self.critic_after_actor and isinstance(self._ws_critic, _CriticTiles):
+                    # the fused actor holds every CU's whole register file: a critic
+                    # running beside it delays its workgroups.  The critic's tiles
+                    # follow it instead, beside the actor's weight-gradient GEMMs
+                    def fork():
+                        self._side.wait_stream(cur)
+                        with torch.cuda.stream(self._side):
+                            critic_all(multi, own)
+                    actor_all(multi, after_actor=fork)
+                else:
+                    with torch.cuda.stream(self._side):
+                        critic_all(multi, own)
+                    actor_all(multi)
                 cur.wait_stream(self._side)
                 if own:
                     for g in [logstd.grad] + wa:

@@ -94,7 +94,8 @@ def kernels():
                                                        ctypes.byref(ct.net), L.ptr(acc), L.ptr(ct.work), st()), "t"))
     print(f"qs_ppo_critic_tiles (4096 x 216)          {us:8.2f} us  {fl / us / 1e6:6.1f} TFLOP/s", flush=True)
     for name, a, b, M, part in (("W1", ct.dz1T, ct.xT, ct.I, ct.pw1), ("W2", ct.dz2T, ct.h1T, 256, ct.pw2)):
-        us = timed(lambda: L.check(lib.qs_wgrad_t(ct.KcP, 256, M, L.ptr(a), L.ptr(b), ct.S, L.ptr(part), st()), "w"))
+        us = timed(lambda: L.check(lib.qs_wgrad_t(ct.KcP, ct.ld, 256, M, L.ptr(a), L.ptr(b), ct.S, L.ptr(part), st()),
+                                   "w"))
         print(f"qs_wgrad_t critic {name} S={ct.S}                  {us:8.2f} us  "
               f"{2 * mb * 256 * M / us / 1e6:6.1f} TFLOP/s", flush=True)
 
@@ -104,8 +105,8 @@ def main():
     if "kernels" in which:
         kernels()
     if "C3" in which:
-        for v in (dict(critic_tiles=True), dict(critic_tiles=False), dict(critic_tiles=True, side_stream=False),
-                  dict(critic_tiles=False, side_stream=False)):
+        for v in (dict(critic_tiles=True), dict(critic_tiles=True, critic_after_actor=False), dict(critic_tiles=False),
+                  dict(critic_tiles=True, side_stream=False), dict(critic_tiles=False, side_stream=False)):
             us, path = per_minibatch_us("C3", **v)
             print(f"C3  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "ref" in which:

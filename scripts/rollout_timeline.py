@@ -9,7 +9,10 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 pat = sys.argv[2] if len(sys.argv) > 2 else "step_kernel"
 idx = [i for i, r in enumerate(rows) if pat in r["Kernel_Name"]]
-a, b = idx[len(idx) // 2], idx[len(idx) // 2 + 1]
+# consecutive launches inside one rollout: the pair with the median period (a
+# pair that straddles a PPO update is far longer)
+pairs = sorted(zip(idx[:-1], idx[1:]), key=lambda ab: int(rows[ab[1]]["Start_Timestamp"]) - int(rows[ab[0]]["Start_Timestamp"]))
+a, b = pairs[len(pairs) // 4]
 t0 = int(rows[a]["Start_Timestamp"])
 fam = collections.defaultdict(float)
 for r in rows[a:b]:
