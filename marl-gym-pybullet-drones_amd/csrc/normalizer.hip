@@ -13,10 +13,9 @@
 // 256 columns, takes its range's mean and sum of squared deviations in two
 // passes over rows it re-reads from L2 (float64, lanes of the same column
 // combined in lane order through LDS), and the last workgroup to arrive merges
-// the range partials in row-range order with the parallel-variance formula
-// (Chan et al.; the same merge normalization.py:42-60 applies to the running
-// statistics), then applies that update in place in normalization.py's
-// operation order.  Fixed orders throughout: a replay is bit-identical.  The
+// the range partials in row-range order (the global mean first, then the
+// parallel-variance sum Σ M2_b + n_b·(mean_b − mean)²), then applies
+// normalization.py:42-60's update in place in its operation order.  Fixed orders throughout: a replay is bit-identical.  The
 // normalisation is a second, elementwise launch (float64 arithmetic, float32
 // out).  HBM-bound: 4 B read per element for the moments (plus an L2 re-read),
 // 4 B read + 4 B written for the normalisation.
@@ -34,7 +33,7 @@ int nfail(int code, const std::string& m) { g_nerr = m; return code; }
 
 constexpr int kRmsBlock = 256;
 constexpr int kRmsRowsMin = 16;     // rows per workgroup at least
-constexpr int kRmsRangesMax = 512;  // row ranges at most (partials and the merge stay small)
+constexpr int kRmsRangesMax = 64;   // row ranges at most: the last workgroup's merge walks them per column
 
 struct RmsShape {
   long long R;
@@ -112,16 +111,23 @@ __global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, cons
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // the batch moments: the ranges merged in order (parallel variance)
   const double cnt = sums ? 0.0 : *count;   // (the multi-rank form has no statistics)
+  // mean = Σ n_b·mean_b / N, then M2 = Σ (M2_b + n_b·(mean_b − mean)²): the
+  // parallel-variance merge with the global mean known (no division per range;
+  // a sequential Chan merge of 512 ranges with an fp64 division each took
+  // ~600 µs in one workgroup), ranges in order
+  const double na = (double)s.R;
   for (int c = t; c < s.C; c += kRmsBlock) {
-    double na = n_b[0], ma = mean_b[c], qa = m2_b[c];
-    for (int b = 1; b < s.GR; ++b) {
-      const double nbb = n_b[b], mb = mean_b[(size_t)b * s.C + c], qb = m2_b[(size_t)b * s.C + c];
-      const double n = na + nbb, d = mb - ma;
-      ma = ma + d * nbb / n;
-      qa = qa + qb + d * d * na * nbb / n;
-      na = n;
+    double sm = 0.0;
+#pragma unroll 8
+    for (int b = 0; b < s.GR; ++b) sm += n_b[b] * mean_b[(size_t)b * s.C + c];
+    const double bm = sm / na;
+    double qa = 0.0;
+#pragma unroll 8
+    for (int b = 0; b < s.GR; ++b) {
+      const double d = mean_b[(size_t)b * s.C + c] - bm;
+      qa += m2_b[(size_t)b * s.C + c] + n_b[b] * (d * d);
     }
-    const double bm = ma, bv = qa / na;   // np.mean, np.var (ddof 0)
+    const double bv = qa / na;   // np.mean, np.var (ddof 0)
     if (sums) {   // several ranks: this rank's Σx and Σx² (merged across ranks by the caller)
       sums[c] = bm * na;
       sums[s.C + c] = qa + bm * bm * na;

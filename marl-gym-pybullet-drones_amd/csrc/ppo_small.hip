@@ -130,71 +130,111 @@ __device__ __forceinline__ double s_powi(double b, unsigned t) {
   return r;
 }
 
-// c0 / c1 += Σ over nq quads of A_b[j][κ]·B[κ][j] (κ = 16t + 4g + e): the A
-// rows of the wave's two hidden blocks from L2 (elements past I zero), eight
-// quads of loads in flight ahead of the MFMAs; the B row (an activation row)
-// from LDS.  Latency-bound otherwise: one L2 round trip per quad.
+// Branch-free operand loads: the index is clamped into the row and the value
+// selected, so every load is issued unconditionally (conditional loads made the
+// compiler wait for all outstanding loads before each use: one L2 round trip
+// per quad, 6x the MFMA time)
+__device__ __forceinline__ float4 s_ld4s(const float* row, int k0, int I) {   // scalar (any I)
+  float4 r;
+  r.x = row[min(k0, I - 1)];
+  r.y = row[min(k0 + 1, I - 1)];
+  r.z = row[min(k0 + 2, I - 1)];
+  r.w = row[min(k0 + 3, I - 1)];
+  if (k0 >= I) r.x = 0.f;
+  if (k0 + 1 >= I) r.y = 0.f;
+  if (k0 + 2 >= I) r.z = 0.f;
+  if (k0 + 3 >= I) r.w = 0.f;
+  return r;
+}
+
+// c0 / c1 += Σ over NQ quads of A_b[j][κ]·B[κ][j] (κ = 16t + 4g + e): the A
+// rows of the wave's two hidden blocks from L2 (VEC: whole float4s of a 256-wide
+// row; otherwise scalars, elements past I zero), kSRing quads of loads in
+// flight ahead of the MFMAs; the B row (an activation row) from LDS.  NQ is a
+// compile-time count: the loop unrolls fully and the load counter waits are
+// exact.
 constexpr int kSRing = 8;
-__device__ __forceinline__ void s_contract2(const float* wrow0, const float* wrow1, int I, const float* brow, int nq,
-                                            int g, f32x4& c0, f32x4& c1) {
-  float4 ra[kSRing], rb[kSRing];
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_contract2(const float* wrow0, const float* wrow1, int I, const float* brow, int g,
+                                            f32x4& c0, f32x4& c1) {
+  constexpr int R = NQ < kSRing ? NQ : kSRing;
+  auto ld = [&](const float* row, int t) {
+    if constexpr (VEC) return *reinterpret_cast<const float4*>(row + 16 * t + 4 * g);
+    else return s_ld4s(row, 16 * t + 4 * g, I);
+  };
+  float4 ra[R], rb[R];
 #pragma unroll
-  for (int t = 0; t < kSRing; ++t)
-    if (t < nq) {
-      ra[t] = s_ld4(wrow0, 16 * t + 4 * g, I);
-      rb[t] = s_ld4(wrow1, 16 * t + 4 * g, I);
-    }
-  for (int t0 = 0; t0 < nq; t0 += kSRing) {
+  for (int t = 0; t < R; ++t) {
+    ra[t] = ld(wrow0, t);
+    rb[t] = ld(wrow1, t);
+  }
 #pragma unroll
-    for (int u = 0; u < kSRing; ++u) {
-      const int t = t0 + u;
-      if (t < nq) {
-        const float4 a0 = ra[u], a1 = rb[u];
-        if (t + kSRing < nq) {
-          ra[u] = s_ld4(wrow0, 16 * (t + kSRing) + 4 * g, I);
-          rb[u] = s_ld4(wrow1, 16 * (t + kSRing) + 4 * g, I);
-        }
-        const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
-        c0 = s_mfma(a0.x, bv.x, c0);
-        c1 = s_mfma(a1.x, bv.x, c1);
-        c0 = s_mfma(a0.y, bv.y, c0);
-        c1 = s_mfma(a1.y, bv.y, c1);
-        c0 = s_mfma(a0.z, bv.z, c0);
-        c1 = s_mfma(a1.z, bv.z, c1);
-        c0 = s_mfma(a0.w, bv.w, c0);
-        c1 = s_mfma(a1.w, bv.w, c1);
-      }
+  for (int t = 0; t < NQ; ++t) {
+    const float4 a0 = ra[t % R], a1 = rb[t % R];
+    if (t + R < NQ) {
+      ra[t % R] = ld(wrow0, t + R);
+      rb[t % R] = ld(wrow1, t + R);
     }
+    const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+    __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the loads next to their use
+    c0 = s_mfma(a0.x, bv.x, c0);
+    c1 = s_mfma(a1.x, bv.x, c1);
+    c0 = s_mfma(a0.y, bv.y, c0);
+    c1 = s_mfma(a1.y, bv.y, c1);
+    c0 = s_mfma(a0.z, bv.z, c0);
+    c1 = s_mfma(a1.z, bv.z, c1);
+    c0 = s_mfma(a0.w, bv.w, c0);
+    c1 = s_mfma(a1.w, bv.w, c1);
   }
 }
 
-// c += Σ over nq quads of A[j][rows]·B[rows][j] with both operands transposed
-// rows in global memory (brow NULL: zeros), eight quads of loads ahead
+// layer 1 over nq = ⌈I/16⌉ quads (1..16): the compile-time count by dispatch
+__device__ __forceinline__ void s_contract_in(const float* wrow0, const float* wrow1, int I, const float* brow, int nq,
+                                              int g, f32x4& c0, f32x4& c1) {
+  switch (nq) {
+#define S_CASE(n) case n: s_contract2<n, false>(wrow0, wrow1, I, brow, g, c0, c1); break;
+    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
+    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
+    default: s_contract2<16, false>(wrow0, wrow1, I, brow, g, c0, c1); break;
+#undef S_CASE
+  }
+}
+
+// c += Σ over NQ quads of A[j][rows]·B[rows][j], both operands transposed rows
+// in global memory, kSRing quads of loads ahead; compile-time NQ
+template <int NQ>
+__device__ __forceinline__ void s_wgrad_acc_n(const float* arow, const float* brow, int g, f32x4& c) {
+  constexpr int R = NQ < kSRing ? NQ : kSRing;
+  float4 ra[R], rb[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    ra[t] = *reinterpret_cast<const float4*>(arow + 16 * t + 4 * g);
+    rb[t] = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+  }
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const float4 av = ra[t % R], bv = rb[t % R];
+    if (t + R < NQ) {
+      ra[t % R] = *reinterpret_cast<const float4*>(arow + 16 * (t + R) + 4 * g);
+      rb[t % R] = *reinterpret_cast<const float4*>(brow + 16 * (t + R) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
+    c = s_mfma(av.x, bv.x, c);
+    c = s_mfma(av.y, bv.y, c);
+    c = s_mfma(av.z, bv.z, c);
+    c = s_mfma(av.w, bv.w, c);
+  }
+}
+// any nq: whole blocks of 16 quads, then the remainder by dispatch
 __device__ __forceinline__ void s_wgrad_acc(const float* arow, const float* brow, int nq, int g, f32x4& c) {
-  float4 ra[kSRing], rb[kSRing];
-  const float4 zero = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < kSRing; ++t)
-    if (t < nq) {
-      ra[t] = *reinterpret_cast<const float4*>(arow + 16 * t + 4 * g);
-      rb[t] = brow ? *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g) : zero;
-    }
-  for (int t0 = 0; t0 < nq; t0 += kSRing) {
-#pragma unroll
-    for (int u = 0; u < kSRing; ++u) {
-      const int t = t0 + u;
-      if (t < nq) {
-        const float4 av = ra[u], bv = rb[u];
-        if (t + kSRing < nq) {
-          ra[u] = *reinterpret_cast<const float4*>(arow + 16 * (t + kSRing) + 4 * g);
-          rb[u] = brow ? *reinterpret_cast<const float4*>(brow + 16 * (t + kSRing) + 4 * g) : zero;
-        }
-        c = s_mfma(av.x, bv.x, c);
-        c = s_mfma(av.y, bv.y, c);
-        c = s_mfma(av.z, bv.z, c);
-        c = s_mfma(av.w, bv.w, c);
-      }
-    }
+  int t = 0;
+  for (; t + 16 <= nq; t += 16) s_wgrad_acc_n<16>(arow + 16 * t, brow + 16 * t, g, c);
+  switch (nq - t) {
+#define S_CASE(n) case n: s_wgrad_acc_n<n>(arow + 16 * t, brow + 16 * t, g, c); break;
+    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
+    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
+#undef S_CASE
+    default: break;
   }
 }
 
@@ -241,8 +281,8 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   {
     const float* w1 = N.p + N.w1;
-    s_contract2(w1 + (size_t)(16 * b0 + j) * I, w1 + (size_t)(16 * b0 + 16 + j) * I, I, xs + j * XS, Ip / 16, g, z[0],
-                z[1]);
+    s_contract_in(w1 + (size_t)(16 * b0 + j) * I, w1 + (size_t)(16 * b0 + 16 + j) * I, I, xs + j * XS, Ip / 16, g,
+                  z[0], z[1]);
   }
   float h1[2][4];
 #pragma unroll
@@ -260,7 +300,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   const float* w2 = N.p + N.w2;
   auto contract = [&](const float* wrow0, const float* wrow1, const float* brow) {
     f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
-    s_contract2(wrow0, wrow1, kSH, brow, kSH / 16, g, c0, c1);
+    s_contract2<kSH / 16, true>(wrow0, wrow1, kSH, brow, g, c0, c1);
     z[0] = c0;
     z[1] = c1;
   };
@@ -520,7 +560,7 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
         const int Kin = which == 1 ? N.I : kSH;
         const int kcol = 16 * kb + j;
         const float* arow = dzT + (size_t)(16 * nb + j) * KS;
-        const float* brow = kcol < Kin ? xT + (size_t)kcol * KS : nullptr;
+        const float* brow = xT + (size_t)min(kcol, Kin - 1) * KS;   // (columns past Kin are not stored)
         // dW[16nb + 4g + r][16kb + j] = Σ_rows dZ[row][n]·X[row][k], rows in MFMA order
         f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
         s_wgrad_acc(arow, brow, KP / 16, g, c);
@@ -596,7 +636,7 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
   const int rows = KP / S, r0 = s * rows;
   const int m = 16 * mb + j;
   const float* arow = AT + (size_t)(16 * nb + j) * ld + r0;
-  const float* brow = m < M ? XT + (size_t)m * ld + r0 : nullptr;
+  const float* brow = XT + (size_t)min(m, M - 1) * ld + r0;   // (columns past M are not stored)
   f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
   s_wgrad_acc(arow, brow, rows / 16, g, c);
   if (m < M)

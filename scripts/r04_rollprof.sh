@@ -11,4 +11,7 @@ rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/prof_${TAG}.log; exi
 f=$(find gpurun_out/prof_${TAG} -name "*kernel_trace.csv" | head -1)
 python3 scripts/rollout_timeline.py "$f" "$PAT" > gpurun_out/${TAG}_timeline.txt
 tail -16 gpurun_out/${TAG}_timeline.txt
+# the headline C3 trainer leg's rollout step (always in the bench's MAPPO legs)
+python3 scripts/rollout_timeline.py "$f" "step_kernel<float, 0, 4, 30, 1, 0>" > gpurun_out/${TAG}_timeline_c3.txt
+tail -14 gpurun_out/${TAG}_timeline_c3.txt
 rm -rf gpurun_out/prof_${TAG}
