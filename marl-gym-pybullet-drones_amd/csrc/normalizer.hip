@@ -9,16 +9,16 @@
 // float64 column reductions (a Welford reduce_kernel of ~200 µs and a mean of
 // ~90 µs at C4's 8 192 × 135) were most of a C4 rollout step.
 //
-// Here the moments are one launch: each workgroup owns a row range × up to
-// 256 columns, takes its range's mean and sum of squared deviations in two
-// passes over rows it re-reads from L2 (float64, lanes of the same column
-// combined in lane order through LDS), and the last workgroup to arrive merges
-// the range partials in row-range order (the global mean first, then the
-// parallel-variance sum Σ M2_b + n_b·(mean_b − mean)²), then applies
-// normalization.py:42-60's update in place in its operation order.  Fixed orders throughout: a replay is bit-identical.  The
-// normalisation is a second, elementwise launch (float64 arithmetic, float32
-// out).  HBM-bound: 4 B read per element for the moments (plus an L2 re-read),
-// 4 B read + 4 B written for the normalisation.
+// Here the moments are two launches: one workgroup per 16-row tile reads its
+// contiguous span once into LDS and forms every column's tile mean and sum of
+// squared deviations (two passes from LDS, float64); then the tiles are merged
+// per column by 64 threads and a fixed LDS tree (the batch mean first, then
+// the parallel-variance sum Σ M2_t + n_t·(mean_t − mean)²) and
+// normalization.py:42-60's update applied in place in its operation order.
+// Fixed orders throughout: a replay is bit-identical.  The normalisation is a
+// third, elementwise launch (float64 arithmetic, float32 out).  HBM-bound: 4 B
+// read per element for the moments, 4 B read + 4 B written for the
+// normalisation.
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -32,136 +32,144 @@ thread_local std::string g_nerr;
 int nfail(int code, const std::string& m) { g_nerr = m; return code; }
 
 constexpr int kRmsBlock = 256;
-constexpr int kRmsRowsMin = 16;     // rows per workgroup at least
-constexpr int kRmsRangesMax = 64;   // row ranges at most: the last workgroup's merge walks them per column
+constexpr int kRmsRows = 16;        // rows per tile (one workgroup each)
+constexpr int kRmsMergeCols = 4;    // columns per merge workgroup (64 threads each)
 
 struct RmsShape {
   long long R;
-  int C, GR, GC;   // row ranges, column blocks of <= 256 columns
+  int C, GR;   // tiles of kRmsRows rows
 };
 
 __host__ __device__ inline RmsShape rms_shape(long long R, int C) {
   RmsShape s;
   s.R = R;
   s.C = C;
-  long long gr = (R + kRmsRowsMin - 1) / kRmsRowsMin;
-  s.GR = (int)(gr < kRmsRangesMax ? gr : kRmsRangesMax);
-  s.GC = (C + kRmsBlock - 1) / kRmsBlock;
+  s.GR = (int)((R + kRmsRows - 1) / kRmsRows);
   return s;
 }
 
-// work: [counter (64 B)] [n_b: GR doubles] [mean_b: GR·C] [m2_b: GR·C]
-inline long long rms_work_bytes(const RmsShape& s) { return 64 + 8LL * s.GR * (1 + 2LL * s.C); }
+// work: [counter (64 B)] [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(16, R − 16t) rows)
+inline long long rms_work_bytes(const RmsShape& s) { return 64 + 16LL * s.GR * s.C; }
 
-__global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, const float* __restrict__ x,
-                                                                double* __restrict__ mean, double* __restrict__ var,
-                                                                double* __restrict__ count, double* __restrict__ sums,
-                                                                unsigned* __restrict__ counter) {
-  __shared__ double lds[kRmsBlock];
-  __shared__ bool last;
-  const int t = threadIdx.x;
-  const int rb = blockIdx.x, cb = blockIdx.y;
-  const int c0 = cb * kRmsBlock;
-  const int CW = min(kRmsBlock, s.C - c0);   // this block's columns
-  const int P = kRmsBlock / CW;              // row lanes per column
-  const int lane = t / CW, col = c0 + t % CW;
-  const bool act = lane < P;
-  const long long r0 = s.R * rb / s.GR, r1 = s.R * (rb + 1) / s.GR;
-  const double nb = (double)(r1 - r0);
-  double* n_b = reinterpret_cast<double*>(reinterpret_cast<char*>(counter) + 64);
-  double* mean_b = n_b + s.GR;
+// Launch 1: one workgroup per 16-row tile; the tile's rows are one contiguous
+// span of x, read once (coalesced) into LDS, then every column's mean and sum
+// of squared deviations over the tile's rows (two passes from LDS, float64).
+__global__ void __launch_bounds__(kRmsBlock) rms_tile_kernel(RmsShape s, const float* __restrict__ x,
+                                                             unsigned* __restrict__ work) {
+  extern __shared__ float tile[];   // [rows][C]
+  const int t = threadIdx.x, b = blockIdx.x;
+  const long long r0 = (long long)b * kRmsRows;
+  const int nr = (int)min((long long)kRmsRows, s.R - r0);
+  const float* src = x + r0 * s.C;
+  const int n = nr * s.C;
+  for (int i = t; i < n; i += kRmsBlock) tile[i] = src[i];
+  __syncthreads();
+  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
   double* m2_b = mean_b + (size_t)s.GR * s.C;
-
-  // pass 1: the range's column sums (lanes in order)
-  double a = 0.0;
-  if (act)
-    for (long long r = r0 + lane; r < r1; r += P) a += (double)x[(size_t)r * s.C + col];
-  lds[t] = a;
-  __syncthreads();
-  double m = 0.0;
-  if (act) {
-    double sum = 0.0;
-    for (int p = 0; p < P; ++p) sum += lds[p * CW + t % CW];
-    m = sum / nb;
-  }
-  __syncthreads();
-  // pass 2: Σ (x − m)² of the range (the rows are L2-resident from pass 1)
-  double q = 0.0;
-  if (act)
-    for (long long r = r0 + lane; r < r1; r += P) {
-      const double d = (double)x[(size_t)r * s.C + col] - m;
+  for (int c = t; c < s.C; c += kRmsBlock) {
+    double a = 0.0;
+    for (int r = 0; r < nr; ++r) a += (double)tile[r * s.C + c];
+    const double m = a / (double)nr;
+    double q = 0.0;
+    for (int r = 0; r < nr; ++r) {
+      const double d = (double)tile[r * s.C + c] - m;
       q += d * d;
     }
-  lds[t] = q;
-  __syncthreads();
-  if (t < CW) {
-    double m2 = 0.0;
-    for (int p = 0; p < P; ++p) m2 += lds[p * CW + t];
-    mean_b[(size_t)rb * s.C + col] = m;
-    m2_b[(size_t)rb * s.C + col] = m2;
-    if (cb == 0 && t == 0) n_b[rb] = nb;
+    mean_b[(size_t)b * s.C + c] = m;
+    m2_b[(size_t)b * s.C + c] = q;
   }
+}
+
+// Launch 2: kRmsMergeCols columns per workgroup, 64 threads per column, each
+// thread over the tiles t ≡ lane (mod 64) in order, the lanes combined by a
+// fixed LDS tree: the batch mean Σ n_t·mean_t / R first, then M2 = Σ (M2_t +
+// n_t·(mean_t − mean)²) (the parallel-variance merge with the mean known), then
+// normalization.py:42-60's update of the running statistics in its operation
+// order.  Every workgroup reads the running count before arriving; the last to
+// arrive writes the new count.
+__device__ __forceinline__ double rms_lane_sum(double v, double* red, int col, int lane) {
+  red[col * 64 + lane] = v;
   __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    last = atomicAdd(counter, 1u) == gridDim.x * gridDim.y - 1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    if (lane < o) red[col * 64 + lane] += red[col * 64 + lane + o];
+    __syncthreads();
   }
+  const double r = red[col * 64];
   __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // the batch moments: the ranges merged in order (parallel variance)
+  return r;
+}
+
+__global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double* __restrict__ mean,
+                                                              double* __restrict__ var, double* __restrict__ count,
+                                                              double* __restrict__ sums, unsigned* __restrict__ work) {
+  __shared__ double red[kRmsMergeCols * 64];
+  __shared__ bool last;
+  const int t = threadIdx.x, col = t >> 6, lane = t & 63;
+  const int c = blockIdx.x * kRmsMergeCols + col;
+  const bool cv = c < s.C;
+  const double* mean_b = reinterpret_cast<const double*>(reinterpret_cast<const char*>(work) + 64);
+  const double* m2_b = mean_b + (size_t)s.GR * s.C;
   const double cnt = sums ? 0.0 : *count;   // (the multi-rank form has no statistics)
-  // mean = Σ n_b·mean_b / N, then M2 = Σ (M2_b + n_b·(mean_b − mean)²): the
-  // parallel-variance merge with the global mean known (no division per range;
-  // a sequential Chan merge of 512 ranges with an fp64 division each took
-  // ~600 µs in one workgroup), ranges in order
+  auto nrows = [&](int tt) { return (double)min((long long)kRmsRows, s.R - (long long)tt * kRmsRows); };
+  double a = 0.0;
+  if (cv)
+    for (int tt = lane; tt < s.GR; tt += 64) a += nrows(tt) * mean_b[(size_t)tt * s.C + c];
   const double na = (double)s.R;
-  for (int c = t; c < s.C; c += kRmsBlock) {
-    double sm = 0.0;
-#pragma unroll 8
-    for (int b = 0; b < s.GR; ++b) sm += n_b[b] * mean_b[(size_t)b * s.C + c];
-    const double bm = sm / na;
-    double qa = 0.0;
-#pragma unroll 8
-    for (int b = 0; b < s.GR; ++b) {
-      const double d = mean_b[(size_t)b * s.C + c] - bm;
-      qa += m2_b[(size_t)b * s.C + c] + n_b[b] * (d * d);
+  const double bm = rms_lane_sum(a, red, col, lane) / na;
+  double q = 0.0;
+  if (cv)
+    for (int tt = lane; tt < s.GR; tt += 64) {
+      const double d = mean_b[(size_t)tt * s.C + c] - bm;
+      q += m2_b[(size_t)tt * s.C + c] + nrows(tt) * (d * d);
     }
+  const double qa = rms_lane_sum(q, red, col, lane);
+  if (cv && lane == 0) {
     const double bv = qa / na;   // np.mean, np.var (ddof 0)
     if (sums) {   // several ranks: this rank's Σx and Σx² (merged across ranks by the caller)
       sums[c] = bm * na;
       sums[s.C + c] = qa + bm * bm * na;
-      continue;
+    } else {
+      // normalization.py:42-60, in its operation order
+      const double delta = bm - mean[c];
+      const double tot = cnt + na;
+      const double new_mean = mean[c] + delta * na / tot;
+      const double m_a = var[c] * cnt;
+      const double m_b = bv * na;
+      const double M2 = m_a + m_b + delta * delta * cnt * na / (cnt + na);
+      var[c] = M2 / (cnt + na);
+      mean[c] = new_mean;
     }
-    // normalization.py:42-60, in its operation order
-    const double delta = bm - mean[c];
-    const double tot = cnt + na;
-    const double new_mean = mean[c] + delta * na / tot;
-    const double m_a = var[c] * cnt;
-    const double m_b = bv * na;
-    const double M2 = m_a + m_b + delta * delta * cnt * na / (cnt + na);
-    var[c] = M2 / (cnt + na);
-    mean[c] = new_mean;
   }
-  __syncthreads();   // every column read the old count
+  __syncthreads();
   if (t == 0) {
-    if (sums) sums[2 * s.C] = (double)s.R;
-    else *count = (double)s.R + cnt;
-    *counter = 0u;
+    __threadfence();
+    last = atomicAdd(work, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && t == 0) {
+    if (sums) sums[2 * s.C] = na;
+    else *count = na + cnt;
+    *work = 0u;
   }
 }
 
 // out = clip((x − mean) / sqrt(var + eps), −clip, clip) in float64, stored as
 // float32 (MeanStdNormalizer.__call__, normalization.py:110-113); NaN passes
 // through like torch.clamp
-__global__ void rms_normalize_kernel(long long n, int C, const float* __restrict__ x, const double* __restrict__ mean,
-                                     const double* __restrict__ var, double eps, double clip, float* __restrict__ out) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int c = (int)(i % C);
-    double y = ((double)x[i] - mean[c]) / sqrt(var[c] + eps);
-    y = y < -clip ? -clip : (y > clip ? clip : y);
-    out[i] = (float)y;
+__global__ void __launch_bounds__(kRmsBlock) rms_normalize_kernel(long long R, int C, const float* __restrict__ x,
+                                                                   const double* __restrict__ mean,
+                                                                   const double* __restrict__ var, double eps,
+                                                                   double clip, float* __restrict__ out) {
+  // one row per workgroup step (no per-element modulo): threads over its columns
+  for (long long r = blockIdx.x; r < R; r += gridDim.x) {
+    const float* xr = x + r * C;
+    float* orow = out + r * C;
+    for (int c = threadIdx.x; c < C; c += kRmsBlock) {
+      double y = ((double)xr[c] - mean[c]) / sqrt(var[c] + eps);
+      y = y < -clip ? -clip : (y > clip ? clip : y);
+      orow[c] = (float)y;
+    }
   }
 }
 }  // namespace
@@ -179,10 +187,14 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
                   void* work, void* stream) {
   if (R <= 0 || C <= 0 || !x || !work || (!sums && (!mean || !var || !count)))
     return nfail(QS_E_INVALID, "qs_rms_update: bad argument");
-  if (R > (1LL << 40) || (long long)R * C > (1LL << 46)) return nfail(QS_E_INVALID, "qs_rms_update: batch too large");
+  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || (long long)C * kRmsRows * 4 > 64 * 1024)
+    return nfail(QS_E_INVALID, "qs_rms_update: batch too large (at most 1 024 columns)");
   const RmsShape s = rms_shape(R, C);
-  hipLaunchKernelGGL(rms_moments_kernel, dim3((unsigned)s.GR, (unsigned)s.GC), dim3(kRmsBlock), 0,
-                     (hipStream_t)stream, s, x, mean, var, count, sums, (unsigned*)work);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR), dim3(kRmsBlock), (size_t)C * kRmsRows * 4, st, s, x,
+                     (unsigned*)work);
+  hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)((C + kRmsMergeCols - 1) / kRmsMergeCols)), dim3(kRmsBlock), 0,
+                     st, s, mean, var, count, sums, (unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_update: ") + hipGetErrorString(e));
 }
@@ -190,11 +202,9 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
 int qs_rms_normalize(int64_t R, int32_t C, const float* x, const double* mean, const double* var, double eps,
                      double clip, float* out, void* stream) {
   if (R <= 0 || C <= 0 || !x || !mean || !var || !out) return nfail(QS_E_INVALID, "qs_rms_normalize: bad argument");
-  const long long n = (long long)R * C;
-  const int block = 256;
-  const long long grid = std::min<long long>((n + block - 1) / block, 4096);
-  hipLaunchKernelGGL(rms_normalize_kernel, dim3((unsigned)grid), dim3(block), 0, (hipStream_t)stream, n, (int)C, x,
-                     mean, var, eps, clip, out);
+  const long long grid = std::min<long long>(R, 8192);
+  hipLaunchKernelGGL(rms_normalize_kernel, dim3((unsigned)grid), dim3(kRmsBlock), 0, (hipStream_t)stream, (long long)R,
+                     (int)C, x, mean, var, eps, clip, out);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_normalize: ") + hipGetErrorString(e));
 }

@@ -51,6 +51,11 @@ constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of the Adam kernel
 constexpr int kSVecWG = 4;             // Adam workgroups for the vector parameters
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
+// Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
+// forward/backward tile uses ~53 KB and would otherwise be packed up to three
+// to a CU while other CUs idle (the grids are one workgroup per CU or fewer);
+// the weight-gradient workgroups two to a CU.
+constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024;
 
 __host__ __device__ constexpr int s_ip(int I) { return (I + 15) & ~15; }       // input padded to whole quads
 __host__ __device__ constexpr int s_xs(int I) { return ((I + 31) & ~31) + 4; } // LDS row stride of the X tile
@@ -96,17 +101,6 @@ __device__ __forceinline__ float s_tanh(float x) {   // learner.hip's m3_tanh
 }
 __device__ __forceinline__ f32x4 s_mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-// elements k0 .. k0+3 of a row of I floats (zero past I); one float4 when the
-// row is 16-byte aligned and whole
-__device__ __forceinline__ float4 s_ld4(const float* row, int k0, int I) {
-  if ((I & 3) == 0) return k0 < I ? *reinterpret_cast<const float4*>(row + k0) : float4{0.f, 0.f, 0.f, 0.f};
-  float4 r;
-  r.x = k0 < I ? row[k0] : 0.f;
-  r.y = k0 + 1 < I ? row[k0 + 1] : 0.f;
-  r.z = k0 + 2 < I ? row[k0 + 2] : 0.f;
-  r.w = k0 + 3 < I ? row[k0 + 3] : 0.f;
-  return r;
 }
 template <int CTRL>
 __device__ __forceinline__ float s_dpp(float v) {
@@ -707,8 +701,14 @@ int qs_wgrad_t(int64_t KP, int64_t ld, int32_t N, int32_t M, const float* AT, co
       !XT || !partial || ld * (int64_t)(N > M ? N : M) >= (int64_t(1) << 31))
     return sfail(QS_E_INVALID, "qs_wgrad_t: bad argument (N a multiple of 16, KP a multiple of 16·S, ld >= KP "
                                "a multiple of 4)");
+  static const bool attr = (hipFuncSetAttribute((const void*)wgrad_t_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
+                            hipFuncSetAttribute((const void*)ppo_small_adam_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
+                            true);
+  (void)attr;
   const long long waves = (long long)(N / 16) * ((M + 15) / 16) * S;
-  hipLaunchKernelGGL(wgrad_t_kernel, dim3((unsigned)((waves + kSAW - 1) / kSAW)), dim3(64 * kSAW), 0,
+  hipLaunchKernelGGL(wgrad_t_kernel, dim3((unsigned)((waves + kSAW - 1) / kSAW)), dim3(64 * kSAW), kSReserveW,
                      (hipStream_t)stream, (int)N, (int)M, (int)KP, (int)ld, (int)S, AT, XT, partial);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_wgrad_t: ") + hipGetErrorString(e));
@@ -791,10 +791,10 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
 
 static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
   switch (P.a.A) {
-    case 1: hipLaunchKernelGGL(ppo_small_fb_kernel<1>, dim3(grid), dim3(kSBlock), 0, st, P); break;
-    case 2: hipLaunchKernelGGL(ppo_small_fb_kernel<2>, dim3(grid), dim3(kSBlock), 0, st, P); break;
-    case 3: hipLaunchKernelGGL(ppo_small_fb_kernel<3>, dim3(grid), dim3(kSBlock), 0, st, P); break;
-    default: hipLaunchKernelGGL(ppo_small_fb_kernel<4>, dim3(grid), dim3(kSBlock), 0, st, P); break;
+    case 1: hipLaunchKernelGGL(ppo_small_fb_kernel<1>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
+    case 2: hipLaunchKernelGGL(ppo_small_fb_kernel<2>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
+    case 3: hipLaunchKernelGGL(ppo_small_fb_kernel<3>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
+    default: hipLaunchKernelGGL(ppo_small_fb_kernel<4>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
   }
 }
 
@@ -813,9 +813,13 @@ int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* id
     return sfail(QS_E_INVALID, "qs_ppo_small_step: minibatch above QS_PPO_SMALL_MAX_ROWS actor rows");
   hipStream_t st = (hipStream_t)stream;
   s_launch_fb(P, L.nA + L.nC, st);
+  static const bool attr = (hipFuncSetAttribute((const void*)ppo_small_adam_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
+                            true);
+  (void)attr;
   const int nTiles = 16 * (s_ip(actor->in) / 16) + 256 + 16 * (s_ip(critic->in) / 16) + 256;
   const int grid = (nTiles + kSAW - 1) / kSAW + kSVecWG;
-  hipLaunchKernelGGL(ppo_small_adam_kernel, dim3(grid), dim3(64 * kSAW), 0, st, P, nTiles);
+  hipLaunchKernelGGL(ppo_small_adam_kernel, dim3(grid), dim3(64 * kSAW), kSReserveW, st, P, nTiles);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_small_step: ") + hipGetErrorString(e));
 }
