@@ -76,9 +76,11 @@ def timed(fn, reps=40):
     return e0.elapsed_time(e1) / reps / 10 * 1e3
 
 
-def kernels():
-    """The critic-tile launch and its split-K weight gradients at the C3 shape."""
-    D, O, A, mb, T, E = SHAPES["C3"]
+def kernels(mb=None):
+    """The critic-tile launch and its split-K weight gradients at the C3 shape
+    (mb: another minibatch size, to see how the launch scales with its tiles)."""
+    D, O, A, mb0, T, E = SHAPES["C3"]
+    mb = mb or mb0
     osp, asp = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O))), Box(-np.ones((D, A)), np.ones((D, A)))
     agent = MAPPOAgent(osp, asp, hidden_dim=256, opt_epochs=1, mini_batch_size=mb, use_graphs=False, device=dev)
     buf = MAPPOBuffer(osp, asp, T, E, include_global_state=True, device=dev)
@@ -92,7 +94,7 @@ def kernels():
     fl = 2 * mb * (D * O * 256 + 2 * 256 * 256 + 256)
     us = timed(lambda: L.check(lib.qs_ppo_critic_tiles(mb, D, L.ptr(buf.obs), L.ptr(idx), L.ptr(buf.ret_env),
                                                        ctypes.byref(ct.net), L.ptr(acc), L.ptr(ct.work), st()), "t"))
-    print(f"qs_ppo_critic_tiles (4096 x 216)          {us:8.2f} us  {fl / us / 1e6:6.1f} TFLOP/s", flush=True)
+    print(f"qs_ppo_critic_tiles ({mb:5d} x 216)          {us:8.2f} us  {fl / us / 1e6:6.1f} TFLOP/s", flush=True)
     for name, a, b, M, part in (("W1", ct.dz1T, ct.xT, ct.I, ct.pw1), ("W2", ct.dz2T, ct.h1T, 256, ct.pw2)):
         us = timed(lambda: L.check(lib.qs_wgrad_t(ct.KcP, ct.ld, 256, M, L.ptr(a), L.ptr(b), ct.S, L.ptr(part), st()),
                                    "w"))
@@ -104,6 +106,9 @@ def main():
     which = sys.argv[1:] or ["kernels", "C3", "ref", "C4"]
     if "kernels" in which:
         kernels()
+    if "scale" in which:
+        for mb in (256, 1024, 2048):
+            kernels(mb)
     if "C3" in which:
         for v in (dict(critic_tiles=True), dict(critic_tiles=True, critic_after_actor=False), dict(critic_tiles=False),
                   dict(critic_tiles=True, side_stream=False), dict(critic_tiles=False, side_stream=False)):
