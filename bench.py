@@ -96,7 +96,7 @@ def parse():
     p.add_argument("--w1-stream", type=int, default=1, help="learner: actor dW1 GEMM on a third stream beside dW2")
     p.add_argument("--fused-max-a", type=int, default=None,
                    help="learner: widest actor output on the fused actor kernel (default: the agent's _F16_MAX_A)")
-    p.add_argument("--critic-tiles", type=int, default=1,
+    p.add_argument("--critic-tiles", type=int, default=0,
                    help="learner: the critic on qs_ppo_critic_tiles + qs_wgrad_t (0 = qs_mlp3w kernels + GEMMs)")
     p.add_argument("--small-rows", type=int, default=None,
                    help="learner: minibatches of at most this many actor rows on qs_ppo_small_step (0 = never)")

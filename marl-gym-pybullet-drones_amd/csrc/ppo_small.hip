@@ -42,8 +42,9 @@ thread_local std::string g_serr;
 int sfail(int code, const std::string& m) { g_serr = m; return code; }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kSW = 8;                 // waves per workgroup of the forward/backward kernel
+constexpr int kSW = 16;                // waves per workgroup of the forward/backward kernel
 constexpr int kSBlock = 64 * kSW;
+constexpr int kSBPW = 256 / 16 / kSW;  // hidden blocks of 16 per wave (1: four waves a SIMD hide each other's chains)
 constexpr int kSH = 256;               // hidden width
 constexpr int kSHS = kSH + 4;          // LDS row stride of the hidden exchange (4 mod 32 floats)
 constexpr int kSMaxI = 256;            // widest input
@@ -182,14 +183,51 @@ __device__ __forceinline__ void s_contract2(const float* wrow0, const float* wro
   }
 }
 
+// one hidden block: c += Σ over NQ quads, the even and odd quads in two
+// accumulators (independent MFMA chains), added at the end
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_contract1(const float* wrow, int I, const float* brow, int g, f32x4& c) {
+  constexpr int R = NQ < kSRing ? NQ : kSRing;
+  auto ld = [&](int t) {
+    if constexpr (VEC) return *reinterpret_cast<const float4*>(wrow + 16 * t + 4 * g);
+    else return s_ld4s(wrow, 16 * t + 4 * g, I);
+  };
+  float4 ra[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) ra[t] = ld(t);
+  f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const float4 a = ra[t % R];
+    if (t + R < NQ) ra[t % R] = ld(t + R);
+    const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4& acc = (t & 1) ? c1 : c;
+    acc = s_mfma(a.x, bv.x, acc);
+    acc = s_mfma(a.y, bv.y, acc);
+    acc = s_mfma(a.z, bv.z, acc);
+    acc = s_mfma(a.w, bv.w, acc);
+  }
+  c += c1;
+}
+
+// the wave's hidden blocks (kSBPW of them) against one B row: layer 1 over nq
+// = ⌈I/16⌉ quads (1..16, the compile-time count by dispatch) or a 256-wide row
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_contract_w(const float* wrow0, int rstride, int I, const float* brow, int g,
+                                             f32x4 (&z)[kSBPW]) {
+  if constexpr (kSBPW == 2) s_contract2<NQ, VEC>(wrow0, wrow0 + (size_t)16 * rstride, I, brow, g, z[0], z[1]);
+  else s_contract1<NQ, VEC>(wrow0, I, brow, g, z[0]);
+}
+
 // layer 1 over nq = ⌈I/16⌉ quads (1..16): the compile-time count by dispatch
-__device__ __forceinline__ void s_contract_in(const float* wrow0, const float* wrow1, int I, const float* brow, int nq,
-                                              int g, f32x4& c0, f32x4& c1) {
+__device__ __forceinline__ void s_contract_in(const float* wrow0, int I, const float* brow, int nq, int g,
+                                              f32x4 (&z)[kSBPW]) {
   switch (nq) {
-#define S_CASE(n) case n: s_contract2<n, false>(wrow0, wrow1, I, brow, g, c0, c1); break;
+#define S_CASE(n) case n: s_contract_w<n, false>(wrow0, I, I, brow, g, z); break;
     S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
     S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
-    default: s_contract2<16, false>(wrow0, wrow1, I, brow, g, c0, c1); break;
+    default: s_contract_w<16, false>(wrow0, I, I, brow, g, z); break;
 #undef S_CASE
   }
 }
@@ -270,17 +308,15 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     }
   }
   __syncthreads();
-  const int b0 = 2 * w;   // the wave's hidden blocks b0, b0 + 1
+  const int b0 = kSBPW * w;   // the wave's hidden blocks b0 .. b0 + kSBPW − 1
   // ---- layer 1: Z1ᵀ[16b + 4g + r][row j] in register r of lane (g, j)
-  f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  {
-    const float* w1 = N.p + N.w1;
-    s_contract_in(w1 + (size_t)(16 * b0 + j) * I, w1 + (size_t)(16 * b0 + 16 + j) * I, I, xs + j * XS, Ip / 16, g,
-                  z[0], z[1]);
-  }
-  float h1[2][4];
+  f32x4 z[kSBPW];
 #pragma unroll
-  for (int bb = 0; bb < 2; ++bb) {
+  for (int bb = 0; bb < kSBPW; ++bb) z[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s_contract_in(N.p + N.w1 + (size_t)(16 * b0 + j) * I, I, xs + j * XS, Ip / 16, g, z);
+  float h1[kSBPW][4];
+#pragma unroll
+  for (int bb = 0; bb < kSBPW; ++bb) {
     const int h0 = 16 * (b0 + bb) + 4 * g;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -292,18 +328,17 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   __syncthreads();
   // ---- layer 2: Z2ᵀ = W2·H1ᵀ (W2 rows straight from L2, four quads ahead)
   const float* w2 = N.p + N.w2;
-  auto contract = [&](const float* wrow0, const float* wrow1, const float* brow) {
-    f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
-    s_contract2<kSH / 16, true>(wrow0, wrow1, kSH, brow, g, c0, c1);
-    z[0] = c0;
-    z[1] = c1;
+  auto contract = [&](const float* wrow0, const float* brow) {
+#pragma unroll
+    for (int bb = 0; bb < kSBPW; ++bb) z[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    s_contract_w<kSH / 16, true>(wrow0, kSH, kSH, brow, g, z);
   };
-  contract(w2 + (size_t)(16 * b0 + j) * kSH, w2 + (size_t)(16 * b0 + 16 + j) * kSH, h1s + j * kSHS);
-  float h2[2][4], hs[A];
+  contract(w2 + (size_t)(16 * b0 + j) * kSH, h1s + j * kSHS);
+  float h2[kSBPW][4], hs[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) hs[a] = 0.f;
 #pragma unroll
-  for (int bb = 0; bb < 2; ++bb)
+  for (int bb = 0; bb < kSBPW; ++bb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int h = 16 * (b0 + bb) + 4 * g + r;
@@ -395,7 +430,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   float* pa = (POL ? W.partAa : W.partAc) + (size_t)tile * (kSH + A * kSH + A);
   float* pb = (POL ? W.partBa : W.partBc) + (size_t)tile * kSH;
 #pragma unroll
-  for (int bb = 0; bb < 2; ++bb) {
+  for (int bb = 0; bb < kSBPW; ++bb) {
     const int h0 = 16 * (b0 + bb) + 4 * g;
     float d4[4];
 #pragma unroll
@@ -425,9 +460,9 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     }
   __syncthreads();
   // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (rows of the transposed copy), dZ1 = dH1 ⊙ (1 − H1²)
-  contract(N.w2t + (size_t)(16 * b0 + j) * kSH, N.w2t + (size_t)(16 * b0 + 16 + j) * kSH, dz2s + j * kSHS);
+  contract(N.w2t + (size_t)(16 * b0 + j) * kSH, dz2s + j * kSHS);
 #pragma unroll
-  for (int bb = 0; bb < 2; ++bb) {
+  for (int bb = 0; bb < kSBPW; ++bb) {
     const int h0 = 16 * (b0 + bb) + 4 * g;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

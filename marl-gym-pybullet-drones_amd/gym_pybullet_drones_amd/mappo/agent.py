@@ -877,9 +877,10 @@ class MAPPOAgent:
         # one rank, fused actor: the critic's sums + Adam on the side stream too (its own
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
-        # with the fused actor, the critic's step on qs_ppo_critic_tiles + qs_wgrad_t
-        # (False: the qs_mlp3w kernels and hipBLASLt weight-gradient GEMMs)
-        self.critic_tiles = kwargs.get('critic_tiles', True)
+        # (opt-in) with the fused actor, the critic's step on qs_ppo_critic_tiles +
+        # qs_wgrad_t instead of the qs_mlp3w kernels and hipBLASLt weight-gradient
+        # GEMMs (measured slower at the C3 shape)
+        self.critic_tiles = kwargs.get('critic_tiles', False)
         # ... after the fused actor kernel, beside its weight gradients (False: beside the actor kernel)
         self.critic_after_actor = kwargs.get('critic_after_actor', True)
         # minibatches of at most _SMALL_MAX_ROWS actor rows on qs_ppo_small_step (one

@@ -234,14 +234,16 @@ def test_direct_update_side_stream_bit_identical(graphs, E, T):
     assert torch.equal(a_side.critic_opt.flat, a_join.critic_opt.flat)
     assert torch.equal(a_side.critic_opt.exp_avg, a_join.critic_opt.exp_avg)
     assert r_side == r_join
-    # the critic on the qs_mlp3w kernels + hipBLASLt GEMMs instead of qs_ppo_critic_tiles + qs_wgrad_t
-    assert type(a_side._ws_critic).__name__ == "_CriticTiles"
-    a_m3, r_m3 = _hidden256_update(graphs, E, T, critic_tiles=False)
-    assert type(a_m3._ws_critic).__name__ == "_M3Work"
-    torch.testing.assert_close(a_side.critic_opt.flat, a_m3.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
-    torch.testing.assert_close(a_side.actor_opt.flat, a_m3.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
-    for k in r_side:
-        assert r_side[k] == pytest.approx(r_m3[k], rel=1e-5, abs=1e-7)
+    # the critic on qs_ppo_critic_tiles + qs_wgrad_t (opt-in) instead of the qs_mlp3w kernels + GEMMs,
+    # after the fused actor (default) or beside it
+    assert type(a_side._ws_critic).__name__ == "_M3Work"
+    for after in (True, False):
+        a_t, r_t = _hidden256_update(graphs, E, T, critic_tiles=True, critic_after_actor=after)
+        assert type(a_t._ws_critic).__name__ == "_CriticTiles"
+        torch.testing.assert_close(a_t.critic_opt.flat, a_side.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
+        torch.testing.assert_close(a_t.actor_opt.flat, a_side.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
+        for k in r_side:
+            assert r_t[k] == pytest.approx(r_side[k], rel=1e-5, abs=1e-7)
     a_fused, r_fused = _hidden256_update(graphs, E, T, direct=False)
     # (the fused path's critic, at 128 rows, is plain torch: ulp-level gradient
     # differences, which Adam's normalised steps carry up to ~lr/60 per step; 4 steps)
