@@ -142,63 +142,94 @@ __device__ __forceinline__ float4 s_ld4s(const float* row, int k0, int I) {   //
   return r;
 }
 
-// z[bb] += Σ over nq quads of A_b[j][κ]·B[κ][j] (κ = 16t + 4g + e) for the
-// wave's kSBPW hidden blocks: the A rows from L2 (VEC: whole float4s of a
-// 256-wide row; otherwise scalars, elements past I zero), the B row (an
-// activation row) from LDS.  A rolled loop of four-quad steps with the loads of
-// the next step issued before this step's MFMAs; the prefetch index is
-// clamped into the row (the loads past the end re-read the last quad) so no
-// load is conditional: the compiler's wait counts stay exact.  Rolled on
-// purpose: fully unrolled contractions made the kernel's code ~20 KB per path,
-// and a launch waited ~45 µs on instruction fetch before its first tile did
-// any work.  With one block per wave the even and odd quads go to two
-// accumulators (independent MFMA chains), added at the end.
-constexpr int kSU = 4;   // quads per loop step
-constexpr int kSRing = 8;   // quads of loads in flight in the weight gradients
-template <bool VEC>
-__device__ __forceinline__ float4 s_ldq(const float* row, int t, int I, int g) {
-  if constexpr (VEC) return *reinterpret_cast<const float4*>(row + 16 * t + 4 * g);
-  else return s_ld4s(row, 16 * t + 4 * g, I);
-}
-template <bool VEC>
-__device__ __forceinline__ void s_contract(const float* wrow0, int rstride, int I, const float* brow, int nq, int g,
-                                           f32x4 (&z)[kSBPW]) {
-  const int last = nq - 1;
-  float4 ra[kSBPW][kSU];
-  f32x4 zo[kSBPW];
+// c0 / c1 += Σ over NQ quads of A_b[j][κ]·B[κ][j] (κ = 16t + 4g + e): the A
+// rows of the wave's two hidden blocks from L2 (VEC: whole float4s of a 256-wide
+// row; otherwise scalars, elements past I zero), kSRing quads of loads in
+// flight ahead of the MFMAs; the B row (an activation row) from LDS.  NQ is a
+// compile-time count: the loop unrolls fully and the load counter waits are
+// exact.
+constexpr int kSRing = 8;
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_contract2(const float* wrow0, const float* wrow1, int I, const float* brow, int g,
+                                            f32x4& c0, f32x4& c1) {
+  constexpr int R = NQ < kSRing ? NQ : kSRing;
+  auto ld = [&](const float* row, int t) {
+    if constexpr (VEC) return *reinterpret_cast<const float4*>(row + 16 * t + 4 * g);
+    else return s_ld4s(row, 16 * t + 4 * g, I);
+  };
+  float4 ra[R], rb[R];
 #pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb) {
-    zo[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < kSU; ++u) ra[bb][u] = s_ldq<VEC>(wrow0 + (size_t)bb * 16 * rstride, min(u, last), I, g);
+  for (int t = 0; t < R; ++t) {
+    ra[t] = ld(wrow0, t);
+    rb[t] = ld(wrow1, t);
   }
-#pragma unroll 1
-  for (int t0 = 0; t0 < nq; t0 += kSU) {
-    float4 a[kSBPW][kSU];
 #pragma unroll
-    for (int bb = 0; bb < kSBPW; ++bb)
-#pragma unroll
-      for (int u = 0; u < kSU; ++u) {
-        a[bb][u] = ra[bb][u];
-        ra[bb][u] = s_ldq<VEC>(wrow0 + (size_t)bb * 16 * rstride, min(t0 + kSU + u, last), I, g);
-      }
-    __builtin_amdgcn_sched_barrier(0);   // the next step's loads stay ahead of these MFMAs
-#pragma unroll
-    for (int u = 0; u < kSU; ++u) {
-      if (t0 + u >= nq) break;
-      const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * (t0 + u) + 4 * g);
-#pragma unroll
-      for (int bb = 0; bb < kSBPW; ++bb) {
-        f32x4& acc = (kSBPW == 1 && (u & 1)) ? zo[bb] : z[bb];
-        acc = s_mfma(a[bb][u].x, bv.x, acc);
-        acc = s_mfma(a[bb][u].y, bv.y, acc);
-        acc = s_mfma(a[bb][u].z, bv.z, acc);
-        acc = s_mfma(a[bb][u].w, bv.w, acc);
-      }
+  for (int t = 0; t < NQ; ++t) {
+    const float4 a0 = ra[t % R], a1 = rb[t % R];
+    if (t + R < NQ) {
+      ra[t % R] = ld(wrow0, t + R);
+      rb[t % R] = ld(wrow1, t + R);
     }
+    const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+    __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the loads next to their use
+    c0 = s_mfma(a0.x, bv.x, c0);
+    c1 = s_mfma(a1.x, bv.x, c1);
+    c0 = s_mfma(a0.y, bv.y, c0);
+    c1 = s_mfma(a1.y, bv.y, c1);
+    c0 = s_mfma(a0.z, bv.z, c0);
+    c1 = s_mfma(a1.z, bv.z, c1);
+    c0 = s_mfma(a0.w, bv.w, c0);
+    c1 = s_mfma(a1.w, bv.w, c1);
   }
+}
+
+// one hidden block: c += Σ over NQ quads, the even and odd quads in two
+// accumulators (independent MFMA chains), added at the end
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_contract1(const float* wrow, int I, const float* brow, int g, f32x4& c) {
+  constexpr int R = NQ < kSRing ? NQ : kSRing;
+  auto ld = [&](int t) {
+    if constexpr (VEC) return *reinterpret_cast<const float4*>(wrow + 16 * t + 4 * g);
+    else return s_ld4s(wrow, 16 * t + 4 * g, I);
+  };
+  float4 ra[R];
 #pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb) z[bb] += zo[bb];
+  for (int t = 0; t < R; ++t) ra[t] = ld(t);
+  f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const float4 a = ra[t % R];
+    if (t + R < NQ) ra[t % R] = ld(t + R);
+    const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4& acc = (t & 1) ? c1 : c;
+    acc = s_mfma(a.x, bv.x, acc);
+    acc = s_mfma(a.y, bv.y, acc);
+    acc = s_mfma(a.z, bv.z, acc);
+    acc = s_mfma(a.w, bv.w, acc);
+  }
+  c += c1;
+}
+
+// the wave's hidden blocks (kSBPW of them) against one B row: layer 1 over nq
+// = ⌈I/16⌉ quads (1..16, the compile-time count by dispatch) or a 256-wide row
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_contract_w(const float* wrow0, int rstride, int I, const float* brow, int g,
+                                             f32x4 (&z)[kSBPW]) {
+  if constexpr (kSBPW == 2) s_contract2<NQ, VEC>(wrow0, wrow0 + (size_t)16 * rstride, I, brow, g, z[0], z[1]);
+  else s_contract1<NQ, VEC>(wrow0, I, brow, g, z[0]);
+}
+
+// layer 1 over nq = ⌈I/16⌉ quads (1..16): the compile-time count by dispatch
+__device__ __forceinline__ void s_contract_in(const float* wrow0, int I, const float* brow, int nq, int g,
+                                              f32x4 (&z)[kSBPW]) {
+  switch (nq) {
+#define S_CASE(n) case n: s_contract_w<n, false>(wrow0, I, I, brow, g, z); break;
+    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
+    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
+    default: s_contract_w<16, false>(wrow0, I, I, brow, g, z); break;
+#undef S_CASE
+  }
 }
 
 // c += Σ over NQ quads of A[j][rows]·B[rows][j], both operands transposed rows
@@ -282,7 +313,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   f32x4 z[kSBPW];
 #pragma unroll
   for (int bb = 0; bb < kSBPW; ++bb) z[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s_contract<false>(N.p + N.w1 + (size_t)(16 * b0 + j) * I, I, I, xs + j * XS, Ip / 16, g, z);
+  s_contract_in(N.p + N.w1 + (size_t)(16 * b0 + j) * I, I, xs + j * XS, Ip / 16, g, z);
   float h1[kSBPW][4];
 #pragma unroll
   for (int bb = 0; bb < kSBPW; ++bb) {
@@ -300,7 +331,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   auto contract = [&](const float* wrow0, const float* brow) {
 #pragma unroll
     for (int bb = 0; bb < kSBPW; ++bb) z[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    s_contract<true>(wrow0, kSH, kSH, brow, kSH / 16, g, z);
+    s_contract_w<kSH / 16, true>(wrow0, kSH, kSH, brow, g, z);
   };
   contract(w2 + (size_t)(16 * b0 + j) * kSH, h1s + j * kSHS);
   float h2[kSBPW][4], hs[A];
