@@ -142,66 +142,36 @@ __device__ __forceinline__ float4 s_ld4s(const float* row, int k0, int I) {   //
   return r;
 }
 
-// c0 / c1 += Σ over NQ quads of A_b[j][κ]·B[κ][j] (κ = 16t + 4g + e): the A
-// rows of the wave's two hidden blocks from L2 (VEC: whole float4s of a 256-wide
-// row; otherwise scalars, elements past I zero), kSRing quads of loads in
-// flight ahead of the MFMAs; the B row (an activation row) from LDS.  NQ is a
-// compile-time count: the loop unrolls fully and the load counter waits are
-// exact.
+// A wave's weight-row stream for one contraction: c += Σ over NQ quads of
+// A[j][κ]·B[κ][j] (κ = 16t + 4g + e) for the wave's hidden block, the A row
+// from L2 (VEC: whole float4s of a 256-wide row; otherwise scalars, elements
+// past I zero, branch-free), the B row (an activation row) from LDS.  The first
+// kSRing quads are loaded by s_prefill — issued phases ahead of the contraction,
+// so their latency hides behind earlier work — and s_run keeps kSRing quads in
+// flight (compile-time NQ: the loop unrolls fully and the load counter waits
+// are exact; the scheduling barrier keeps the loads ahead of the MFMAs).  The
+// even and odd quads go to two accumulators (independent MFMA chains).
 constexpr int kSRing = 8;
-template <int NQ, bool VEC>
-__device__ __forceinline__ void s_contract2(const float* wrow0, const float* wrow1, int I, const float* brow, int g,
-                                            f32x4& c0, f32x4& c1) {
-  constexpr int R = NQ < kSRing ? NQ : kSRing;
-  auto ld = [&](const float* row, int t) {
-    if constexpr (VEC) return *reinterpret_cast<const float4*>(row + 16 * t + 4 * g);
-    else return s_ld4s(row, 16 * t + 4 * g, I);
-  };
-  float4 ra[R], rb[R];
-#pragma unroll
-  for (int t = 0; t < R; ++t) {
-    ra[t] = ld(wrow0, t);
-    rb[t] = ld(wrow1, t);
-  }
-#pragma unroll
-  for (int t = 0; t < NQ; ++t) {
-    const float4 a0 = ra[t % R], a1 = rb[t % R];
-    if (t + R < NQ) {
-      ra[t % R] = ld(wrow0, t + R);
-      rb[t % R] = ld(wrow1, t + R);
-    }
-    const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
-    __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the loads next to their use
-    c0 = s_mfma(a0.x, bv.x, c0);
-    c1 = s_mfma(a1.x, bv.x, c1);
-    c0 = s_mfma(a0.y, bv.y, c0);
-    c1 = s_mfma(a1.y, bv.y, c1);
-    c0 = s_mfma(a0.z, bv.z, c0);
-    c1 = s_mfma(a1.z, bv.z, c1);
-    c0 = s_mfma(a0.w, bv.w, c0);
-    c1 = s_mfma(a1.w, bv.w, c1);
-  }
+template <bool VEC>
+__device__ __forceinline__ float4 s_ldq(const float* row, int t, int I, int g) {
+  if constexpr (VEC) return *reinterpret_cast<const float4*>(row + 16 * t + 4 * g);
+  else return s_ld4s(row, 16 * t + 4 * g, I);
 }
-
-// one hidden block: c += Σ over NQ quads, the even and odd quads in two
-// accumulators (independent MFMA chains), added at the end
 template <int NQ, bool VEC>
-__device__ __forceinline__ void s_contract1(const float* wrow, int I, const float* brow, int g, f32x4& c) {
-  constexpr int R = NQ < kSRing ? NQ : kSRing;
-  auto ld = [&](int t) {
-    if constexpr (VEC) return *reinterpret_cast<const float4*>(wrow + 16 * t + 4 * g);
-    else return s_ld4s(wrow, 16 * t + 4 * g, I);
-  };
-  float4 ra[R];
+__device__ __forceinline__ void s_prefill(float4 (&ra)[kSRing], const float* wrow, int I, int g) {
 #pragma unroll
-  for (int t = 0; t < R; ++t) ra[t] = ld(t);
+  for (int t = 0; t < (NQ < kSRing ? NQ : kSRing); ++t) ra[t] = s_ldq<VEC>(wrow, t, I, g);
+}
+template <int NQ, bool VEC>
+__device__ __forceinline__ void s_run(float4 (&ra)[kSRing], const float* wrow, int I, const float* brow, int g,
+                                      f32x4& c) {
   f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NQ; ++t) {
-    const float4 a = ra[t % R];
-    if (t + R < NQ) ra[t % R] = ld(t + R);
+    const float4 a = ra[t % kSRing];
+    if (t + kSRing < NQ) ra[t % kSRing] = s_ldq<VEC>(wrow, t + kSRing, I, g);
     const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
-    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the loads next to their use
     f32x4& acc = (t & 1) ? c1 : c;
     acc = s_mfma(a.x, bv.x, acc);
     acc = s_mfma(a.y, bv.y, acc);
@@ -210,27 +180,15 @@ __device__ __forceinline__ void s_contract1(const float* wrow, int I, const floa
   }
   c += c1;
 }
-
-// the wave's hidden blocks (kSBPW of them) against one B row: layer 1 over nq
-// = ⌈I/16⌉ quads (1..16, the compile-time count by dispatch) or a 256-wide row
-template <int NQ, bool VEC>
-__device__ __forceinline__ void s_contract_w(const float* wrow0, int rstride, int I, const float* brow, int g,
-                                             f32x4 (&z)[kSBPW]) {
-  if constexpr (kSBPW == 2) s_contract2<NQ, VEC>(wrow0, wrow0 + (size_t)16 * rstride, I, brow, g, z[0], z[1]);
-  else s_contract1<NQ, VEC>(wrow0, I, brow, g, z[0]);
-}
-
 // layer 1 over nq = ⌈I/16⌉ quads (1..16): the compile-time count by dispatch
-__device__ __forceinline__ void s_contract_in(const float* wrow0, int I, const float* brow, int nq, int g,
-                                              f32x4 (&z)[kSBPW]) {
-  switch (nq) {
-#define S_CASE(n) case n: s_contract_w<n, false>(wrow0, I, I, brow, g, z); break;
-    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
-    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
-    default: s_contract_w<16, false>(wrow0, I, I, brow, g, z); break;
-#undef S_CASE
+#define S_NQ_SWITCH(nq, CALL)                                                                       \
+  switch (nq) {                                                                                     \
+    case 1: CALL(1); break; case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; \
+    case 5: CALL(5); break; case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; \
+    case 9: CALL(9); break; case 10: CALL(10); break; case 11: CALL(11); break;                   \
+    case 12: CALL(12); break; case 13: CALL(13); break; case 14: CALL(14); break;                 \
+    case 15: CALL(15); break; default: CALL(16); break;                                             \
   }
-}
 
 // c += Σ over NQ quads of A[j][rows]·B[rows][j], both operands transposed rows
 // in global memory, kSRing quads of loads ahead; compile-time NQ
@@ -275,10 +233,11 @@ __device__ __forceinline__ void s_wgrad_acc(const float* arow, const float* brow
 // otherwise the critic (value head).
 template <int A, bool POL>
 __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, float* xs, float* h1s, float* dz2s,
-                                       float (*hp)[16], double (*ls_w)[2 + kSMaxA]) {
+                                       float* prm, float (*hp)[16], double (*ls_w)[2 + kSMaxA]) {
+  static_assert(kSBPW == 1, "one hidden block per wave");
   constexpr int NL = POL ? 2 + A : 1;   // loss sums: policy, approx_kl, d logstd[A] | value
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
-  const int I = N.I, XS = s_xs(I), Ip = s_ip(I);
+  const int I = N.I, XS = s_xs(I), Ip = s_ip(I), nq1 = Ip / 16;
   const int K = POL ? P.mb * P.D : P.mb;
   const int KP = POL ? P.KaS : P.KcS;   // the transposed rows' stride
   const int r0 = tile * 16;
@@ -287,66 +246,97 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   float* h1T = POL ? W.h1aT : W.h1cT;
   float* dz2T = POL ? W.dz2aT : W.dz2cT;
   float* dz1T = POL ? W.dz1aT : W.dz1cT;
-  // ---- the X tile: LDS rows (zero-padded) and the transposed copy the weight
-  // gradients read (rows past K are zeros)
+  const int b0 = w, h0 = 16 * b0 + 4 * g;   // the wave's hidden block; lane (g, j): units h0 .. h0 + 3 of row j
+  const float* w1row = N.p + N.w1 + (size_t)(16 * b0 + j) * I;
+  const float* w2row = N.p + N.w2 + (size_t)(16 * b0 + j) * kSH;
+  const float* w2trow = N.w2t + (size_t)(16 * b0 + j) * kSH;
+  // ---- every independent load first, so the tile pays one or two memory
+  // round trips before its first MFMA instead of one per phase: the first
+  // quads of both forward contractions' weight rows, the head's per-row inputs,
+  // the X tile (gathered through idx), and the biases / head into LDS
+  float4 ring1[kSRing], ring2[kSRing];
+#define S_PRE1(n) s_prefill<n, false>(ring1, w1row, I, g)
+  S_NQ_SWITCH(nq1, S_PRE1)
+#undef S_PRE1
+  s_prefill<16, true>(ring2, w2row, kSH, g);
+  const int R = r0 + j;
+  const bool rv = R < K;
+  float hact[A], hlpo = 0.f;
+  double had = 0.0;
+  if constexpr (POL) {
+    const long long ei = rv ? R / P.D : 0;
+    const long long e_idx = rv ? P.idx[ei] : 0;
+    const long long gi = e_idx * P.D + (R - ei * P.D);
+#pragma unroll
+    for (int a = 0; a < A; ++a) hact[a] = rv ? P.act[gi * A + a] : 0.f;
+    if (rv) {
+      hlpo = P.logp_old[gi];
+      had = P.adv[e_idx];
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < A; ++a) hact[a] = 0.f;
+    if (rv) had = P.ret[P.idx[R]];   // the value head's return
+  }
   {
-    // every load of the tile first (one gather latency), then the LDS / global writes
     constexpr int kXU = (16 * kSMaxI + kSBlock - 1) / kSBlock;
     float v[kXU];
-    const int rr = tid & 15, R = r0 + rr;
-    const long long src = R < K ? (POL ? (P.idx[R / P.D] * P.D + R % P.D) : P.idx[R]) * I : -1;
+    const int rr = tid & 15, Rx = r0 + rr;
+    const long long src = Rx < K ? (POL ? (P.idx[Rx / P.D] * P.D + Rx % P.D) : P.idx[Rx]) * I : -1;
 #pragma unroll
     for (int u = 0; u < kXU; ++u) {
       const int k = (tid >> 4) + u * (kSBlock / 16);
       v[u] = src >= 0 && k < I ? P.X[src + k] : 0.f;
     }
+    // biases and head: prm = [b1 | b2 | W3 (A rows) | b3 | logstd]
+    for (int e = tid; e < 2 * kSH + A * kSH + 2 * A; e += kSBlock) {
+      float pv;
+      if (e < kSH) pv = N.p[N.b1 + e];
+      else if (e < 2 * kSH) pv = N.p[N.b2 + e - kSH];
+      else if (e < 2 * kSH + A * kSH) pv = N.p[N.w3 + e - 2 * kSH];
+      else if (e < 2 * kSH + A * kSH + A) pv = N.p[N.b3 + e - 2 * kSH - A * kSH];
+      else pv = POL ? N.p[N.logstd + e - 2 * kSH - A * kSH - A] : 0.f;
+      prm[e] = pv;
+    }
 #pragma unroll
     for (int u = 0; u < kXU; ++u) {
       const int k = (tid >> 4) + u * (kSBlock / 16);
       if (k < Ip) xs[rr * XS + k] = v[u];
-      if (k < I) xT[(size_t)k * KP + R] = v[u];
+      if (k < I) xT[(size_t)k * KP + Rx] = v[u];
     }
   }
   __syncthreads();
-  const int b0 = kSBPW * w;   // the wave's hidden blocks b0 .. b0 + kSBPW − 1
-  // ---- layer 1: Z1ᵀ[16b + 4g + r][row j] in register r of lane (g, j)
-  f32x4 z[kSBPW];
+  const float* sb1 = prm;
+  const float* sb2 = prm + kSH;
+  const float* sw3 = prm + 2 * kSH;
+  const float* sb3 = prm + 2 * kSH + A * kSH;
+  const float* slogstd = sb3 + A;
+  // ---- layer 1: Z1ᵀ[h0 + r][row j] in register r of lane (g, j)
+  f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+#define S_RUN1(n) s_run<n, false>(ring1, w1row, I, xs + j * XS, g, z)
+  S_NQ_SWITCH(nq1, S_RUN1)
+#undef S_RUN1
+  float h1[4];
 #pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb) z[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s_contract_in(N.p + N.w1 + (size_t)(16 * b0 + j) * I, I, xs + j * XS, Ip / 16, g, z);
-  float h1[kSBPW][4];
-#pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb) {
-    const int h0 = 16 * (b0 + bb) + 4 * g;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      h1[bb][r] = s_tanh(z[bb][r] + N.p[N.b1 + h0 + r]);
-      h1T[(size_t)(h0 + r) * KP + r0 + j] = h1[bb][r];
-    }
-    *reinterpret_cast<float4*>(h1s + j * kSHS + h0) = float4{h1[bb][0], h1[bb][1], h1[bb][2], h1[bb][3]};
-  }
+  for (int r = 0; r < 4; ++r) h1[r] = s_tanh(z[r] + sb1[h0 + r]);
+  *reinterpret_cast<float4*>(h1s + j * kSHS + h0) = float4{h1[0], h1[1], h1[2], h1[3]};
   __syncthreads();
-  // ---- layer 2: Z2ᵀ = W2·H1ᵀ (W2 rows straight from L2, four quads ahead)
-  const float* w2 = N.p + N.w2;
-  auto contract = [&](const float* wrow0, const float* brow) {
+  // ---- layer 2: Z2ᵀ = W2·H1ᵀ (its ring filled at the start); the backward's ring filled behind it
+  z = f32x4{0.f, 0.f, 0.f, 0.f};
+  s_run<16, true>(ring2, w2row, kSH, h1s + j * kSHS, g, z);
+  s_prefill<16, true>(ring1, w2trow, kSH, g);
 #pragma unroll
-    for (int bb = 0; bb < kSBPW; ++bb) z[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    s_contract_w<kSH / 16, true>(wrow0, kSH, kSH, brow, g, z);
-  };
-  contract(w2 + (size_t)(16 * b0 + j) * kSH, h1s + j * kSHS);
-  float h2[kSBPW][4], hs[A];
+  for (int r = 0; r < 4; ++r) h1T[(size_t)(h0 + r) * KP + r0 + j] = h1[r];   // (after the loads above)
+  float h2[4], hs[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) hs[a] = 0.f;
 #pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb)
+  for (int r = 0; r < 4; ++r) {
+    h2[r] = s_tanh(z[r] + sb2[h0 + r]);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = 16 * (b0 + bb) + 4 * g + r;
-      h2[bb][r] = s_tanh(z[bb][r] + N.p[N.b2 + h]);
-#pragma unroll
-      for (int a = 0; a < A; ++a) hs[a] += h2[bb][r] * N.p[N.w3 + a * kSH + h];
-    }
-  // the head: the wave's partial dot of row j (lane groups g added), then the 8 waves in order
+    for (int a = 0; a < A; ++a) hs[a] += h2[r] * sw3[a * kSH + h0 + r];
+  }
+  // the head: the wave's partial dot of row j (lane groups g added), then the waves in order
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     float t = hs[a] + __shfl_xor(hs[a], 16, 64);
@@ -354,15 +344,13 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     if (g == 0) hp[w * A + a][j] = t;
   }
   __syncthreads();
-  const int R = r0 + j;
-  const bool rv = R < K;
   float mu[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     float t = hp[a][j];
 #pragma unroll
     for (int v = 1; v < kSW; ++v) t += hp[v * A + a][j];
-    mu[a] = t + N.p[N.b3 + a];
+    mu[a] = t + sb3[a];
   }
   // ---- the loss head of row j (every wave forms it; wave 0, lane group 0 counts it)
   float dout[A];
@@ -374,27 +362,25 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     float sd[A], lsd[A], var2[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      sd[a] = expf(N.p[N.logstd + a]);
+      sd[a] = expf(slogstd[a]);
       lsd[a] = logf(sd[a]);
       var2[a] = 2.0f * (sd[a] * sd[a]);
     }
     const float lc = (float)log(sqrt(2.0 * M_PI));
     const float lo = 1.0f - P.clip, hi = 1.0f + P.clip;
     const double G = -1.0 / (double)K;
-    const long long ei = rv ? R / P.D : 0;
-    const long long gi = rv ? P.idx[ei] * P.D + (R - ei * P.D) : 0;
     float t1[A], logp = 0.0f;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const float m = mu[a] * P.scale;
-      t1[a] = (rv ? P.act[gi * A + a] : 0.f) - m;
+      t1[a] = hact[a] - m;
       const float t4 = (float)((double)(-(t1[a] * t1[a])) / (double)var2[a]);
       const float lp = (t4 - lsd[a]) - lc;
       logp = a == 0 ? lp : logp + lp;
     }
-    const float lpo = rv ? P.logp_old[gi] : 0.f;
+    const float lpo = hlpo;
     const float ratio = expf(logp - lpo);
-    const double ad = rv ? P.adv[P.idx[ei]] : 0.0;
+    const double ad = had;
     const float rc = fminf(fmaxf(ratio, lo), hi);
     const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
     const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
@@ -416,7 +402,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   } else {
     // compute_value_loss (AG:642-683, centralized, unclipped): qs_value_head's arithmetic
     if (rv) {
-      const double rt = P.ret[P.idx[R]];
+      const double rt = had;
       double rs = 0;
       for (int d = 0; d < P.D; ++d) rs += rt;
       const double diff = (double)mu[0] - rs / (double)P.D;
@@ -429,29 +415,24 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   // ---- dZ2 = (dout·W3) ⊙ (1 − H2²); the tile's b2 / W3 / b3 partial rows (row sums over j)
   float* pa = (POL ? W.partAa : W.partAc) + (size_t)tile * (kSH + A * kSH + A);
   float* pb = (POL ? W.partBa : W.partBc) + (size_t)tile * kSH;
+  float d4[4];
 #pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb) {
-    const int h0 = 16 * (b0 + bb) + 4 * g;
-    float d4[4];
+  for (int r = 0; r < 4; ++r) {
+    const int h = h0 + r;
+    float gg = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = h0 + r;
-      float gg = 0.f;
+    for (int a = 0; a < A; ++a) gg += dout[a] * sw3[a * kSH + h];
+    const float hv = h2[r];
+    d4[r] = gg * (1.f - hv * hv);
+    const float sb = s_row_sum(d4[r]);
+    if (j == 0) pa[h] = sb;
 #pragma unroll
-      for (int a = 0; a < A; ++a) gg += dout[a] * N.p[N.w3 + a * kSH + h];
-      const float hv = h2[bb][r];
-      d4[r] = gg * (1.f - hv * hv);
-      dz2T[(size_t)h * KP + R] = d4[r];
-      const float sb = s_row_sum(d4[r]);
-      if (j == 0) pa[h] = sb;
-#pragma unroll
-      for (int a = 0; a < A; ++a) {
-        const float sw = s_row_sum(dout[a] * hv);
-        if (j == 0) pa[kSH + a * kSH + h] = sw;
-      }
+    for (int a = 0; a < A; ++a) {
+      const float sw = s_row_sum(dout[a] * hv);
+      if (j == 0) pa[kSH + a * kSH + h] = sw;
     }
-    *reinterpret_cast<float4*>(dz2s + j * kSHS + h0) = float4{d4[0], d4[1], d4[2], d4[3]};
   }
+  *reinterpret_cast<float4*>(dz2s + j * kSHS + h0) = float4{d4[0], d4[1], d4[2], d4[3]};
   if (w == 0)
 #pragma unroll
     for (int a = 0; a < A; ++a) {
@@ -459,19 +440,18 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
       if (l == 0) pa[kSH + A * kSH + a] = t;
     }
   __syncthreads();
-  // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (rows of the transposed copy), dZ1 = dH1 ⊙ (1 − H1²)
-  contract(N.w2t + (size_t)(16 * b0 + j) * kSH, dz2s + j * kSHS);
+  // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (rows of the transposed copy; ring filled during the head), dZ1 = dH1 ⊙ (1 − H1²)
+  z = f32x4{0.f, 0.f, 0.f, 0.f};
+  s_run<16, true>(ring1, w2trow, kSH, dz2s + j * kSHS, g, z);
 #pragma unroll
-  for (int bb = 0; bb < kSBPW; ++bb) {
-    const int h0 = 16 * (b0 + bb) + 4 * g;
+  for (int r = 0; r < 4; ++r) dz2T[(size_t)(h0 + r) * KP + R] = d4[r];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float u = h1[bb][r];
-      const float d = z[bb][r] * (1.f - u * u);
-      dz1T[(size_t)(h0 + r) * KP + R] = d;
-      const float sb = s_row_sum(d);
-      if (j == 0) pb[h0 + r] = sb;
-    }
+  for (int r = 0; r < 4; ++r) {
+    const float u = h1[r];
+    const float d = z[r] * (1.f - u * u);
+    dz1T[(size_t)(h0 + r) * KP + R] = d;
+    const float sb = s_row_sum(d);
+    if (j == 0) pb[h0 + r] = sb;
   }
   // ---- the tile's loss sums (wave 0, rows in order), then the net's last tile
   if (w == 0 && g == 0)
@@ -483,9 +463,9 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     double* lp = POL ? W.lossa + (size_t)tile * NL : W.lossc + tile;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      double s = 0.0;
-      for (int q = 0; q < 16; ++q) s += ls_w[q][k];
-      lp[k] = s;
+      double sacc = 0.0;
+      for (int q = 0; q < 16; ++q) sacc += ls_w[q][k];
+      lp[k] = sacc;
     }
     __threadfence();
     const int ntiles = POL ? P.nA : P.nC;
@@ -509,7 +489,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     float ent = 0.0f;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      const float lsd = logf(expf(N.p[N.logstd + a]));
+      const float lsd = logf(expf(slogstd[a]));
       ent = a == 0 ? (0.5f + lc) + lsd : ent + ((0.5f + lc) + lsd);
     }
 #pragma unroll
@@ -529,8 +509,9 @@ __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
   __shared__ float dz2s[16 * kSHS];
   __shared__ float hp[kSW * kSMaxA][16];
   __shared__ double ls_w[16][2 + kSMaxA];
-  if ((int)blockIdx.x < P.nA) s_tile<A, true>(P, P.a, blockIdx.x, xs, h1s, dz2s, hp, ls_w);
-  else s_tile<1, false>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, hp, ls_w);
+  __shared__ float prm[2 * kSH + kSMaxA * kSH + 2 * kSMaxA];
+  if ((int)blockIdx.x < P.nA) s_tile<A, true>(P, P.a, blockIdx.x, xs, h1s, dz2s, prm, hp, ls_w);
+  else s_tile<1, false>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, prm, hp, ls_w);
 }
 
 // ---------------------------------------------------------------- launch 2
