@@ -160,8 +160,10 @@ class Ranks:
         """Every rank's queued work done, then all ranks together."""
         self.sync()
         if self.dist:
+            # the barrier is itself device work under RCCL: drain it too (one rank
+            # has nothing to wait for, so its window ends at the first sync)
             self.dist.barrier()
-        self.sync()
+            self.sync()
 
     def max(self, seconds):
         if not self.dist:

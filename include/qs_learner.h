@@ -24,6 +24,9 @@
  *   MeanStdNormalizer.__call__ / RunningMeanStd.update            qs_rms_update,
  *     (safe_control_gym normalization.py:13-120): torch float64      qs_rms_normalize
  *     column reductions per rollout step
+ *   MAPPOActorCritic.step sampling (agent.py:389-415,              qs_policy_sample,
+ *     distributions.py:9-33) and the rollout's done / mask /        qs_rollout_record
+ *     reward bookkeeping (MP:818-845): torch elementwise launches
  *
  * All pointers are device pointers; every call is asynchronous on `stream`
  * (hipStream_t as void*) and contains no host synchronisation, so it can be
@@ -290,6 +293,21 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
 int qs_rms_normalize(int64_t R, int32_t C, const float* x, const double* mean, const double* var, double eps,
                      double clip, float* out, void* stream);
 const char* qs_rms_last_error(void);
+
+/* The rollout's per-step glue (rollout.hip).  qs_policy_sample: mean [K][A]
+ * (the actor MLP's output), logstd [A], eps [K][A] (standard normal draws) →
+ * act [K][A] = (mean·loc_scale + exp(logstd)·eps)·(post_scale ? act_scale : 1)
+ * and logp [K] = Σ_a Normal(mean·loc_scale, exp(logstd)).log_prob(act)
+ * (MAPPOActorCritic.step's batched branch, agent.py:389-415; Normal,
+ * distributions.py:9-33), 1 <= A <= 4.  qs_rollout_record: done =
+ * terminated | truncated (uint8 [E]); mask_dst = 1 − done, done_dst = done,
+ * rew_dst = rew_src (each optional, float32 [E]) — MP:818-845's buffer
+ * writes. */
+int qs_policy_sample(int64_t K, int32_t A, const float* mean, const float* logstd, float loc_scale, float act_scale,
+                     int32_t post_scale, const float* eps, float* act, float* logp, void* stream);
+int qs_rollout_record(int64_t E, const uint8_t* terminated, const uint8_t* truncated, const float* rew_src,
+                      float* rew_dst, float* mask_dst, float* done_dst, void* stream);
+const char* qs_rollout_last_error(void);
 
 /* One PPO minibatch at small batch sizes (the reference's own learner shape,
  * learn_mappo.py:196-216: mini_batch_size 32 → 256 actor rows) in two

@@ -461,8 +461,9 @@ def _mlp256(fb, mlp, logstd, w2t, lib_struct):
 
 
 # widest actor output the fused actor step takes (qs_mlp3f_actor: A <= 4;
-# bench.py --fused-max-a)
-_F16_MAX_A = 1
+# bench.py --fused-max-a).  Measured on C4's 4-wide VEL actor: 237-250 us per
+# minibatch fused vs ~292 on the two-kernel path
+_F16_MAX_A = 4
 
 
 class _CriticTiles:
@@ -521,8 +522,8 @@ class _CriticTiles:
 
 
 def _f16_ok(mlp):
-    """The fused actor step takes the one-action-output actor with inputs <= 128
-    wide (the bench's ONE_D_* actors), up to _F16_MAX_A outputs; other widths
+    """The fused actor step takes actors with inputs <= 128 wide and 1 ..
+    _F16_MAX_A outputs (the ONE_D_* actors, Spiral's VEL actor); other widths
     keep the two-kernel path."""
     f0, _, f2 = mlp.fcs
     return 1 <= f2.out_features <= _F16_MAX_A and f0.in_features <= 128
@@ -563,25 +564,35 @@ class MLP(nn.Module):
         return (n1 in ok_n and n2 in ok_n and a <= (1 if n2 == 512 else 4)
                 and all(p.grad is not None and p.grad.is_contiguous() for p in self.parameters()))
 
-    def _infer_fused(self, x):
+    def _infer_fused(self, x, repack=True):
         """Inference forward (the rollout's batched actor, AG:389-415) through
-        qs_mlp3_fwd without the saved activations."""
+        qs_mlp3_fwd without the saved activations.  repack=False reuses the
+        pack image of the previous call (the rollout graph packs the weights at
+        its first control step only: they change between rollouts, not inside
+        one)."""
         lib, st = L.load(), _stream()
         f0, f1, f2 = self.fcs
         K, I, A = x.shape[0], x.shape[1], f2.out_features
-        pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device=x.device, dtype=torch.float32)
-        L.check(lib.qs_mlp3_pack(I, 256, L.ptr(f0.weight), L.ptr(f1.weight), L.ptr(pack), st), "qs_mlp3_pack")
+        pack = getattr(self, '_inf_pack', None)
+        if pack is None or pack.device != x.device or pack.numel() != int(lib.qs_mlp3_pack_floats(I)):
+            pack = self._inf_pack = torch.empty(int(lib.qs_mlp3_pack_floats(I)), device=x.device, dtype=torch.float32)
+            repack = True
+        if repack:
+            L.check(lib.qs_mlp3_pack(I, 256, L.ptr(f0.weight), L.ptr(f1.weight), L.ptr(pack), st), "qs_mlp3_pack")
         out = torch.empty((K, A), device=x.device, dtype=x.dtype)
         L.check(lib.qs_mlp3_fwd(K, I, 256, A, L.ptr(x), L.ptr(pack), L.ptr(f0.bias), L.ptr(f1.bias), L.ptr(f2.weight),
                                 L.ptr(f2.bias), None, None, L.ptr(out), st), "qs_mlp3_fwd")
         return out
 
-    def forward(self, x):
-        if (not torch.is_grad_enabled() and self._tanh3 and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32
-                and x.shape[1] <= 1024 and self.fcs[0].out_features == 256
+    def _infer_ok(self, x):
+        return (not torch.is_grad_enabled() and self._tanh3 and x.is_cuda and x.dim() == 2
+                and x.dtype == torch.float32 and x.shape[1] <= 1024 and self.fcs[0].out_features == 256
                 and self.fcs[1].out_features == 256 and self.fcs[2].out_features <= 4
-                and _m3_shape_ok(x.shape[0], x.shape[1])):
-            return self._infer_fused(x.contiguous())
+                and _m3_shape_ok(x.shape[0], x.shape[1]))
+
+    def forward(self, x, repack=True):
+        if self._infer_ok(x):
+            return self._infer_fused(x.contiguous(), repack)
         if self._fused_ok(x):
             f0, f1, f2 = self.fcs
             return _TanhMLP3.apply(x.contiguous(), f0.weight, f0.bias, f1.weight, f1.bias, f2.weight, f2.bias)
@@ -680,21 +691,47 @@ class MAPPOActorCritic(nn.Module):
         return self.actor
 
     @torch.no_grad()
-    def step(self, obs, get_global_obs_fn=None):
-        """Batched branch of AG:389-415 on device tensors: obs (E, D, O) or (E·D, O)."""
+    def step(self, obs, get_global_obs_fn=None, out=None, repack=True):
+        """Batched branch of AG:389-415 on device tensors: obs (E, D, O) or (E·D, O).
+        On the GPU with the fused inference MLP: the actor's forward, then one
+        qs_policy_sample launch for the sample and its log-probability (the
+        same torch.randn draws as the torch path); out = (act, logp) buffers of
+        shapes (E, D, A), (E, D, 1) receive them in place (the rollout slot).
+        repack: see MLP._infer_fused."""
         shape = obs.shape
         flat = obs.reshape(-1, self.obs_dim)
-        dist = self.actor.dist(flat)
-        act = dist.sample()
-        if self.action_scale != 1.0:
-            act = act * self.action_scale
-        logp = dist.log_prob(act)
         if len(shape) == 3:
             E, D = shape[0], shape[1]
         else:
             D = self.num_agents
             E = flat.shape[0] // D
-        return act.reshape(E, D, -1), torch.zeros(E, D, 1, device=obs.device), logp.reshape(E, D, 1)
+        pi = self.actor.pi_net
+        if pi._infer_ok(flat) and self.act_dim <= 4:
+            mean = pi(flat.contiguous(), repack)
+            K, A = mean.shape
+            eps = torch.randn((K, A), dtype=mean.dtype, device=mean.device)
+            if out is not None:
+                act, logp = out
+                if not (act.is_contiguous() and logp.is_contiguous() and act.numel() == K * A and logp.numel() == K
+                        and act.dtype == torch.float32 and logp.dtype == torch.float32):
+                    raise ValueError("step: out buffers must be contiguous float32 of (E, D, A) and (E, D, 1)")
+            else:
+                act = torch.empty((E, D, A), dtype=torch.float32, device=mean.device)
+                logp = torch.empty((E, D, 1), dtype=torch.float32, device=mean.device)
+            L.check(L.load().qs_policy_sample(K, A, L.ptr(mean), L.ptr(self.actor.logstd), float(self.actor.action_scale),
+                                              float(self.action_scale), int(self.action_scale != 1.0), L.ptr(eps),
+                                              L.ptr(act), L.ptr(logp), _stream()), "qs_policy_sample")
+            return act, torch.zeros(E, D, 1, device=obs.device), logp
+        dist = self.actor.dist(flat)
+        act = dist.sample()
+        if self.action_scale != 1.0:
+            act = act * self.action_scale
+        logp = dist.log_prob(act)
+        act, logp = act.reshape(E, D, -1), logp.reshape(E, D, 1)
+        if out is not None:
+            out[0].copy_(act)
+            out[1].copy_(logp)
+        return act, torch.zeros(E, D, 1, device=obs.device), logp
 
     @torch.no_grad()
     def act(self, obs):
@@ -882,7 +919,9 @@ class MAPPOAgent:
         # GEMMs (measured slower at the C3 shape)
         self.critic_tiles = kwargs.get('critic_tiles', False)
         # ... after the fused actor kernel, beside its weight gradients (False: beside the actor kernel)
-        self.critic_after_actor = kwargs.get('critic_after_actor', True)
+        # the critic's chain forked behind the fused actor launch (beside its
+        # weight-gradient GEMMs) rather than beside it; None: for the critic tiles
+        self.critic_after_actor = kwargs.get('critic_after_actor', None)
         # minibatches of at most _SMALL_MAX_ROWS actor rows on qs_ppo_small_step (one
         # rank); False: always the split-K direct iteration
         self.small = kwargs.get('small', True)
@@ -1119,7 +1158,10 @@ class MAPPOAgent:
             if self.side_stream:
                 own = not multi and self.critic_adam_side
                 self._side.wait_stream(cur)
-                if self.critic_after_actor and isinstance(self._ws_critic, _CriticTiles):
+                after = self.critic_after_actor
+                if after is None:
+                    after = isinstance(self._ws_critic, _CriticTiles)
+                if after:
                     # the fused actor holds every CU's whole register file: a critic
                     # running beside it delays its workgroups.  The critic's tiles
                     # follow it instead, beside the actor's weight-gradient GEMMs

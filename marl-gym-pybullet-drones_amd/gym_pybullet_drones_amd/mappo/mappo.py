@@ -27,6 +27,7 @@ every terminal state: one count per (drone, reason), the categories of the reaso
 strings (crash / flip / out_of_bounds, MH:225-238) — the counts that loop was
 written to collect.
 """
+import ctypes
 import os
 import random
 import time
@@ -36,6 +37,7 @@ import numpy as np
 import torch
 import torch.distributed as tdist
 
+from .. import _lib as L
 from ..utils.enums import ActionType, Physics
 from ..vec_env import SwarmVecEnv, VecRecordEpisodeStatistics
 from .agent import MAPPOAgent
@@ -342,21 +344,35 @@ class MAPPO:
         """One control step of every env, entirely on the device (MP:647-1027)."""
         swarm = self.env.venv.swarm
         obs_t = rollouts.next_obs_slots[t]
-        act, _, logp = self.agent.ac.step(obs_t)
-        rollouts.act[t].copy_(act)
-        rollouts.logp[t].copy_(logp)
+        # the actor's pack image is refreshed at the first step of a rollout (the
+        # weights only change between rollouts); act / logp land in the slot
+        self.agent.ac.step(obs_t, out=(rollouts.act[t], rollouts.logp[t]), repack=t == 0)
         target = self._raw_obs if self.norm_obs else rollouts.next_obs_slots[t + 1]
         if not warmup:
             swarm.step(rollouts.act[t], obs=target, reward=self._rew_raw[t], terminated=self._te[t],
                        truncated=self._tr[t], reasons=self._reasons[t])
-        done = (self._te[t] | self._tr[t]).float()
-        rew = self._rew_raw[t]
         if self.norm_obs:
-            rollouts.next_obs_slots[t + 1].copy_(self.obs_normalizer(self._raw_obs))
+            self.obs_normalizer(self._raw_obs, out=rollouts.next_obs_slots[t + 1])
+        E = self._te.shape[1]
+        native = self._te.is_cuda and self._rew_raw.dtype == torch.float32
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream) if native else None
+        if st is not None and not self.norm_reward:
+            # done = terminated | truncated, the mask and the reward in one launch (MP:818-845)
+            L.check(L.load().qs_rollout_record(E, L.ptr(self._te[t]), L.ptr(self._tr[t]), L.ptr(self._rew_raw[t]),
+                                               L.ptr(rollouts.rew_env[t]), L.ptr(rollouts.mask_env[t]), None, st),
+                    "qs_rollout_record")
+            return
+        if st is not None:
+            done = torch.empty((E,), dtype=torch.float32, device=self._te.device)
+            L.check(L.load().qs_rollout_record(E, L.ptr(self._te[t]), L.ptr(self._tr[t]), None, None,
+                                               L.ptr(rollouts.mask_env[t]), L.ptr(done), st), "qs_rollout_record")
+        else:
+            done = (self._te[t] | self._tr[t]).float()
+            rollouts.mask_env[t].copy_(1 - done)
+        rew = self._rew_raw[t]
         if self.norm_reward:
             rew = self.reward_normalizer(rew, done)
         rollouts.rew_env[t].copy_(rew)
-        rollouts.mask_env[t].copy_(1 - done)
 
     def _capture_rollout(self, rollouts):
         # warm-up: load every torch kernel of the step outside the capture (lazy module

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../marl-gym-pybullet-drones_amd"
 name=$1; extra=$2
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -I../include -DQS_DEV_BUILD $extra"
 mkdir -p build/dev/$name
-for u in quadswarm step_mh step_spiral step_marl learner normalizer ppo_small; do
+for u in quadswarm step_mh step_spiral step_marl learner normalizer ppo_small rollout; do
   /opt/rocm/bin/hipcc $FLAGS -c -o build/dev/$name/$u.o csrc/$u.hip &
 done
 wait

@@ -5,7 +5,10 @@ variants are compared on the same box:
   ref  D=8,  O=27,  A=1, mini_batch_size 32   (learn_mappo.py:199: 256 actor rows)
   C4   D=5,  O=119, A=4, mini_batch_size 4096 (Spiral VEL)
 plus the critic-tile kernels alone at the C3 shape.
-  python scripts/learner_mb.py [C3|ref|C4|kernels ...]"""
+plus `ablate`: the C3 minibatch with one piece at a time made a no-op (the
+numbers are meaningless then, the time is what the rest costs: the piece's
+share of the critical path).
+  python scripts/learner_mb.py [C3|ref|C4|kernels|scale|ablate ...]"""
 import ctypes
 import os
 import sys
@@ -102,6 +105,39 @@ def kernels(mb=None):
               f"{2 * mb * 256 * M / us / 1e6:6.1f} TFLOP/s", flush=True)
 
 
+def ablate():
+    """C3 per-minibatch time with each piece removed (a no-op launch)."""
+    lib = L.load()
+    noop = lambda *a: 0
+    M3, F16, FB = agent_mod._M3Work, agent_mod._F16Work, agent_mod.FlatBuffers
+    pieces = {
+        "actor kernel": [(lib, "qs_mlp3f_actor", noop)],
+        "actor dW2": [(F16, "_splitk_rm", lambda self, dst, dy, x, part, S:
+                       None if dst is self.mlp.fcs[1].weight.grad else ORIG_RM(self, dst, dy, x, part, S))],
+        "actor dW1": [(F16, "_splitk_rm", lambda self, dst, dy, x, part, S:
+                       None if dst is self.mlp.fcs[0].weight.grad else ORIG_RM(self, dst, dy, x, part, S))],
+        "critic (all)": [(lib, "qs_mlp3_fwd_rows", noop), (lib, "qs_value_head", noop), (lib, "qs_mlp3_bwd", noop),
+                         (M3, "_splitk", lambda *a: None)],
+        "critic GEMMs": [(M3, "_splitk", lambda *a: None)],
+        "sum+adam": [(FB, "sum_adam", staticmethod(lambda *a: None))],
+        "sums (pre-adam)": [(agent_mod, "_flush_sums", lambda *a: None)],
+    }
+    global ORIG_RM
+    ORIG_RM = F16._splitk_rm
+    base, path = per_minibatch_us("C3", critic_tiles=False)
+    print(f"ablate  full                       {base:8.1f} us/minibatch  [{path}]", flush=True)
+    for name, patches in pieces.items():
+        saved = [(o, a, o.__dict__[a] if isinstance(o, type) else getattr(o, a)) for o, a, _ in patches]
+        for o, a, f in patches:
+            setattr(o, a, f)
+        try:
+            us, _ = per_minibatch_us("C3", critic_tiles=False)
+        finally:
+            for o, a, f in saved:
+                setattr(o, a, f)
+        print(f"ablate  without {name:18s} {us:8.1f} us/minibatch  (share {base - us:6.1f})", flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["kernels", "C3", "ref", "C4"]
     if "kernels" in which:
@@ -110,20 +146,31 @@ def main():
         for mb in (256, 1024, 2048):
             kernels(mb)
     if "C3" in which:
-        for v in (dict(critic_tiles=True), dict(critic_tiles=True, critic_after_actor=False), dict(critic_tiles=False),
-                  dict(critic_tiles=True, side_stream=False), dict(critic_tiles=False, side_stream=False)):
+        for v in (dict(critic_tiles=False), dict(critic_tiles=False, critic_after_actor=True),
+                  dict(critic_tiles=False, critic_adam_side=True),
+                  dict(critic_tiles=False, critic_after_actor=True, critic_adam_side=True),
+                  dict(critic_tiles=True), dict(critic_tiles=False, side_stream=False)):
             us, path = per_minibatch_us("C3", **v)
             print(f"C3  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "ref" in which:
         for v in (dict(small=True), dict(small=False)):
             us, path = per_minibatch_us("ref", reps=2, **v)
             print(f"ref {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "dw1" in which:
+        # dW1's row-chunk GEMMs: rows per chunk (the default: 1 024)
+        for m in (1024, 2048, 4096, 8192):
+            agent_mod._SPLITK_MIN_ROWS[(32768, 27)] = m
+            us, path = per_minibatch_us("C3", critic_tiles=False)
+            print(f"C3  dW1 chunk rows {m:<37d} {us:8.1f} us/minibatch  [{path}]", flush=True)
+        agent_mod._SPLITK_MIN_ROWS.pop((32768, 27))
+    if "ablate" in which:
+        ablate()
     if "C4" in which:
         for a in (1, 4):
             agent_mod._F16_MAX_A = a
             us, path = per_minibatch_us("C4")
             print(f"C4  fused_max_a={a:<43d} {us:8.1f} us/minibatch  [{path}]", flush=True)
-        agent_mod._F16_MAX_A = 1
+        agent_mod._F16_MAX_A = 4
 
 
 if __name__ == "__main__":
