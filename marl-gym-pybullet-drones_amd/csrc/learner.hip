@@ -2322,7 +2322,10 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
 // the 8-wave-per-tile kernels below 512 tiles (too few waves otherwise) and for
 // wide inputs (their X tile is staged through LDS once, where the 4-tile
 // kernel gathers every lane's row per k-quad)
-static bool m3_wide(int64_t K, int32_t I) { return K < 16384 || I > 64; }
+#ifndef QS_M3_WIDE_I
+#define QS_M3_WIDE_I 64   // widest input of the 4-wave kernel (dev builds probe others)
+#endif
+static bool m3_wide(int64_t K, int32_t I) { return K < 16384 || I > QS_M3_WIDE_I; }
 int32_t qs_mlp3_tiles(int64_t K, int32_t I) { return (int32_t)(m3_wide(K, I) ? (K + 31) / 32 : (K + 127) / 128); }   // partial rows
 
 int64_t qs_mlp3_pack_floats(int32_t I) {

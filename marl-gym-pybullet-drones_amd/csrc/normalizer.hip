@@ -9,9 +9,9 @@
 // float64 column reductions (a Welford reduce_kernel of ~200 µs and a mean of
 // ~90 µs at C4's 8 192 × 135) were most of a C4 rollout step.
 //
-// Here the moments are two launches: one workgroup per 16-row tile reads its
-// contiguous span once into LDS and forms every column's tile mean and sum of
-// squared deviations (two passes from LDS, float64); then the tiles are merged
+// Here the moments are two launches: one thread per column of each 64-row tile
+// holds the tile's column in registers and forms its mean and sum of squared
+// deviations (two passes, float64); then the tiles are merged
 // per column by 64 threads and a fixed LDS tree (the batch mean first, then
 // the parallel-variance sum Σ M2_t + n_t·(mean_t − mean)²) and
 // normalization.py:42-60's update applied in place in its operation order.
@@ -32,7 +32,7 @@ thread_local std::string g_nerr;
 int nfail(int code, const std::string& m) { g_nerr = m; return code; }
 
 constexpr int kRmsBlock = 256;
-constexpr int kRmsRows = 16;        // rows per tile (one workgroup each)
+constexpr int kRmsRows = 64;        // rows per tile (one thread per column each)
 constexpr int kRmsMergeCols = 4;    // columns per merge workgroup (64 threads each)
 
 struct RmsShape {
@@ -48,36 +48,39 @@ __host__ __device__ inline RmsShape rms_shape(long long R, int C) {
   return s;
 }
 
-// work: [counter (64 B)] [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(16, R − 16t) rows)
+// work: [counter (64 B)] [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(64, R − 64t) rows)
 inline long long rms_work_bytes(const RmsShape& s) { return 64 + 16LL * s.GR * s.C; }
 
-// Launch 1: one workgroup per 16-row tile; the tile's rows are one contiguous
-// span of x, read once (coalesced) into LDS, then every column's mean and sum
-// of squared deviations over the tile's rows (two passes from LDS, float64).
+// Launch 1: one thread per (tile, column): the tile's 64 rows of the column
+// into registers (every load issued before the first use; a wave's loads are
+// 64 consecutive columns of a row), then the tile mean and the sum of squared
+// deviations from it (two passes over the registers, float64).
 __global__ void __launch_bounds__(kRmsBlock) rms_tile_kernel(RmsShape s, const float* __restrict__ x,
                                                              unsigned* __restrict__ work) {
-  extern __shared__ float tile[];   // [rows][C]
-  const int t = threadIdx.x, b = blockIdx.x;
+  const int c = blockIdx.y * kRmsBlock + threadIdx.x, b = blockIdx.x;
+  if (c >= s.C) return;
   const long long r0 = (long long)b * kRmsRows;
   const int nr = (int)min((long long)kRmsRows, s.R - r0);
-  const float* src = x + r0 * s.C;
-  const int n = nr * s.C;
-  for (int i = t; i < n; i += kRmsBlock) tile[i] = src[i];
-  __syncthreads();
-  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
-  double* m2_b = mean_b + (size_t)s.GR * s.C;
-  for (int c = t; c < s.C; c += kRmsBlock) {
-    double a = 0.0;
-    for (int r = 0; r < nr; ++r) a += (double)tile[r * s.C + c];
-    const double m = a / (double)nr;
-    double q = 0.0;
-    for (int r = 0; r < nr; ++r) {
-      const double d = (double)tile[r * s.C + c] - m;
+  const float* src = x + r0 * s.C + c;
+  float v[kRmsRows];
+#pragma unroll
+  for (int r = 0; r < kRmsRows; ++r) v[r] = r < nr ? __builtin_nontemporal_load(src + (long long)r * s.C) : 0.0f;
+  double a = 0.0;
+#pragma unroll
+  for (int r = 0; r < kRmsRows; ++r)
+    if (r < nr) a += (double)v[r];
+  const double m = a / (double)nr;
+  double q = 0.0;
+#pragma unroll
+  for (int r = 0; r < kRmsRows; ++r)
+    if (r < nr) {
+      const double d = (double)v[r] - m;
       q += d * d;
     }
-    mean_b[(size_t)b * s.C + c] = m;
-    m2_b[(size_t)b * s.C + c] = q;
-  }
+  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
+  double* m2_b = mean_b + (size_t)s.GR * s.C;
+  mean_b[(size_t)b * s.C + c] = m;
+  m2_b[(size_t)b * s.C + c] = q;
 }
 
 // Launch 2: kRmsMergeCols columns per workgroup, 64 threads per column, each
@@ -156,19 +159,43 @@ __global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double
 
 // out = clip((x − mean) / sqrt(var + eps), −clip, clip) in float64, stored as
 // float32 (MeanStdNormalizer.__call__, normalization.py:110-113); NaN passes
-// through like torch.clamp
-__global__ void __launch_bounds__(kRmsBlock) rms_normalize_kernel(long long R, int C, const float* __restrict__ x,
+// through like torch.clamp.  Over the flat [R·C] array, four consecutive
+// elements per thread (one 16-byte load and store where x and out allow it),
+// their columns from one division.
+__device__ __forceinline__ float rms_norm1(float xv, const double* __restrict__ mean, const double* __restrict__ var,
+                                           int c, double eps, double clip) {
+  double y = ((double)xv - mean[c]) / sqrt(var[c] + eps);
+  y = y < -clip ? -clip : (y > clip ? clip : y);
+  return (float)y;
+}
+
+typedef float rms_f4 __attribute__((ext_vector_type(4)));
+
+template <bool VEC>
+__global__ void __launch_bounds__(kRmsBlock) rms_normalize_kernel(long long N, int C, const float* __restrict__ x,
                                                                    const double* __restrict__ mean,
                                                                    const double* __restrict__ var, double eps,
                                                                    double clip, float* __restrict__ out) {
-  // one row per workgroup step (no per-element modulo): threads over its columns
-  for (long long r = blockIdx.x; r < R; r += gridDim.x) {
-    const float* xr = x + r * C;
-    float* orow = out + r * C;
-    for (int c = threadIdx.x; c < C; c += kRmsBlock) {
-      double y = ((double)xr[c] - mean[c]) / sqrt(var[c] + eps);
-      y = y < -clip ? -clip : (y > clip ? clip : y);
-      orow[c] = (float)y;
+  const long long nq = (N + 3) / 4;
+  for (long long q = (long long)blockIdx.x * kRmsBlock + threadIdx.x; q < nq; q += (long long)gridDim.x * kRmsBlock) {
+    const long long i0 = q * 4;
+    int c = (int)(i0 % C);
+    if (VEC && i0 + 4 <= N) {
+      const rms_f4 v = __builtin_nontemporal_load(reinterpret_cast<const rms_f4*>(x) + q);
+      rms_f4 o;
+      o.x = rms_norm1(v.x, mean, var, c, eps, clip);
+      c = c + 1 == C ? 0 : c + 1;
+      o.y = rms_norm1(v.y, mean, var, c, eps, clip);
+      c = c + 1 == C ? 0 : c + 1;
+      o.z = rms_norm1(v.z, mean, var, c, eps, clip);
+      c = c + 1 == C ? 0 : c + 1;
+      o.w = rms_norm1(v.w, mean, var, c, eps, clip);
+      __builtin_nontemporal_store(o, reinterpret_cast<rms_f4*>(out) + q);
+    } else {
+      for (long long i = i0; i < N && i < i0 + 4; ++i) {
+        out[i] = rms_norm1(x[i], mean, var, c, eps, clip);
+        c = c + 1 == C ? 0 : c + 1;
+      }
     }
   }
 }
@@ -187,12 +214,12 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
                   void* work, void* stream) {
   if (R <= 0 || C <= 0 || !x || !work || (!sums && (!mean || !var || !count)))
     return nfail(QS_E_INVALID, "qs_rms_update: bad argument");
-  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || (long long)C * kRmsRows * 4 > 64 * 1024)
-    return nfail(QS_E_INVALID, "qs_rms_update: batch too large (at most 1 024 columns)");
+  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || C > 65535 * kRmsBlock || (R + kRmsRows - 1) / kRmsRows > (1LL << 31) - 1)
+    return nfail(QS_E_INVALID, "qs_rms_update: batch too large");
   const RmsShape s = rms_shape(R, C);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR), dim3(kRmsBlock), (size_t)C * kRmsRows * 4, st, s, x,
-                     (unsigned*)work);
+  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR, (unsigned)((C + kRmsBlock - 1) / kRmsBlock)), dim3(kRmsBlock),
+                     0, st, s, x, (unsigned*)work);
   hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)((C + kRmsMergeCols - 1) / kRmsMergeCols)), dim3(kRmsBlock), 0,
                      st, s, mean, var, count, sums, (unsigned*)work);
   hipError_t e = hipGetLastError();
@@ -202,9 +229,15 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
 int qs_rms_normalize(int64_t R, int32_t C, const float* x, const double* mean, const double* var, double eps,
                      double clip, float* out, void* stream) {
   if (R <= 0 || C <= 0 || !x || !mean || !var || !out) return nfail(QS_E_INVALID, "qs_rms_normalize: bad argument");
-  const long long grid = std::min<long long>(R, 8192);
-  hipLaunchKernelGGL(rms_normalize_kernel, dim3((unsigned)grid), dim3(kRmsBlock), 0, (hipStream_t)stream, (long long)R,
-                     (int)C, x, mean, var, eps, clip, out);
+  const long long N = (long long)R * C, nq = (N + 3) / 4;
+  const unsigned grid = (unsigned)std::min<long long>((nq + kRmsBlock - 1) / kRmsBlock, 8192);
+  const bool vec = ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL(rms_normalize_kernel<true>, dim3(grid), dim3(kRmsBlock), 0, (hipStream_t)stream, N, (int)C, x,
+                       mean, var, eps, clip, out);
+  else
+    hipLaunchKernelGGL(rms_normalize_kernel<false>, dim3(grid), dim3(kRmsBlock), 0, (hipStream_t)stream, N, (int)C, x,
+                       mean, var, eps, clip, out);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_normalize: ") + hipGetErrorString(e));
 }

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-it}
 PT="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
-timeout -k 10 300 $PT tests/test_gpu_normalizer.py tests/test_gpu_learner.py -k "small or norm or rms or side_stream" > gpurun_out/${TAG}_new.log 2>&1
+timeout -k 10 300 $PT tests/test_gpu_rollout_glue.py tests/test_gpu_train_step.py tests/test_gpu_normalizer.py tests/test_gpu_learner.py -k "${TESTK:-small or norm or rms or side_stream or sample or record or step or train}" > gpurun_out/${TAG}_new.log 2>&1
 rc=$?; tail -3 gpurun_out/${TAG}_new.log; [ $rc -eq 0 ] || exit $rc
 if [ "${FULL:-1}" = "1" ]; then
   timeout -k 10 600 $PT tests -m gpu > gpurun_out/${TAG}_pytest.log 2>&1
