@@ -2322,10 +2322,12 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
 // the 8-wave-per-tile kernels below 512 tiles (too few waves otherwise) and for
 // wide inputs (their X tile is staged through LDS once, where the 4-tile
 // kernel gathers every lane's row per k-quad)
-#ifndef QS_M3_WIDE_I
-#define QS_M3_WIDE_I 64   // widest input of the 4-wave kernel (dev builds probe others)
-#endif
-static bool m3_wide(int64_t K, int32_t I) { return K < 16384 || I > QS_M3_WIDE_I; }
+// The 4-wave kernel (128 rows per workgroup, one workgroup per CU) below 16 384
+// rows leaves CUs idle; above 64 inputs its per-lane X loads cost more than the
+// 8-wave kernel's LDS tile, except with whole rounds of workgroups (measured
+// with scripts/mlp3_fwd_probe.py: K 65 536 × I 72 116.5 µs vs 133.6 wide,
+// K 40 960 × I 119 127.4 vs 96.7)
+static bool m3_wide(int64_t K, int32_t I) { return K < 16384 || I > (K >= 65536 ? 72 : 64); }
 int32_t qs_mlp3_tiles(int64_t K, int32_t I) { return (int32_t)(m3_wide(K, I) ? (K + 31) / 32 : (K + 127) / 128); }   // partial rows
 
 int64_t qs_mlp3_pack_floats(int32_t I) {

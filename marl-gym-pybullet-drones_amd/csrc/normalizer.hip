@@ -9,9 +9,9 @@
 // float64 column reductions (a Welford reduce_kernel of ~200 µs and a mean of
 // ~90 µs at C4's 8 192 × 135) were most of a C4 rollout step.
 //
-// Here the moments are two launches: one thread per column of each 64-row tile
-// holds the tile's column in registers and forms its mean and sum of squared
-// deviations (two passes, float64); then the tiles are merged
+// Here the moments are two launches: each 64-row tile's columns are held in
+// registers (16 rows per wave) and give the tile's column means and sums of
+// squared deviations (two passes, float64); then the tiles are merged
 // per column by 64 threads and a fixed LDS tree (the batch mean first, then
 // the parallel-variance sum Σ M2_t + n_t·(mean_t − mean)²) and
 // normalization.py:42-60's update applied in place in its operation order.
@@ -51,36 +51,53 @@ __host__ __device__ inline RmsShape rms_shape(long long R, int C) {
 // work: [counter (64 B)] [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(64, R − 64t) rows)
 inline long long rms_work_bytes(const RmsShape& s) { return 64 + 16LL * s.GR * s.C; }
 
-// Launch 1: one thread per (tile, column): the tile's 64 rows of the column
-// into registers (every load issued before the first use; a wave's loads are
-// 64 consecutive columns of a row), then the tile mean and the sum of squared
-// deviations from it (two passes over the registers, float64).
+// Launch 1: one workgroup per (64-row tile, 64 columns); wave w holds rows
+// 16w .. 16w+15 of the lane's column in registers (every load issued before
+// the first use; a wave's load is 64 consecutive columns of one row).  The
+// tile mean, then the sum of squared deviations from it (two passes over the
+// registers, float64), each combined over the four waves in wave order.
+constexpr int kRmsRowsW = kRmsRows / 4;
 __global__ void __launch_bounds__(kRmsBlock) rms_tile_kernel(RmsShape s, const float* __restrict__ x,
                                                              unsigned* __restrict__ work) {
-  const int c = blockIdx.y * kRmsBlock + threadIdx.x, b = blockIdx.x;
-  if (c >= s.C) return;
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane, b = blockIdx.x;
+  const bool cv = c < s.C;
   const long long r0 = (long long)b * kRmsRows;
   const int nr = (int)min((long long)kRmsRows, s.R - r0);
-  const float* src = x + r0 * s.C + c;
-  float v[kRmsRows];
+  const int rw = kRmsRowsW * w;
+  const float* src = x + (r0 + rw) * s.C + (cv ? c : 0);
+  float v[kRmsRowsW];
+  if (nr == kRmsRows) {
 #pragma unroll
-  for (int r = 0; r < kRmsRows; ++r) v[r] = r < nr ? __builtin_nontemporal_load(src + (long long)r * s.C) : 0.0f;
+    for (int r = 0; r < kRmsRowsW; ++r) v[r] = cv ? __builtin_nontemporal_load(src + (long long)r * s.C) : 0.0f;
+  } else {
+#pragma unroll
+    for (int r = 0; r < kRmsRowsW; ++r) v[r] = cv && rw + r < nr ? src[(long long)r * s.C] : 0.0f;
+  }
   double a = 0.0;
 #pragma unroll
-  for (int r = 0; r < kRmsRows; ++r)
-    if (r < nr) a += (double)v[r];
-  const double m = a / (double)nr;
+  for (int r = 0; r < kRmsRowsW; ++r)
+    if (rw + r < nr) a += (double)v[r];
+  red[w][lane] = a;
+  __syncthreads();
+  const double m = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) / (double)nr;
   double q = 0.0;
 #pragma unroll
-  for (int r = 0; r < kRmsRows; ++r)
-    if (r < nr) {
+  for (int r = 0; r < kRmsRowsW; ++r)
+    if (rw + r < nr) {
       const double d = (double)v[r] - m;
       q += d * d;
     }
-  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
-  double* m2_b = mean_b + (size_t)s.GR * s.C;
-  mean_b[(size_t)b * s.C + c] = m;
-  m2_b[(size_t)b * s.C + c] = q;
+  __syncthreads();
+  red[w][lane] = q;
+  __syncthreads();
+  if (w == 0 && cv) {
+    double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
+    double* m2_b = mean_b + (size_t)s.GR * s.C;
+    mean_b[(size_t)b * s.C + c] = m;
+    m2_b[(size_t)b * s.C + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  }
 }
 
 // Launch 2: kRmsMergeCols columns per workgroup, 64 threads per column, each
@@ -159,23 +176,35 @@ __global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double
 
 // out = clip((x − mean) / sqrt(var + eps), −clip, clip) in float64, stored as
 // float32 (MeanStdNormalizer.__call__, normalization.py:110-113); NaN passes
-// through like torch.clamp.  Over the flat [R·C] array, four consecutive
-// elements per thread (one 16-byte load and store where x and out allow it),
-// their columns from one division.
-__device__ __forceinline__ float rms_norm1(float xv, const double* __restrict__ mean, const double* __restrict__ var,
-                                           int c, double eps, double clip) {
-  double y = ((double)xv - mean[c]) / sqrt(var[c] + eps);
+// through like torch.clamp.  Each workgroup first forms sqrt(var + eps) of
+// every column once into LDS (with the means), then walks the flat [R·C]
+// array four consecutive elements per thread (one 16-byte load and store
+// where x and out allow it), their columns from one division.
+constexpr int kRmsNormLdsCols = 2048;   // columns staged in LDS (wider: read from global)
+
+__device__ __forceinline__ float rms_norm1(float xv, double m, double sd, double clip) {
+  double y = ((double)xv - m) / sd;
   y = y < -clip ? -clip : (y > clip ? clip : y);
   return (float)y;
 }
 
 typedef float rms_f4 __attribute__((ext_vector_type(4)));
 
-template <bool VEC>
+template <bool VEC, bool LDS>
 __global__ void __launch_bounds__(kRmsBlock) rms_normalize_kernel(long long N, int C, const float* __restrict__ x,
                                                                    const double* __restrict__ mean,
                                                                    const double* __restrict__ var, double eps,
                                                                    double clip, float* __restrict__ out) {
+  __shared__ double smean[LDS ? kRmsNormLdsCols : 1], ssd[LDS ? kRmsNormLdsCols : 1];
+  if constexpr (LDS) {
+    for (int c = threadIdx.x; c < C; c += kRmsBlock) {
+      smean[c] = mean[c];
+      ssd[c] = sqrt(var[c] + eps);
+    }
+    __syncthreads();
+  }
+  auto mu = [&](int c) { return LDS ? smean[c] : mean[c]; };
+  auto sd = [&](int c) { return LDS ? ssd[c] : sqrt(var[c] + eps); };
   const long long nq = (N + 3) / 4;
   for (long long q = (long long)blockIdx.x * kRmsBlock + threadIdx.x; q < nq; q += (long long)gridDim.x * kRmsBlock) {
     const long long i0 = q * 4;
@@ -183,17 +212,17 @@ __global__ void __launch_bounds__(kRmsBlock) rms_normalize_kernel(long long N, i
     if (VEC && i0 + 4 <= N) {
       const rms_f4 v = __builtin_nontemporal_load(reinterpret_cast<const rms_f4*>(x) + q);
       rms_f4 o;
-      o.x = rms_norm1(v.x, mean, var, c, eps, clip);
+      o.x = rms_norm1(v.x, mu(c), sd(c), clip);
       c = c + 1 == C ? 0 : c + 1;
-      o.y = rms_norm1(v.y, mean, var, c, eps, clip);
+      o.y = rms_norm1(v.y, mu(c), sd(c), clip);
       c = c + 1 == C ? 0 : c + 1;
-      o.z = rms_norm1(v.z, mean, var, c, eps, clip);
+      o.z = rms_norm1(v.z, mu(c), sd(c), clip);
       c = c + 1 == C ? 0 : c + 1;
-      o.w = rms_norm1(v.w, mean, var, c, eps, clip);
+      o.w = rms_norm1(v.w, mu(c), sd(c), clip);
       __builtin_nontemporal_store(o, reinterpret_cast<rms_f4*>(out) + q);
     } else {
       for (long long i = i0; i < N && i < i0 + 4; ++i) {
-        out[i] = rms_norm1(x[i], mean, var, c, eps, clip);
+        out[i] = rms_norm1(x[i], mu(c), sd(c), clip);
         c = c + 1 == C ? 0 : c + 1;
       }
     }
@@ -214,11 +243,11 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
                   void* work, void* stream) {
   if (R <= 0 || C <= 0 || !x || !work || (!sums && (!mean || !var || !count)))
     return nfail(QS_E_INVALID, "qs_rms_update: bad argument");
-  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || C > 65535 * kRmsBlock || (R + kRmsRows - 1) / kRmsRows > (1LL << 31) - 1)
+  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || C > 65535 * 64 || (R + kRmsRows - 1) / kRmsRows > (1LL << 31) - 1)
     return nfail(QS_E_INVALID, "qs_rms_update: batch too large");
   const RmsShape s = rms_shape(R, C);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR, (unsigned)((C + kRmsBlock - 1) / kRmsBlock)), dim3(kRmsBlock),
+  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR, (unsigned)((C + 63) / 64)), dim3(kRmsBlock),
                      0, st, s, x, (unsigned*)work);
   hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)((C + kRmsMergeCols - 1) / kRmsMergeCols)), dim3(kRmsBlock), 0,
                      st, s, mean, var, count, sums, (unsigned*)work);
@@ -230,14 +259,15 @@ int qs_rms_normalize(int64_t R, int32_t C, const float* x, const double* mean, c
                      double clip, float* out, void* stream) {
   if (R <= 0 || C <= 0 || !x || !mean || !var || !out) return nfail(QS_E_INVALID, "qs_rms_normalize: bad argument");
   const long long N = (long long)R * C, nq = (N + 3) / 4;
-  const unsigned grid = (unsigned)std::min<long long>((nq + kRmsBlock - 1) / kRmsBlock, 8192);
-  const bool vec = ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  if (vec)
-    hipLaunchKernelGGL(rms_normalize_kernel<true>, dim3(grid), dim3(kRmsBlock), 0, (hipStream_t)stream, N, (int)C, x,
-                       mean, var, eps, clip, out);
-  else
-    hipLaunchKernelGGL(rms_normalize_kernel<false>, dim3(grid), dim3(kRmsBlock), 0, (hipStream_t)stream, N, (int)C, x,
-                       mean, var, eps, clip, out);
+  // a grid of at most 1 024 workgroups: each stages the columns' statistics once
+  const unsigned grid = (unsigned)std::min<long long>((nq + kRmsBlock - 1) / kRmsBlock, 1024);
+  const bool vec = ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0), lds = C <= kRmsNormLdsCols;
+  hipStream_t st = (hipStream_t)stream;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kRmsBlock), 0, st, N, (int)C, x, mean, var, eps, clip, out);
+  };
+  if (vec) lds ? go(rms_normalize_kernel<true, true>) : go(rms_normalize_kernel<true, false>);
+  else lds ? go(rms_normalize_kernel<false, true>) : go(rms_normalize_kernel<false, false>);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_normalize: ") + hipGetErrorString(e));
 }

@@ -105,8 +105,8 @@ def kernels(mb=None):
               f"{2 * mb * 256 * M / us / 1e6:6.1f} TFLOP/s", flush=True)
 
 
-def ablate():
-    """C3 per-minibatch time with each piece removed (a no-op launch)."""
+def ablate(shape="C3"):
+    """Per-minibatch time with each piece removed (a no-op launch)."""
     lib = L.load()
     noop = lambda *a: 0
     M3, F16, FB = agent_mod._M3Work, agent_mod._F16Work, agent_mod.FlatBuffers
@@ -124,18 +124,18 @@ def ablate():
     }
     global ORIG_RM
     ORIG_RM = F16._splitk_rm
-    base, path = per_minibatch_us("C3", critic_tiles=False)
-    print(f"ablate  full                       {base:8.1f} us/minibatch  [{path}]", flush=True)
+    base, path = per_minibatch_us(shape, critic_tiles=False)
+    print(f"ablate {shape} full                       {base:8.1f} us/minibatch  [{path}]", flush=True)
     for name, patches in pieces.items():
         saved = [(o, a, o.__dict__[a] if isinstance(o, type) else getattr(o, a)) for o, a, _ in patches]
         for o, a, f in patches:
             setattr(o, a, f)
         try:
-            us, _ = per_minibatch_us("C3", critic_tiles=False)
+            us, _ = per_minibatch_us(shape, critic_tiles=False)
         finally:
             for o, a, f in saved:
                 setattr(o, a, f)
-        print(f"ablate  without {name:18s} {us:8.1f} us/minibatch  (share {base - us:6.1f})", flush=True)
+        print(f"ablate {shape} without {name:18s} {us:8.1f} us/minibatch  (share {base - us:6.1f})", flush=True)
 
 
 def main():
@@ -165,6 +165,8 @@ def main():
         agent_mod._SPLITK_MIN_ROWS.pop((32768, 27))
     if "ablate" in which:
         ablate()
+    if "ablate4" in which:
+        ablate("C4")
     if "C4" in which:
         for a in (1, 4):
             agent_mod._F16_MAX_A = a

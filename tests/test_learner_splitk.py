@@ -68,7 +68,7 @@ def _plain(net, x, g):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows,din,hidden,A", [(32768, 27, 256, 1), (4096, 216, 256, 1), (8192, 72, 256, 4),
-                                               (16400, 595, 256, 2), (32768, 119, 256, 4),
+                                               (16400, 595, 256, 2), (32768, 119, 256, 4), (65536, 72, 256, 1),
                                                (4096, 30, 64, 2), (2048, 20, 512, 1)])
 def test_fused_tanh_mlp_matches_autograd(rows, din, hidden, A):
     """_TanhMLP3 (hipBLASLt GEMMs + qs_mlp_* kernels, grads accumulated into .grad
@@ -107,7 +107,7 @@ def test_fused_tanh_mlp_matches_autograd(rows, din, hidden, A):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows,din,A", [(32768, 27, 1), (20000, 72, 4)])
+@pytest.mark.parametrize("rows,din,A", [(32768, 27, 1), (20000, 72, 4), (65536, 72, 1), (40960, 119, 4)])
 def test_fused_inference_forward(rows, din, A):
     """The rollout's no-grad actor forward through qs_mlp3_fwd (no saved activations)
     against the plain nn.Linear / torch.tanh forward."""
