@@ -914,6 +914,7 @@ class MAPPOAgent:
         # one rank, fused actor: the critic's sums + Adam on the side stream too (its own
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
+        self.side_priority = kwargs.get('side_priority', 0)
         # (opt-in) with the fused actor, the critic's step on qs_ppo_critic_tiles +
         # qs_wgrad_t instead of the qs_mlp3w kernels and hipBLASLt weight-gradient
         # GEMMs (measured slower at the C3 shape)
@@ -1114,7 +1115,9 @@ class MAPPOAgent:
         ta, tc, wa, wc = [], [], [], []
         cur = torch.cuda.current_stream()
         if self.side_stream and (getattr(self, '_side', None) is None or self._side.device != cur.device):
-            self._side = torch.cuda.Stream(device=cur.device)
+            # side_priority -1: the critic's stream outranks the actor's, so its next
+            # launch is dispatched ahead of the fused actor's queued workgroups
+            self._side = torch.cuda.Stream(device=cur.device, priority=self.side_priority)
         fused = isinstance(self._ws_actor, _F16Work)
 
         def critic_fwd():

@@ -32,8 +32,9 @@ def per_minibatch_us(shape, reps=3, **variant):
     D, O, A, mb, T, E = SHAPES[shape]
     osp, asp = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O))), Box(-np.ones((D, A)), np.ones((D, A)))
     torch.manual_seed(0)
+    variant.setdefault("use_graphs", True)
     agent = MAPPOAgent(osp, asp, hidden_dim=256, opt_epochs=1, mini_batch_size=mb, entropy_coef=0.005,
-                       target_kl=1e9, use_graphs=True, device=dev, **variant)
+                       target_kl=1e9, device=dev, **variant)
     buf = MAPPOBuffer(osp, asp, T, E, include_global_state=True, device=dev)
     buf.next_obs_slots.normal_()
     buf.act.normal_()
@@ -138,18 +139,38 @@ def ablate(shape="C3"):
         print(f"ablate {shape} without {name:18s} {us:8.1f} us/minibatch  (share {base - us:6.1f})", flush=True)
 
 
+def gemms():
+    """The fused actor's weight-gradient GEMMs alone (graph-timed), as _F16Work._splitk_rm
+    issues them: dW2 = dZ2ᵀ·H1 and dW1 = dZ1ᵀ·Xa over row chunks, at C3's and C4's
+    actor rows."""
+    for name, K, I in (("C3", 32768, 27), ("C4", 20480, 119)):
+        dz = torch.randn((K, 256), device=dev)
+        h1 = torch.randn((K, 256), device=dev)
+        xa = torch.randn((K, I), device=dev)
+        for what, b, m in (("dW2", h1, 2048), ("dW1", xa, 1024)):
+            S = agent_mod._splitk_chunks(K, m)
+            part = torch.empty((S, 256, b.shape[1]), device=dev)
+            fn = lambda: torch.bmm(dz.view(S, K // S, -1).transpose(1, 2), b.view(S, K // S, -1), out=part)
+            us = timed(fn)
+            print(f"{name} {what} bmm S={S:2d} ({K} x 256 x {b.shape[1]})   {us:8.2f} us  "
+                  f"{2 * K * 256 * b.shape[1] / us / 1e6:6.1f} TFLOP/s", flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["kernels", "C3", "ref", "C4"]
     if "kernels" in which:
         kernels()
+    if "gemms" in which:
+        gemms()
     if "scale" in which:
         for mb in (256, 1024, 2048):
             kernels(mb)
     if "C3" in which:
-        for v in (dict(critic_tiles=False), dict(critic_tiles=False, critic_after_actor=True),
-                  dict(critic_tiles=False, critic_adam_side=True),
-                  dict(critic_tiles=False, critic_after_actor=True, critic_adam_side=True),
-                  dict(critic_tiles=True), dict(critic_tiles=False, side_stream=False)):
+        for v in (dict(critic_tiles=False), dict(critic_tiles=False, side_priority=-1),
+                  dict(critic_tiles=False, side_priority=-1, critic_adam_side=True),
+                  dict(critic_tiles=False, side_priority=-1, critic_after_actor=True),
+                  dict(critic_tiles=False, use_graphs=False), dict(critic_tiles=False, use_graphs=False, side_priority=-1),
+                  dict(critic_tiles=False, side_stream=False)):
             us, path = per_minibatch_us("C3", **v)
             print(f"C3  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "ref" in which:
