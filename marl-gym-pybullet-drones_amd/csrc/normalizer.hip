@@ -9,14 +9,14 @@
 // float64 column reductions (a Welford reduce_kernel of ~200 µs and a mean of
 // ~90 µs at C4's 8 192 × 135) were most of a C4 rollout step.
 //
-// Here the moments are two launches: each 64-row tile's columns are held in
+// Here the moments are one launch: each 64-row tile's columns are held in
 // registers (16 rows per wave) and give the tile's column means and sums of
-// squared deviations (two passes, float64); then the tiles are merged
-// per column by 64 threads and a fixed LDS tree (the batch mean first, then
-// the parallel-variance sum Σ M2_t + n_t·(mean_t − mean)²) and
-// normalization.py:42-60's update applied in place in its operation order.
-// Fixed orders throughout: a replay is bit-identical.  The normalisation is a
-// third, elementwise launch (float64 arithmetic, float32 out).  HBM-bound: 4 B
+// squared deviations (two passes, float64); the last tile of each 64-column
+// block merges the block's tiles (the batch mean first, then the
+// parallel-variance sum Σ M2_t + n_t·(mean_t − mean)²) and applies
+// normalization.py:42-60's update in place in its operation order.  Fixed
+// orders throughout: a replay is bit-identical.  The normalisation is a
+// second, elementwise launch (float64 arithmetic, float32 out).  HBM-bound: 4 B
 // read per element for the moments, 4 B read + 4 B written for the
 // normalisation.
 
@@ -32,12 +32,12 @@ thread_local std::string g_nerr;
 int nfail(int code, const std::string& m) { g_nerr = m; return code; }
 
 constexpr int kRmsBlock = 256;
-constexpr int kRmsRows = 64;        // rows per tile (one thread per column each)
-constexpr int kRmsMergeCols = 4;    // columns per merge workgroup (64 threads each)
+constexpr int kRmsRows = 64;        // rows per tile
+constexpr int kRmsCols = 64;        // columns per workgroup (one per lane)
 
 struct RmsShape {
   long long R;
-  int C, GR;   // tiles of kRmsRows rows
+  int C, GR, NCB;   // tiles of kRmsRows rows, blocks of kRmsCols columns
 };
 
 __host__ __device__ inline RmsShape rms_shape(long long R, int C) {
@@ -45,106 +45,102 @@ __host__ __device__ inline RmsShape rms_shape(long long R, int C) {
   s.R = R;
   s.C = C;
   s.GR = (int)((R + kRmsRows - 1) / kRmsRows);
+  s.NCB = (C + kRmsCols - 1) / kRmsCols;
   return s;
 }
 
-// work: [counter (64 B)] [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(64, R − 64t) rows)
-inline long long rms_work_bytes(const RmsShape& s) { return 64 + 16LL * s.GR * s.C; }
+// work: [total counter (64 B)] [column-block counters: NCB u32, padded to 64 B]
+//       [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(64, R − 64t) rows)
+__host__ __device__ inline long long rms_cbc_bytes(const RmsShape& s) { return ((4LL * s.NCB + 63) / 64) * 64; }
+inline long long rms_work_bytes(const RmsShape& s) { return 64 + rms_cbc_bytes(s) + 16LL * s.GR * s.C; }
 
-// Launch 1: one workgroup per (64-row tile, 64 columns); wave w holds rows
-// 16w .. 16w+15 of the lane's column in registers (every load issued before
-// the first use; a wave's load is 64 consecutive columns of one row).  The
-// tile mean, then the sum of squared deviations from it (two passes over the
-// registers, float64), each combined over the four waves in wave order.
-constexpr int kRmsRowsW = kRmsRows / 4;
-__global__ void __launch_bounds__(kRmsBlock) rms_tile_kernel(RmsShape s, const float* __restrict__ x,
-                                                             unsigned* __restrict__ work) {
-  __shared__ double red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + lane, b = blockIdx.x;
-  const bool cv = c < s.C;
-  const long long r0 = (long long)b * kRmsRows;
-  const int nr = (int)min((long long)kRmsRows, s.R - r0);
-  const int rw = kRmsRowsW * w;
-  const float* src = x + (r0 + rw) * s.C + (cv ? c : 0);
-  float v[kRmsRowsW];
-  if (nr == kRmsRows) {
-#pragma unroll
-    for (int r = 0; r < kRmsRowsW; ++r) v[r] = cv ? __builtin_nontemporal_load(src + (long long)r * s.C) : 0.0f;
-  } else {
-#pragma unroll
-    for (int r = 0; r < kRmsRowsW; ++r) v[r] = cv && rw + r < nr ? src[(long long)r * s.C] : 0.0f;
-  }
-  double a = 0.0;
-#pragma unroll
-  for (int r = 0; r < kRmsRowsW; ++r)
-    if (rw + r < nr) a += (double)v[r];
-  red[w][lane] = a;
+// Σ over the four waves' values of one lane in wave order (float64)
+__device__ __forceinline__ double rms_wave_sum(double (*red)[64], double v, int w, int lane) {
+  red[w][lane] = v;
   __syncthreads();
-  const double m = (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]) / (double)nr;
-  double q = 0.0;
-#pragma unroll
-  for (int r = 0; r < kRmsRowsW; ++r)
-    if (rw + r < nr) {
-      const double d = (double)v[r] - m;
-      q += d * d;
-    }
-  __syncthreads();
-  red[w][lane] = q;
-  __syncthreads();
-  if (w == 0 && cv) {
-    double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
-    double* m2_b = mean_b + (size_t)s.GR * s.C;
-    mean_b[(size_t)b * s.C + c] = m;
-    m2_b[(size_t)b * s.C + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-  }
-}
-
-// Launch 2: kRmsMergeCols columns per workgroup, 64 threads per column, each
-// thread over the tiles t ≡ lane (mod 64) in order, the lanes combined by a
-// fixed LDS tree: the batch mean Σ n_t·mean_t / R first, then M2 = Σ (M2_t +
-// n_t·(mean_t − mean)²) (the parallel-variance merge with the mean known), then
-// normalization.py:42-60's update of the running statistics in its operation
-// order.  Every workgroup reads the running count before arriving; the last to
-// arrive writes the new count.
-__device__ __forceinline__ double rms_lane_sum(double v, double* red, int col, int lane) {
-  red[col * 64 + lane] = v;
-  __syncthreads();
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    if (lane < o) red[col * 64 + lane] += red[col * 64 + lane + o];
-    __syncthreads();
-  }
-  const double r = red[col * 64];
+  const double r = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
   __syncthreads();
   return r;
 }
 
-__global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double* __restrict__ mean,
-                                                              double* __restrict__ var, double* __restrict__ count,
-                                                              double* __restrict__ sums, unsigned* __restrict__ work) {
-  __shared__ double red[kRmsMergeCols * 64];
+// One launch: a workgroup per (64-row tile, 64 columns).  Wave w holds rows
+// 16w .. 16w+15 of the lane's column in registers (every load issued before
+// the first use; a wave's load is 64 consecutive columns of one row) and the
+// tile's column mean, then its sum of squared deviations from that mean
+// (two passes over the registers, float64) are formed.  The last tile to
+// arrive at a column block merges that block's tiles (the four waves over the
+// tiles t ≡ w mod 4, then in wave order): the batch mean Σ n_t·mean_t / R,
+// then M2 = Σ (M2_t + n_t·(mean_t − mean)²) (the parallel-variance merge with
+// the mean known), then normalization.py:42-60's update of the running
+// statistics in its operation order.  The last column block to finish writes
+// the new count.  Every order is fixed: a replay is bit-identical.
+__global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, const float* __restrict__ x,
+                                                                double* __restrict__ mean, double* __restrict__ var,
+                                                                double* __restrict__ count, double* __restrict__ sums,
+                                                                unsigned* __restrict__ work) {
+  __shared__ double red[4][64];
   __shared__ bool last;
-  const int t = threadIdx.x, col = t >> 6, lane = t & 63;
-  const int c = blockIdx.x * kRmsMergeCols + col;
+  constexpr int RW = kRmsRows / 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y * kRmsCols + lane, b = blockIdx.x;
   const bool cv = c < s.C;
-  const double* mean_b = reinterpret_cast<const double*>(reinterpret_cast<const char*>(work) + 64);
-  const double* m2_b = mean_b + (size_t)s.GR * s.C;
+  const long long r0 = (long long)b * kRmsRows;
+  const int nr = (int)min((long long)kRmsRows, s.R - r0);
+  const int rw = RW * w;
+  const float* src = x + (r0 + rw) * s.C + (cv ? c : 0);
+  float v[RW];
+  if (nr == kRmsRows) {
+#pragma unroll
+    for (int r = 0; r < RW; ++r) v[r] = cv ? __builtin_nontemporal_load(src + (long long)r * s.C) : 0.0f;
+  } else {
+#pragma unroll
+    for (int r = 0; r < RW; ++r) v[r] = cv && rw + r < nr ? src[(long long)r * s.C] : 0.0f;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+    if (rw + r < nr) a += (double)v[r];
+  const double m = rms_wave_sum(red, a, w, lane) / (double)nr;
+  double q = 0.0;
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+    if (rw + r < nr) {
+      const double d = (double)v[r] - m;
+      q += d * d;
+    }
+  q = rms_wave_sum(red, q, w, lane);
+  unsigned* total = work;
+  unsigned* cbc = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + 64);
+  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64 + rms_cbc_bytes(s));
+  double* m2_b = mean_b + (size_t)s.GR * s.C;
+  if (w == 0 && cv) {
+    mean_b[(size_t)b * s.C + c] = m;
+    m2_b[(size_t)b * s.C + c] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&cbc[blockIdx.y], 1u) == (unsigned)s.GR - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // the column block's merge (every tile's moments are visible: each arrived after a fence)
   const double cnt = sums ? 0.0 : *count;   // (the multi-rank form has no statistics)
   auto nrows = [&](int tt) { return (double)min((long long)kRmsRows, s.R - (long long)tt * kRmsRows); };
-  double a = 0.0;
+  double ma = 0.0;
   if (cv)
-    for (int tt = lane; tt < s.GR; tt += 64) a += nrows(tt) * mean_b[(size_t)tt * s.C + c];
+    for (int tt = w; tt < s.GR; tt += 4) ma += nrows(tt) * mean_b[(size_t)tt * s.C + c];
   const double na = (double)s.R;
-  const double bm = rms_lane_sum(a, red, col, lane) / na;
-  double q = 0.0;
+  const double bm = rms_wave_sum(red, ma, w, lane) / na;
+  double mq = 0.0;
   if (cv)
-    for (int tt = lane; tt < s.GR; tt += 64) {
+    for (int tt = w; tt < s.GR; tt += 4) {
       const double d = mean_b[(size_t)tt * s.C + c] - bm;
-      q += m2_b[(size_t)tt * s.C + c] + nrows(tt) * (d * d);
+      mq += m2_b[(size_t)tt * s.C + c] + nrows(tt) * (d * d);
     }
-  const double qa = rms_lane_sum(q, red, col, lane);
-  if (cv && lane == 0) {
+  const double qa = rms_wave_sum(red, mq, w, lane);
+  if (w == 0 && cv) {
     const double bv = qa / na;   // np.mean, np.var (ddof 0)
     if (sums) {   // several ranks: this rank's Σx and Σx² (merged across ranks by the caller)
       sums[c] = bm * na;
@@ -162,15 +158,14 @@ __global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double
     }
   }
   __syncthreads();
-  if (t == 0) {
+  if (threadIdx.x == 0) {
+    cbc[blockIdx.y] = 0u;   // every tile of this block has arrived
     __threadfence();
-    last = atomicAdd(work, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && t == 0) {
-    if (sums) sums[2 * s.C] = na;
-    else *count = na + cnt;
-    *work = 0u;
+    if (atomicAdd(total, 1u) == (unsigned)s.NCB - 1) {
+      if (sums) sums[2 * s.C] = na;
+      else *count = na + cnt;
+      *total = 0u;
+    }
   }
 }
 
@@ -243,14 +238,11 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
                   void* work, void* stream) {
   if (R <= 0 || C <= 0 || !x || !work || (!sums && (!mean || !var || !count)))
     return nfail(QS_E_INVALID, "qs_rms_update: bad argument");
-  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || C > 65535 * 64 || (R + kRmsRows - 1) / kRmsRows > (1LL << 31) - 1)
+  if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || C > 65535 * kRmsCols || (R + kRmsRows - 1) / kRmsRows > (1LL << 31) - 1)
     return nfail(QS_E_INVALID, "qs_rms_update: batch too large");
   const RmsShape s = rms_shape(R, C);
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR, (unsigned)((C + 63) / 64)), dim3(kRmsBlock),
-                     0, st, s, x, (unsigned*)work);
-  hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)((C + kRmsMergeCols - 1) / kRmsMergeCols)), dim3(kRmsBlock), 0,
-                     st, s, mean, var, count, sums, (unsigned*)work);
+  hipLaunchKernelGGL(rms_moments_kernel, dim3((unsigned)s.GR, (unsigned)s.NCB), dim3(kRmsBlock), 0, (hipStream_t)stream,
+                     s, x, mean, var, count, sums, (unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_update: ") + hipGetErrorString(e));
 }

@@ -721,7 +721,7 @@ class MAPPOActorCritic(nn.Module):
             L.check(L.load().qs_policy_sample(K, A, L.ptr(mean), L.ptr(self.actor.logstd), float(self.actor.action_scale),
                                               float(self.action_scale), int(self.action_scale != 1.0), L.ptr(eps),
                                               L.ptr(act), L.ptr(logp), _stream()), "qs_policy_sample")
-            return act, torch.zeros(E, D, 1, device=obs.device), logp
+            return act, self._zero_values(E, D, obs.device), logp
         dist = self.actor.dist(flat)
         act = dist.sample()
         if self.action_scale != 1.0:
@@ -732,6 +732,20 @@ class MAPPOActorCritic(nn.Module):
             out[0].copy_(act)
             out[1].copy_(logp)
         return act, torch.zeros(E, D, 1, device=obs.device), logp
+
+    def _zero_values(self, E, D, device):
+        """The per-agent value placeholder of step() (zeros, as the reference's),
+        one shared read-only tensor per shape: no fill launch per control step.
+        Not cached while a graph is being captured (its memory would belong to
+        the graph's pool)."""
+        key = (E, D, str(device))
+        z = getattr(self, '_zv', None)
+        if z is not None and z[0] == key:
+            return z[1]
+        v = torch.zeros(E, D, 1, device=device)
+        if not (v.is_cuda and torch.cuda.is_current_stream_capturing()):
+            self._zv = (key, v)
+        return v
 
     @torch.no_grad()
     def act(self, obs):
