@@ -432,14 +432,12 @@ struct MlpSumTasks {
 struct SegOf {
   int s[kMlpMaxTasks];   // the Adam segment of each task's destination
 };
-// A block is 16 waves; a task's G partial rows are split over Wg = min(16,
-// pow2 ≥ G) wave slices (wave slice w sums rows g ≡ w mod Wg in order, eight
-// rows' loads in flight), and the 16 / Wg wave groups of the block take
-// 256-column spans (lane l: columns l + 64j, j < 4 — every load a coalesced
-// 256-B wave access).  The slices are combined in slice order: per column the
-// same fixed order as mlp_sum_partials_kernel (rows g ≡ w mod 16 in order, then
-// w = 0..15), so both give the same bits.
 constexpr int kMlpSumCols = 4;
+// a task of at least this many partial rows (the fused kernels' per-tile bias
+// rows: 2 048 at C3) takes one column per lane and 32 rows in flight, so its
+// slices finish in 4 batches instead of 16 (the same per-column order)
+constexpr int kMlpSumTallG = 512;
+__host__ __device__ __forceinline__ int mlp_sum_cols(int G) { return G >= kMlpSumTallG ? 1 : kMlpSumCols; }
 __device__ __forceinline__ int mlp_sum_wg(int G) {
   int w = 1;
   while (w < G && w < 16) w <<= 1;
@@ -448,12 +446,10 @@ __device__ __forceinline__ int mlp_sum_wg(int G) {
 // fin(ti, dst, u, pv): the block's result u for a column of task ti (dst its
 // destination element); pv = pre(ti, dst), issued by the finishing waves before
 // their partial-row loads so that its memory latency overlaps theirs
-template <class Fin, class Pre>
-__device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin, Pre pre) {
-  constexpr int W = kMlpSumBlock / 64, C = kMlpSumCols;
-  __shared__ float lds[W][64 * C];
-  int ti = 0;
-  while (ti + 1 < tasks.n && (int)blockIdx.x >= tasks.start[ti + 1]) ++ti;
+template <int C, int U, class Fin, class Pre>
+__device__ __forceinline__ void mlp_sum_body(const MlpSumTasks& tasks, int ti, float (*lds)[64 * kMlpSumCols], Fin fin,
+                                             Pre pre) {
+  constexpr int W = kMlpSumBlock / 64;
   const MlpSumTask& T = tasks.t[ti];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int Wg = mlp_sum_wg(T.G), ws = wv % Wg, cg = wv / Wg;
@@ -472,8 +468,7 @@ __device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin,
 #pragma unroll
   for (int j = 0; j < C; ++j) t[j] = 0.f;
   int g = ws;
-  constexpr int U = 8;   // rows per batch: 32 loads in flight per lane
-  for (; g + (U - 1) * Wg < T.G; g += U * Wg) {
+  for (; g + (U - 1) * Wg < T.G; g += U * Wg) {   // U rows' loads in flight per column
     float v[U][C];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -505,6 +500,22 @@ __device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin,
     for (int k = 1; k < Wg; ++k) u += lds[cg * Wg + k][lane + 64 * j];
     fin(ti, dst_of(c), u, pv[j]);
   }
+}
+
+// A block is 16 waves; a task's G partial rows are split over Wg = min(16,
+// pow2 ≥ G) wave slices (wave slice w sums rows g ≡ w mod Wg in order), and
+// the 16 / Wg wave groups of the block take 64·C-column spans (lane l: columns
+// l + 64j, j < C — every load a coalesced 256-B wave access).  The slices are
+// combined in slice order: per column the same fixed order as
+// mlp_sum_partials_kernel (rows g ≡ w mod 16 in order, then w = 0..15), so
+// both give the same bits.
+template <class Fin, class Pre>
+__device__ __forceinline__ void mlp_sum_block(const MlpSumTasks& tasks, Fin fin, Pre pre) {
+  __shared__ float lds[kMlpSumBlock / 64][64 * kMlpSumCols];
+  int ti = 0;
+  while (ti + 1 < tasks.n && (int)blockIdx.x >= tasks.start[ti + 1]) ++ti;
+  if (mlp_sum_cols(tasks.t[ti].G) == 1) mlp_sum_body<1, 32>(tasks, ti, lds, fin, pre);
+  else mlp_sum_body<kMlpSumCols, 8>(tasks, ti, lds, fin, pre);
 }
 
 __global__ void __launch_bounds__(kMlpSumBlock) mlp_sum_multi_kernel(MlpSumTasks tasks) {
@@ -2300,7 +2311,7 @@ static int build_sum_tasks(int32_t n, const int32_t* G, const int64_t* P, const 
     T.start[i] = blocks;
     int wg = 1;   // mlp_sum_wg
     while (wg < G[i] && wg < 16) wg <<= 1;
-    const int64_t span = (int64_t)(kMlpSumBlock / 64 / wg) * 64 * kMlpSumCols;   // columns per block
+    const int64_t span = (int64_t)(kMlpSumBlock / 64 / wg) * 64 * mlp_sum_cols(G[i]);   // columns per block
     blocks += (int)((P[i] + span - 1) / span);
   }
   T.start[n] = blocks;

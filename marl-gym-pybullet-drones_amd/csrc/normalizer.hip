@@ -128,17 +128,40 @@ __global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, cons
   // the column block's merge (every tile's moments are visible: each arrived after a fence)
   const double cnt = sums ? 0.0 : *count;   // (the multi-rank form has no statistics)
   auto nrows = [&](int tt) { return (double)min((long long)kRmsRows, s.R - (long long)tt * kRmsRows); };
+  // wave w takes tiles t ≡ w (mod 4) in order, kMergeU of them per batch with
+  // every load of the batch issued first (the merge is the kernel's tail)
+  constexpr int kMergeU = 16;
+  const int cc = cv ? c : 0;
   double ma = 0.0;
-  if (cv)
-    for (int tt = w; tt < s.GR; tt += 4) ma += nrows(tt) * mean_b[(size_t)tt * s.C + c];
+  for (int t0 = w; t0 < s.GR; t0 += 4 * kMergeU) {
+    double mv[kMergeU];
+#pragma unroll
+    for (int u = 0; u < kMergeU; ++u) {
+      const int tt = t0 + 4 * u;
+      mv[u] = tt < s.GR ? mean_b[(size_t)tt * s.C + cc] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kMergeU; ++u)
+      if (t0 + 4 * u < s.GR) ma += nrows(t0 + 4 * u) * mv[u];
+  }
   const double na = (double)s.R;
   const double bm = rms_wave_sum(red, ma, w, lane) / na;
   double mq = 0.0;
-  if (cv)
-    for (int tt = w; tt < s.GR; tt += 4) {
-      const double d = mean_b[(size_t)tt * s.C + c] - bm;
-      mq += m2_b[(size_t)tt * s.C + c] + nrows(tt) * (d * d);
+  for (int t0 = w; t0 < s.GR; t0 += 4 * kMergeU) {
+    double mv[kMergeU], qv[kMergeU];
+#pragma unroll
+    for (int u = 0; u < kMergeU; ++u) {
+      const int tt = t0 + 4 * u;
+      mv[u] = tt < s.GR ? mean_b[(size_t)tt * s.C + cc] : 0.0;
+      qv[u] = tt < s.GR ? m2_b[(size_t)tt * s.C + cc] : 0.0;
     }
+#pragma unroll
+    for (int u = 0; u < kMergeU; ++u)
+      if (t0 + 4 * u < s.GR) {
+        const double d = mv[u] - bm;
+        mq += qv[u] + nrows(t0 + 4 * u) * (d * d);
+      }
+  }
   const double qa = rms_wave_sum(red, mq, w, lane);
   if (w == 0 && cv) {
     const double bv = qa / na;   // np.mean, np.var (ddof 0)
