@@ -58,6 +58,21 @@ constexpr int kSPad = 16;              // floats past the padded rows in a trans
 // the weight-gradient workgroups two to a CU.
 constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024;
 
+#ifdef QS_TILE_STAMPS
+// dev builds only: s_memrealtime (100 MHz) at the tile's phase boundaries,
+// workgroup thread 0, [blockIdx][8] (scripts/tile_stamps.py)
+constexpr int kStampWG = 4096;
+__device__ unsigned long long g_tile_stamps[kStampWG * 8];
+#define S_STAMP(k)                                                                                              \
+  do {                                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < kStampWG) g_tile_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define S_STAMP(k) \
+  do {             \
+  } while (0)
+#endif
+
 __host__ __device__ constexpr int s_ip(int I) { return (I + 15) & ~15; }       // input padded to whole quads
 __host__ __device__ constexpr int s_xs(int I) { return ((I + 31) & ~31) + 4; } // LDS row stride of the X tile
 
@@ -254,6 +269,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   // round trips before its first MFMA instead of one per phase: the first
   // quads of both forward contractions' weight rows, the head's per-row inputs,
   // the X tile (gathered through idx), and the biases / head into LDS
+  S_STAMP(0);
   float4 ring1[kSRing], ring2[kSRing];
 #define S_PRE1(n) s_prefill<n, false>(ring1, w1row, I, g)
   S_NQ_SWITCH(nq1, S_PRE1)
@@ -306,6 +322,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     }
   }
   __syncthreads();
+  S_STAMP(1);
   const float* sb1 = prm;
   const float* sb2 = prm + kSH;
   const float* sw3 = prm + 2 * kSH;
@@ -321,6 +338,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   for (int r = 0; r < 4; ++r) h1[r] = s_tanh(z[r] + sb1[h0 + r]);
   *reinterpret_cast<float4*>(h1s + j * kSHS + h0) = float4{h1[0], h1[1], h1[2], h1[3]};
   __syncthreads();
+  S_STAMP(2);
   // ---- layer 2: Z2ᵀ = W2·H1ᵀ (its ring filled at the start); the backward's ring filled behind it
   z = f32x4{0.f, 0.f, 0.f, 0.f};
   s_run<16, true>(ring2, w2row, kSH, h1s + j * kSHS, g, z);
@@ -344,6 +362,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     if (g == 0) hp[w * A + a][j] = t;
   }
   __syncthreads();
+  S_STAMP(3);
   float mu[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) {
@@ -433,6 +452,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     }
   }
   *reinterpret_cast<float4*>(dz2s + j * kSHS + h0) = float4{d4[0], d4[1], d4[2], d4[3]};
+  S_STAMP(4);
   if (w == 0)
 #pragma unroll
     for (int a = 0; a < A; ++a) {
@@ -458,6 +478,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
 #pragma unroll
     for (int k = 0; k < NL; ++k) ls_w[j][k] = ls[k];
   __syncthreads();
+  S_STAMP(5);
   __shared__ bool last;
   if (tid == 0) {
     double* lp = POL ? W.lossa + (size_t)tile * NL : W.lossc + tile;
@@ -472,16 +493,26 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     last = atomicAdd(W.cnt + (POL ? 0 : 64), 1u) == (unsigned)ntiles - 1;
   }
   __syncthreads();
-  if (!last || tid != 0) return;
+  S_STAMP(6);
+  if (!last || w != 0) return;
+  // the net's last tile: wave 0 sums the tiles' loss rows (lane q: tiles q, q + 64, ...
+  // in order), then a fixed xor butterfly over the lanes (every lane ends with the
+  // same bits: each level adds the same two operands)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  W.cnt[POL ? 0 : 64] = 0u;
   const int ntiles = POL ? P.nA : P.nC;
   double tot[NL];
 #pragma unroll
   for (int k = 0; k < NL; ++k) tot[k] = 0.0;
-  for (int t = 0; t < ntiles; ++t)
+  for (int t = l; t < ntiles; t += 64)
 #pragma unroll
     for (int k = 0; k < NL; ++k) tot[k] += (POL ? W.lossa[(size_t)t * NL + k] : W.lossc[t]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < NL; ++k) tot[k] += __shfl_xor(tot[k], o, 64);
+  if (l != 0) return;
+  S_STAMP(7);
+  W.cnt[POL ? 0 : 64] = 0u;
   if constexpr (!POL) {
     P.acc[1] += 0.5 * (tot[0] / (double)P.mb);
   } else {
@@ -600,17 +631,31 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
       int u = actor ? e : e - na;
       float gsum = 0.f;
       long long i;
+      // Σ over the tiles' partial rows in tile order, eight rows' loads in flight
+      auto colsum = [&](const float* base, int stride) {
+        float acc = 0.f;
+        int t = 0;
+        for (; t + 8 <= nt; t += 8) {
+          float v[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = base[(size_t)(t + q) * stride];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc += v[q];
+        }
+        for (; t < nt; ++t) acc += base[(size_t)t * stride];
+        return acc;
+      };
       if (u < kSH) {                       // b1: Σ dZ1
-        for (int t = 0; t < nt; ++t) gsum += pB[(size_t)t * kSH + u];
+        gsum = colsum(pB + u, kSH);
         i = N.b1 + u;
       } else if ((u -= kSH) < kSH) {       // b2: Σ dZ2
-        for (int t = 0; t < nt; ++t) gsum += pA[(size_t)t * PA + u];
+        gsum = colsum(pA + u, PA);
         i = N.b2 + u;
       } else if ((u -= kSH) < AA * kSH) {  // W3: Σ dout·H2
-        for (int t = 0; t < nt; ++t) gsum += pA[(size_t)t * PA + kSH + u];
+        gsum = colsum(pA + kSH + u, PA);
         i = N.w3 + u;
       } else if ((u -= AA * kSH) < AA) {   // b3: Σ dout
-        for (int t = 0; t < nt; ++t) gsum += pA[(size_t)t * PA + kSH + AA * kSH + u];
+        gsum = colsum(pA + kSH + AA * kSH + u, PA);
         i = N.b3 + u;
       } else {                             // logstd (the actor's loss tail)
         u -= AA;
@@ -865,5 +910,14 @@ int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* 
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_critic_tiles: ") + hipGetErrorString(e));
 }
+
+#ifdef QS_TILE_STAMPS
+int qs_dev_tile_stamps(unsigned long long* host, int64_t n) {
+  if (n > (int64_t)kStampWG * 8) n = (int64_t)kStampWG * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tile_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? QS_OK
+             : QS_E_HIP;
+}
+#endif
 
 }  // extern "C"

@@ -179,7 +179,7 @@ def main():
             print(f"ref {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "dw1" in which:
         # dW1's row-chunk GEMMs: rows per chunk (the default: 1 024)
-        for m in (1024, 2048, 4096, 8192):
+        for m in (256, 512, 1024, 2048):
             agent_mod._SPLITK_MIN_ROWS[(32768, 27)] = m
             us, path = per_minibatch_us("C3", critic_tiles=False)
             print(f"C3  dW1 chunk rows {m:<37d} {us:8.1f} us/minibatch  [{path}]", flush=True)
