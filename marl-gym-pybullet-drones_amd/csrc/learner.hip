@@ -436,7 +436,10 @@ constexpr int kMlpSumCols = 4;
 // a task of at least this many partial rows (the fused kernels' per-tile bias
 // rows: 2 048 at C3) takes one column per lane and 32 rows in flight, so its
 // slices finish in 4 batches instead of 16 (the same per-column order)
-constexpr int kMlpSumTallG = 512;
+#ifndef QS_SUM_TALL_G
+#define QS_SUM_TALL_G 512   // dev builds probe other thresholds
+#endif
+constexpr int kMlpSumTallG = QS_SUM_TALL_G;
 __host__ __device__ __forceinline__ int mlp_sum_cols(int G) { return G >= kMlpSumTallG ? 1 : kMlpSumCols; }
 __device__ __forceinline__ int mlp_sum_wg(int G) {
   int w = 1;

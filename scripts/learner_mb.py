@@ -160,6 +160,11 @@ def main():
     which = sys.argv[1:] or ["kernels", "C3", "ref", "C4"]
     if "kernels" in which:
         kernels()
+    if "base" in which:   # the defaults at C3 and C4 (e.g. to compare two builds via QS_DEV_LIB)
+        for shape in ("C3", "C4"):
+            us, path = per_minibatch_us(shape)
+            print(f"{os.environ.get('QS_DEV_LIB', 'default'):>24s} {shape} default {us:8.1f} us/minibatch  [{path}]",
+                  flush=True)
     if "gemms" in which:
         gemms()
     if "scale" in which:

@@ -253,6 +253,26 @@ def test_direct_update_side_stream_bit_identical(graphs, E, T):
         assert r_side[k] == pytest.approx(r_fused[k], rel=1e-5, abs=1e-7)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_direct_update_fused_actor_four_outputs(graphs):
+    """The fused actor kernel on a 4-output actor (Spiral's VEL actions, the C4
+    trainer config; _F16_MAX_A = 4): the direct iteration with and without the
+    side stream agree bit for bit, and with the autograd-driven iteration within
+    Adam's step tolerance."""
+    E, T, D, A = 128, 8, 5, 4
+    a_side, r_side = _hidden256_update(graphs, E, T, D=D, A=A)
+    assert a_side._direct_ok() and type(a_side._ws_actor).__name__ == "_F16Work"
+    a_one, r_one = _hidden256_update(graphs, E, T, D=D, A=A, side_stream=False)
+    assert torch.equal(a_side.actor_opt.flat, a_one.actor_opt.flat)
+    assert torch.equal(a_side.critic_opt.flat, a_one.critic_opt.flat)
+    assert r_side == r_one
+    a_ref, r_ref = _hidden256_update(graphs, E, T, D=D, A=A, direct=False)
+    torch.testing.assert_close(a_side.actor_opt.flat, a_ref.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
+    torch.testing.assert_close(a_side.critic_opt.flat, a_ref.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
+    for k in r_side:
+        assert r_side[k] == pytest.approx(r_ref[k], rel=1e-5, abs=1e-7)
+
+
 @pytest.mark.parametrize("E,T,D,A", [(8, 8, 8, 1), (32, 8, 8, 1), (5, 6, 8, 1), (16, 4, 5, 4), (3, 2, 16, 1)])
 @pytest.mark.parametrize("graphs", [False, True])
 def test_small_update_matches_autograd(graphs, E, T, D, A):
