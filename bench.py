@@ -76,6 +76,7 @@ def parse():
     p.add_argument("--drones", type=int, default=8)
     p.add_argument("--act", default="one_d_pid")
     p.add_argument("--slots", type=int, default=32, help="rollout-buffer slots the obs ring cycles through")
+    p.add_argument("--graph-steps", type=int, default=512, help="control steps per captured HIP graph of the sim legs")
     p.add_argument("--no-stagger", action="store_true", help="start every env at episode step 0")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -344,17 +345,19 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
     for t in range(args.warmup):
         step(t % slots)
     torch.cuda.synchronize()
-    # The rollout loop is captured as a HIP graph of `slots` step launches (one per
-    # rollout-buffer slot), plus one of the remainder so that exactly `steps` run;
-    # the host launches one graph per `slots` steps instead of one kernel per step.
-    n_full, rem = divmod(args.steps, slots)
+    # The rollout loop is captured as HIP graphs of up to --graph-steps step launches
+    # each (the obs ring cycling through its `slots` buffers inside a graph), so that
+    # exactly `steps` run: a window of 484 steps is one replay, not 16 (each graph
+    # boundary cost ~9 µs of idle device time between the replays)
+    gsteps = max(1, min(args.graph_steps, args.steps))
+    n_full, rem = divmod(args.steps, gsteps)
     stream = torch.cuda.Stream()
     graphs = []
-    for n in ([slots] if n_full else []) + ([rem] if rem else []):
+    for n in ([gsteps] if n_full else []) + ([rem] if rem else []):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream):
             for k in range(n):
-                step(k)
+                step(k % slots)
         graphs.append((g, n))
     torch.cuda.synchronize()
     # one untimed replay of each graph: a graph's first launch also uploads it to

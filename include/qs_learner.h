@@ -336,6 +336,8 @@ typedef struct qs_mlp256 {
   int64_t w1, b1, w2, b2, w3, b3, logstd;   /* element offsets in params (logstd -1: none) */
   int32_t in, out;     /* input width (<= 256), outputs (actor <= 4, critic 1) */
   float lr, beta1, beta2, eps;
+  float* w1p;          /* NULL, or [256][in padded to 16] = W1 with zero columns past in: the
+                          step keeps it current and reads layer 1 as whole float4 quads */
 } qs_mlp256;
 int64_t qs_ppo_small_work_bytes(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A);
 int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,

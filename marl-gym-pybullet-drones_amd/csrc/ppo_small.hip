@@ -85,6 +85,7 @@ struct SNet {   // one 256-wide tanh MLP inside its flat Adam buffers (qs_mlp256
   long long w1, b1, w2, b2, w3, b3, logstd;
   int I, A;
   float lr, beta1, beta2, eps;
+  float* w1p;   // NULL or W1 padded to s_ip(I) columns (zeros past I), kept current by the Adam launch
 };
 
 struct SWork {   // workspace views (qs_ppo_small_work_bytes)
@@ -246,7 +247,7 @@ __device__ __forceinline__ void s_wgrad_acc(const float* arow, const float* brow
 // ---------------------------------------------------------------- launch 1
 // One 16-row tile of one net: POL = the actor (policy head over A outputs),
 // otherwise the critic (value head).
-template <int A, bool POL>
+template <int A, bool POL, bool V1>
 __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, float* xs, float* h1s, float* dz2s,
                                        float* prm, float (*hp)[16], double (*ls_w)[2 + kSMaxA]) {
   static_assert(kSBPW == 1, "one hidden block per wave");
@@ -262,7 +263,10 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   float* dz2T = POL ? W.dz2aT : W.dz2cT;
   float* dz1T = POL ? W.dz1aT : W.dz1cT;
   const int b0 = w, h0 = 16 * b0 + 4 * g;   // the wave's hidden block; lane (g, j): units h0 .. h0 + 3 of row j
-  const float* w1row = N.p + N.w1 + (size_t)(16 * b0 + j) * I;
+  // layer 1's rows: the padded copy as whole float4 quads when there is one,
+  // otherwise the parameter rows with clamped scalar loads
+  // (V1: the launch checked that the net has the copy)
+  const float* w1row = V1 ? N.w1p + (size_t)(16 * b0 + j) * Ip : N.p + N.w1 + (size_t)(16 * b0 + j) * I;
   const float* w2row = N.p + N.w2 + (size_t)(16 * b0 + j) * kSH;
   const float* w2trow = N.w2t + (size_t)(16 * b0 + j) * kSH;
   // ---- every independent load first, so the tile pays one or two memory
@@ -272,8 +276,14 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   S_STAMP(0);
   float4 ring1[kSRing], ring2[kSRing];
 #define S_PRE1(n) s_prefill<n, false>(ring1, w1row, I, g)
-  S_NQ_SWITCH(nq1, S_PRE1)
+#define S_PRE1V(n) s_prefill<n, true>(ring1, w1row, Ip, g)
+  if constexpr (V1) {
+    S_NQ_SWITCH(nq1, S_PRE1V)
+  } else {
+    S_NQ_SWITCH(nq1, S_PRE1)
+  }
 #undef S_PRE1
+#undef S_PRE1V
   s_prefill<16, true>(ring2, w2row, kSH, g);
   const int R = r0 + j;
   const bool rv = R < K;
@@ -331,8 +341,14 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   // ---- layer 1: Z1ᵀ[h0 + r][row j] in register r of lane (g, j)
   f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
 #define S_RUN1(n) s_run<n, false>(ring1, w1row, I, xs + j * XS, g, z)
-  S_NQ_SWITCH(nq1, S_RUN1)
+#define S_RUN1V(n) s_run<n, true>(ring1, w1row, Ip, xs + j * XS, g, z)
+  if constexpr (V1) {
+    S_NQ_SWITCH(nq1, S_RUN1V)
+  } else {
+    S_NQ_SWITCH(nq1, S_RUN1)
+  }
 #undef S_RUN1
+#undef S_RUN1V
   float h1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) h1[r] = s_tanh(z[r] + sb1[h0 + r]);
@@ -533,7 +549,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   }
 }
 
-template <int A>
+template <int A, bool V1>
 __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
   __shared__ float xs[16 * s_xs(kSMaxI)];
   __shared__ float h1s[16 * kSHS];
@@ -541,8 +557,8 @@ __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
   __shared__ float hp[kSW * kSMaxA][16];
   __shared__ double ls_w[16][2 + kSMaxA];
   __shared__ float prm[2 * kSH + kSMaxA * kSH + 2 * kSMaxA];
-  if ((int)blockIdx.x < P.nA) s_tile<A, true>(P, P.a, blockIdx.x, xs, h1s, dz2s, prm, hp, ls_w);
-  else s_tile<1, false>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, prm, hp, ls_w);
+  if ((int)blockIdx.x < P.nA) s_tile<A, true, V1>(P, P.a, blockIdx.x, xs, h1s, dz2s, prm, hp, ls_w);
+  else s_tile<1, false, V1>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, prm, hp, ls_w);
 }
 
 // ---------------------------------------------------------------- launch 2
@@ -553,7 +569,7 @@ struct STile {
 };
 
 __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, float bc1, float bc2s, float* w2t,
-                                       int n, int k) {
+                                       int n, int k, float* w1p = nullptr) {
   // torch.optim.Adam (amsgrad=False, weight_decay=0): learner.hip's adam_elem
   const float p = N.p[i], m = N.m[i], v = N.v[i];
   const float m1 = m + (1.0f - N.beta1) * (g - m);
@@ -564,6 +580,7 @@ __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, floa
   const float p1 = p - (N.lr / bc1) * (m1 / denom);
   N.p[i] = p1;
   if (w2t) w2t[(size_t)k * kSH + n] = p1;
+  if (w1p) w1p[(size_t)n * s_ip(N.I) + k] = p1;
 }
 
 __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int nTiles) {
@@ -611,7 +628,8 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
           for (int r = 0; r < 4; ++r) {
             const int n = 16 * nb + 4 * g + r;
             const long long i = (which == 1 ? N.w1 : N.w2) + (long long)n * Kin + kcol;
-            s_adam(N, i, c[r], sc[si][0], sc[si][1], which == 2 ? N.w2t : nullptr, n, kcol);
+            s_adam(N, i, c[r], sc[si][0], sc[si][1], which == 2 ? N.w2t : nullptr, n, kcol,
+                   which == 1 ? N.w1p : nullptr);
           }
         }
       }
@@ -836,6 +854,7 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
     n.beta1 = q->beta1;
     n.beta2 = q->beta2;
     n.eps = q->eps;
+    n.w1p = q->w1p;
     return n;
   };
   P.a = net(actor);
@@ -851,11 +870,14 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
 }
 
 static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
+  // layer 1 from the padded W1 copies when every net in the launch has one
+  const bool v1 = P.c.w1p && (P.nA == 0 || P.a.w1p);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); };
   switch (P.a.A) {
-    case 1: hipLaunchKernelGGL(ppo_small_fb_kernel<1>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
-    case 2: hipLaunchKernelGGL(ppo_small_fb_kernel<2>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
-    case 3: hipLaunchKernelGGL(ppo_small_fb_kernel<3>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
-    default: hipLaunchKernelGGL(ppo_small_fb_kernel<4>, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); break;
+    case 1: v1 ? go(ppo_small_fb_kernel<1, true>) : go(ppo_small_fb_kernel<1, false>); break;
+    case 2: v1 ? go(ppo_small_fb_kernel<2, true>) : go(ppo_small_fb_kernel<2, false>); break;
+    case 3: v1 ? go(ppo_small_fb_kernel<3, true>) : go(ppo_small_fb_kernel<3, false>); break;
+    default: v1 ? go(ppo_small_fb_kernel<4, true>) : go(ppo_small_fb_kernel<4, false>); break;
   }
 }
 

@@ -83,7 +83,8 @@ class QsMlp256(ctypes.Structure):
                 ("w1", ctypes.c_int64), ("b1", ctypes.c_int64), ("w2", ctypes.c_int64), ("b2", ctypes.c_int64),
                 ("w3", ctypes.c_int64), ("b3", ctypes.c_int64), ("logstd", ctypes.c_int64),
                 ("in_", ctypes.c_int32), ("out", ctypes.c_int32),
-                ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
+                ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("w1p", ctypes.c_void_p)]
 
 
 class QuadSwarmError(RuntimeError):

@@ -443,8 +443,9 @@ class _F16Work(_M3Work):
 _SMALL_MAX_ROWS = 2048
 
 
-def _mlp256(fb, mlp, logstd, w2t, lib_struct):
-    """qs_mlp256 of a 256-wide tanh MLP (and the actor's logstd) inside FlatBuffers fb."""
+def _mlp256(fb, mlp, logstd, w2t, lib_struct, w1p=None):
+    """qs_mlp256 of a 256-wide tanh MLP (and the actor's logstd) inside FlatBuffers fb;
+    w1p: the padded W1 copy qs_ppo_small_step keeps current (None: no copy)."""
     ids = [id(p) for p in fb.params]
     off = lambda t: fb.offsets[ids.index(id(t))][0] if t is not None else -1
     f0, f1, f2 = mlp.fcs
@@ -457,6 +458,7 @@ def _mlp256(fb, mlp, logstd, w2t, lib_struct):
     q.logstd = off(logstd)
     q.in_, q.out = f0.in_features, f2.out_features
     q.lr, q.beta1, q.beta2, q.eps = fb.lr, fb.betas[0], fb.betas[1], fb.eps
+    q.w1p = w1p.data_ptr() if w1p is not None else None
     return q
 
 
@@ -1103,8 +1105,7 @@ class MAPPOAgent:
             self._ws_actor.repack()
             self._ws_critic.repack()
         if getattr(self, '_sm_key', None) is not None:
-            for w2t, mlp in zip(self._sm_w2t, (self.ac.actor.pi_net, self.ac.critic.v_net)):
-                w2t.copy_(mlp.fcs[1].weight.t())
+            self._sm_refresh()
         self._reduce_buf.zero_()
 
     def _iteration_direct(self, rollouts, idx, acc):
@@ -1280,11 +1281,21 @@ class MAPPOAgent:
                                             pa.fcs[2].out_features))
         self._sm_work = torch.zeros(n, dtype=torch.uint8, device=self.device)
         self._sm_w2t = [torch.empty((256, 256), device=self.device) for _ in range(2)]
-        self._sm_nets = (_mlp256(self.actor_opt, pa, self.ac.actor.logstd, self._sm_w2t[0], L.QsMlp256),
-                         _mlp256(self.critic_opt, pc, None, self._sm_w2t[1], L.QsMlp256))
+        # W1 padded to whole 16-column quads (zeros past the input width): layer 1's
+        # rows read as float4s (scalar clamped loads took ~4x as long)
+        self._sm_w1p = [torch.zeros((256, (m.fcs[0].in_features + 15) // 16 * 16), device=self.device)
+                        for m in (pa, pc)]
+        self._sm_nets = (_mlp256(self.actor_opt, pa, self.ac.actor.logstd, self._sm_w2t[0], L.QsMlp256,
+                                 self._sm_w1p[0]),
+                         _mlp256(self.critic_opt, pc, None, self._sm_w2t[1], L.QsMlp256, self._sm_w1p[1]))
         self._sm_key = (mb, D)
-        for w2t, mlp in zip(self._sm_w2t, (pa, pc)):
+        self._sm_refresh()
+
+    def _sm_refresh(self):
+        """The small path's W2ᵀ and padded W1 copies from the current weights."""
+        for w2t, w1p, mlp in zip(self._sm_w2t, self._sm_w1p, (self.ac.actor.pi_net, self.ac.critic.v_net)):
             w2t.copy_(mlp.fcs[1].weight.t())
+            w1p[:, :mlp.fcs[0].in_features].copy_(mlp.fcs[0].weight)
 
     def _iteration_small(self, rollouts, idx, acc):
         """One minibatch in two launches (qs_ppo_small_step): the actor's forward,
