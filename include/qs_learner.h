@@ -284,7 +284,7 @@ const char* qs_learner_last_error(void);
  * normalization.py:42-60's operation order (RunningMeanStd.update); with
  * sums != NULL nothing is updated and this rank's [Σx (C) | Σx² (C) | R] are
  * written to sums[2C + 1] instead (the multi-rank path all-reduces them).
- * work: qs_rms_work_bytes(R, C) bytes, zeroed once (the launch leaves it zero).
+ * work: qs_rms_work_bytes(R, C) bytes of scratch (tile moments and the saved count).
  * qs_rms_normalize: out[R][C] = float32(clip((x − mean)/sqrt(var + eps),
  * −clip, clip)) in float64 (normalization.py:110-113). */
 int64_t qs_rms_work_bytes(int64_t R, int32_t C);

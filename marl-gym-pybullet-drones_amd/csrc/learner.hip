@@ -1461,7 +1461,9 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
       lossp[(size_t)blockIdx.x * NL + k] = s;
     }
     F_STAMP(6);
+#ifndef QS_F_NOFENCE   // dev probe: the cost of the agent-scope release (results of the loss sums undefined)
     __threadfence();
+#endif
     last = atomicAdd(count, 1u) == gridDim.x - 1;
   }
   __syncthreads();

@@ -9,14 +9,16 @@
 // float64 column reductions (a Welford reduce_kernel of ~200 µs and a mean of
 // ~90 µs at C4's 8 192 × 135) were most of a C4 rollout step.
 //
-// Here the moments are one launch: each 64-row tile's columns are held in
+// Here the moments are two launches: each 64-row tile's columns are held in
 // registers (16 rows per wave) and give the tile's column means and sums of
-// squared deviations (two passes, float64); the last tile of each 64-column
-// block merges the block's tiles (the batch mean first, then the
-// parallel-variance sum Σ M2_t + n_t·(mean_t − mean)²) and applies
-// normalization.py:42-60's update in place in its operation order.  Fixed
-// orders throughout: a replay is bit-identical.  The normalisation is a
-// second, elementwise launch (float64 arithmetic, float32 out).  HBM-bound: 4 B
+// squared deviations (two passes, float64); then a workgroup per 64 columns
+// merges the tiles (the batch mean first, then the parallel-variance sum
+// Σ M2_t + n_t·(mean_t − mean)²) and applies normalization.py:42-60's update
+// in place in its operation order.  No atomics or fences: an agent-scope
+// release per workgroup writes back the XCD's L2 and cost ~40 µs over 1 280
+// workgroups when the merge was folded into the tile launch.  Fixed orders
+// throughout: a replay is bit-identical.  The normalisation is a third,
+// elementwise launch (float64 arithmetic, float32 out).  HBM-bound: 4 B
 // read per element for the moments, 4 B read + 4 B written for the
 // normalisation.
 
@@ -49,10 +51,9 @@ __host__ __device__ inline RmsShape rms_shape(long long R, int C) {
   return s;
 }
 
-// work: [total counter (64 B)] [column-block counters: NCB u32, padded to 64 B]
+// work: [the running count before this update (one double, 64 B)]
 //       [mean_b: GR·C] [m2_b: GR·C]   (tile t has min(64, R − 64t) rows)
-__host__ __device__ inline long long rms_cbc_bytes(const RmsShape& s) { return ((4LL * s.NCB + 63) / 64) * 64; }
-inline long long rms_work_bytes(const RmsShape& s) { return 64 + rms_cbc_bytes(s) + 16LL * s.GR * s.C; }
+inline long long rms_work_bytes(const RmsShape& s) { return 64 + 16LL * s.GR * s.C; }
 
 // Σ over the four waves' values of one lane in wave order (float64)
 __device__ __forceinline__ double rms_wave_sum(double (*red)[64], double v, int w, int lane) {
@@ -63,23 +64,16 @@ __device__ __forceinline__ double rms_wave_sum(double (*red)[64], double v, int 
   return r;
 }
 
-// One launch: a workgroup per (64-row tile, 64 columns).  Wave w holds rows
+// Launch 1: a workgroup per (64-row tile, 64 columns).  Wave w holds rows
 // 16w .. 16w+15 of the lane's column in registers (every load issued before
-// the first use; a wave's load is 64 consecutive columns of one row) and the
-// tile's column mean, then its sum of squared deviations from that mean
-// (two passes over the registers, float64) are formed.  The last tile to
-// arrive at a column block merges that block's tiles (the four waves over the
-// tiles t ≡ w mod 4, then in wave order): the batch mean Σ n_t·mean_t / R,
-// then M2 = Σ (M2_t + n_t·(mean_t − mean)²) (the parallel-variance merge with
-// the mean known), then normalization.py:42-60's update of the running
-// statistics in its operation order.  The last column block to finish writes
-// the new count.  Every order is fixed: a replay is bit-identical.
-__global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, const float* __restrict__ x,
-                                                                double* __restrict__ mean, double* __restrict__ var,
-                                                                double* __restrict__ count, double* __restrict__ sums,
-                                                                unsigned* __restrict__ work) {
+// the first use; a wave's load is 64 consecutive columns of one row), then the
+// tile's column mean and its sum of squared deviations from that mean (two
+// passes over the registers, float64, the waves combined in order).  Block
+// (0, 0) also saves the running count for launch 2 (which rewrites it).
+__global__ void __launch_bounds__(kRmsBlock) rms_tile_kernel(RmsShape s, const float* __restrict__ x,
+                                                             const double* __restrict__ count,
+                                                             unsigned* __restrict__ work) {
   __shared__ double red[4][64];
-  __shared__ bool last;
   constexpr int RW = kRmsRows / 4;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * kRmsCols + lane, b = blockIdx.x;
@@ -109,29 +103,37 @@ __global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, cons
       q += d * d;
     }
   q = rms_wave_sum(red, q, w, lane);
-  unsigned* total = work;
-  unsigned* cbc = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + 64);
-  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64 + rms_cbc_bytes(s));
+  double* mean_b = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + 64);
   double* m2_b = mean_b + (size_t)s.GR * s.C;
   if (w == 0 && cv) {
     mean_b[(size_t)b * s.C + c] = m;
     m2_b[(size_t)b * s.C + c] = q;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(&cbc[blockIdx.y], 1u) == (unsigned)s.GR - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // the column block's merge (every tile's moments are visible: each arrived after a fence)
-  const double cnt = sums ? 0.0 : *count;   // (the multi-rank form has no statistics)
-  auto nrows = [&](int tt) { return (double)min((long long)kRmsRows, s.R - (long long)tt * kRmsRows); };
-  // wave w takes tiles t ≡ w (mod 4) in order, kMergeU of them per batch with
-  // every load of the batch issued first (the merge is the kernel's tail)
-  constexpr int kMergeU = 16;
+  if (count && b == 0 && blockIdx.y == 0 && threadIdx.x == 0) *reinterpret_cast<double*>(work) = *count;
+}
+
+// Launch 2: a workgroup per 64 columns merges the tiles (the four waves over the
+// tiles t ≡ w mod 4, sixteen loads in flight, then in wave order): the batch
+// mean Σ n_t·mean_t / R, then M2 = Σ (M2_t + n_t·(mean_t − mean)²) (the
+// parallel-variance merge with the mean known), then normalization.py:42-60's
+// update of the running statistics in its operation order, from the count
+// launch 1 saved; block 0 writes the new count.  No atomics, no fences (the
+// launch boundary orders launch 1's writes), every order fixed: a replay is
+// bit-identical.
+__global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double* __restrict__ mean,
+                                                              double* __restrict__ var, double* __restrict__ count,
+                                                              double* __restrict__ sums,
+                                                              const unsigned* __restrict__ work) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * kRmsCols + lane;
+  const bool cv = c < s.C;
   const int cc = cv ? c : 0;
+  const double* mean_b = reinterpret_cast<const double*>(reinterpret_cast<const char*>(work) + 64);
+  const double* m2_b = mean_b + (size_t)s.GR * s.C;
+  const double cnt = sums ? 0.0 : *reinterpret_cast<const double*>(work);   // (the multi-rank form has no statistics)
+  auto nrows = [&](int tt) { return (double)min((long long)kRmsRows, s.R - (long long)tt * kRmsRows); };
+  constexpr int kMergeU = 16;
   double ma = 0.0;
   for (int t0 = w; t0 < s.GR; t0 += 4 * kMergeU) {
     double mv[kMergeU];
@@ -180,15 +182,9 @@ __global__ void __launch_bounds__(kRmsBlock) rms_moments_kernel(RmsShape s, cons
       mean[c] = new_mean;
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    cbc[blockIdx.y] = 0u;   // every tile of this block has arrived
-    __threadfence();
-    if (atomicAdd(total, 1u) == (unsigned)s.NCB - 1) {
-      if (sums) sums[2 * s.C] = na;
-      else *count = na + cnt;
-      *total = 0u;
-    }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (sums) sums[2 * s.C] = na;
+    else *count = na + cnt;
   }
 }
 
@@ -264,8 +260,11 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
   if (R > (1LL << 40) || (long long)R * C > (1LL << 46) || C > 65535 * kRmsCols || (R + kRmsRows - 1) / kRmsRows > (1LL << 31) - 1)
     return nfail(QS_E_INVALID, "qs_rms_update: batch too large");
   const RmsShape s = rms_shape(R, C);
-  hipLaunchKernelGGL(rms_moments_kernel, dim3((unsigned)s.GR, (unsigned)s.NCB), dim3(kRmsBlock), 0, (hipStream_t)stream,
-                     s, x, mean, var, count, sums, (unsigned*)work);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR, (unsigned)s.NCB), dim3(kRmsBlock), 0, st, s, x,
+                     sums ? nullptr : count, (unsigned*)work);
+  hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)s.NCB), dim3(kRmsBlock), 0, st, s, mean, var, count, sums,
+                     (const unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_update: ") + hipGetErrorString(e));
 }

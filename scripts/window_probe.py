@@ -8,6 +8,11 @@ import time
 
 import torch
 
+if os.environ.get("WP_SPIN"):   # hipDeviceScheduleSpin on torch's own HIP runtime, before its context exists
+    import ctypes
+    hip = [l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l][0]
+    assert ctypes.CDLL(hip).hipSetDeviceFlags(1) == 0
+
 sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "marl-gym-pybullet-drones_amd")]
 from gym_pybullet_drones_amd.envs import QuadSwarm, grid_layout  # noqa: E402
 
@@ -50,6 +55,9 @@ def events_window():
 
 
 ev = []
+ev_end = torch.cuda.Event()
+
+
 def kernel_us():
     a, b = events_window()
     ev.append(a.elapsed_time(b) * 1e3)
@@ -61,6 +69,7 @@ print(f"sync + sync                        {med(lambda: (torch.cuda.synchronize(
 print(f"replay + sync                      {med(lambda: (g.replay(), torch.cuda.synchronize())):8.1f} us")
 print(f"replay + stream sync               {med(lambda: (g.replay(), cur.synchronize())):8.1f} us")
 print(f"events + replay + 2 sync (bench)   {med(events_window):8.1f} us")
+print(f"replay + event sync                {med(lambda: (ev_end.record(cur) if g.replay() is None else None, ev_end.synchronize())):8.1f} us")
 med(kernel_us)
 print(f"event-timed graph                  {statistics.median(ev):8.1f} us  ({statistics.median(ev) / K:.2f} us/step)")
 sw.close()
