@@ -155,15 +155,16 @@ struct qs_handle {
   std::vector<double> orig_host;
 };
 
-// Envs per one-wave workgroup: ⌊64/D⌋, halved while the grid holds fewer than
-// kEpbWaves waves per SIMD (at most QS_EPB_HALVINGS times).  The step is
-// latency-bound per wave (loads → PID → substeps → reward → stores in one
-// dependent chain), so a grid under two waves per SIMD leaves the SIMDs idle
-// between its waves' phases; more, emptier waves overlap them (Spiral C4:
-// 683 waves of 12 envs for 1 024 SIMDs).  Results do not depend on it: every
-// per-env quantity is formed inside the env's own lanes.
+// Envs per one-wave workgroup: ⌊64/D⌋, a launch parameter (P.EPB).  A dev build
+// may halve it while the grid holds fewer than kEpbWaves waves per SIMD (at
+// most QS_EPB_HALVINGS times), to overlap more waves' latency chains on an
+// under-filled grid (Spiral C4: 683 waves of 12 envs for 1 024 SIMDs) — but
+// every wave pays the same load → PID → substeps → reward → store chain, and
+// one halving made C4 11.6 → 18.2 µs (as round 2's probe found), so the
+// default is none.  Results do not depend on it: every per-env quantity is
+// formed inside the env's own lanes.
 #ifndef QS_EPB_HALVINGS
-#define QS_EPB_HALVINGS 1
+#define QS_EPB_HALVINGS 0   // measured: one halving made Spiral C4 11.6 -> 18.2 µs; dev builds probe it
 #endif
 static constexpr int kEpbWaves = 2;
 static int envs_per_wave(const qs_handle* h) {
