@@ -367,9 +367,12 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
     torch.cuda.synchronize()
     plan = [graphs[0]] * n_full + ([graphs[-1]] if rem else [])
     _, ended0 = sw.episode_log(cap=0)
-    ranks.fence()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     cur = torch.cuda.current_stream()
+    for a, b in ev:   # a torch Event creates its HIP event at its first record: not inside the window
+        a.record(cur)
+        b.record(cur)
+    ranks.fence()
     t0 = time.perf_counter()
     for (g, n), (a, b) in zip(plan, ev):
         a.record(cur)
