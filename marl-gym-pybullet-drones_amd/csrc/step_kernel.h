@@ -673,12 +673,15 @@ template <int K> __device__ __forceinline__ void dw16_pair(float px, float py, f
     f = f - back;
   }
 }
+// Four independent partial sums (pairs K ≡ 1, 2, 3, 0 mod 4), added at the end:
+// the eight pair terms no longer wait on one 15-deep subtraction chain (two
+// waves per SIMD could not hide it, C5's SQ counters)
 __device__ __forceinline__ float downwash16(float px, float py, float pz) {
-  float f = 0.f;
-  dw16_pair<1>(px, py, pz, f); dw16_pair<2>(px, py, pz, f); dw16_pair<3>(px, py, pz, f);
-  dw16_pair<4>(px, py, pz, f); dw16_pair<5>(px, py, pz, f); dw16_pair<6>(px, py, pz, f);
-  dw16_pair<7>(px, py, pz, f); dw16_pair<8>(px, py, pz, f);
-  return f;
+  float f1 = 0.f, f2 = 0.f, f3 = 0.f, f4 = 0.f;
+  dw16_pair<1>(px, py, pz, f1); dw16_pair<2>(px, py, pz, f2); dw16_pair<3>(px, py, pz, f3);
+  dw16_pair<4>(px, py, pz, f4); dw16_pair<5>(px, py, pz, f1); dw16_pair<6>(px, py, pz, f2);
+  dw16_pair<7>(px, py, pz, f3); dw16_pair<8>(px, py, pz, f4);
+  return (f1 + f2) + (f3 + f4);
 }
 
 
