@@ -44,3 +44,39 @@ def test_oracle_exports():
     lib = qs_oracle.lib()
     for n in ("qso_create", "qso_reset", "qso_step", "qso_state_io", "qso_reset_envs", "qso_gae", "qso_dsl_pid"):
         assert hasattr(lib, n)
+
+
+def test_ctypes_records_match_the_headers(tmp_path):
+    """The ctypes mirrors of the C-ABI records (qs_spec, qs_mlp256) have the headers'
+    size and field offsets: a C program built with gcc against include/*.h prints
+    them (a field added on one side only would shift every later field)."""
+    import subprocess
+    from gym_pybullet_drones_amd import _lib as L
+    recs = {"qs_spec": L.QsSpec, "qs_dims": L.QsDims, "qs_step_out": L.QsStepOut, "qs_mlp256": L.QsMlp256}
+    ctype_name = {"in_": "in"}   # Python keyword renamed in the mirror
+    lines = ["#include <stddef.h>", "#include <stdio.h>", '#include "quadswarm.h"', '#include "qs_learner.h"',
+             "int main(void) {"]
+    for rec, cls in recs.items():
+        lines.append(f'  printf("{rec} size %zu\\n", sizeof({rec}));')
+        for f in cls._fields_:
+            name = ctype_name.get(f[0], f[0])
+            lines.append(f'  printf("{rec} {f[0]} %zu\\n", offsetof({rec}, {name}));')
+    lines.append('  printf("qs_episode_rec size %zu\\n", sizeof(qs_episode_rec));')
+    for name in L.EPISODE_DTYPE.names:   # the numpy view of the episode-log records
+        lines.append(f'  printf("qs_episode_rec {name} %zu\\n", offsetof(qs_episode_rec, {name}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        rec, field, val = line.split()
+        got[(rec, field)] = int(val)
+    for rec, cls in recs.items():
+        assert got[(rec, "size")] == ctypes.sizeof(cls), rec
+        for f in cls._fields_:
+            assert got[(rec, f[0])] == getattr(cls, f[0]).offset, (rec, f[0])
+    assert got[("qs_episode_rec", "size")] == L.EPISODE_DTYPE.itemsize
+    for name in L.EPISODE_DTYPE.names:
+        assert got[("qs_episode_rec", name)] == L.EPISODE_DTYPE.fields[name][1], name
