@@ -78,8 +78,6 @@ def parse():
     p.add_argument("--slots", type=int, default=32, help="rollout-buffer slots the obs ring cycles through")
     p.add_argument("--graph-steps", type=int, default=512, help="control steps per captured HIP graph of the sim legs")
     p.add_argument("--no-stagger", action="store_true", help="start every env at episode step 0")
-    p.add_argument("--rewarm", type=int, default=0, help="dev: untimed graph replays right before the timed window")
-    p.add_argument("--rewarm-before", type=int, default=0, help="dev: untimed graph replays before the episode count")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--mappo", type=int, default=1, help="also time full MAPPO train steps (0 = skip)")
@@ -368,18 +366,12 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
         g.replay()
     torch.cuda.synchronize()
     plan = [graphs[0]] * n_full + ([graphs[-1]] if rem else [])
-    for _ in range(args.rewarm_before):   # dev probe: the same replays, before the episode count
-        for g, _n in graphs:
-            g.replay()
     _, ended0 = sw.episode_log(cap=0)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     cur = torch.cuda.current_stream()
     for a, b in ev:   # a torch Event creates its HIP event at its first record: not inside the window
         a.record(cur)
         b.record(cur)
-    for _ in range(args.rewarm):   # dev probe: more untimed replays right before the window
-        for g, _n in graphs:
-            g.replay()
     ranks.fence()
     t0 = time.perf_counter()
     for (g, n), (a, b) in zip(plan, ev):
