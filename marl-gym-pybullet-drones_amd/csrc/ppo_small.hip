@@ -9,8 +9,10 @@
 // dependent launches per minibatch.  Here a minibatch is two launches:
 //
 //  1. ppo_small_fb_kernel: one workgroup per 16-row tile (actor tiles first,
-//     then critic tiles), the hidden width split over its 8 waves (wave w owns
-//     hidden blocks 2w, 2w+1): layer 1, layer 2, the head (a fixed-order sum of
+//     then critic tiles), the hidden width split over its 16 waves (wave w owns
+//     hidden block w; four waves a SIMD hide each other's MFMA chains): layer 1
+//     (from a copy of W1 padded to whole quads when the caller keeps one), layer
+//     2, the head (a fixed-order sum of
 //     the waves' partial dots through LDS), the PPO policy / value head
 //     (AG:602-683), dZ2, dH1 = dZ2·W2 and dZ1, with the activations exchanged
 //     between the waves through LDS.  v_mfma_f32_16x16x4_f32: lane (g, j)
@@ -23,12 +25,14 @@
 //  2. ppo_small_adam_kernel: one wave per 16×16 weight tile computes its
 //     gradient over the whole minibatch (fixed order: no partials, no atomics)
 //     and applies Adam to it in place (actor gated by approx_kl, AG:731-734), W2
-//     also written transposed for the next minibatch's dH1; the vector
+//     also written transposed for the next minibatch's dH1 (and W1 into its
+//     padded copy); the vector
 //     parameters (biases, head, logstd) from the tile partials.  The last
 //     workgroup commits the step counts.
 //
-// MFMA-bound per CU: a 16-row actor tile is 16·(32·256 + 2·256²) MACs =
-// 272 MFMAs a wave, two waves a SIMD (~7 µs); the whole minibatch is 0.13 GFLOP.
+// MFMA-bound per CU: a 16-row tile is one workgroup on one CU; the critic's
+// (216 inputs) ~6 MFLOP takes ≥ ~10 µs at one CU's share of the fp32 MFMA peak
+// (phase stamps: DESIGN.md §4d); the whole minibatch is 0.13 GFLOP.
 
 #include <hip/hip_runtime.h>
 #include <cmath>
