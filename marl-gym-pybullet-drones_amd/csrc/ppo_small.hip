@@ -572,10 +572,11 @@ struct STile {
   int which, nb, kb;   // W1 / W2, output block, input block
 };
 
+// p / m / v of element i loaded by the caller ahead of the gradient (their
+// latency hides behind the gradient's loads)
 __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, float bc1, float bc2s, float* w2t,
-                                       int n, int k, float* w1p = nullptr) {
+                                       int n, int k, float* w1p, float p, float m, float v) {
   // torch.optim.Adam (amsgrad=False, weight_decay=0): learner.hip's adam_elem
-  const float p = N.p[i], m = N.m[i], v = N.v[i];
   const float m1 = m + (1.0f - N.beta1) * (g - m);
   const float v1 = v * N.beta2 + (1.0f - N.beta2) * g * g;
   N.m[i] = m1;
@@ -623,6 +624,16 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
         const int kcol = 16 * kb + j;
         const float* arow = dzT + (size_t)(16 * nb + j) * KS;
         const float* brow = xT + (size_t)min(kcol, Kin - 1) * KS;   // (columns past Kin are not stored)
+        // the four elements' parameter and moments first (clamped: unconditional loads)
+        long long ei[4];
+        float pp[4], pm[4], pv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ei[r] = (which == 1 ? N.w1 : N.w2) + (long long)(16 * nb + 4 * g + r) * Kin + min(kcol, Kin - 1);
+          pp[r] = N.p[ei[r]];
+          pm[r] = N.m[ei[r]];
+          pv[r] = N.v[ei[r]];
+        }
         // dW[16nb + 4g + r][16kb + j] = Σ_rows dZ[row][n]·X[row][k], rows in MFMA order
         f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
         s_wgrad_acc(arow, brow, KP / 16, g, c);
@@ -631,9 +642,8 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int n = 16 * nb + 4 * g + r;
-            const long long i = (which == 1 ? N.w1 : N.w2) + (long long)n * Kin + kcol;
-            s_adam(N, i, c[r], sc[si][0], sc[si][1], which == 2 ? N.w2t : nullptr, n, kcol,
-                   which == 1 ? N.w1p : nullptr);
+            s_adam(N, ei[r], c[r], sc[si][0], sc[si][1], which == 2 ? N.w2t : nullptr, n, kcol,
+                   which == 1 ? N.w1p : nullptr, pp[r], pm[r], pv[r]);
           }
         }
       }
@@ -667,25 +677,30 @@ __global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int 
         for (; t < nt; ++t) acc += base[(size_t)t * stride];
         return acc;
       };
+      // the element and its partial-row column first, then its parameter and
+      // moments (in flight during the column sum)
+      const float* col = nullptr;
+      int cstride = 0;
       if (u < kSH) {                       // b1: Σ dZ1
-        gsum = colsum(pB + u, kSH);
+        col = pB + u; cstride = kSH;
         i = N.b1 + u;
       } else if ((u -= kSH) < kSH) {       // b2: Σ dZ2
-        gsum = colsum(pA + u, PA);
+        col = pA + u; cstride = PA;
         i = N.b2 + u;
       } else if ((u -= kSH) < AA * kSH) {  // W3: Σ dout·H2
-        gsum = colsum(pA + kSH + u, PA);
+        col = pA + kSH + u; cstride = PA;
         i = N.w3 + u;
       } else if ((u -= AA * kSH) < AA) {   // b3: Σ dout
-        gsum = colsum(pA + kSH + AA * kSH + u, PA);
+        col = pA + kSH + AA * kSH + u; cstride = PA;
         i = N.b3 + u;
       } else {                             // logstd (the actor's loss tail)
         u -= AA;
-        gsum = P.w.dlogstd[u];
         i = N.logstd + u;
       }
+      const float p0 = N.p[i], m0 = N.m[i], v0 = N.v[i];
+      gsum = col ? colsum(col, cstride) : P.w.dlogstd[u];
       const int si = actor ? 0 : 1;
-      s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0);
+      s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, p0, m0, v0);
     }
   }
   __syncthreads();
