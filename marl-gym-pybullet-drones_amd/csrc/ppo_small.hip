@@ -54,7 +54,7 @@ constexpr int kSHS = kSH + 4;          // LDS row stride of the hidden exchange 
 constexpr int kSMaxI = 256;            // widest input
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of the Adam kernel
-constexpr int kSVecWG = 4;             // Adam workgroups for the vector parameters
+constexpr int kSVecWG = 4;             // Adam workgroups for the vector parameters (8 measured no faster)
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
 // Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
 // forward/backward tile uses ~53 KB and would otherwise be packed up to three
