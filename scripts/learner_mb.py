@@ -189,6 +189,12 @@ def main():
             us, path = per_minibatch_us("C3", critic_tiles=False)
             print(f"C3  dW1 chunk rows {m:<37d} {us:8.1f} us/minibatch  [{path}]", flush=True)
         agent_mod._SPLITK_MIN_ROWS.pop((32768, 27))
+    if "prio" in which:   # the default and side_priority=-1 interleaved (the first variant of a process runs cold)
+        for shape in ("C3", "C4"):
+            for v in (dict(), dict(side_priority=-1), dict(), dict(side_priority=-1), dict(critic_adam_side=True),
+                      dict(side_priority=-1, critic_adam_side=True), dict()):
+                us, path = per_minibatch_us(shape, **v)
+                print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "C4v" in which:   # learner variants at C4 (critic I = 595)
         for v in (dict(critic_tiles=False), dict(critic_tiles=False, critic_adam_side=True),
                   dict(critic_tiles=False, side_priority=-1), dict(critic_tiles=False, side_stream=False),
