@@ -140,6 +140,16 @@ int qs_mlp3_fwd(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, cons
 int qs_mlp3_fwd_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
                      const float* pack, const float* b1, const float* b2, const float* W3, const float* b3, float* H1T,
                      float* H2T, float* out, void* stream);
+/* qs_mlp3_fwd_rows with the centralized critic's value head folded in (A = 1;
+ * compute_value_loss, AG:642-683, with qs_value_head's arithmetic): dv[r] =
+ * (v_r − mean_d ret[rows[r]])/K and acc[1] += ½·mean over the K rows of
+ * (v − mean_d ret)²; D: agents per env-timestep (the reference's mean over
+ * them); work: qs_mlp3_value_work_bytes(K) bytes, zeroed once (left zero). */
+int64_t qs_mlp3_value_work_bytes(int64_t K);
+int qs_mlp3_fwd_rows_value(int64_t K, int32_t I, int32_t D, const float* X, const int64_t* rows, float* Xg,
+                           const float* pack, const float* b1, const float* b2, const float* W3, const float* b3,
+                           float* H1T, float* H2T, float* out, const double* ret, float* dv, double* acc, void* work,
+                           void* stream);
 /* qs_mlp3_fwd over groups of G consecutive rows: row r of the batch is
  * X[rows[r / G]·G + r % G] (K a multiple of G).  The actor's minibatch read
  * straight from the rollout table [T·E·D][O] with rows = the sampled

@@ -1882,6 +1882,18 @@ __device__ __forceinline__ f32x16 m3w_contract(const float4* __restrict__ mat, i
   return z;
 }
 
+// The centralized critic's value head folded into its forward (qs_mlp3_fwd_rows_value):
+// compute_value_loss (AG:642-683) per row as qs_value_head does it, its loss sum
+// from the last workgroup.  dv == NULL: the plain forward.
+struct M3ValueHead {
+  const double* ret;   // [T·E] returns; row r's is ret[rows[r]]
+  float* dv;           // [K] d(value loss)/dv
+  double* lossp;       // [grid] per-workgroup Σ (v − ret)²
+  double* acc;         // acc[1] += ½·mean
+  unsigned* count;     // arrival counter (left zero)
+  int D, mb;
+};
+
 template <int A>
 __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I, const float* __restrict__ X,
                                                               const float* __restrict__ pack,
@@ -1891,7 +1903,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
                                                               const float* __restrict__ b3, float* __restrict__ H1T,
                                                               float* __restrict__ H2T, float* __restrict__ out,
                                                               const long long* __restrict__ rows,
-                                                              float* __restrict__ Xg, int G) {
+                                                              float* __restrict__ Xg, int G, M3ValueHead vh) {
   // LDS: the X tile during layer 1, then the H1ᵀ exchange
   extern __shared__ float lds[];   // m3w_lds_floats(Ip)
   __shared__ float hp[kM3WWaves][A][64];
@@ -1986,6 +1998,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
 #pragma unroll
   for (int a = 0; a < A; ++a) hp[w][a][lane] = hs[a] + __shfl_xor(hs[a], 32, 64);
   __syncthreads();
+  float v0 = 0.f;
   if (w == 0 && h == 0 && rv)
 #pragma unroll
     for (int a = 0; a < A; ++a) {
@@ -1993,7 +2006,43 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
 #pragma unroll
       for (int k = 1; k < kM3WWaves; ++k) t += hp[k][a][lane];
       out[r * A + a] = t + b3[a];
+      if (a == 0) v0 = t + b3[a];
     }
+  if (!vh.dv) return;   // (kernel-uniform)
+  // the value head (qs_value_head's arithmetic): dv = (v − mean_d ret)/mb, and
+  // the tile's Σ (v − mean_d ret)² over its rows in lane order
+  __shared__ bool vlast;
+  if (w == 0) {
+    double sq = 0.0;
+    if (h == 0 && rv) {
+      const double rt = vh.ret[rows[r]];
+      double rs = 0;
+      for (int d = 0; d < vh.D; ++d) rs += rt;
+      const double diff = (double)v0 - rs / (double)vh.D;
+      vh.dv[r] = (float)(diff / (double)vh.mb);
+      sq = diff * diff;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);   // within each half: lanes 0..31 hold the rows
+    if (lane == 0) {
+      vh.lossp[blockIdx.x] = sq;
+      __threadfence();
+      vlast = atomicAdd(vh.count, 1u) == gridDim.x - 1;
+    }
+  }
+  __syncthreads();
+  if (!vlast || w != 0) return;
+  // the last workgroup: the tiles' sums (lane q: tiles q, q + 64, ... in order),
+  // then a fixed xor butterfly (every lane the same bits)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double tot = 0.0;
+  for (unsigned b = lane; b < gridDim.x; b += 64) tot += vh.lossp[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  if (lane == 0) {
+    vh.acc[1] += 0.5 * (tot / (double)vh.mb);
+    *vh.count = 0u;
+  }
 }
 
 template <int A>
@@ -2362,13 +2411,15 @@ int qs_mlp3_pack(int32_t I, int32_t N, const float* W1, const float* W2, float* 
 
 static int mlp3_fwd_launch(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, float* Xg,
                            int32_t G, const float* pack, const float* b1, const float* b2, const float* W3,
-                           const float* b3, float* H1T, float* H2T, float* out, void* stream, const char* name) {
+                           const float* b3, float* H1T, float* H2T, float* out, void* stream, const char* name,
+                           M3ValueHead vh = M3ValueHead{}) {
   if (K <= 0 || K * kM3N * 4 >= (int64_t(1) << 31) || K * (int64_t)I * 4 >= (int64_t(1) << 31) || I <= 0 || I > 1024 || N != kM3N || A < 1 || A > 4 || !X || !pack ||
       !b1 || !b2 || !W3 || !b3 || (!H1T) != (!H2T) || !out)
     return fail(QS_E_INVALID, std::string(name) + ": bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
   if (G < 1 || (G > 1 && Xg)) return fail(QS_E_INVALID, std::string(name) + ": bad group size");
   // the row-gathering form with a gathered copy (G = 1) is the 8-wave kernel's
   const bool wide = (rows && G == 1) || m3_wide(K, I);
+  if (vh.dv && (!wide || A != 1)) return fail(QS_E_INVALID, std::string(name) + ": the value head needs the 8-wave kernel and A = 1");
   const unsigned grid = (unsigned)(wide ? (K + 31) / 32 : qs_mlp3_tiles(K, I));
   const unsigned lds = wide ? (unsigned)(m3w_lds_floats((I + 31) & ~31) * sizeof(float)) : 0u;
   const long long* rr = (const long long*)rows;
@@ -2379,7 +2430,7 @@ static int mlp3_fwd_launch(int64_t K, int32_t I, int32_t N, int32_t A, const flo
   auto gow = [&](auto kern) {
     if (lds > 65536u) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kM3WBlock), lds, (hipStream_t)stream, (long long)K, (int)I, X, pack, b1,
-                       b2, W3, b3, H1T, H2T, out, rr, Xg, (int)G);
+                       b2, W3, b3, H1T, H2T, out, rr, Xg, (int)G, vh);
   };
   if (rows && !wide) {
     switch (A) {
@@ -2410,6 +2461,26 @@ int qs_mlp3_fwd_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X,
                      float* H2T, float* out, void* stream) {
   if (!rows) return fail(QS_E_INVALID, "qs_mlp3_fwd_rows: rows is NULL");
   return mlp3_fwd_launch(K, I, N, A, X, rows, Xg, 1, pack, b1, b2, W3, b3, H1T, H2T, out, stream, "qs_mlp3_fwd_rows");
+}
+
+int64_t qs_mlp3_value_work_bytes(int64_t K) { return K > 0 ? 64 + 8 * ((K + 31) / 32) : 0; }
+
+int qs_mlp3_fwd_rows_value(int64_t K, int32_t I, int32_t D, const float* X, const int64_t* rows, float* Xg,
+                           const float* pack, const float* b1, const float* b2, const float* W3, const float* b3,
+                           float* H1T, float* H2T, float* out, const double* ret, float* dv, double* acc, void* work,
+                           void* stream) {
+  if (!rows || !ret || !dv || !acc || !work || D <= 0 || K <= 0 || K > (1LL << 31) - 1)
+    return fail(QS_E_INVALID, "qs_mlp3_fwd_rows_value: bad argument");
+  M3ValueHead vh;
+  vh.ret = ret;
+  vh.dv = dv;
+  vh.count = (unsigned*)work;
+  vh.lossp = (double*)((char*)work + 64);
+  vh.acc = acc;
+  vh.D = D;
+  vh.mb = (int)K;
+  return mlp3_fwd_launch(K, I, kM3N, 1, X, rows, Xg, 1, pack, b1, b2, W3, b3, H1T, H2T, out, stream,
+                         "qs_mlp3_fwd_rows_value", vh);
 }
 
 int qs_mlp3_fwd_group_rows(int64_t K, int32_t I, int32_t N, int32_t A, const float* X, const int64_t* rows, int32_t G,

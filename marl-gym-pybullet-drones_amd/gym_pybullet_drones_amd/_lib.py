@@ -68,7 +68,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
            "qs_wgrad_rm", "qs_learner_last_error", "qs_rms_work_bytes", "qs_rms_update", "qs_rms_normalize",
-           "qs_rms_last_error", "qs_policy_sample", "qs_rollout_record", "qs_rollout_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error",
+           "qs_rms_last_error", "qs_mlp3_value_work_bytes", "qs_mlp3_fwd_rows_value", "qs_policy_sample", "qs_rollout_record", "qs_rollout_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error",
            "qs_ppo_small_layout", "qs_ppo_critic_tiles", "qs_wgrad_t")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
 QS_PACK_W2T = 1 << 17   # pack_I flag: a [256][256] W2ᵀ copy (include/qs_learner.h)
@@ -162,6 +162,8 @@ def load():
     L.qs_learner_last_error.restype = ctypes.c_char_p
     L.qs_rms_last_error.restype = ctypes.c_char_p
     L.qs_rollout_last_error.restype = ctypes.c_char_p
+    L.qs_mlp3_value_work_bytes.argtypes = [i64]
+    L.qs_mlp3_fwd_rows_value.argtypes = [i64, ctypes.c_int32, ctypes.c_int32] + [vp] * 16
     L.qs_policy_sample.argtypes = [i64, ctypes.c_int32, vp, vp, f32, f32, ctypes.c_int32, vp, vp, vp, vp]
     L.qs_rollout_record.argtypes = [i64] + [vp] * 7
     L.qs_ppo_small_last_error.restype = ctypes.c_char_p
@@ -184,6 +186,7 @@ def load():
     L.qs_mlp3f_work_bytes.restype = i64
     L.qs_mlp_sum_adam_work_bytes.restype = i64
     L.qs_rms_work_bytes.restype = i64
+    L.qs_mlp3_value_work_bytes.restype = i64
     L.qs_ppo_small_work_bytes.restype = i64
     L.qs_mlp_sum_adam_work_bytes.argtypes = []
     _lib = L

@@ -293,6 +293,17 @@ class _M3Work:
                     "qs_mlp3_fwd_rows")
         return self.out
 
+    def forward_value(self, x, rows, xg, ret, D, dv, acc, work):
+        """The critic forward over the gathered rows with compute_value_loss's head
+        folded in (qs_mlp3_fwd_rows_value): dv = d(value loss)/dv, acc[1] += the loss."""
+        lib, st = L.load(), _stream()
+        f0, f1, f2 = self.mlp.fcs
+        L.check(lib.qs_mlp3_fwd_rows_value(self.K, self.I, int(D), L.ptr(x), L.ptr(rows), L.ptr(xg), L.ptr(self.pack),
+                                           L.ptr(f0.bias), L.ptr(f1.bias), L.ptr(f2.weight), L.ptr(f2.bias),
+                                           L.ptr(self.h1), L.ptr(self.h2), L.ptr(self.out), L.ptr(ret), L.ptr(dv),
+                                           L.ptr(acc), L.ptr(work), st), "qs_mlp3_fwd_rows_value")
+        return self.out
+
     def pack_segment(self, fb):
         """(pack, w1 offset, w2 offset, I) of this MLP inside FlatBuffers fb."""
         f0, f1, _ = self.mlp.fcs
@@ -931,6 +942,8 @@ class MAPPOAgent:
         # launch).  Opt-in: measured slower (update 2 077 vs 1 961 ms)
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
         self.side_priority = kwargs.get('side_priority', 0)
+        # the critic's value head folded into its forward launch (qs_mlp3_fwd_rows_value)
+        self.fused_value_head = kwargs.get('fused_value_head', True)
         # (opt-in) with the fused actor, the critic's step on qs_ppo_critic_tiles +
         # qs_wgrad_t instead of the qs_mlp3w kernels and hipBLASLt weight-gradient
         # GEMMs (measured slower at the C3 shape)
@@ -1090,6 +1103,7 @@ class MAPPOAgent:
         tiles = f16 and self.critic_tiles and pc.fcs[0].in_features <= 256 and pc.fcs[2].out_features == 1
         self._ws_critic = _CriticTiles(self, mb, D) if tiles else _M3Work(pc, mb, self.device)
         self._vh_work = torch.zeros(int(lib.qs_ppo_heads_work_bytes(mb, D)), dtype=torch.uint8, device=self.device)
+        self._fv_work = torch.zeros(int(lib.qs_mlp3_value_work_bytes(mb)), dtype=torch.uint8, device=self.device)
         self._xg = torch.empty((mb, D * O), device=self.device)
         self._dmean = torch.empty(mb * D, A, device=self.device)
         self._dv = torch.empty(mb, 1, device=self.device)
@@ -1153,9 +1167,15 @@ class MAPPOAgent:
                         _flush_sums(tc)
                         self._exchange_bucket(self._critic_bucket, world)
                 else:
-                    v = critic_fwd()
-                    L.check(lib.qs_value_head(mb, D, L.ptr(idx), L.ptr(rollouts.ret_env), L.ptr(v), L.ptr(self._dv),
-                                              L.ptr(acc), L.ptr(self._vh_work), _stream()), "qs_value_head")
+                    if self.fused_value_head:
+                        # the value head inside the critic forward: one launch fewer on the critic's chain
+                        self._ws_critic.forward_value(rollouts.obs.reshape(T * E, D * O), idx, self._xg, rollouts.ret_env,
+                                                      D, self._dv, acc, self._fv_work)
+                    else:
+                        v = critic_fwd()
+                        L.check(lib.qs_value_head(mb, D, L.ptr(idx), L.ptr(rollouts.ret_env), L.ptr(v),
+                                                  L.ptr(self._dv), L.ptr(acc), L.ptr(self._vh_work), _stream()),
+                                "qs_value_head")
                     critic_bwd(exchange)
                 if own_adam:
                     # the critic's Adam is ungated: its sums and step run here, beside

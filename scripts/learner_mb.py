@@ -195,6 +195,11 @@ def main():
                       dict(side_priority=-1, critic_adam_side=True), dict()):
                 us, path = per_minibatch_us(shape, **v)
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "vh" in which:   # the critic's value head folded into its forward vs the separate launch, interleaved
+        for shape in ("C3", "C4"):
+            for v in (dict(), dict(fused_value_head=False), dict(), dict(fused_value_head=False), dict()):
+                us, path = per_minibatch_us(shape, **v)
+                print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "C4v" in which:   # learner variants at C4 (critic I = 595)
         for v in (dict(critic_tiles=False), dict(critic_tiles=False, critic_adam_side=True),
                   dict(critic_tiles=False, side_priority=-1), dict(critic_tiles=False, side_stream=False),

@@ -253,6 +253,23 @@ def test_direct_update_side_stream_bit_identical(graphs, E, T):
         assert r_side[k] == pytest.approx(r_fused[k], rel=1e-5, abs=1e-7)
 
 
+@pytest.mark.parametrize("E,T", [(256, 16), (32, 8)])
+def test_direct_update_fused_value_head_bit_identical(E, T):
+    """The critic's value head folded into its forward (qs_mlp3_fwd_rows_value)
+    gives the same dv, hence bit-identical weights and moments, as the separate
+    qs_value_head launch; the value-loss statistic differs only in its summation
+    order."""
+    a_f, r_f = _hidden256_update(True, E, T)
+    assert a_f.fused_value_head and type(a_f._ws_critic).__name__ == "_M3Work"
+    a_s, r_s = _hidden256_update(True, E, T, fused_value_head=False)
+    assert torch.equal(a_f.actor_opt.flat, a_s.actor_opt.flat)
+    assert torch.equal(a_f.critic_opt.flat, a_s.critic_opt.flat)
+    assert torch.equal(a_f.critic_opt.exp_avg_sq, a_s.critic_opt.exp_avg_sq)
+    for k in r_f:
+        assert r_f[k] == pytest.approx(r_s[k], rel=1e-12, abs=1e-15)
+    assert int(a_f._fv_work[:4].sum()) == 0   # the arrival counter is left zero for the next replay
+
+
 @pytest.mark.parametrize("graphs", [False, True])
 def test_direct_update_fused_actor_four_outputs(graphs):
     """The fused actor kernel on a 4-output actor (Spiral's VEL actions, the C4
