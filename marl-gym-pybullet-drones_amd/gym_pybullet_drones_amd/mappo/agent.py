@@ -943,7 +943,7 @@ class MAPPOAgent:
         self.critic_adam_side = kwargs.get('critic_adam_side', False)
         self.side_priority = kwargs.get('side_priority', 0)
         # the critic's value head folded into its forward launch (qs_mlp3_fwd_rows_value)
-        self.fused_value_head = kwargs.get('fused_value_head', True)
+        self.fused_value_head = kwargs.get('fused_value_head', False)
         # (opt-in) with the fused actor, the critic's step on qs_ppo_critic_tiles +
         # qs_wgrad_t instead of the qs_mlp3w kernels and hipBLASLt weight-gradient
         # GEMMs (measured slower at the C3 shape)

@@ -197,7 +197,7 @@ def main():
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "vh" in which:   # the critic's value head folded into its forward vs the separate launch, interleaved
         for shape in ("C3", "C4"):
-            for v in (dict(), dict(fused_value_head=False), dict(), dict(fused_value_head=False), dict()):
+            for v in (dict(), dict(fused_value_head=True), dict(), dict(fused_value_head=True), dict()):
                 us, path = per_minibatch_us(shape, **v)
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "C4v" in which:   # learner variants at C4 (critic I = 595)

@@ -259,7 +259,7 @@ def test_direct_update_fused_value_head_bit_identical(E, T):
     gives the same dv, hence bit-identical weights and moments, as the separate
     qs_value_head launch; the value-loss statistic differs only in its summation
     order."""
-    a_f, r_f = _hidden256_update(True, E, T)
+    a_f, r_f = _hidden256_update(True, E, T, fused_value_head=True)
     assert a_f.fused_value_head and type(a_f._ws_critic).__name__ == "_M3Work"
     a_s, r_s = _hidden256_update(True, E, T, fused_value_head=False)
     assert torch.equal(a_f.actor_opt.flat, a_s.actor_opt.flat)
