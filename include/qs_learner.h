@@ -24,6 +24,8 @@
  *   MeanStdNormalizer.__call__ / RunningMeanStd.update            qs_rms_update,
  *     (safe_control_gym normalization.py:13-120): torch float64      qs_rms_normalize
  *     column reductions per rollout step
+ *   the critic forward + compute_value_loss head (AG:642-683)     qs_mlp3_fwd_rows_value
+ *     in one launch (opt-in)
  *   MAPPOActorCritic.step sampling (agent.py:389-415,              qs_policy_sample,
  *     distributions.py:9-33) and the rollout's done / mask /        qs_rollout_record
  *     reward bookkeeping (MP:818-845): torch elementwise launches
