@@ -195,6 +195,9 @@ def main():
                       dict(side_priority=-1, critic_adam_side=True), dict()):
                 us, path = per_minibatch_us(shape, **v)
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "one" in which:   # the default C3 iteration alone (for a kernel trace: scripts/learner_timeline.py)
+        us, path = per_minibatch_us("C3")
+        print(f"C3  default {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "vh" in which:   # the critic's value head folded into its forward vs the separate launch, interleaved
         for shape in ("C3", "C4"):
             for v in (dict(), dict(fused_value_head=True), dict(), dict(fused_value_head=True), dict()):
