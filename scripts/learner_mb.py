@@ -198,6 +198,13 @@ def main():
     if "one" in which:   # the default C3 iteration alone (for a kernel trace: scripts/learner_timeline.py)
         us, path = per_minibatch_us("C3")
         print(f"C3  default {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "w1" in which:   # the actor's dW1 beside dW2 on a third stream (default) vs after it, interleaved
+        for shape in ("C3", "C4"):
+            for w1s in (True, False, True, False, True):
+                agent_mod._F16Work.w1_stream = w1s
+                us, path = per_minibatch_us(shape)
+                print(f"{shape}  w1_stream={w1s!s:48s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+        agent_mod._F16Work.w1_stream = True
     if "vh" in which:   # the critic's value head folded into its forward vs the separate launch, interleaved
         for shape in ("C3", "C4"):
             for v in (dict(), dict(fused_value_head=True), dict(), dict(fused_value_head=True), dict()):
