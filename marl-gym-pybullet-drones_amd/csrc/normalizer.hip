@@ -112,60 +112,71 @@ __global__ void __launch_bounds__(kRmsBlock) rms_tile_kernel(RmsShape s, const f
   if (count && b == 0 && blockIdx.y == 0 && threadIdx.x == 0) *reinterpret_cast<double*>(work) = *count;
 }
 
-// Launch 2: a workgroup per 64 columns merges the tiles (the four waves over the
-// tiles t ≡ w mod 4, sixteen loads in flight, then in wave order): the batch
-// mean Σ n_t·mean_t / R, then M2 = Σ (M2_t + n_t·(mean_t − mean)²) (the
-// parallel-variance merge with the mean known), then normalization.py:42-60's
-// update of the running statistics in its operation order, from the count
-// launch 1 saved; block 0 writes the new count.  No atomics, no fences (the
-// launch boundary orders launch 1's writes), every order fixed: a replay is
-// bit-identical.
+// Launch 2: a workgroup per 16 columns merges the tiles: 16 slices of the
+// workgroup's threads take the tiles t ≡ slice (mod 16), eight loads in flight,
+// and the slices are added in order through LDS: the batch mean Σ n_t·mean_t / R,
+// then M2 = Σ (M2_t + n_t·(mean_t − mean)²) (the parallel-variance merge with
+// the mean known), then normalization.py:42-60's update of the running
+// statistics in its operation order, from the count launch 1 saved; block 0
+// writes the new count.  No atomics, no fences (the launch boundary orders
+// launch 1's writes), every order fixed: a replay is bit-identical.
+constexpr int kRmsMergeCols = 16, kRmsSlices = kRmsBlock / kRmsMergeCols;
+__device__ __forceinline__ double rms_slice_sum(double (*red)[kRmsMergeCols], double v, int sl, int cl) {
+  red[sl][cl] = v;
+  __syncthreads();
+  double r = red[0][cl];
+#pragma unroll
+  for (int k = 1; k < kRmsSlices; ++k) r += red[k][cl];
+  __syncthreads();
+  return r;
+}
+
 __global__ void __launch_bounds__(kRmsBlock) rms_merge_kernel(RmsShape s, double* __restrict__ mean,
                                                               double* __restrict__ var, double* __restrict__ count,
                                                               double* __restrict__ sums,
                                                               const unsigned* __restrict__ work) {
-  __shared__ double red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * kRmsCols + lane;
+  __shared__ double red[kRmsSlices][kRmsMergeCols];
+  const int cl = threadIdx.x % kRmsMergeCols, sl = threadIdx.x / kRmsMergeCols;
+  const int c = blockIdx.x * kRmsMergeCols + cl;
   const bool cv = c < s.C;
   const int cc = cv ? c : 0;
   const double* mean_b = reinterpret_cast<const double*>(reinterpret_cast<const char*>(work) + 64);
   const double* m2_b = mean_b + (size_t)s.GR * s.C;
   const double cnt = sums ? 0.0 : *reinterpret_cast<const double*>(work);   // (the multi-rank form has no statistics)
   auto nrows = [&](int tt) { return (double)min((long long)kRmsRows, s.R - (long long)tt * kRmsRows); };
-  constexpr int kMergeU = 16;
+  constexpr int kMergeU = 8;
   double ma = 0.0;
-  for (int t0 = w; t0 < s.GR; t0 += 4 * kMergeU) {
+  for (int t0 = sl; t0 < s.GR; t0 += kRmsSlices * kMergeU) {
     double mv[kMergeU];
 #pragma unroll
     for (int u = 0; u < kMergeU; ++u) {
-      const int tt = t0 + 4 * u;
+      const int tt = t0 + kRmsSlices * u;
       mv[u] = tt < s.GR ? mean_b[(size_t)tt * s.C + cc] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kMergeU; ++u)
-      if (t0 + 4 * u < s.GR) ma += nrows(t0 + 4 * u) * mv[u];
+      if (t0 + kRmsSlices * u < s.GR) ma += nrows(t0 + kRmsSlices * u) * mv[u];
   }
   const double na = (double)s.R;
-  const double bm = rms_wave_sum(red, ma, w, lane) / na;
+  const double bm = rms_slice_sum(red, ma, sl, cl) / na;
   double mq = 0.0;
-  for (int t0 = w; t0 < s.GR; t0 += 4 * kMergeU) {
+  for (int t0 = sl; t0 < s.GR; t0 += kRmsSlices * kMergeU) {
     double mv[kMergeU], qv[kMergeU];
 #pragma unroll
     for (int u = 0; u < kMergeU; ++u) {
-      const int tt = t0 + 4 * u;
+      const int tt = t0 + kRmsSlices * u;
       mv[u] = tt < s.GR ? mean_b[(size_t)tt * s.C + cc] : 0.0;
       qv[u] = tt < s.GR ? m2_b[(size_t)tt * s.C + cc] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kMergeU; ++u)
-      if (t0 + 4 * u < s.GR) {
+      if (t0 + kRmsSlices * u < s.GR) {
         const double d = mv[u] - bm;
-        mq += qv[u] + nrows(t0 + 4 * u) * (d * d);
+        mq += qv[u] + nrows(t0 + kRmsSlices * u) * (d * d);
       }
   }
-  const double qa = rms_wave_sum(red, mq, w, lane);
-  if (w == 0 && cv) {
+  const double qa = rms_slice_sum(red, mq, sl, cl);
+  if (sl == 0 && cv) {
     const double bv = qa / na;   // np.mean, np.var (ddof 0)
     if (sums) {   // several ranks: this rank's Σx and Σx² (merged across ranks by the caller)
       sums[c] = bm * na;
@@ -263,7 +274,8 @@ int qs_rms_update(int64_t R, int32_t C, const float* x, double* mean, double* va
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(rms_tile_kernel, dim3((unsigned)s.GR, (unsigned)s.NCB), dim3(kRmsBlock), 0, st, s, x,
                      sums ? nullptr : count, (unsigned*)work);
-  hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)s.NCB), dim3(kRmsBlock), 0, st, s, mean, var, count, sums,
+  hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)((C + kRmsMergeCols - 1) / kRmsMergeCols)), dim3(kRmsBlock), 0, st,
+                     s, mean, var, count, sums,
                      (const unsigned*)work);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : nfail(QS_E_HIP, std::string("qs_rms_update: ") + hipGetErrorString(e));
