@@ -11,7 +11,7 @@
 //
 // Here the moments are two launches: each 64-row tile's columns are held in
 // registers (16 rows per wave) and give the tile's column means and sums of
-// squared deviations (two passes, float64); then a workgroup per 64 columns
+// squared deviations (two passes, float64); then a workgroup per 16 columns
 // merges the tiles (the batch mean first, then the parallel-variance sum
 // Σ M2_t + n_t·(mean_t − mean)²) and applies normalization.py:42-60's update
 // in place in its operation order.  No atomics or fences: an agent-scope
