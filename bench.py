@@ -61,8 +61,33 @@ import torch  # noqa: E402
 from gym_pybullet_drones_amd.envs.swarm import grid_layout  # noqa: E402
 
 METRIC = "agent-steps/sec, MultiHover 8-drone MAPPO @ 1/2/4/8 GPU vs PyBullet CPU"
-BYTES_PER_AGENT_STEP = {"one_d_pid": 418.0, "vel": 790.0, "rpm": 720.0}
+
+
+def bytes_per_agent_step(act="one_d_pid", task="multihover", D=8, precision=4):
+    """SURVEY §8(d)'s algorithmic HBM bytes per agent-step, per field, with each
+    field in the step kernel's own buffer type (csrc/step_kernel.h Params): the
+    agent state st, the MultiHover target and the reward are `real` (float32, or
+    float64 in the precision-8 build); the action, the action history and the
+    obs are float32 in both builds (BRL:307-319 emits a float32 obs once the
+    history holds float32 actions).  Per drone: action A read; state S read +
+    written (S = 29 with the PID state of the PID action types, else 20); target
+    3 read (MultiHover only); history H·A (the H−1 older entries read, one
+    written); obs O written.  Per env, over its D drones: the step counter
+    read + written (8 B), the reward, two flag bytes."""
+    real = 8 if precision == 8 else 4
+    A = {"one_d_pid": 1, "one_d_rpm": 1, "rpm": 4, "vel": 4, "pid": 3}[act]
+    H = 24 if task == "spiral" else 15            # ctrl 48 Hz / 30 Hz: BRL:66 (SURVEY §8 derived sizes)
+    O = 12 + H * A + (11 if task == "spiral" else 0)
+    S = 29 if act in ("one_d_pid", "vel", "pid") else 20
+    target = 3 * real if task != "spiral" else 0
+    per_drone = 4 * A + 2 * S * real + target + 4 * H * A + 4 * O
+    per_env = 8 + real + 2
+    return per_drone + per_env / D
+
+
+BYTES_PER_AGENT_STEP = {a: bytes_per_agent_step(a) for a in ("one_d_pid", "vel", "rpm")}   # D = 8: 417.75 / 789.75 / 717.75
 HBM_PEAK_GBS = 8000.0
+CPU_WORKERS = 22   # the reference's num_workers (README.md:38-39: 22 workers x 8 envs)
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector rate
 EPISODE_STEPS = {"multihover": 242, "spiral": 578}   # SURVEY §8 derived sizes
 
@@ -222,8 +247,11 @@ def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dy
     import qs_oracle
     D = D or args.drones
     act = act or args.act
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 22, os.cpu_count() or 1))
+    # the reference topology: 22 workers x 8 envs (README.md:38-39, BASELINE.md:35-37),
+    # 22 OpenMP threads whatever OMP_NUM_THREADS says (num_threads(22) in the oracle's
+    # loop); host_cpu() records the CPUs this process may use and the quota, and
+    # whether 22 threads oversubscribe them
+    threads = CPU_WORKERS
     E = 176
     ophys, oaux = ("pyb", ("dw",)) if physics == "pyb_dw" else (physics, tuple(aux))
     kw = dict(initial_xyzs=grid_layout(D)) if task == "multihover" and D >= 6 else {}
@@ -243,8 +271,11 @@ def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dy
         # next chunk: double, but no longer than the rest of the budget at the last chunk's rate
         chunk = max(1, min(2 * chunk, int((seconds - dt) / max(dc / chunk, 1e-9)) + 1))
     sim.close()
+    host = host_cpu()
+    host["threads"] = threads
+    host["oversubscribed"] = threads > min(host["nproc"] or threads, host["cpu_quota"] or threads)
     return {"value": E * D * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
-            "host": host_cpu(),
+            "host": host,
             "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {task} {E} envs x "
                       f"{D} drones, {act}, {physics}{'+' + '+'.join(aux) if aux else ''}, {steps} random-policy "
                       f"ctrl steps, OpenMP {threads} threads, {dt:.1f} s"}
@@ -263,23 +294,33 @@ def host_cpu():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count()
-    return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count(),
+    quota = None
+    try:   # cgroup v2 CPU quota ("max" = none): the box's CPU share
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count(), "cpu_quota": quota,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def pmc_traffic(E, D, act):
+def pmc_traffic(E, D, act, precision=4):
     """HBM bytes per step-kernel launch from the newest committed PMC summary of this
-    workload (profiles/rNN_pmc_traffic.json: FETCH_SIZE/WRITE_SIZE passes, calibrated;
-    scripts/gpu_prof.sh).  The counters need rocprofv3 around the process, so the
-    bench reports the committed measurement of the same kernel and names its source."""
+    workload (profiles/rNN_pmc_traffic*.json: FETCH_SIZE/WRITE_SIZE passes, calibrated;
+    scripts/gpu_prof.sh, scripts/r05_pmc64.sh).  The counters need rocprofv3 around
+    the process, so the bench reports the committed measurement of the same kernel
+    and names its source.  precision 8: the fp64 kernel's summary."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))):
+    want = {"envs": E, "drones": D, "act": act}
+    if precision != 4:
+        want["precision"] = precision
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == {"envs": E, "drones": D, "act": act}:
+        if d.get("workload") == want:
             best = (f, d)
     if best is None:
         return None, None
@@ -289,13 +330,17 @@ def pmc_traffic(E, D, act):
 # BASELINE.json configs other than the headline one, each timed as its own
 # random-policy rollout on one rank (bytes per agent-step: SURVEY §8(d)).
 EXTRA_CONFIGS = {
-    "C2": dict(task="multihover", drones=4, envs=4096, act="rpm", physics="dyn", aux=(), bytes=720.0,
+    "C2": dict(task="multihover", drones=4, envs=4096, act="rpm", physics="dyn", aux=(),
+               bytes=bytes_per_agent_step("rpm", "multihover", 4),
                label="MultiHover 4-drone x 4096 envs, ActionType.RPM, Physics.DYN"),
-    "C3_vel": dict(task="multihover", drones=8, envs=16384, act="vel", physics="dyn", aux=(), bytes=790.0,
+    "C3_vel": dict(task="multihover", drones=8, envs=16384, act="vel", physics="dyn", aux=(),
+                   bytes=bytes_per_agent_step("vel", "multihover", 8),
                    label="MultiHover 8-drone x 16384 envs, ActionType.VEL, Physics.DYN"),
-    "C4": dict(task="spiral", drones=5, envs=8192, act="vel", physics="dyn", aux=(), bytes=1111.0,
+    "C4": dict(task="spiral", drones=5, envs=8192, act="vel", physics="dyn", aux=(),
+               bytes=bytes_per_agent_step("vel", "spiral", 5),
                label="Spiral 5-drone x 8192 envs, ActionType.VEL, Physics.DYN"),
-    "C5": dict(task="multihover", drones=16, envs=8192, act="one_d_pid", physics="pyb_dw", aux=(), bytes=418.0,
+    "C5": dict(task="multihover", drones=16, envs=8192, act="one_d_pid", physics="pyb_dw", aux=(),
+               bytes=bytes_per_agent_step("one_d_pid", "multihover", 16),
                label="MultiHover 16-drone x 8192 envs, ActionType.ONE_D_PID, Physics.PYB_DW (O(D^2) downwash)"),
 }
 
@@ -442,9 +487,9 @@ STRONG_LEGS = {
                global_mb=4096, **LEARN_MAPPO,
                label="MultiHover 16-drone x 8192 envs, PYB_DW (BASELINE configs[4]); learn_mappo.py:196-216"),
 }
-STRONG_SIM = {"C3": ("one_d_pid", "dyn", "multihover", 8, 16384, 418.0),
-              "C4": ("vel", "dyn", "spiral", 5, 8192, 1111.0),
-              "C5": ("one_d_pid", "pyb_dw", "multihover", 16, 8192, 418.0)}
+STRONG_SIM = {"C3": ("one_d_pid", "dyn", "multihover", 8, 16384, bytes_per_agent_step("one_d_pid", "multihover", 8)),
+              "C4": ("vel", "dyn", "spiral", 5, 8192, bytes_per_agent_step("vel", "spiral", 5)),
+              "C5": ("one_d_pid", "pyb_dw", "multihover", 16, 8192, bytes_per_agent_step("one_d_pid", "multihover", 16))}
 
 
 def leg_plan(args, world):
@@ -614,7 +659,8 @@ def main():
     E, D = args.envs, args.drones
     progress("headline rollout leg")
     value, elapsed, kern_ms, steps, eps_done = sim_leg(args, ranks, "dyn")
-    nbytes = BYTES_PER_AGENT_STEP.get(args.act, 418.0) * E * D
+    bpas = bytes_per_agent_step(args.act, "multihover", D)
+    nbytes = bpas * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
     pyb = fp64 = mappo = mappo32 = mappo_cfgs = configs = None
     mappo_strong, configs_strong = {}, {}
@@ -622,12 +668,16 @@ def main():
         if kind == "sim" and name == "fp64":   # the headline rollout in the reference's float64
             progress("headline rollout leg, float64")
             fv, fel, fk, _, _ = sim_leg(args, ranks, "dyn", precision=8)
+            b64 = bytes_per_agent_step(args.act, "multihover", D, precision=8)
+            t64, t64_src = pmc_traffic(E, D, args.act, precision=8)
             fp64 = {"value": fv, "unit": "agent-steps/s", "kernel_ms": fk, "ms_per_step": fel / args.steps * 1e3,
-                    "dtype": "f64", "roofline_frac": nbytes * 2 / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act, 418.0) * 2,
-                    "what": "the same C3 rollout with every state field, reward and the physics in float64 (the "
-                            "reference's numpy precision); obs float32 as the reference emits them; bytes: the "
-                            "float32 figure doubled (state, history and reward in f64)"}
+                    "dtype": "f64", "roofline_frac": b64 * E * D / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "bytes_per_agent_step": b64,
+                    "traffic": t64, "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": t64_src,
+                    "algorithmic_bytes_per_launch": b64 * E * D,
+                    "what": "the same C3 rollout with every state field, target, reward and the physics in float64 "
+                            "(the reference's numpy precision); action, history and obs float32 as in the kernel's "
+                            "buffers (bench.bytes_per_agent_step)"}
         elif kind == "sim" and name == "pyb":   # the same rollout under Physics.PYB (the reference's training default)
             pv, _, pk, _, _ = sim_leg(args, ranks, "pyb")
             pyb = {"value": pv, "unit": "agent-steps/s", "kernel_ms": pk,
@@ -689,7 +739,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": nbytes,
-                         "kernel_ms": kern_ms, "bytes_per_agent_step": BYTES_PER_AGENT_STEP.get(args.act)},
+                         "kernel_ms": kern_ms, "bytes_per_agent_step": bpas},
             "timing": {"wall_ms_per_step": elapsed / steps * 1e3, "event_ms_per_step": kern_ms,
                        "fixed_wall_us_per_window": (elapsed / steps * 1e3 - kern_ms) * steps * 1e3,
                        "what": "wall: barrier + device sync on both sides of the K steps (the value); event: HIP "

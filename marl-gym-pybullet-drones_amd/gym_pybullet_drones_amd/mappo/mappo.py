@@ -332,7 +332,9 @@ class MAPPO:
                                          batch_size=self.num_envs, include_global_state=self.centralized_critic,
                                          global_state_dim=self.global_state_dim, device=self.device)
             E, D = self.num_envs, self.num_agents
-            self._rew_raw = torch.zeros((self.rollout_steps, E), device=self.device)
+            # the simulator's reward dtype (float64 at precision=8, the reference's
+            # numpy reward); the buffer's rew_env row takes it as float32
+            self._rew_raw = torch.zeros((self.rollout_steps, E), dtype=self.env.venv.swarm.rdtype, device=self.device)
             self._te = torch.zeros((self.rollout_steps, E), dtype=torch.uint8, device=self.device)
             self._tr = torch.zeros((self.rollout_steps, E), dtype=torch.uint8, device=self.device)
             self._raw_obs = torch.zeros((E, D, self.obs_dim), device=self.device)

@@ -31,7 +31,13 @@ class RunningMeanStd:
         self.count = torch.full((), epsilon, dtype=torch.float64, device=device)
 
     def _hip_ok(self, arr):
-        return arr.is_cuda and arr.dtype == torch.float32 and arr.dim() >= 1 and arr.shape[0] > 0
+        """The HIP kernels take a float32 device batch whose rows are exactly this
+        normaliser's shape (C = numel / rows = mean.numel(): the kernels index the
+        float64 statistics by column).  Anything else — an unbatched (D, O) obs, a
+        2-D (E·D, O) batch for a (D, O) normaliser — takes the torch expressions,
+        which broadcast like the reference's numpy."""
+        return (arr.is_cuda and arr.dtype == torch.float32 and arr.dim() >= 1 and arr.shape[0] > 0
+                and arr.numel() // arr.shape[0] == self.mean.numel())
 
     def _work(self, R, C):
         key = (R, C)
@@ -169,13 +175,14 @@ class RewardStdNormalizer(MeanStdNormalizer):
         self.ret = None
 
     def __call__(self, x, dones):
-        """normalization.py:147-160: the discounted return is tracked in the
-        reward's own dtype (np.zeros_like(x); float32 · γ stays float32, NEP 50),
-        its moments feed the running statistics, and the reward is only scaled."""
+        """normalization.py:147-160: the discounted return (np.zeros_like(x) of the
+        reference's float64 rewards — MultiHoverAviary._computeReward's numpy
+        state arithmetic — so float64 here whatever the reward's dtype), its
+        moments feed the running statistics, and the reward is only scaled."""
         if not self.read_only:
             if self.ret is None:
-                self.ret = torch.zeros_like(x)
-            self.ret = self.ret * self.gamma + x
+                self.ret = torch.zeros_like(x, dtype=torch.float64)
+            self.ret = self.ret * self.gamma + x.to(torch.float64)
             self.rms.update(self.ret.reshape(-1))
             self.ret = torch.where(dones.bool(), torch.zeros_like(self.ret), self.ret)
         x64 = x.to(torch.float64)

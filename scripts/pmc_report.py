@@ -25,7 +25,7 @@ def per_kernel(rows, counter):
     return acc
 
 
-def main(fetch_dir, write_dir, calib_bytes, agents, alg_bytes, envs=16384, drones=8, act="one_d_pid"):
+def main(fetch_dir, write_dir, calib_bytes, agents, alg_bytes, envs=16384, drones=8, act="one_d_pid", precision=4):
     f = per_kernel(load(fetch_dir), "FETCH_SIZE")
     w = per_kernel(load(write_dir), "WRITE_SIZE")
     cal = [k for k in f if "calib_copy" in k][0]
@@ -38,9 +38,11 @@ def main(fetch_dir, write_dir, calib_bytes, agents, alg_bytes, envs=16384, drone
            "step_traffic_bytes": sf + sw, "traffic_per_agent_step": (sf + sw) / agents,
            "algorithmic_per_agent_step": alg_bytes, "launches": len(f[step]),
            "workload": {"envs": envs, "drones": drones, "act": act}}
+    if int(precision) != 4:   # the fp64 kernel's summary (float32 workloads keep the round-1 key set)
+        out["workload"]["precision"] = int(precision)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2], float(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5]),
-         *(int(x) for x in sys.argv[6:8]), *sys.argv[8:9])
+         *(int(x) for x in sys.argv[6:8]), *sys.argv[8:10])

@@ -66,3 +66,18 @@ def test_bench_two_ranks_lists_strong_legs():
     _, one = _run_bench("--dry-run", "--dry-ms", "1", "--steps", "2", "--warmup", "0")
     assert not any(g["scaling"] == "strong" for g in one["legs"])
     assert ("mappo", "ref", "weak") in {(g["kind"], g["name"], g["scaling"]) for g in one["legs"]}
+
+
+def test_bytes_per_agent_step_matches_survey():
+    """bench.bytes_per_agent_step reproduces SURVEY §8(d)'s per-config figures
+    (C2 720, C3 418 / VEL 790, C4 1111, C5 418 B, rounded there) and prices the
+    precision-8 build with float32 action, history and obs (the kernel's buffer
+    types) and float64 state, target and reward: 662.25 B for C3, not 2 x 418."""
+    import bench
+    b = bench.bytes_per_agent_step
+    assert round(b("rpm", "multihover", 4)) == 720
+    assert round(b("one_d_pid", "multihover", 8)) == 418
+    assert round(b("vel", "multihover", 8)) == 790
+    assert round(b("vel", "spiral", 5)) == 1111
+    assert abs(b("one_d_pid", "multihover", 16) - 418) < 1.2   # (SURVEY: "= C3 per agent"; per-env bytes / 16)
+    assert b("one_d_pid", "multihover", 8, precision=8) == 4 + 2 * 29 * 8 + 3 * 8 + 15 * 4 + 27 * 4 + 18 / 8

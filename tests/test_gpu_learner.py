@@ -182,10 +182,13 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
-def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, **variant):
+def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, logp_shift=0.0, run=True, **variant):
     """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
     iteration's configuration) from fixed weights, data and permutations
-    (small=False unless given: the split-K direct iteration at every size)."""
+    (small=False unless given: the split-K direct iteration at every size).
+    logp_shift: added to every old log-probability (approx_kl of the first
+    minibatch = the shift + the 0.001-scale noise's mean).  run=False: the
+    agent as initialised, no update."""
     from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
     from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
     from gym_pybullet_drones_amd.utils.spaces import Box
@@ -204,10 +207,12 @@ def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, **vari
     with torch.no_grad():
         d = agent.ac.actor.dist(buf.obs.reshape(-1, O))
         buf.logp.copy_(d.log_prob(buf.act.reshape(-1, A)).reshape(T, E, D, 1)
-                       + 0.001 * torch.randn(T, E, D, 1, device="cuda"))
+                       + 0.001 * torch.randn(T, E, D, 1, device="cuda") + logp_shift)
     buf.ret_env.normal_()
     buf.adv_env.normal_()
     buf.t, buf.full = 0, True
+    if not run:
+        return agent, None
     gen = torch.Generator(device="cuda")
     gen.manual_seed(5)
     res = agent.update(buf, generator=gen)
@@ -312,10 +317,39 @@ def test_small_update_matches_autograd(graphs, E, T, D, A):
     for k in r_small:
         assert r_small[k] == pytest.approx(r_ref[k], rel=1e-5, abs=1e-7), k
     if took_small:
-        # the transposed W2 copies stayed current through the Adam steps
-        for w2t, mlp in zip(a_small._sm_w2t, (a_small.ac.actor.pi_net, a_small.ac.critic.v_net)):
-            assert torch.equal(w2t, mlp.fcs[1].weight.t())
+        _assert_small_copies_current(a_small)
     assert mb > 0
+
+
+def _assert_small_copies_current(agent):
+    """The small path's transposed W2 copies and padded W1 copies equal the
+    weights after the Adam steps (the pad columns stay zero)."""
+    for w2t, w1p, mlp in zip(agent._sm_w2t, agent._sm_w1p, (agent.ac.actor.pi_net, agent.ac.critic.v_net)):
+        I = mlp.fcs[0].in_features
+        assert torch.equal(w2t, mlp.fcs[1].weight.t())
+        assert torch.equal(w1p[:, :I], mlp.fcs[0].weight)
+        assert not w1p[:, I:].any()
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_small_update_kl_gate_closed(graphs):
+    """qs_ppo_small_step with the actor's KL gate closed (AG:731-734): old
+    log-probabilities 0.02 above the current ones put approx_kl above
+    1.5·target_kl = 0.015 on every minibatch, so the actor's weight tiles,
+    vector parameters and logstd are skipped and its step count is not
+    committed, while the critic steps every time — as the autograd-driven
+    iteration's gated Adam does."""
+    a_small, r_small = _hidden256_update(graphs, 8, 8, small=True, logp_shift=0.02)
+    assert a_small._sm_key is not None
+    a_init, _ = _hidden256_update(graphs, 8, 8, small=True, run=False)
+    a_ref, r_ref = _hidden256_update(graphs, 8, 8, direct=False, logp_shift=0.02)
+    assert float(a_small.actor_opt.step) == float(a_ref.actor_opt.step) == 0.0
+    assert float(a_small.critic_opt.step) == float(a_ref.critic_opt.step) == 4.0
+    assert torch.equal(a_small.actor_opt.flat, a_init.actor_opt.flat)   # not one actor element moved
+    assert not a_small.actor_opt.exp_avg.any() and not a_small.actor_opt.exp_avg_sq.any()
+    torch.testing.assert_close(a_small.critic_opt.flat, a_ref.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
+    assert r_small['approx_kl'] > 0.015 and r_small['approx_kl'] == pytest.approx(r_ref['approx_kl'], rel=1e-5)
+    _assert_small_copies_current(a_small)
 
 
 def test_small_update_replay_deterministic():

@@ -106,3 +106,22 @@ def test_rms_rejects_bad_arguments():
         L.check(lib.qs_rms_update(0, 4, None, None, None, None, None, None, None), "qs_rms_update")
     with pytest.raises(L.QuadSwarmError, match="qs_rms_normalize"):
         L.check(lib.qs_rms_normalize(4, 0, None, None, None, 1e-8, 10.0, None, None), "qs_rms_normalize")
+
+
+@pytest.mark.parametrize("batch", [(4, 27), (8, 1, 27)])
+def test_rms_mismatched_shape_takes_the_broadcasting_path(batch):
+    """A batch whose rows are not the normaliser's shape — an unbatched (D, O)
+    obs, or (E, 1, O) rows for a (D, O) normaliser — must not reach the
+    kernels (they would index mean / var by the batch's column count): it takes
+    the torch expressions, whose results equal the same expressions on the CPU
+    (numpy broadcasting in the reference)."""
+    from gym_pybullet_drones_amd.mappo.normalization import MeanStdNormalizer
+    rng = np.random.default_rng(13)
+    D, O = 4, 27
+    norms = [MeanStdNormalizer(shape=(D, O), clip=10.0, epsilon=1e-8, device=dev) for dev in ("cuda", "cpu")]
+    for k in range(2):
+        x = (rng.normal(size=batch) * 2 + 0.5).astype(np.float32)
+        y = [n(torch.as_tensor(x, device=n.rms.mean.device)) for n in norms]
+        np.testing.assert_allclose(norms[0].rms.mean.cpu().numpy(), norms[1].rms.mean.numpy(), rtol=1e-12)
+        np.testing.assert_allclose(norms[0].rms.var.cpu().numpy(), norms[1].rms.var.numpy(), rtol=1e-12)
+        np.testing.assert_allclose(y[0].cpu().numpy(), y[1].numpy(), rtol=1e-6)

@@ -261,3 +261,25 @@ def test_train_step_termination_counts_without_reference_compat(tmp_path):
     assert counts == {k: v for k, v in want.items() if v}
     assert sum(counts.values()) > 0   # random RPM actions end episodes within 40 steps
     m.close()
+
+
+@pytest.mark.parametrize("norm_reward", [False, True])
+def test_train_step_at_float64_precision(tmp_path, norm_reward):
+    """An aviary built with precision=8 (float64 state and reward, the
+    reference's numpy precision) trains: the raw reward row takes the
+    simulator's float64 reward, the buffer stores it as float32, and the
+    float64 reward equals the float32 buffer row up to that rounding."""
+    from gym_pybullet_drones_amd.envs import MultiHoverAviary
+    from gym_pybullet_drones_amd.mappo import MAPPO
+    from gym_pybullet_drones_amd.utils.enums import ActionType
+    env_func = lambda seed=0, **kw: MultiHoverAviary(num_drones=4, act=ActionType.RPM, precision=8)
+    m = MAPPO(env_func, output_dir=str(tmp_path), use_gpu=True, seed=0, hidden_dim=64, rollout_batch_size=16,
+              rollout_steps=12, mini_batch_size=32, opt_epochs=1, norm_reward=norm_reward)
+    m.reset()
+    res = m.train_step()
+    assert m._rew_raw.dtype == torch.float64
+    assert all(np.isfinite(res[k]) for k in ('policy_loss', 'value_loss'))
+    if not norm_reward:
+        rb = m._rollouts.rew_env
+        np.testing.assert_array_equal(rb.cpu().numpy(), m._rew_raw.float().cpu().numpy())
+    m.close()

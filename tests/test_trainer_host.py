@@ -70,9 +70,11 @@ def test_fused_mlp_row_limits():
 
 def test_reward_std_normalizer_matches_reference_restatement():
     """RewardStdNormalizer (normalization.py:123-160) against a numpy restatement
-    of the reference: the return tracked in float32 (np.zeros_like of the float32
-    reward), its float64 running moments, the reward scaled (not centred) and
-    clipped, the return cleared on done.  Off in both reference trainer configs
+    of the reference with its own dtypes: float64 rewards (MultiHoverAviary's
+    numpy reward), the return tracked in float64 (np.zeros_like of the reward),
+    its float64 running moments, the reward scaled (not centred) and clipped,
+    the return cleared on done.  A float32 reward (this port's rollout buffer)
+    gives the same float64 return.  Off in both reference trainer configs
     (learn_mappo.py / env_select_learn_mappo.py: norm_reward False), kept for
     the MAPPO constructor's norm_reward switch."""
     import numpy as np
@@ -80,26 +82,61 @@ def test_reward_std_normalizer_matches_reference_restatement():
     from gym_pybullet_drones_amd.mappo.normalization import RewardStdNormalizer
     rng = np.random.default_rng(4)
     E, gamma = 64, 0.99
-    norm = RewardStdNormalizer(gamma=gamma, clip=10.0, epsilon=1e-8, device="cpu")
-    mean, var, count, ret = 0.0, 1.0, 1e-4, None
-    for t in range(40):
-        x = (rng.normal(size=E) * 0.3 - 1.0).astype(np.float32)
-        dones = rng.random(E) < 0.05
-        got = norm(torch.as_tensor(x), torch.as_tensor(dones)).numpy()
-        # the reference (numpy, with float64 batch moments as this port computes them)
-        ret = np.zeros_like(x) if ret is None else ret
-        ret = ret * np.float32(gamma) + x
-        assert ret.dtype == np.float32
-        r64 = ret.astype(np.float64)
-        bm, bv, bc = r64.mean(0), r64.var(0), E
-        delta = bm - mean
-        tot = count + bc
-        mean, var, count = (mean + delta * bc / tot,
-                            (var * count + bv * bc + delta * delta * count * bc / (count + bc)) / (count + bc),
-                            bc + count)
-        ret[dones] = 0
-        want = np.clip(x / np.sqrt(var + 1e-8), -10.0, 10.0).astype(np.float32)
-        np.testing.assert_array_equal(norm.ret.numpy(), ret)
-        np.testing.assert_allclose(float(norm.rms.var), var, rtol=1e-12)
-        np.testing.assert_allclose(got, want, rtol=1e-6, atol=0)
-    assert got.dtype == np.float32
+    for dt in (np.float64, np.float32):
+        norm = RewardStdNormalizer(gamma=gamma, clip=10.0, epsilon=1e-8, device="cpu")
+        mean, var, count, ret = 0.0, 1.0, 1e-4, None
+        for t in range(40):
+            x = (rng.normal(size=E) * 0.3 - 1.0).astype(dt)
+            dones = rng.random(E) < 0.05
+            got = norm(torch.as_tensor(x), torch.as_tensor(dones)).numpy()
+            # the reference (numpy): its reward is float64
+            x64 = x.astype(np.float64)
+            ret = np.zeros_like(x64) if ret is None else ret
+            ret = ret * gamma + x64
+            assert ret.dtype == np.float64
+            bm, bv, bc = ret.mean(0), ret.var(0), E
+            delta = bm - mean
+            tot = count + bc
+            mean, var, count = (mean + delta * bc / tot,
+                                (var * count + bv * bc + delta * delta * count * bc / (count + bc)) / (count + bc),
+                                bc + count)
+            ret[dones] = 0
+            want = np.clip(x64 / np.sqrt(var + 1e-8), -10.0, 10.0).astype(dt)
+            assert norm.ret.dtype == torch.float64
+            np.testing.assert_array_equal(norm.ret.numpy(), ret)
+            np.testing.assert_allclose(float(norm.rms.var), var, rtol=1e-12)
+            np.testing.assert_allclose(got, want, rtol=1e-6, atol=0)
+        assert got.dtype == dt
+
+
+def test_rms_hip_path_only_for_matching_columns():
+    """The HIP normaliser kernels index the float64 statistics by column, so a
+    batch takes them only when its rows have the normaliser's shape; other
+    shapes (an unbatched (D, O) obs, a 2-D (E·D, O) batch for a (D, O)
+    normaliser) take the broadcasting torch expressions.  Checked
+    on the guard itself (no GPU here) with a stand-in device batch."""
+    import torch
+    from gym_pybullet_drones_amd.mappo.normalization import RunningMeanStd
+    rms = RunningMeanStd(shape=(3, 5))
+
+    class Batch:   # what _hip_ok reads of a CUDA tensor
+        is_cuda, dtype = True, torch.float32
+
+        def __init__(self, *shape):
+            self.shape = shape
+
+        def dim(self):
+            return len(self.shape)
+
+        def numel(self):
+            n = 1
+            for s in self.shape:
+                n *= s
+            return n
+
+    assert rms._hip_ok(Batch(64, 3, 5))        # (E, D, O)
+    assert rms._hip_ok(Batch(64, 15))          # (E, D·O)
+    assert not rms._hip_ok(Batch(3, 5))        # unbatched (D, O)
+    assert not rms._hip_ok(Batch(192, 5))      # (E·D, O)
+    assert not rms._hip_ok(Batch(0, 3, 5))
+    assert not rms._hip_ok(torch.zeros(4, 3, 5))   # CPU tensor
