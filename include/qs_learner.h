@@ -321,16 +321,18 @@ int qs_rollout_record(int64_t E, const uint8_t* terminated, const uint8_t* trunc
                       float* rew_dst, float* mask_dst, float* done_dst, void* stream);
 const char* qs_rollout_last_error(void);
 
-/* One PPO minibatch at small batch sizes (the reference's own learner shape,
- * learn_mappo.py:196-216: mini_batch_size 32 → 256 actor rows) in two
+/* One PPO minibatch on 16-row tiles (the reference's own learner shape,
+ * learn_mappo.py:196-216: mini_batch_size 32 → 256 actor rows, and each rank's
+ * share of a minibatch split over G ranks) in two or three
  * launches, replacing qs_mlp3f_actor / qs_mlp3w_* / qs_value_head / the
  * weight-gradient GEMMs / qs_mlp_sum_adam there: the actor's forward, policy
  * loss head (AG:602-640) and backward and the critic's forward, value head
  * (AG:642-683) and backward in 16-row tiles, then every weight gradient
- * summed over the whole minibatch and applied by Adam in place (the actor's
- * step gated on approx_kl <= kl_thr when gate != 0, AG:731-734; the critic's
- * always, AG:757-760).  Both nets are 256-wide tanh MLPs (nn.Linear layout,
- * row-major [out][in]) inside flat parameter / Adam buffers; w2t is a
+ * summed over the whole minibatch (32×32 blocks, K-chunks past 1 024 rows
+ * summed in chunk order) and applied by Adam in place (the actor's step gated
+ * on approx_kl <= kl_thr when gate != 0, AG:731-734; the critic's always,
+ * AG:757-760).  Both nets are 256-wide tanh MLPs (nn.Linear layout, row-major
+ * [out][in], at most 640 inputs) inside flat parameter / Adam buffers; w2t is a
  * [256][256] transposed copy of W2, formed by the caller once and kept current
  * by the step.  obs is the rollout's obs table [T·E·D][O] (actor rows) =
  * [T·E][D·O] (critic rows), idx[mb] int64 env-timesteps; act [T·E·D][A],
@@ -338,7 +340,7 @@ const char* qs_rollout_last_error(void);
  * and acc[0..3] += policy, value, entropy loss, approx_kl, as qs_ppo_heads.
  * work: qs_ppo_small_work_bytes(mb, D, actor in, critic in, A) bytes, zeroed
  * once (the launches leave their counters zero). */
-#define QS_PPO_SMALL_MAX_ROWS 8192   /* mb·D at most */
+#define QS_PPO_SMALL_MAX_ROWS 16384   /* mb·D at most */
 typedef struct qs_mlp256 {
   float* params;       /* flat parameter buffer of the net (FlatBuffers)     */
   float* exp_avg;      /* Adam moments, same layout                           */
@@ -346,7 +348,7 @@ typedef struct qs_mlp256 {
   float* step;         /* Adam step count (float32, device)                  */
   float* w2t;          /* [256][256] = W2ᵀ                                    */
   int64_t w1, b1, w2, b2, w3, b3, logstd;   /* element offsets in params (logstd -1: none) */
-  int32_t in, out;     /* input width (<= 256), outputs (actor <= 4, critic 1) */
+  int32_t in, out;     /* input width (<= 640), outputs (actor <= 4, critic 1) */
   float lr, beta1, beta2, eps;
   float* w1p;          /* NULL, or [256][in padded to 16] = W1 with zero columns past in: the
                           step keeps it current and reads layer 1 as whole float4 quads */
@@ -356,15 +358,35 @@ int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* id
                       const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
                       float ent_coef, int32_t gate, float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic,
                       float* kl_out, double* acc, void* work, void* stream);
+/* The multi-rank form of qs_ppo_small_step (AG:702-772 with the gradient
+ * all-reduce of SURVEY §8(e)): qs_ppo_small_grads runs the same launches with
+ * this rank's minibatch gradients written (not applied) into grad_a / grad_c
+ * (the nets' flat gradient buffers, the params' layout: every parameter
+ * element written, logstd included) and kl_out[0] = this rank's approx_kl.
+ * The caller all-reduces (sum) [grad_c | grad_a | kl_out]; qs_ppo_small_adam
+ * then applies Adam from the sums ÷ grad_div (the world size; the actor gated
+ * on the summed approx_kl ÷ grad_div <= kl_thr when gate != 0) and keeps the
+ * W2ᵀ / padded W1 copies current.  One rank (grad_div 1) gives
+ * qs_ppo_small_step's bits.  work: the same workspace (its counters). */
+int qs_ppo_small_grads(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
+                       const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
+                       float ent_coef, const qs_mlp256* actor, const qs_mlp256* critic, float* grad_a, float* grad_c,
+                       float* kl_out, double* acc, void* work, void* stream);
+int qs_ppo_small_adam(int32_t mb, int32_t D, const qs_mlp256* actor, const qs_mlp256* critic, const float* grad_a,
+                      const float* grad_c, float grad_div, int32_t gate, float kl_thr, const float* kl, void* work,
+                      void* stream);
 const char* qs_ppo_small_last_error(void);
-/* The workspace's parts: off[0..15] byte offsets of xaT, h1aT, dz2aT, dz1aT,
- * xcT, h1cT, dz2cT, dz1cT (transposed [width][rows padded to 16]), partAa,
- * partBa, partAc, partBc (per-tile partial rows [tile][256 + 256·A + A] =
- * Σ dZ2 | Σ dout·H2 | Σ dout, and [tile][256] = Σ dZ1), dlogstd, the loss
- * partials, the counters; off[16..19] = actor tiles, critic tiles, padded
- * actor rows, padded critic rows; off[20] = bytes; off[21..22] = the row
- * strides of the actor's / critic's transposed buffers.  Ia = 0: the critic-only
- * layout of qs_ppo_critic_tiles. */
+/* The workspace's parts (off[QS_PPO_SMALL_LAYOUT_N]): off[0..15] byte offsets
+ * of xaT, h1aT, dz2aT, dz1aT, xcT, h1cT, dz2cT, dz1cT (transposed [width][rows
+ * padded to 16]), partAa, partBa, partAc, partBc (per-tile partial rows
+ * [tile][256 + 256·A + A] = Σ dZ2 | Σ dout·H2 | Σ dout, and [tile][256] = Σ dZ1),
+ * dlogstd, the loss partials, the counters; off[16..19] = actor tiles, critic
+ * tiles, padded actor rows, padded critic rows; off[20] = bytes; off[21..22] =
+ * the row strides of the actor's / critic's transposed buffers; off[23..26] =
+ * byte offsets of the weight gradients' K-chunk partials [S][256][M padded to
+ * 32] (actor W1, W2, critic W1, W2); off[27..28] = the actor's / critic's
+ * K-chunks S.  Ia = 0: the critic-only layout of qs_ppo_critic_tiles. */
+#define QS_PPO_SMALL_LAYOUT_N 29
 int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off);
 /* The critic half of qs_ppo_small_step's first launch at any minibatch size:
  * the critic's forward, value head (AG:642-683, acc[1] += value loss) and

@@ -1,19 +1,22 @@
-// ppo_small.hip — one PPO minibatch at small batch sizes in two launches
-// (include/qs_learner.h: qs_ppo_small_step).
+// ppo_small.hip — one PPO minibatch on 16-row tiles, in two or three launches
+// (include/qs_learner.h: qs_ppo_small_step; the multi-rank form
+// qs_ppo_small_grads → all-reduce → qs_ppo_small_adam).
 //
 // The reference's own learner shape (learn_mappo.py:196-216 at README.md:38-39's
 // 176 envs: mini_batch_size 32 env-timesteps = 256 actor rows of 27 and 32
 // critic rows of 216, hidden 256, 14 080 minibatches per update) is pure
-// latency: the large-batch path (qs_mlp3f_actor + split-K GEMMs + qs_mlp_sum_adam,
-// built for 32 768 rows) streams every weight through two CUs and chains ~10
-// dependent launches per minibatch.  Here a minibatch is two launches:
+// latency, and so is every rank's share of a minibatch once SURVEY §8(e)
+// partitions the global one over G ranks (C3 at G = 8: 4 096 actor rows, 512
+// critic rows): the large-batch path (qs_mlp3f_actor + split-K GEMMs +
+// qs_mlp_sum_adam, built for 32 768 rows) streams every weight through a few
+// CUs and chains ~10 dependent launches per minibatch.  Here:
 //
 //  1. ppo_small_fb_kernel: one workgroup per 16-row tile (actor tiles first,
 //     then critic tiles), the hidden width split over its 16 waves (wave w owns
 //     hidden block w; four waves a SIMD hide each other's MFMA chains): layer 1
-//     (from a copy of W1 padded to whole quads when the caller keeps one), layer
-//     2, the head (a fixed-order sum of
-//     the waves' partial dots through LDS), the PPO policy / value head
+//     (from a copy of W1 padded to whole quads when the caller keeps one; inputs
+//     up to 640 wide: Spiral's 595-wide critic), layer 2, the head (a fixed-order
+//     sum of the waves' partial dots through LDS), the PPO policy / value head
 //     (AG:602-683), dZ2, dH1 = dZ2·W2 and dZ1, with the activations exchanged
 //     between the waves through LDS.  v_mfma_f32_16x16x4_f32: lane (g, j)
 //     supplies A[j][κ] and B[κ][j] with κ = 16t + 4g + e for the four steps e of
@@ -22,17 +25,27 @@
 //     read is conflict-free).  Writes the transposed activations [h][K] (the
 //     weight gradients' float4 operands), per-tile bias / head partial rows,
 //     and from the last tile of each net the loss sums (ppo_heads_kernel's tail).
-//  2. ppo_small_adam_kernel: one wave per 16×16 weight tile computes its
-//     gradient over the whole minibatch (fixed order: no partials, no atomics)
-//     and applies Adam to it in place (actor gated by approx_kl, AG:731-734), W2
-//     also written transposed for the next minibatch's dH1 (and W1 into its
-//     padded copy); the vector
-//     parameters (biases, head, logstd) from the tile partials.  The last
-//     workgroup commits the step counts.
+//  2. ppo_small_wgrad_kernel: one 4-wave workgroup per 32×32 block of a weight
+//     matrix and K-chunk (the chunk's quads split over the waves, each wave a
+//     2×2 grid of MFMA tiles: four independent accumulator chains, four float4
+//     operands per 16 MFMAs), the waves' sums added in wave order through LDS.
+//     One chunk per block (S = 1, small minibatches): the gradient goes straight
+//     into its sink — Adam in place (actor gated by approx_kl, AG:731-734; W2
+//     also written transposed for the next minibatch's dH1, W1 into its padded
+//     copy) or the gradient buffer (the multi-rank form); otherwise the chunk
+//     partials.  Four more workgroups reduce the vector parameters (biases,
+//     head, logstd) from the tile partials.
+//  3. ppo_small_apply_kernel (S > 1 only): the chunk partials summed in chunk
+//     order into the same sinks; the last workgroup commits the step counts.
+// Multi-rank: qs_ppo_small_grads runs 1–3 with the gradient
+// buffers as the sink (this rank's minibatch mean); the caller all-reduces
+// [critic grads | actor grads | approx_kl]; qs_ppo_small_adam is launch 3's
+// Adam from those buffers (÷ the world size, the KL gate on the global mean).
+// One rank forced through that path gives the fused step's bits.
 //
 // MFMA-bound per CU: a 16-row tile is one workgroup on one CU; the critic's
 // (216 inputs) ~6 MFLOP takes ≥ ~10 µs at one CU's share of the fp32 MFMA peak
-// (phase stamps: DESIGN.md §4d); the whole minibatch is 0.13 GFLOP.
+// (phase stamps: DESIGN.md §4d).
 
 #include <hip/hip_runtime.h>
 #include <cmath>
@@ -51,16 +64,21 @@ constexpr int kSBlock = 64 * kSW;
 constexpr int kSBPW = 256 / 16 / kSW;  // hidden blocks of 16 per wave (1: four waves a SIMD hide each other's chains)
 constexpr int kSH = 256;               // hidden width
 constexpr int kSHS = kSH + 4;          // LDS row stride of the hidden exchange (4 mod 32 floats)
-constexpr int kSMaxI = 256;            // widest input
+constexpr int kSMaxI = 640;            // widest input (Spiral's centralized critic: 5 × 119 = 595)
+constexpr int kSNarrowI = 256;         // the forward/backward instance for inputs up to this width (smaller LDS X tile)
 constexpr int kSMaxA = 4;
-constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of the Adam kernel
-constexpr int kSVecWG = 4;             // Adam workgroups for the vector parameters (8 measured no faster)
+constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
+constexpr int kSGW = 4;                // waves per weight-gradient workgroup (one 32×32 block and K-chunk)
+constexpr int kSGQ = 64;               // quads (16 rows) per weight-gradient workgroup before K is split in chunks
+constexpr int kSMaxS = 32;             // most K-chunks per net
+constexpr int kSVecWG = 4;             // workgroups for the vector parameters (8 measured no faster)
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
 // Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
-// forward/backward tile uses ~53 KB and would otherwise be packed up to three
-// to a CU while other CUs idle (the grids are one workgroup per CU or fewer);
-// the weight-gradient workgroups two to a CU.
-constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024;
+// forward/backward tile uses ~53 KB (the narrow instance) and would otherwise be
+// packed up to three to a CU while other CUs idle (the grids are one workgroup
+// per CU or fewer); qs_wgrad_t's workgroups two to a CU, the weight-gradient
+// kernel's three.
+constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024, kSReserveG = 40 * 1024;
 
 #ifdef QS_TILE_STAMPS
 // dev builds only: s_memrealtime (100 MHz) at the tile's phase boundaries,
@@ -96,7 +114,17 @@ struct SWork {   // workspace views (qs_ppo_small_work_bytes)
   float *xaT, *h1aT, *dz2aT, *dz1aT, *xcT, *h1cT, *dz2cT, *dz1cT;
   float *partAa, *partBa, *partAc, *partBc, *dlogstd;
   double *lossa, *lossc;
-  unsigned* cnt;   // [0] actor tiles, [64] critic tiles, [128] Adam workgroups
+  unsigned* cnt;   // [0] actor tiles, [64] critic tiles, [128] weight-gradient workgroups, [160] apply workgroups
+  float* wpart[4];   // K-chunk partials [S][256][Mp] of actor W1, actor W2, critic W1, critic W2 (Mp: M padded to 32)
+};
+
+// Where the reduced gradients go (launches 2 and 3)
+enum { SINK_PART = 0, SINK_ADAM = 1, SINK_GRAD = 2 };
+struct SGrad {
+  int S[2];          // K-chunks per net (actor, critic)
+  int sink;          // the final sink: SINK_ADAM (one rank) or SINK_GRAD (this rank's gradient, for the all-reduce)
+  float* g[2];       // SINK_GRAD / qs_ppo_small_adam: the nets' gradient buffers (flat, the params' layout)
+  float gdiv;        // qs_ppo_small_adam: the all-reduced sums ÷ gdiv (the world size), approx_kl too
 };
 
 struct SArgs {
@@ -114,6 +142,7 @@ struct SArgs {
   double* acc;
   SNet a, c;
   SWork w;
+  SGrad G;
 };
 
 __device__ __forceinline__ float s_tanh(float x) {   // learner.hip's m3_tanh
@@ -210,6 +239,41 @@ __device__ __forceinline__ void s_run(float4 (&ra)[kSRing], const float* wrow, i
     case 15: CALL(15); break; default: CALL(16); break;                                             \
   }
 
+// Layer 1 over nq = ⌈I/16⌉ quads: the ring was prefilled with the first quads
+// phases ahead (s_prefill<min(nq, 16)>); up to 16 quads by one compile-time run,
+// wider inputs (WIDE: up to kSMaxI) in 16-quad blocks that refill the ring at
+// their start, then the remainder
+template <bool VEC, bool WIDE>
+__device__ __forceinline__ void s_layer1(float4 (&ring)[kSRing], const float* wrow, int I, const float* brow, int g,
+                                         int nq, f32x4& z) {
+#define S_RUNL(n) s_run<n, VEC>(ring, wrow, I, brow, g, z)
+  if (!WIDE || nq <= 16) {
+    S_NQ_SWITCH(nq, S_RUNL)
+    return;
+  }
+#undef S_RUNL
+  if constexpr (WIDE) {
+    s_run<16, VEC>(ring, wrow, I, brow, g, z);
+    int t = 16;
+    for (; t + 16 <= nq; t += 16) {
+      s_prefill<16, VEC>(ring, wrow + 16 * t, I - 16 * t, g);
+      s_run<16, VEC>(ring, wrow + 16 * t, I - 16 * t, brow + 16 * t, g, z);
+    }
+    if (t < nq) {
+      const float* wr = wrow + 16 * t;
+      const float* br = brow + 16 * t;
+      const int Ir = I - 16 * t;
+#define S_REM(n)                          \
+  {                                       \
+    s_prefill<n, VEC>(ring, wr, Ir, g);   \
+    s_run<n, VEC>(ring, wr, Ir, br, g, z); \
+  }
+      S_NQ_SWITCH(nq - t, S_REM)
+#undef S_REM
+    }
+  }
+}
+
 // c += Σ over NQ quads of A[j][rows]·B[rows][j], both operands transposed rows
 // in global memory, kSRing quads of loads ahead; compile-time NQ
 template <int NQ>
@@ -251,7 +315,7 @@ __device__ __forceinline__ void s_wgrad_acc(const float* arow, const float* brow
 // ---------------------------------------------------------------- launch 1
 // One 16-row tile of one net: POL = the actor (policy head over A outputs),
 // otherwise the critic (value head).
-template <int A, bool POL, bool V1>
+template <int A, bool POL, bool V1, int MAXI>
 __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, float* xs, float* h1s, float* dz2s,
                                        float* prm, float (*hp)[16], double (*ls_w)[2 + kSMaxA]) {
   static_assert(kSBPW == 1, "one hidden block per wave");
@@ -288,7 +352,9 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   }
 #undef S_PRE1
 #undef S_PRE1V
-  s_prefill<16, true>(ring2, w2row, kSH, g);
+  // (the wide instance fills layer 2's ring after layer 1: both rings live
+  // across a many-block layer 1 would not fit in the 128 registers of a 16-wave workgroup)
+  if constexpr (MAXI <= kSNarrowI) s_prefill<16, true>(ring2, w2row, kSH, g);
   const int R = r0 + j;
   const bool rv = R < K;
   float hact[A], hlpo = 0.f;
@@ -309,7 +375,7 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     if (rv) had = P.ret[P.idx[R]];   // the value head's return
   }
   {
-    constexpr int kXU = (16 * kSMaxI + kSBlock - 1) / kSBlock;
+    constexpr int kXU = (16 * MAXI + kSBlock - 1) / kSBlock;
     float v[kXU];
     const int rr = tid & 15, Rx = r0 + rr;
     const long long src = Rx < K ? (POL ? (P.idx[Rx / P.D] * P.D + Rx % P.D) : P.idx[Rx]) * I : -1;
@@ -344,15 +410,8 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   const float* slogstd = sb3 + A;
   // ---- layer 1: Z1ᵀ[h0 + r][row j] in register r of lane (g, j)
   f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-#define S_RUN1(n) s_run<n, false>(ring1, w1row, I, xs + j * XS, g, z)
-#define S_RUN1V(n) s_run<n, true>(ring1, w1row, Ip, xs + j * XS, g, z)
-  if constexpr (V1) {
-    S_NQ_SWITCH(nq1, S_RUN1V)
-  } else {
-    S_NQ_SWITCH(nq1, S_RUN1)
-  }
-#undef S_RUN1
-#undef S_RUN1V
+  s_layer1<V1, (MAXI > kSNarrowI)>(ring1, w1row, V1 ? Ip : I, xs + j * XS, g, nq1, z);
+  if constexpr (MAXI > kSNarrowI) s_prefill<16, true>(ring2, w2row, kSH, g);
   float h1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) h1[r] = s_tanh(z[r] + sb1[h0 + r]);
@@ -553,25 +612,19 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   }
 }
 
-template <int A, bool V1>
+template <int A, bool V1, int MAXI>
 __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
-  __shared__ float xs[16 * s_xs(kSMaxI)];
+  __shared__ float xs[16 * s_xs(MAXI)];
   __shared__ float h1s[16 * kSHS];
   __shared__ float dz2s[16 * kSHS];
   __shared__ float hp[kSW * kSMaxA][16];
   __shared__ double ls_w[16][2 + kSMaxA];
   __shared__ float prm[2 * kSH + kSMaxA * kSH + 2 * kSMaxA];
-  if ((int)blockIdx.x < P.nA) s_tile<A, true, V1>(P, P.a, blockIdx.x, xs, h1s, dz2s, prm, hp, ls_w);
-  else s_tile<1, false, V1>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, prm, hp, ls_w);
+  if ((int)blockIdx.x < P.nA) s_tile<A, true, V1, MAXI>(P, P.a, blockIdx.x, xs, h1s, dz2s, prm, hp, ls_w);
+  else s_tile<1, false, V1, MAXI>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, prm, hp, ls_w);
 }
 
-// ---------------------------------------------------------------- launch 2
-struct STile {
-  const SNet* n;
-  bool actor;
-  int which, nb, kb;   // W1 / W2, output block, input block
-};
-
+// ---------------------------------------------------------------- launches 2 and 3
 // p / m / v of element i loaded by the caller ahead of the gradient (their
 // latency hides behind the gradient's loads)
 __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, float bc1, float bc2s, float* w2t,
@@ -588,126 +641,305 @@ __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, floa
   if (w1p) w1p[(size_t)n * s_ip(N.I) + k] = p1;
 }
 
-__global__ void __launch_bounds__(64 * kSAW) ppo_small_adam_kernel(SArgs P, int nTiles) {
-  __shared__ float sc[2][2];
-  __shared__ bool last;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+// Adam's bias corrections of both nets from their step counts (float32 of the
+// float64 powers, as learner.hip), and whether the actor's KL gate is open
+__device__ __forceinline__ void s_adam_scalars(const SArgs& P, float (&sc)[2][2], int tid) {
   if (tid < 2) {
     const SNet& N = tid == 0 ? P.a : P.c;
     const unsigned t = (unsigned)(*N.step) + 1u;
     sc[tid][0] = (float)(1.0 - s_powi((double)N.beta1, t));
     sc[tid][1] = (float)sqrt(1.0 - s_powi((double)N.beta2, t));
   }
-  const bool open_a = !P.gate || *P.kl_out <= P.kl_thr;
-  __syncthreads();
-  const int nwg_tiles = (nTiles + kSAW - 1) / kSAW;
-  if ((int)blockIdx.x < nwg_tiles) {
-    const int T = blockIdx.x * kSAW + w;
-    if (T < nTiles) {
-      // tile T → (net, layer, output block, input block); the actor's first
-      const int a1 = 16 * (s_ip(P.a.I) / 16), c1 = 16 * (s_ip(P.c.I) / 16);
-      int u = T;
-      bool actor = true;
-      int which = 1;
-      if (u < a1) { which = 1; }
-      else if ((u -= a1) < 256) { which = 2; }
-      else if ((u -= 256) < c1) { actor = false; which = 1; }
-      else { u -= c1; actor = false; which = 2; }
-      const SNet& N = actor ? P.a : P.c;
-      if (!actor || open_a) {
-        const int nin = which == 1 ? s_ip(N.I) / 16 : 16;
-        const int nb = u / nin, kb = u - nb * nin;
-        const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
-        const float* dzT = actor ? (which == 1 ? P.w.dz1aT : P.w.dz2aT) : (which == 1 ? P.w.dz1cT : P.w.dz2cT);
-        const float* xT = actor ? (which == 1 ? P.w.xaT : P.w.h1aT) : (which == 1 ? P.w.xcT : P.w.h1cT);
-        const int Kin = which == 1 ? N.I : kSH;
-        const int kcol = 16 * kb + j;
-        const float* arow = dzT + (size_t)(16 * nb + j) * KS;
-        const float* brow = xT + (size_t)min(kcol, Kin - 1) * KS;   // (columns past Kin are not stored)
-        // the four elements' parameter and moments first (clamped: unconditional loads)
-        long long ei[4];
-        float pp[4], pm[4], pv[4];
+}
+__device__ __forceinline__ bool s_gate_open(const SArgs& P) {
+  return !P.gate || *P.kl_out / P.G.gdiv <= P.kl_thr;
+}
+
+// One reduced gradient element of a weight matrix into the final sink: Adam in
+// place (with the W2ᵀ / padded W1 copies), or the net's gradient buffer
+__device__ __forceinline__ void s_sink_w(const SArgs& P, const SNet& N, bool actor, int sink, long long i, float g,
+                                         const float (&sc)[2][2], bool w2, int n, int k) {
+  const int si = actor ? 0 : 1;
+  if (sink == SINK_GRAD) {
+    P.G.g[si][i] = g;
+    return;
+  }
+  s_adam(N, i, g, sc[si][0], sc[si][1], w2 ? N.w2t : nullptr, n, k, w2 ? nullptr : N.w1p, N.p[i], N.m[i], N.v[i]);
+}
+
+// The vector parameters of both nets (b1, b2, W3, b3 and the actor's logstd),
+// element e of [actor's | critic's]: the flat index and the gradient, from the
+// tile partial rows (fixed tile order, eight rows' loads in flight) or, FROM_G,
+// from the gradient buffers ÷ gdiv.  false: past the end.
+template <bool FROM_G>
+__device__ __forceinline__ bool s_vec_elem(const SArgs& P, int e, bool& actor, long long& i, float& gsum) {
+  const int A = P.a.A;
+  const int na = 2 * kSH + A * kSH + 2 * A, nc = 2 * kSH + kSH + 1;
+  if (e >= na + nc) return false;
+  actor = e < na;
+  const SNet& N = actor ? P.a : P.c;
+  const int AA = actor ? A : 1, nt = actor ? P.nA : P.nC;
+  const float* pA = actor ? P.w.partAa : P.w.partAc;
+  const float* pB = actor ? P.w.partBa : P.w.partBc;
+  const int PA = kSH + AA * kSH + AA;
+  int u = actor ? e : e - na;
+  const float* col = nullptr;
+  int cstride = 0;
+  if (u < kSH) {                       // b1: Σ dZ1
+    col = pB + u; cstride = kSH;
+    i = N.b1 + u;
+  } else if ((u -= kSH) < kSH) {       // b2: Σ dZ2
+    col = pA + u; cstride = PA;
+    i = N.b2 + u;
+  } else if ((u -= kSH) < AA * kSH) {  // W3: Σ dout·H2
+    col = pA + kSH + u; cstride = PA;
+    i = N.w3 + u;
+  } else if ((u -= AA * kSH) < AA) {   // b3: Σ dout
+    col = pA + kSH + AA * kSH + u; cstride = PA;
+    i = N.b3 + u;
+  } else {                             // logstd (the actor's loss tail)
+    u -= AA;
+    i = N.logstd + u;
+  }
+  if constexpr (FROM_G) {
+    gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
+    return true;
+  }
+  if (!col) {
+    gsum = P.w.dlogstd[u];
+    return true;
+  }
+  float acc = 0.f;
+  int t = 0;
+  for (; t + 8 <= nt; t += 8) {
+    float v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          ei[r] = (which == 1 ? N.w1 : N.w2) + (long long)(16 * nb + 4 * g + r) * Kin + min(kcol, Kin - 1);
-          pp[r] = N.p[ei[r]];
-          pm[r] = N.m[ei[r]];
-          pv[r] = N.v[ei[r]];
-        }
-        // dW[16nb + 4g + r][16kb + j] = Σ_rows dZ[row][n]·X[row][k], rows in MFMA order
-        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-        s_wgrad_acc(arow, brow, KP / 16, g, c);
-        if (kcol < Kin) {
-          const int si = actor ? 0 : 1;
+    for (int q = 0; q < 8; ++q) v[q] = col[(size_t)(t + q) * cstride];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc += v[q];
+  }
+  for (; t < nt; ++t) acc += col[(size_t)t * cstride];
+  gsum = acc;
+  return true;
+}
+
+// A weight matrix's 32×32 blocks: W1 [256][I] (⌈I/32⌉ column blocks) then W2
+// [256][256]; nblk(N) blocks per net
+__device__ __forceinline__ int s_mb1(int I) { return (I + 31) / 32; }
+__host__ __device__ inline int s_nblk(int I) { return 8 * ((I + 31) / 32) + 64; }
+
+// c[bi][bj] += Σ over NQ quads of dZᵀ[n0 + 16bi + j][rows]·Xᵀ[m0 + 16bj + j][rows]
+// (a 2×2 grid of 16×16 MFMA tiles: four independent chains, four float4
+// operands per 16 MFMAs), R quads of loads ahead; compile-time NQ
+template <int NQ>
+__device__ __forceinline__ void s_wgrad22_n(const float* a0, const float* a1, const float* b0, const float* b1, int g,
+                                            f32x4 (&c)[4]) {
+  constexpr int R = NQ < 4 ? NQ : 4;
+  float4 ra0[R], ra1[R], rb0[R], rb1[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    ra0[t] = *reinterpret_cast<const float4*>(a0 + 16 * t + 4 * g);
+    ra1[t] = *reinterpret_cast<const float4*>(a1 + 16 * t + 4 * g);
+    rb0[t] = *reinterpret_cast<const float4*>(b0 + 16 * t + 4 * g);
+    rb1[t] = *reinterpret_cast<const float4*>(b1 + 16 * t + 4 * g);
+  }
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const float4 x0 = ra0[t % R], x1 = ra1[t % R], y0 = rb0[t % R], y1 = rb1[t % R];
+    if (t + R < NQ) {
+      ra0[t % R] = *reinterpret_cast<const float4*>(a0 + 16 * (t + R) + 4 * g);
+      ra1[t % R] = *reinterpret_cast<const float4*>(a1 + 16 * (t + R) + 4 * g);
+      rb0[t % R] = *reinterpret_cast<const float4*>(b0 + 16 * (t + R) + 4 * g);
+      rb1[t % R] = *reinterpret_cast<const float4*>(b1 + 16 * (t + R) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
+#define S_Q4(E)                        \
+  c[0] = s_mfma(x0.E, y0.E, c[0]);     \
+  c[1] = s_mfma(x0.E, y1.E, c[1]);     \
+  c[2] = s_mfma(x1.E, y0.E, c[2]);     \
+  c[3] = s_mfma(x1.E, y1.E, c[3]);
+    S_Q4(x) S_Q4(y) S_Q4(z) S_Q4(w)
+#undef S_Q4
+  }
+}
+// any nq: whole blocks of 16 quads, then the remainder by dispatch
+__device__ __forceinline__ void s_wgrad22(const float* a0, const float* a1, const float* b0, const float* b1, int nq,
+                                          int g, f32x4 (&c)[4]) {
+  int t = 0;
+  for (; t + 16 <= nq; t += 16) s_wgrad22_n<16>(a0 + 16 * t, a1 + 16 * t, b0 + 16 * t, b1 + 16 * t, g, c);
+  switch (nq - t) {
+#define S_CASE(n) case n: s_wgrad22_n<n>(a0 + 16 * t, a1 + 16 * t, b0 + 16 * t, b1 + 16 * t, g, c); break;
+    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
+    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
+#undef S_CASE
+    default: break;
+  }
+}
+
+// Launch 2.  Workgroups [0, Σ blocks·S): one 32×32 weight block and K-chunk
+// each (actor's first, the chunks of a block adjacent); then kSVecWG for the
+// vector parameters.  SINK: where the weight blocks' sums go — SINK_PART (the
+// chunk partials, reduced by launch 3) or, when both nets have one chunk,
+// P.G.sink.  The vector parameters always go to P.G.sink; with SINK_ADAM
+// (one chunk, Adam) the last workgroup commits the step counts.
+template <int SINK>
+__global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P) {
+  __shared__ float red[kSGW - 1][16][64];
+  __shared__ float sc[2][2];
+  __shared__ bool last;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  s_adam_scalars(P, sc, tid);
+  const bool open_a = P.G.sink != SINK_ADAM || s_gate_open(P);
+  __syncthreads();
+  const int nwa = s_nblk(P.a.I) * P.G.S[0], nwc = s_nblk(P.c.I) * P.G.S[1];
+  const int blk = blockIdx.x;
+  if (blk < nwa + nwc) {
+    const bool actor = blk < nwa;
+    const int S = P.G.S[actor ? 0 : 1];
+    const int T = actor ? blk : blk - nwa;
+    const int s = T % S, u = T / S;
+    const SNet& N = actor ? P.a : P.c;
+    // a closed gate skips the actor's Adam (the partials of SINK_PART are formed
+    // regardless: launch 3 reads the gate)
+    if (SINK != SINK_ADAM || !actor || open_a) {
+      const int mb1 = s_mb1(N.I);
+      const bool l1 = u < 8 * mb1;
+      const int uu = l1 ? u : u - 8 * mb1, ncb = l1 ? mb1 : 8;
+      const int n0 = 32 * (uu / ncb), m0 = 32 * (uu % ncb);
+      const int M = l1 ? N.I : kSH;
+      const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
+      const float* dzT = actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT);
+      const float* xT = actor ? (l1 ? P.w.xaT : P.w.h1aT) : (l1 ? P.w.xcT : P.w.h1cT);
+      // the chunk's quads, split over the waves (contiguous, wave order)
+      const int Q = KP / 16, qc = (Q + S - 1) / S, q0 = min(Q, s * qc), q1 = min(Q, q0 + qc);
+      const int qw = (q1 - q0 + kSGW - 1) / kSGW;
+      const int wa = min(q1, q0 + w * qw), wb = min(q1, wa + qw);
+      const float* a0 = dzT + (size_t)(n0 + j) * KS + 16 * wa;
+      const float* a1 = dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa;
+      // (columns past M are not stored: clamped, their sums discarded)
+      const float* b0 = xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa;
+      const float* b1 = xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa;
+      f32x4 c[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      s_wgrad22(a0, a1, b0, b1, wb - wa, g, c);
+      if (w > 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[w - 1][4 * q + r][l] = c[q][r];
+      __syncthreads();
+      if (w == 0) {
+#pragma unroll
+        for (int v = 0; v < kSGW - 1; ++v)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[q][r] += red[v][4 * q + r][l];
+        const int Mp = l1 ? 32 * mb1 : kSH;
+        float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = m0 + 16 * (q & 1) + j;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int n = 16 * nb + 4 * g + r;
-            s_adam(N, ei[r], c[r], sc[si][0], sc[si][1], which == 2 ? N.w2t : nullptr, n, kcol,
-                   which == 1 ? N.w1p : nullptr, pp[r], pm[r], pv[r]);
+            const int n = n0 + 16 * (q >> 1) + 4 * g + r;
+            if (SINK == SINK_PART) {
+              part[((size_t)s * kSH + n) * Mp + m] = c[q][r];   // (pad columns too: launch 3 skips them)
+            } else if (m < M) {
+              s_sink_w(P, N, actor, SINK, (l1 ? N.w1 : N.w2) + (long long)n * M + m, c[q][r], sc, !l1, n, m);
+            }
           }
         }
       }
     }
   } else {
-    // the vector parameters: b1, b2, W3, b3 (and the actor's logstd) from the tile partials
-    const int A = P.a.A;
-    const int na = 2 * kSH + A * kSH + 2 * A, nc = 2 * kSH + kSH + 1;
-    for (int e = (blockIdx.x - nwg_tiles) * blockDim.x + tid; e < na + nc; e += kSVecWG * blockDim.x) {
-      const bool actor = e < na;
-      if (actor && !open_a) continue;
-      const SNet& N = actor ? P.a : P.c;
-      const int AA = actor ? A : 1, nt = actor ? P.nA : P.nC;
-      const float* pA = actor ? P.w.partAa : P.w.partAc;
-      const float* pB = actor ? P.w.partBa : P.w.partBc;
-      const int PA = kSH + AA * kSH + AA;
-      int u = actor ? e : e - na;
-      float gsum = 0.f;
+    for (int e = (blk - nwa - nwc) * blockDim.x + tid;; e += kSVecWG * blockDim.x) {
+      bool actor;
       long long i;
-      // Σ over the tiles' partial rows in tile order, eight rows' loads in flight
-      auto colsum = [&](const float* base, int stride) {
-        float acc = 0.f;
-        int t = 0;
-        for (; t + 8 <= nt; t += 8) {
-          float v[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = base[(size_t)(t + q) * stride];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc += v[q];
-        }
-        for (; t < nt; ++t) acc += base[(size_t)t * stride];
-        return acc;
-      };
-      // the element and its partial-row column first, then its parameter and
-      // moments (in flight during the column sum)
-      const float* col = nullptr;
-      int cstride = 0;
-      if (u < kSH) {                       // b1: Σ dZ1
-        col = pB + u; cstride = kSH;
-        i = N.b1 + u;
-      } else if ((u -= kSH) < kSH) {       // b2: Σ dZ2
-        col = pA + u; cstride = PA;
-        i = N.b2 + u;
-      } else if ((u -= kSH) < AA * kSH) {  // W3: Σ dout·H2
-        col = pA + kSH + u; cstride = PA;
-        i = N.w3 + u;
-      } else if ((u -= AA * kSH) < AA) {   // b3: Σ dout
-        col = pA + kSH + AA * kSH + u; cstride = PA;
-        i = N.b3 + u;
-      } else {                             // logstd (the actor's loss tail)
-        u -= AA;
-        i = N.logstd + u;
+      float gsum;
+      if (!s_vec_elem<false>(P, e, actor, i, gsum)) break;
+      if (P.G.sink == SINK_GRAD) {
+        P.G.g[actor ? 0 : 1][i] = gsum;
+      } else if (!actor || open_a) {
+        const SNet& N = actor ? P.a : P.c;
+        const int si = actor ? 0 : 1;
+        s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, N.p[i], N.m[i], N.v[i]);
       }
-      const float p0 = N.p[i], m0 = N.m[i], v0 = N.v[i];
-      gsum = col ? colsum(col, cstride) : P.w.dlogstd[u];
-      const int si = actor ? 0 : 1;
-      s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, p0, m0, v0);
     }
   }
+  if (SINK != SINK_ADAM) return;
   __syncthreads();
   if (tid == 0) last = atomicAdd(P.w.cnt + 128, 1u) == gridDim.x - 1;
   __syncthreads();
   if (last && tid == 0) {   // every workgroup read the step counts before arriving
     P.w.cnt[128] = 0u;
+    if (open_a) *P.a.step = *P.a.step + 1.0f;
+    *P.c.step = *P.c.step + 1.0f;
+  }
+}
+
+// Launch 3, one thread per parameter element: FROM_G = false — the weight
+// matrices' chunk partials summed in chunk order (launch 2 did the vector
+// parameters) into P.G.sink; FROM_G = true (qs_ppo_small_adam, after the rank
+// all-reduce) — every parameter's gradient from the gradient buffers ÷ gdiv,
+// into Adam.  Elements: actor W1, W2, critic W1, W2 (row-major, as the
+// parameters), then (FROM_G) the vector parameters.  With Adam the last
+// workgroup commits the step counts.
+template <bool FROM_G>
+__global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
+  __shared__ float sc[2][2];
+  __shared__ bool last;
+  const int tid = threadIdx.x;
+  s_adam_scalars(P, sc, tid);
+  const int sink = FROM_G ? SINK_ADAM : P.G.sink;
+  const bool open_a = sink != SINK_ADAM || s_gate_open(P);
+  __syncthreads();
+  long long e = (long long)blockIdx.x * blockDim.x + tid;
+  const long long nw[4] = {(long long)kSH * P.a.I, (long long)kSH * kSH, (long long)kSH * P.c.I, (long long)kSH * kSH};
+  int part = 0;
+  while (part < 4 && e >= nw[part]) e -= nw[part++];
+  if (part < 4) {
+    const bool actor = part < 2, l1 = (part & 1) == 0;
+    const SNet& N = actor ? P.a : P.c;
+    if (sink != SINK_ADAM || !actor || open_a) {
+      const int M = l1 ? N.I : kSH;
+      const int n = (int)(e / M), m = (int)(e - (long long)n * M);
+      const long long i = (l1 ? N.w1 : N.w2) + e;
+      float gsum;
+      if constexpr (FROM_G) {
+        gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
+      } else {
+        const int S = P.G.S[actor ? 0 : 1];
+        const int Mp = l1 ? 32 * s_mb1(N.I) : kSH;
+        const float* pp = P.w.wpart[part] + (size_t)n * Mp + m;
+        const size_t cs = (size_t)kSH * Mp;
+        float v[kSMaxS];
+#pragma unroll
+        for (int q = 0; q < kSMaxS; ++q) v[q] = q < S ? pp[q * cs] : 0.f;
+        gsum = v[0];
+#pragma unroll
+        for (int q = 1; q < kSMaxS; ++q)
+          if (q < S) gsum += v[q];
+      }
+      s_sink_w(P, N, actor, sink, i, gsum, sc, !l1, n, m);
+    }
+  } else if (FROM_G) {
+    bool actor;
+    long long i;
+    float gsum;
+    if (s_vec_elem<true>(P, (int)e, actor, i, gsum) && (!actor || open_a)) {
+      const SNet& N = actor ? P.a : P.c;
+      const int si = actor ? 0 : 1;
+      s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, N.p[i], N.m[i], N.v[i]);
+    }
+  }
+  if (sink != SINK_ADAM) return;
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(P.w.cnt + 160, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last && tid == 0) {
+    P.w.cnt[160] = 0u;
     if (open_a) *P.a.step = *P.a.step + 1.0f;
     *P.c.step = *P.c.step + 1.0f;
   }
@@ -738,9 +970,16 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
 
 struct SLayout {
   int nA, nC, KaP, KcP, KaS, KcS;
-  long long off[16];
+  int Sa, Sc;   // K-chunks of the weight gradients per net
+  long long off[20];
   long long bytes;
 };
+// K-chunks for a net's weight gradients: one per kSGQ quads of rows, at most kSMaxS
+inline int s_chunks(long long KP) {
+  const long long q = KP / 16;
+  const long long S = (q + kSGQ - 1) / kSGQ;
+  return (int)(S < 1 ? 1 : (S > kSMaxS ? kSMaxS : S));
+}
 // Ia = 0: the critic's tiles only (qs_ppo_critic_tiles), no actor buffers
 SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   SLayout L;
@@ -753,14 +992,19 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   // channel (the critic's weight gradients ran 10x slower at 4 096 rows)
   L.KaS = L.KaP ? L.KaP + kSPad : 0;
   L.KcS = L.KcP + kSPad;
-  const long long sz[16] = {
+  L.Sa = Ia > 0 ? s_chunks(L.KaP) : 0;
+  L.Sc = s_chunks(L.KcP);
+  const long long pw = 4LL * kSH;   // bytes of a [256] partial column run
+  const long long sz[20] = {
       4LL * Ia * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS,   // xaT h1aT dz2aT dz1aT
       4LL * Ic * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS,   // xcT h1cT dz2cT dz1cT
       4LL * L.nA * (kSH + A * kSH + A), 4LL * L.nA * kSH,                           // partAa partBa
       4LL * L.nC * (2 * kSH + 1), 4LL * L.nC * kSH,                                 // partAc partBc
-      4LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192};                   // dlogstd lossa lossc cnt
+      4LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192,                    // dlogstd lossa lossc cnt
+      pw * L.Sa * 32 * ((Ia + 31) / 32), pw * L.Sa * kSH,                           // K-chunk partials: actor W1 W2
+      pw * L.Sc * 32 * ((Ic + 31) / 32), pw * L.Sc * kSH};                          //                  critic W1 W2
   long long o = 0;
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 20; ++i) {
     L.off[i] = o;
     o += (sz[i] + 255) & ~255LL;
   }
@@ -790,6 +1034,9 @@ int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A
   off[20] = L.bytes;
   off[21] = L.KaS;
   off[22] = L.KcS;
+  for (int i = 0; i < 4; ++i) off[23 + i] = L.off[16 + i];
+  off[27] = L.Sa;
+  off[28] = L.Sc;
   return QS_OK;
 }
 
@@ -799,10 +1046,8 @@ int qs_wgrad_t(int64_t KP, int64_t ld, int32_t N, int32_t M, const float* AT, co
       !XT || !partial || ld * (int64_t)(N > M ? N : M) >= (int64_t(1) << 31))
     return sfail(QS_E_INVALID, "qs_wgrad_t: bad argument (N a multiple of 16, KP a multiple of 16·S, ld >= KP "
                                "a multiple of 4)");
-  static const bool attr = (hipFuncSetAttribute((const void*)wgrad_t_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
-                            hipFuncSetAttribute((const void*)ppo_small_adam_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)wgrad_t_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
                             true);
   (void)attr;
   const long long waves = (long long)(N / 16) * ((M + 15) / 16) * S;
@@ -814,6 +1059,8 @@ int qs_wgrad_t(int64_t KP, int64_t ld, int32_t N, int32_t M, const float* AT, co
 
 }  // extern "C"
 
+static void s_bind(SArgs& P, const qs_mlp256* actor, const qs_mlp256* critic, const SLayout& L, void* work);
+
 static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act, const float* logp_old,
                   const double* adv, const double* ret, float action_scale, float clip, float ent_coef, int32_t gate,
                   float kl_thr, const qs_mlp256* actor, const qs_mlp256* critic, float* kl_out, double* acc, void* work,
@@ -824,8 +1071,10 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   const int A = actor->out;
   if (A < 1 || A > kSMaxA || critic->out != 1 || actor->in < 1 || actor->in > kSMaxI || critic->in < 1 ||
       critic->in > kSMaxI || (need_actor && (actor->logstd < 0 || !actor->w2t)) || !critic->w2t)
-    return sfail(QS_E_INVALID, std::string(name) + ": nets must be 256-wide with <= 256 inputs, A <= 4 actor outputs "
+    return sfail(QS_E_INVALID, std::string(name) + ": nets must be 256-wide with <= 640 inputs, A <= 4 actor outputs "
                                                    "(with logstd) and one critic output, W2ᵀ copies given");
+  if ((actor->in > kSNarrowI || critic->in > kSNarrowI) && (!critic->w1p || (need_actor && !actor->w1p)))
+    return sfail(QS_E_INVALID, std::string(name) + ": nets with more than 256 inputs need the padded W1 copies (w1p)");
   if ((actor->w2 & 3) || (critic->w2 & 3) || ((actor->in & 3) == 0 && (actor->w1 & 3)) ||
       ((critic->in & 3) == 0 && (critic->w1 & 3)))
     return sfail(QS_E_INVALID, std::string(name) + ": W1 / W2 must start 16-byte aligned in the flat buffers");
@@ -853,6 +1102,13 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   P.gate = gate;
   P.kl_out = kl_out;
   P.acc = acc;
+  s_bind(P, actor, critic, L, work);
+  return QS_OK;
+}
+
+// The nets, the workspace views of layout L and the chunk counts; the sink:
+// Adam, gradients ÷ 1
+static void s_bind(SArgs& P, const qs_mlp256* actor, const qs_mlp256* critic, const SLayout& L, void* work) {
   auto net = [](const qs_mlp256* q) {
     SNet n;
     n.p = q->params;
@@ -885,19 +1141,45 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   P.w.lossa = (double*)(wb + L.off[13]);
   P.w.lossc = (double*)(wb + L.off[14]);
   P.w.cnt = (unsigned*)(wb + L.off[15]);
-  return QS_OK;
+  for (int i = 0; i < 4; ++i) P.w.wpart[i] = (float*)(wb + L.off[16 + i]);
+  P.G.S[0] = L.Sa;
+  P.G.S[1] = L.Sc;
+  P.G.sink = SINK_ADAM;
+  P.G.g[0] = P.G.g[1] = nullptr;
+  P.G.gdiv = 1.0f;
 }
 
 static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
-  // layer 1 from the padded W1 copies when every net in the launch has one
+  // layer 1 from the padded W1 copies when every net in the launch has one;
+  // the wide instance (a 640-input LDS X tile) only when a net needs it
   const bool v1 = P.c.w1p && (P.nA == 0 || P.a.w1p);
+  const bool wide = P.c.I > kSNarrowI || (P.nA > 0 && P.a.I > kSNarrowI);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); };
+  // (the wide instance reads layer 1 from the padded copies only: s_args
+  // refuses a net wider than kSNarrowI without one)
+#define S_FB(AA)                                                                                   \
+  (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI>)                                               \
+        : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI>) : go(ppo_small_fb_kernel<AA, false, kSNarrowI>)))
   switch (P.a.A) {
-    case 1: v1 ? go(ppo_small_fb_kernel<1, true>) : go(ppo_small_fb_kernel<1, false>); break;
-    case 2: v1 ? go(ppo_small_fb_kernel<2, true>) : go(ppo_small_fb_kernel<2, false>); break;
-    case 3: v1 ? go(ppo_small_fb_kernel<3, true>) : go(ppo_small_fb_kernel<3, false>); break;
-    default: v1 ? go(ppo_small_fb_kernel<4, true>) : go(ppo_small_fb_kernel<4, false>); break;
+    case 1: S_FB(1); break;
+    case 2: S_FB(2); break;
+    case 3: S_FB(3); break;
+    default: S_FB(4); break;
   }
+#undef S_FB
+}
+
+// Launches 2 (and 3 when a net's weight gradients are split in K-chunks) into P.G.sink
+static void s_launch_grad(const SArgs& P, hipStream_t st) {
+  const bool one = P.G.S[0] == 1 && P.G.S[1] == 1;
+  const int grid = s_nblk(P.a.I) * P.G.S[0] + s_nblk(P.c.I) * P.G.S[1] + kSVecWG;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kSGW), kSReserveG, st, P); };
+  if (!one) go(ppo_small_wgrad_kernel<SINK_PART>);
+  else if (P.G.sink == SINK_GRAD) go(ppo_small_wgrad_kernel<SINK_GRAD>);
+  else go(ppo_small_wgrad_kernel<SINK_ADAM>);
+  if (one) return;
+  const long long nel = (long long)kSH * (P.a.I + P.c.I) + 2LL * kSH * kSH;
+  hipLaunchKernelGGL(ppo_small_apply_kernel<false>, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, P);
 }
 
 extern "C" {
@@ -915,15 +1197,60 @@ int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* id
     return sfail(QS_E_INVALID, "qs_ppo_small_step: minibatch above QS_PPO_SMALL_MAX_ROWS actor rows");
   hipStream_t st = (hipStream_t)stream;
   s_launch_fb(P, L.nA + L.nC, st);
-  static const bool attr = (hipFuncSetAttribute((const void*)ppo_small_adam_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSReserveW),
-                            true);
-  (void)attr;
-  const int nTiles = 16 * (s_ip(actor->in) / 16) + 256 + 16 * (s_ip(critic->in) / 16) + 256;
-  const int grid = (nTiles + kSAW - 1) / kSAW + kSVecWG;
-  hipLaunchKernelGGL(ppo_small_adam_kernel, dim3(grid), dim3(64 * kSAW), kSReserveW, st, P, nTiles);
+  s_launch_grad(P, st);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_small_step: ") + hipGetErrorString(e));
+}
+
+int qs_ppo_small_grads(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
+                       const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
+                       float ent_coef, const qs_mlp256* actor, const qs_mlp256* critic, float* grad_a, float* grad_c,
+                       float* kl_out, double* acc, void* work, void* stream) {
+  SArgs P;
+  SLayout L;
+  int rc = s_args(mb, D, obs, idx, act, logp_old, adv, ret, action_scale, clip, ent_coef, 0, 0.f, actor, critic,
+                  kl_out, acc, work, true, P, L, "qs_ppo_small_grads");
+  if (rc != QS_OK) return rc;
+  if (!grad_a || !grad_c) return sfail(QS_E_INVALID, "qs_ppo_small_grads: bad argument");
+  if ((long long)mb * D > QS_PPO_SMALL_MAX_ROWS)
+    return sfail(QS_E_INVALID, "qs_ppo_small_grads: minibatch above QS_PPO_SMALL_MAX_ROWS actor rows");
+  P.G.sink = SINK_GRAD;
+  P.G.g[0] = grad_a;
+  P.G.g[1] = grad_c;
+  hipStream_t st = (hipStream_t)stream;
+  s_launch_fb(P, L.nA + L.nC, st);
+  s_launch_grad(P, st);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_small_grads: ") + hipGetErrorString(e));
+}
+
+int qs_ppo_small_adam(int32_t mb, int32_t D, const qs_mlp256* actor, const qs_mlp256* critic, const float* grad_a,
+                      const float* grad_c, float grad_div, int32_t gate, float kl_thr, const float* kl, void* work,
+                      void* stream) {
+  if (mb <= 0 || D <= 0 || !actor || !critic || !grad_a || !grad_c || !(grad_div > 0.f) || !kl || !work ||
+      actor->out < 1 || actor->out > kSMaxA || actor->in < 1 || actor->in > kSMaxI || critic->in < 1 ||
+      critic->in > kSMaxI || critic->out != 1 || actor->logstd < 0)
+    return sfail(QS_E_INVALID, "qs_ppo_small_adam: bad argument");
+  SArgs P = {};
+  const SLayout L = s_layout(mb, D, actor->in, critic->in, actor->out);
+  s_bind(P, actor, critic, L, work);
+  P.mb = mb;
+  P.D = D;
+  P.nA = L.nA;
+  P.nC = L.nC;
+  P.gate = gate;
+  P.kl_thr = kl_thr;
+  P.kl_out = (float*)kl;   // read only: the all-reduced approx_kl sum (÷ grad_div)
+  P.G.g[0] = (float*)grad_a;
+  P.G.g[1] = (float*)grad_c;
+  P.G.gdiv = grad_div;
+  const int A = actor->out;
+  const long long nel = (long long)kSH * (actor->in + critic->in) + 2LL * kSH * kSH + (2 * kSH + A * kSH + 2 * A) +
+                        (3 * kSH + 1);
+  hipLaunchKernelGGL(ppo_small_apply_kernel<true>, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QS_OK : sfail(QS_E_HIP, std::string("qs_ppo_small_adam: ") + hipGetErrorString(e));
 }
 
 int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const double* ret,

@@ -69,9 +69,11 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
            "qs_wgrad_rm", "qs_learner_last_error", "qs_rms_work_bytes", "qs_rms_update", "qs_rms_normalize",
            "qs_rms_last_error", "qs_mlp3_value_work_bytes", "qs_mlp3_fwd_rows_value", "qs_policy_sample", "qs_rollout_record", "qs_rollout_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error",
-           "qs_ppo_small_layout", "qs_ppo_critic_tiles", "qs_wgrad_t")
+           "qs_ppo_small_layout", "qs_ppo_critic_tiles", "qs_wgrad_t", "qs_ppo_small_grads", "qs_ppo_small_adam")
 QS_PACK_F16 = 1 << 16   # pack_I flag: a qs_mlp3f_pack image (include/qs_learner.h)
 QS_PACK_W2T = 1 << 17   # pack_I flag: a [256][256] W2ᵀ copy (include/qs_learner.h)
+QS_PPO_SMALL_LAYOUT_N = 29   # include/qs_learner.h: entries qs_ppo_small_layout writes
+QS_PPO_SMALL_MAX_ROWS = 16384   # include/qs_learner.h: mb·D at most on qs_ppo_small_step / _grads
 
 _lib = None
 
@@ -173,6 +175,10 @@ def load():
     L.qs_wgrad_t.argtypes = [i64, i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_ppo_small_step.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [f32, f32, f32, ctypes.c_int32, f32]
                                     + [ctypes.POINTER(QsMlp256)] * 2 + [vp] * 4)
+    L.qs_ppo_small_grads.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [f32, f32, f32]
+                                     + [ctypes.POINTER(QsMlp256)] * 2 + [vp] * 6)
+    L.qs_ppo_small_adam.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [ctypes.POINTER(QsMlp256)] * 2 + [vp] * 2
+                                    + [f32, ctypes.c_int32, f32] + [vp] * 3)
     L.qs_rms_work_bytes.argtypes = [i64, ctypes.c_int32]
     L.qs_rms_update.argtypes = [i64, ctypes.c_int32] + [vp] * 7
     L.qs_rms_normalize.argtypes = [i64, ctypes.c_int32, vp, vp, vp, ctypes.c_double, ctypes.c_double, vp, vp]

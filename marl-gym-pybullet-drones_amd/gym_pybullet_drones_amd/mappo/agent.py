@@ -449,9 +449,13 @@ class _F16Work(_M3Work):
 
 
 # the small-minibatch path (qs_ppo_small_step: both nets' forward / backward
-# and the Adam steps in two launches) takes minibatches of at most this many
-# actor rows (mb·D); larger ones run the split-K path (_iteration_direct)
+# in 16-row tiles, the weight gradients and the Adam steps in two or three
+# launches; with several ranks qs_ppo_small_grads + one all-reduce +
+# qs_ppo_small_adam) takes minibatches of at most this many actor rows (mb·D,
+# at most QS_PPO_SMALL_MAX_ROWS); larger ones run the split-K path
+# (_iteration_direct)
 _SMALL_MAX_ROWS = 2048
+_SMALL_MAX_IN = 640   # widest net input the tile kernels take (Spiral's 595-wide critic)
 
 
 def _mlp256(fb, mlp, logstd, w2t, lib_struct, w1p=None):
@@ -492,7 +496,7 @@ class _CriticTiles:
         mlp = agent.ac.critic.v_net
         f0, f1, f2 = mlp.fcs
         self.mlp, self.mb, self.D, self.I = mlp, mb, D, f0.in_features
-        off = (ctypes.c_int64 * 23)()
+        off = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
         L.check(lib.qs_ppo_small_layout(mb, D, 0, self.I, 1, off), "qs_ppo_small_layout")
         self.nC, KcP, ld = int(off[17]), int(off[19]), int(off[22])
         dev = agent.device
@@ -1283,14 +1287,16 @@ class MAPPOAgent:
         FlatBuffers.adam_multi(segs, self._adam_work, packs=packs, zero_grads=True)
 
     def _small_ok(self, rollouts, mb):
-        """qs_ppo_small_step takes the minibatch: one rank, both nets 256-wide tanh
-        MLPs with <= 256 inputs, <= 4 actor outputs, mb·D <= _SMALL_MAX_ROWS."""
-        if not (self.small and self.device.type == 'cuda' and _dist_world() == 1 and not self._force_allreduce):
+        """The tile path takes the minibatch: both nets 256-wide tanh MLPs with
+        <= _SMALL_MAX_IN inputs, <= 4 actor outputs, mb·D <= _SMALL_MAX_ROWS (any
+        number of ranks: qs_ppo_small_grads + the all-reduce + qs_ppo_small_adam)."""
+        if not (self.small and self.device.type == 'cuda'):
             return False
         pa, pc = self.ac.actor.pi_net, self.ac.critic.v_net
-        if not (_m3_ok(pa, 256) and _m3_ok(pc, 256) and pc.fcs[2].out_features == 1):
+        if not (_m3_ok(pa, _SMALL_MAX_IN) and _m3_ok(pc, _SMALL_MAX_IN) and pc.fcs[2].out_features == 1):
             return False
-        return 0 < mb * rollouts.num_agents <= _SMALL_MAX_ROWS and rollouts.obs.is_contiguous()
+        rows = mb * rollouts.num_agents
+        return 0 < rows <= min(_SMALL_MAX_ROWS, L.QS_PPO_SMALL_MAX_ROWS) and rollouts.obs.is_contiguous()
 
     def _small_setup(self, mb, D):
         if getattr(self, '_sm_key', None) == (mb, D):
@@ -1318,19 +1324,35 @@ class MAPPOAgent:
             w1p[:, :mlp.fcs[0].in_features].copy_(mlp.fcs[0].weight)
 
     def _iteration_small(self, rollouts, idx, acc):
-        """One minibatch in two launches (qs_ppo_small_step): the actor's forward,
-        policy loss head and backward and the critic's forward, value head and
-        backward in 16-row tiles, then every gradient summed over the minibatch
-        and applied by the KL-gated Adam (actor) / Adam (critic) in place."""
+        """One minibatch on the tile kernels: the actor's forward, policy loss
+        head and backward and the critic's forward, value head and backward in
+        16-row tiles, then every gradient summed over the minibatch and applied
+        by the KL-gated Adam (actor) / Adam (critic) in place (qs_ppo_small_step).
+        With several ranks: this rank's gradients and approx_kl
+        written into `_reduce_buf` (qs_ppo_small_grads), ONE all-reduce of it
+        (critic | actor | approx_kl), and the Adam steps from the sums ÷ the
+        world size, gated on the global approx_kl (qs_ppo_small_adam)."""
         D, mb = rollouts.num_agents, idx.shape[0]
         self._small_setup(mb, D)
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         na, nc = self._sm_nets
-        L.check(L.load().qs_ppo_small_step(
-            mb, D, L.ptr(rollouts.obs), L.ptr(idx), L.ptr(rollouts.act), L.ptr(rollouts.logp), L.ptr(rollouts.adv_env),
-            L.ptr(rollouts.ret_env), float(self.action_scale), float(self.clip_param), float(self.entropy_coef),
-            int(self.target_kl > 0), float(1.5 * self.target_kl), ctypes.byref(na), ctypes.byref(nc), L.ptr(self._kl),
-            L.ptr(acc), L.ptr(self._sm_work), st), "qs_ppo_small_step")
+        lib = L.load()
+        world = _dist_world()
+        head = (mb, D, L.ptr(rollouts.obs), L.ptr(idx), L.ptr(rollouts.act), L.ptr(rollouts.logp),
+                L.ptr(rollouts.adv_env), L.ptr(rollouts.ret_env), float(self.action_scale), float(self.clip_param),
+                float(self.entropy_coef))
+        gate, thr = int(self.target_kl > 0), float(1.5 * self.target_kl)
+        if not (world > 1 or self._force_allreduce):
+            L.check(lib.qs_ppo_small_step(*head, gate, thr, ctypes.byref(na), ctypes.byref(nc), L.ptr(self._kl),
+                                          L.ptr(acc), L.ptr(self._sm_work), st), "qs_ppo_small_step")
+            return
+        L.check(lib.qs_ppo_small_grads(*head, ctypes.byref(na), ctypes.byref(nc), L.ptr(self.actor_opt.grad),
+                                       L.ptr(self.critic_opt.grad), L.ptr(self._kl), L.ptr(acc), L.ptr(self._sm_work),
+                                       st), "qs_ppo_small_grads")
+        tdist.all_reduce(self._reduce_buf)   # one collective: the sums of [critic | actor | approx_kl]
+        L.check(lib.qs_ppo_small_adam(mb, D, ctypes.byref(na), ctypes.byref(nc), L.ptr(self.actor_opt.grad),
+                                      L.ptr(self.critic_opt.grad), float(world), gate, thr, L.ptr(self._kl),
+                                      L.ptr(self._sm_work), st), "qs_ppo_small_adam")
 
     def _iteration(self, batch, acc):
         """One minibatch: actor step (KL-gated on device), critic step, stat accumulation.

@@ -8,7 +8,9 @@ plus the critic-tile kernels alone at the C3 shape.
 plus `ablate`: the C3 minibatch with one piece at a time made a no-op (the
 numbers are meaningless then, the time is what the rest costs: the piece's
 share of the critical path).
-  python scripts/learner_mb.py [C3|ref|C4|kernels|scale|ablate ...]"""
+plus `ranks`: SURVEY §8(e)'s per-rank shapes (C3 at G = 2/4/8, C4 at 4, C5 at 8)
+through the exchange path on a world-1 process group.
+  python scripts/learner_mb.py [C3|ref|C4|kernels|scale|ablate|ranks ...]"""
 import ctypes
 import os
 import sys
@@ -33,8 +35,10 @@ def per_minibatch_us(shape, reps=3, **variant):
     osp, asp = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O))), Box(-np.ones((D, A)), np.ones((D, A)))
     torch.manual_seed(0)
     variant.setdefault("use_graphs", True)
+    force = variant.pop("force", False)
     agent = MAPPOAgent(osp, asp, hidden_dim=256, opt_epochs=1, mini_batch_size=mb, entropy_coef=0.005,
                        target_kl=1e9, device=dev, **variant)
+    agent._force_allreduce = force
     buf = MAPPOBuffer(osp, asp, T, E, include_global_state=True, device=dev)
     buf.next_obs_slots.normal_()
     buf.act.normal_()
@@ -55,6 +59,38 @@ def per_minibatch_us(shape, reps=3, **variant):
             type(getattr(agent, "_ws_actor", None)).__name__ + "+" + type(getattr(agent, "_ws_critic", None)).__name__)
     agent.release_graphs()
     return e0.elapsed_time(e1) * 1e3 / (reps * nmb), path
+
+
+# SURVEY §8(e)'s per-rank shapes (bench.py STRONG_LEGS at G ranks): D, O, A, per-rank
+# mini_batch_size, T, per-rank envs
+RANK_SHAPES = {"C3/2": (8, 27, 1, 2048, 16, 8192), "C3/4": (8, 27, 1, 1024, 16, 4096),
+               "C3/8": (8, 27, 1, 512, 16, 2048), "C4/4": (5, 119, 4, 1024, 16, 2048),
+               "C5/8": (16, 27, 1, 512, 16, 1024)}
+SHAPES.update(RANK_SHAPES)
+
+
+def world1():
+    """A world-1 RCCL process group, so _force_allreduce runs the exchange path."""
+    import socket
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+
+
+def ranks():
+    """Per-minibatch device time of each per-rank shape through the exchange path
+    (world 1, the all-reduce captured in the graph): the tile path and the split-K
+    direct iteration, and the tile path without the exchange."""
+    world1()
+    agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
+    for shape in RANK_SHAPES:
+        for v in (dict(small=True, force=True), dict(small=False, force=True), dict(small=True, force=False)):
+            us, path = per_minibatch_us(shape, **v)
+            print(f"{shape:5s} {str(v):40s} {us:8.1f} us/minibatch  [{path}]", flush=True)
 
 
 def timed(fn, reps=40):
@@ -195,6 +231,8 @@ def main():
                       dict(side_priority=-1, critic_adam_side=True), dict()):
                 us, path = per_minibatch_us(shape, **v)
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "ranks" in which:
+        ranks()
     if "one" in which:   # the default C3 iteration alone (for a kernel trace: scripts/learner_timeline.py)
         us, path = per_minibatch_us("C3")
         print(f"C3  default {us:8.1f} us/minibatch  [{path}]", flush=True)

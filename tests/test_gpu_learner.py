@@ -182,7 +182,7 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
-def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, logp_shift=0.0, run=True, **variant):
+def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, logp_shift=0.0, run=True, O=27, **variant):
     """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
     iteration's configuration) from fixed weights, data and permutations
     (small=False unless given: the split-K direct iteration at every size).
@@ -192,7 +192,6 @@ def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, logp_s
     from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
     from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
     from gym_pybullet_drones_amd.utils.spaces import Box
-    O = 27
     variant.setdefault('small', False)
     obs_space = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O)))
     act_space = Box(-np.ones((D, A)), np.ones((D, A)))
@@ -295,20 +294,30 @@ def test_direct_update_fused_actor_four_outputs(graphs):
         assert r_side[k] == pytest.approx(r_ref[k], rel=1e-5, abs=1e-7)
 
 
-@pytest.mark.parametrize("E,T,D,A", [(8, 8, 8, 1), (32, 8, 8, 1), (5, 6, 8, 1), (16, 4, 5, 4), (3, 2, 16, 1)])
+@pytest.mark.parametrize("E,T,D,A,O", [(8, 8, 8, 1, 27), (32, 8, 8, 1, 27), (5, 6, 8, 1, 27), (16, 4, 5, 4, 27),
+                                       (3, 2, 16, 1, 27), (64, 16, 8, 1, 27), (32, 8, 16, 1, 27),
+                                       (16, 8, 5, 4, 119), (4, 4, 8, 4, 72)])
 @pytest.mark.parametrize("graphs", [False, True])
-def test_small_update_matches_autograd(graphs, E, T, D, A):
-    """qs_ppo_small_step (the small-minibatch path: two launches per minibatch)
-    against the autograd-driven fused iteration over 2 epochs x 2 minibatches:
+def test_small_update_matches_autograd(graphs, E, T, D, A, O, monkeypatch):
+    """The tile path (qs_ppo_small_step: two launches per minibatch, three
+    when a net's weight gradients are split in K-chunks) against the
+    autograd-driven fused iteration over 2 epochs x 2 minibatches:
     (8, 8, 8): the reference's mini_batch_size 32 (256 actor rows, 32 critic
     rows); (5, 6, 8): 15 env-timesteps, rows not a multiple of the 16-row tile;
-    (16, 4, 5, 4): Spiral's 4-wide VEL actor; (3, 2, 16): 3 critic rows of 432 inputs
-    — past the 256-input limit, so the split-K path must take it."""
-    a_small, r_small = _hidden256_update(graphs, E, T, D=D, A=A, small=True)
+    (16, 4, 5, 4): Spiral's 4-wide VEL actor; (3, 2, 16): 3 critic rows of 432
+    inputs (the wide tile instance); (64, 16, 8): 4 096 actor rows (C3's
+    per-rank shape at G = 8: the actor's weight gradients in 4 K-chunks);
+    (32, 8, 16): C5's drones, a 432-wide critic on 128 rows and 2 048 actor rows;
+    (16, 8, 5, 4, 119): Spiral's obs, a 595-wide critic; (4, 4, 8, 4, 72): a
+    576-wide critic (C3 with VEL actions), past 640 nothing."""
+    from gym_pybullet_drones_amd import _lib as L
+    from gym_pybullet_drones_amd.mappo import agent as agent_mod
+    monkeypatch.setattr(agent_mod, "_SMALL_MAX_ROWS", L.QS_PPO_SMALL_MAX_ROWS)
+    a_small, r_small = _hidden256_update(graphs, E, T, D=D, A=A, O=O, small=True)
     mb = T * E // 2
     took_small = getattr(a_small, '_sm_key', None) is not None
-    assert took_small == (D * 27 <= 256), (D, took_small)
-    a_ref, r_ref = _hidden256_update(graphs, E, T, D=D, A=A, direct=False)
+    assert took_small == (D * O <= 640), (D, O, took_small)
+    a_ref, r_ref = _hidden256_update(graphs, E, T, D=D, A=A, O=O, direct=False)
     # Adam's normalised steps carry ulp-level gradient differences up to ~lr/60 per step; 4 steps
     torch.testing.assert_close(a_small.actor_opt.flat, a_ref.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
     torch.testing.assert_close(a_small.critic_opt.flat, a_ref.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
