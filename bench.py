@@ -130,6 +130,11 @@ def parse():
                    help="learner: the critic's sums + Adam on the side stream (0 = one launch after the join)")
     p.add_argument("--strong", type=int, default=1,
                    help="with N > 1 ranks: also time SURVEY §8(e)'s strong partitions of configs 3-5 (0 = skip)")
+    p.add_argument("--rank-shapes", default="C3/2,C3/4,C3/8,C4/4,C5/8",
+                   help="N = 1: one rank's share of these STRONG_LEGS partitions ('name/G'), timed through the "
+                        "exchange path on a world-1 group ('' = skip)")
+    p.add_argument("--assumed-allreduce-us", type=float, default=30.0,
+                   help="G-GPU all-reduce latency assumed in the rank-shape projections (and twice it)")
     p.add_argument("--dry-run", action="store_true", help="rank plumbing only: gloo on CPU, stand-in steps, no GPU")
     p.add_argument("--dry-ms", type=float, default=2.0, help="--dry-run: ms per stand-in step of rank 0 (rank r: (1+r)x)")
     return p.parse_args()
@@ -516,6 +521,8 @@ def leg_plan(args, world):
             for k, c in STRONG_LEGS.items():
                 if c["global_envs"] % world == 0 and c["global_mb"] % world == 0:
                     plan.append(("mappo", k, "strong", c["global_envs"] // world, c["global_mb"] // world))
+        if world == 1 and args.rank_shapes:
+            plan.append(("mappo", "rank_shapes", "rank-shape", None, None))   # one rank of G, timed on one GPU
     if args.configs:
         for k, c in EXTRA_CONFIGS.items():
             plan.append(("sim", k, "weak", c["envs"], None))
@@ -526,10 +533,12 @@ def leg_plan(args, world):
     return plan
 
 
-def mappo_leg(args, ranks, T, cfg=None):
+def mappo_leg(args, ranks, T, cfg=None, rank_shape=None):
     """Full MAPPO train steps: by default on the bench's C3 envs (learn_mappo.py:196-216
     hyper-parameters, hidden 256, opt_epochs 10; minibatch scaled to the ~100x larger
-    env batch), or one of MAPPO_LEGS."""
+    env batch), or one of MAPPO_LEGS.  rank_shape G: one rank's share of a STRONG_LEGS
+    partition over G ranks, timed on this rank through the exchange path (the
+    gradient all-reduce on the world-1 process group, _force_allreduce)."""
     from gym_pybullet_drones_amd.envs import MultiHoverAviary, SpiralFormationAviary
     from gym_pybullet_drones_amd.mappo import MAPPO
     from gym_pybullet_drones_amd.utils.enums import ActionType, Physics
@@ -537,7 +546,8 @@ def mappo_leg(args, ranks, T, cfg=None):
                            T=T, mb=args.mappo_mb, **LEARN_MAPPO))
     scaling = "weak"
     if "global_envs" in cfg:   # a strong partition (STRONG_LEGS): 1/G of the envs and of the minibatch per rank
-        cfg["envs"], cfg["mb"] = cfg.pop("global_envs") // ranks.world, cfg.pop("global_mb") // ranks.world
+        G = rank_shape or ranks.world
+        cfg["envs"], cfg["mb"] = cfg.pop("global_envs") // G, cfg.pop("global_mb") // G
         scaling = "strong"
     D, E, T, mb = cfg.pop("drones"), cfg.pop("envs"), cfg.pop("T"), cfg.pop("mb")
     task, phys, label = cfg.pop("task"), cfg.pop("physics"), cfg.pop("label", None)
@@ -551,6 +561,7 @@ def mappo_leg(args, ranks, T, cfg=None):
     m = MAPPO(env_func, training=True, seed=0, hidden_dim=256, actor_lr=3e-4, critic_lr=1e-3,
               rollout_steps=T, rollout_batch_size=E, opt_epochs=10,
               mini_batch_size=mb, output_dir="/tmp/qs_bench_mappo", **cfg)
+    m.agent._force_allreduce = bool(rank_shape)
     m.agent.side_stream = bool(args.side_stream)
     m.agent.critic_adam_side = bool(args.critic_adam_side)
     m.agent.critic_tiles = bool(args.critic_tiles)
@@ -567,7 +578,8 @@ def mappo_leg(args, ranks, T, cfg=None):
         k, mm = km.split("x")
         _SPLITK_MIN_ROWS[(int(k), int(mm))] = int(rows)
     m.reset()
-    progress(f"mappo leg {label or 'C3'}: T={T} E={E} D={D} mb={mb}, warm-up train step")
+    progress(f"mappo leg {label or 'C3'}{f' (one rank of {rank_shape})' if rank_shape else ''}: T={T} E={E} D={D} "
+             f"mb={mb}, warm-up train step")
     m.train_step()   # warm-up: graph capture (with N ranks the all-reduce is captured too), lazy kernel loads
     m.time_phases = True
     ranks.fence()
@@ -584,17 +596,19 @@ def mappo_leg(args, ranks, T, cfg=None):
     rollout_graph = m._rollout_graph is not None
     fused_actor = type(getattr(m.agent, "_ws_actor", None)).__name__ == "_F16Work"
     if getattr(m.agent, "_sm_key", None) is not None:
-        learner_path = "qs_ppo_small_step (two launches per minibatch)"
+        learner_path = ("qs_ppo_small_grads + all-reduce + qs_ppo_small_adam" if (world > 1 or rank_shape) else
+                        "qs_ppo_small_step (16-row tiles, 2-3 launches per minibatch)")
     else:
         learner_path = ("qs_mlp3f_actor + bmm dW2" if fused_actor else "qs_mlp3 actor") + (
             " | critic qs_ppo_critic_tiles + qs_wgrad_t" if type(getattr(m.agent, "_ws_critic", None)).__name__
             == "_CriticTiles" else " | critic qs_mlp3w + GEMMs")
+    exchange = int(m.agent._reduce_buf.numel())   # [critic grads | actor grads | approx_kl] floats
     m.close()
     ph = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     upd_flop, roll_flop = mappo_flops(T, E, D, O, A)
     upd_tflops = upd_flop / (ph["update"] * 1e-3) / 1e12
     return {"value": T * E * D * world / dt, "unit": "agent-steps/s", "ms_per_train_step": dt * 1e3,
-            "train_steps": args.mappo_iters, "phase_ms": ph,
+            "train_steps": args.mappo_iters, "phase_ms": ph, "exchange_floats": exchange,
             "learner_roofline": {"bound": "mfma", "achieved": upd_tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                                  "unit": "TFLOP/s", "frac": upd_tflops / FP32_MFMA_PEAK_TFLOPS,
                                  "flop_per_update": upd_flop, "rollout_actor_flop": roll_flop,
@@ -611,7 +625,94 @@ def mappo_leg(args, ranks, T, cfg=None):
                        "graphs": ("rollout + " if rollout_graph else "") + ("update" if graphed else ""),
                        "grad_allreduce": ("one fused all-reduce per minibatch" + (", captured in the update graph"
                                                                                    if graphed else ""))
-                       if world > 1 else None}}
+                       if (world > 1 or rank_shape) else None}}
+
+
+def world1_group():
+    """A world-1 RCCL process group (N = 1 runs), so the rank-shape legs take the
+    multi-rank exchange path (_force_allreduce) with its all-reduce captured."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+        return True
+    return False
+
+
+def allreduce_us(n, reps=10, per_graph=20):
+    """Mean device time of one all-reduce (sum) of n float32 on the current group,
+    as the update graph issues it: `per_graph` all-reduces captured in a HIP graph,
+    replayed `reps` times between HIP events."""
+    import torch.distributed as dist
+    buf = torch.zeros(n, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            dist.all_reduce(buf)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            dist.all_reduce(buf)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * per_graph)
+    del g
+    return us
+
+
+def rank_shapes_leg(args, ranks, c3_one_gpu=None):
+    """SURVEY §8(e)'s per-rank strong shapes timed on ONE GPU through the exchange
+    path: C3 at G = 2 / 4 / 8, C4 at 4, C5 at 8 (--rank-shapes).
+    Each is one rank's MAPPO train step (E/G envs, mini_batch_size/G, the gradient
+    all-reduce on a world-1 group, captured in the update graph).  The G-rank
+    projection replaces the world-1 all-reduce measured here by an assumed G-GPU
+    xGMI all-reduce latency (--assumed-allreduce-us; not measurable on one GPU):
+    value(G) = T·E·D / (train step + minibatches·(assumed − measured world-1)),
+    and against the 1-GPU global configuration (the 'mappo' leg) its speed-up."""
+    own = world1_group()
+    out = {}
+    try:
+        for item in filter(None, args.rank_shapes.split(",")):
+            name, G = item.split("/")
+            G = int(G)
+            cfg = STRONG_LEGS[name]
+            r = mappo_leg(args, ranks, cfg["T"], cfg, rank_shape=G)
+            c = r["config"]
+            n_upd = 10 * c["minibatches_per_epoch"]
+            out[item] = {"workload": f"{c['workload']}: one rank of {G}", "G": G, "envs_per_rank": c["envs_per_gpu"],
+                         "mini_batch_per_rank": c["mini_batch_size"],
+                         "actor_rows_per_minibatch": c["mini_batch_size"] * c["drones"],
+                         "learner_path": c["learner_path"], "phase_ms": r["phase_ms"],
+                         "ms_per_train_step": r["ms_per_train_step"],
+                         "us_per_minibatch": r["phase_ms"]["update"] * 1e3 / n_upd,
+                         "minibatches_per_update": n_upd, "exchange_floats": r.get("exchange_floats")}
+            ar1 = allreduce_us(r["exchange_floats"])
+            out[item]["allreduce_us_world1"] = ar1
+            t_step = r["ms_per_train_step"] * 1e-3
+            agent_steps = c["rollout_steps"] * c["envs_per_gpu"] * G * c["drones"]
+            proj = {}
+            for ar in (args.assumed_allreduce_us, 2 * args.assumed_allreduce_us):
+                t = t_step + n_upd * (ar - ar1) * 1e-6
+                proj[f"allreduce_{ar:g}us"] = {"value": agent_steps / t, "ms_per_train_step": t * 1e3}
+                if name == "C3" and c3_one_gpu:
+                    proj[f"allreduce_{ar:g}us"]["speedup_vs_1gpu"] = agent_steps / t / c3_one_gpu
+                    proj[f"allreduce_{ar:g}us"]["efficiency"] = agent_steps / t / c3_one_gpu / G
+            out[item]["projected_G_ranks"] = proj
+    finally:
+        if own:
+            import torch.distributed as dist
+            torch.cuda.synchronize()
+            dist.destroy_process_group()
+    return out
 
 
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2   # wave64 VALU instr/s: 1024 SIMDs, one per 2 cycles (the fp32 vector rate)
@@ -662,7 +763,7 @@ def main():
     bpas = bytes_per_agent_step(args.act, "multihover", D)
     nbytes = bpas * E * D
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
-    pyb = fp64 = mappo = mappo32 = mappo_cfgs = configs = None
+    pyb = fp64 = mappo = mappo32 = mappo_cfgs = configs = rank_shapes = None
     mappo_strong, configs_strong = {}, {}
     for kind, name, scaling, e_rank, mb_rank in leg_plan(args, world)[1:]:
         if kind == "sim" and name == "fp64":   # the headline rollout in the reference's float64
@@ -684,8 +785,12 @@ def main():
                    "roofline_frac": nbytes / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS}
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 pyb["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, physics="pyb")
+        elif kind == "mappo" and name == "rank_shapes":
+            rank_shapes = rank_shapes_leg(args, ranks, mappo["value"] if mappo else None)
         elif kind == "mappo" and scaling == "strong":
             mappo_strong[name] = mappo_leg(args, ranks, STRONG_LEGS[name]["T"], STRONG_LEGS[name])
+            # the real G-GPU all-reduce of the exchange buffer, as the update graph issues it
+            mappo_strong[name]["allreduce_us"] = allreduce_us(mappo_strong[name]["exchange_floats"])
         elif kind == "mappo" and name == "C3":
             mappo = mappo_leg(args, ranks, args.mappo_steps)
         elif kind == "mappo" and name == "C3_t32":
@@ -750,6 +855,7 @@ def main():
             "mappo": mappo,
             "mappo_t32": mappo32,
             "mappo_configs": mappo_cfgs,
+            "mappo_rank_shapes": rank_shapes,
             "configs": configs,
         }
         if world > 1:

@@ -66,6 +66,9 @@ def test_bench_two_ranks_lists_strong_legs():
     _, one = _run_bench("--dry-run", "--dry-ms", "1", "--steps", "2", "--warmup", "0")
     assert not any(g["scaling"] == "strong" for g in one["legs"])
     assert ("mappo", "ref", "weak") in {(g["kind"], g["name"], g["scaling"]) for g in one["legs"]}
+    # N = 1: the per-rank strong shapes, each timed on one GPU through the exchange path
+    assert ("mappo", "rank_shapes", "rank-shape") in {(g["kind"], g["name"], g["scaling"]) for g in one["legs"]}
+    assert not any(g["name"] == "rank_shapes" for g in line["legs"])
 
 
 def test_bytes_per_agent_step_matches_survey():
