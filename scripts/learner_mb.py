@@ -233,6 +233,12 @@ def main():
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "ranks" in which:
         ranks()
+    for w in which:   # "shape:NAME[:direct]": one shape's tile (or direct) path alone, e.g. under a kernel trace
+        if w.startswith("shape:"):
+            _, name, *rest = w.split(":")
+            agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
+            us, path = per_minibatch_us(name, small=not rest)
+            print(f"{name:5s} {'direct' if rest else 'tile'} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "one" in which:   # the default C3 iteration alone (for a kernel trace: scripts/learner_timeline.py)
         us, path = per_minibatch_us("C3")
         print(f"C3  default {us:8.1f} us/minibatch  [{path}]", flush=True)

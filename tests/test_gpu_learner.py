@@ -182,6 +182,18 @@ def test_ppo_minibatch_update_matches_reference(graphs, fused):
         torch.testing.assert_close(p, q, rtol=0, atol=1e-3 / 60)
 
 
+def adam_close(got, want, lr, steps):
+    """Parameters after `steps` Adam steps from gradients that agree to fp32
+    rounding (another row-sum order): within lr/60 per step, except where a
+    gradient element is near zero — Adam's m/√v then turns its rounding into a
+    step of up to ~lr (m and √v of comparable size at any scale) — so a handful
+    of elements (≤ 1e-4 of them) may differ by up to the steps' full size."""
+    d = (got - want).abs()
+    assert float(d.max()) <= steps * lr * 1.01, float(d.max())
+    far = int((d > steps * lr / 60).sum())
+    assert far <= max(3, int(1e-4 * d.numel())), (far, d.numel())
+
+
 def _hidden256_update(graphs, E=32, T=8, force_allreduce=False, D=8, A=1, logp_shift=0.0, run=True, O=27, **variant):
     """Two epochs x two minibatches of the 256-wide MAPPO update (the direct
     iteration's configuration) from fixed weights, data and permutations
@@ -319,12 +331,14 @@ def test_small_update_matches_autograd(graphs, E, T, D, A, O, monkeypatch):
     assert took_small == (D * O <= 640), (D, O, took_small)
     a_ref, r_ref = _hidden256_update(graphs, E, T, D=D, A=A, O=O, direct=False)
     # Adam's normalised steps carry ulp-level gradient differences up to ~lr/60 per step; 4 steps
-    torch.testing.assert_close(a_small.actor_opt.flat, a_ref.actor_opt.flat, rtol=0, atol=4 * 3e-4 / 60)
-    torch.testing.assert_close(a_small.critic_opt.flat, a_ref.critic_opt.flat, rtol=0, atol=4 * 1e-3 / 60)
+    adam_close(a_small.actor_opt.flat, a_ref.actor_opt.flat, 3e-4, 4)
+    adam_close(a_small.critic_opt.flat, a_ref.critic_opt.flat, 1e-3, 4)
     assert float(a_small.actor_opt.step) == float(a_ref.actor_opt.step)
     assert float(a_small.critic_opt.step) == float(a_ref.critic_opt.step) == 4.0
     for k in r_small:
-        assert r_small[k] == pytest.approx(r_ref[k], rel=1e-5, abs=1e-7), k
+        # approx_kl: a mean of log-probability differences ~1e-3 formed from float32
+        # log-densities ~5 (cancellation), so an absolute bound
+        assert r_small[k] == pytest.approx(r_ref[k], rel=1e-5, abs=1e-6 if k == 'approx_kl' else 1e-7), k
     if took_small:
         _assert_small_copies_current(a_small)
     assert mb > 0
