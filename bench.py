@@ -405,7 +405,8 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
     graphs = []
     for n in ([gsteps] if n_full else []) + ([rem] if rem else []):
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=stream):
+        # thread_local: with N ranks the RCCL watchdog thread may query the fences' events during the capture
+        with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
             for k in range(n):
                 step(k % slots)
         graphs.append((g, n))
@@ -653,7 +654,7 @@ def allreduce_us(n, reps=10, per_graph=20):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):   # (the RCCL watchdog polls from its thread)
         for _ in range(per_graph):
             dist.all_reduce(buf)
     g.replay()

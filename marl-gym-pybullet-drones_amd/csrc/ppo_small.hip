@@ -69,9 +69,9 @@ constexpr int kSNarrowI = 256;         // the forward/backward instance for inpu
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
 constexpr int kSGW = 4;                // waves per weight-gradient workgroup (one 32×32 block and K-chunk)
-constexpr int kSGQ = 64;               // quads (16 rows) per weight-gradient workgroup before K is split in chunks
+constexpr int kSBT1Q = 128;            // quads (16 rows) from which a net's weight gradients take 16×16 blocks
+constexpr int kSGQ = 512;              // quads per K-chunk of 16×16 blocks (longer columns: chunk partials + launch 3)
 constexpr int kSMaxS = 32;             // most K-chunks per net
-constexpr int kSVecWG = 4;             // workgroups for the vector parameters (8 measured no faster)
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
 // Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
 // forward/backward tile uses ~53 KB (the narrow instance) and would otherwise be
@@ -122,6 +122,7 @@ struct SWork {   // workspace views (qs_ppo_small_work_bytes)
 enum { SINK_PART = 0, SINK_ADAM = 1, SINK_GRAD = 2 };
 struct SGrad {
   int S[2];          // K-chunks per net (actor, critic)
+  int bt[2];         // weight-gradient block side per net, in 16-row tiles (1: 16×16, 2: 32×32)
   int sink;          // the final sink: SINK_ADAM (one rank) or SINK_GRAD (this rank's gradient, for the all-reduce)
   float* g[2];       // SINK_GRAD / qs_ppo_small_adam: the nets' gradient buffers (flat, the params' layout)
   float gdiv;        // qs_ppo_small_adam: the all-reduced sums ÷ gdiv (the world size), approx_kl too
@@ -655,36 +656,25 @@ __device__ __forceinline__ bool s_gate_open(const SArgs& P) {
   return !P.gate || *P.kl_out / P.G.gdiv <= P.kl_thr;
 }
 
-// One reduced gradient element of a weight matrix into the final sink: Adam in
-// place (with the W2ᵀ / padded W1 copies), or the net's gradient buffer
-__device__ __forceinline__ void s_sink_w(const SArgs& P, const SNet& N, bool actor, int sink, long long i, float g,
-                                         const float (&sc)[2][2], bool w2, int n, int k) {
-  const int si = actor ? 0 : 1;
-  if (sink == SINK_GRAD) {
-    P.G.g[si][i] = g;
-    return;
-  }
-  s_adam(N, i, g, sc[si][0], sc[si][1], w2 ? N.w2t : nullptr, n, k, w2 ? nullptr : N.w1p, N.p[i], N.m[i], N.v[i]);
-}
-
 // The vector parameters of both nets (b1, b2, W3, b3 and the actor's logstd),
-// element e of [actor's | critic's]: the flat index and the gradient, from the
-// tile partial rows (fixed tile order, eight rows' loads in flight) or, FROM_G,
-// from the gradient buffers ÷ gdiv.  false: past the end.
-template <bool FROM_G>
-__device__ __forceinline__ bool s_vec_elem(const SArgs& P, int e, bool& actor, long long& i, float& gsum) {
+// element e of [actor's | critic's]: its flat index i, and where its gradient
+// is formed — the column of the tile partial rows (col, stride cstride; nt
+// rows, one per tile) or, for logstd, dlogstd[u] (col = NULL).  false: past the end.
+__device__ __forceinline__ bool s_vec_loc(const SArgs& P, int e, bool& actor, long long& i, const float*& col,
+                                          int& cstride, int& nt, int& u) {
   const int A = P.a.A;
   const int na = 2 * kSH + A * kSH + 2 * A, nc = 2 * kSH + kSH + 1;
   if (e >= na + nc) return false;
   actor = e < na;
   const SNet& N = actor ? P.a : P.c;
-  const int AA = actor ? A : 1, nt = actor ? P.nA : P.nC;
+  const int AA = actor ? A : 1;
+  nt = actor ? P.nA : P.nC;
   const float* pA = actor ? P.w.partAa : P.w.partAc;
   const float* pB = actor ? P.w.partBa : P.w.partBc;
   const int PA = kSH + AA * kSH + AA;
-  int u = actor ? e : e - na;
-  const float* col = nullptr;
-  int cstride = 0;
+  u = actor ? e : e - na;
+  col = nullptr;
+  cstride = 0;
   if (u < kSH) {                       // b1: Σ dZ1
     col = pB + u; cstride = kSH;
     i = N.b1 + u;
@@ -701,32 +691,57 @@ __device__ __forceinline__ bool s_vec_elem(const SArgs& P, int e, bool& actor, l
     u -= AA;
     i = N.logstd + u;
   }
-  if constexpr (FROM_G) {
-    gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
-    return true;
-  }
-  if (!col) {
-    gsum = P.w.dlogstd[u];
-    return true;
-  }
-  float acc = 0.f;
-  int t = 0;
-  for (; t + 8 <= nt; t += 8) {
-    float v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = col[(size_t)(t + q) * cstride];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc += v[q];
-  }
-  for (; t < nt; ++t) acc += col[(size_t)t * cstride];
-  gsum = acc;
   return true;
 }
 
 // A weight matrix's 32×32 blocks: W1 [256][I] (⌈I/32⌉ column blocks) then W2
 // [256][256]; nblk(N) blocks per net
-__device__ __forceinline__ int s_mb1(int I) { return (I + 31) / 32; }
-__host__ __device__ inline int s_nblk(int I) { return 8 * ((I + 31) / 32) + 64; }
+// 16·BT-square blocks of W1 [256][I] (⌈I/(16·BT)⌉ column blocks) then W2 [256][256]:
+// s_nblk(I, BT) blocks per net; the chunk partials' rows are s_mp(I) wide for either BT
+__host__ __device__ inline int s_cb(int I, int bt) { return (I + 16 * bt - 1) / (16 * bt); }
+__host__ __device__ inline int s_nblk(int I, int bt) { return (16 / bt) * s_cb(I, bt) + (16 / bt) * (16 / bt); }
+__host__ __device__ inline int s_mp(int I) { return 32 * ((I + 31) / 32); }
+
+// c[0] += Σ over NQ quads of dZᵀ[n0 + j][rows]·Xᵀ[m0 + j][rows] (one 16×16 tile;
+// the even and odd quads on two accumulator chains, added at the end), R quads
+// of loads ahead; compile-time NQ
+template <int NQ>
+__device__ __forceinline__ void s_wgrad11_n(const float* a0, const float* b0, int g, f32x4& c0, f32x4& c1) {
+  constexpr int R = NQ < 8 ? NQ : 8;
+  float4 ra[R], rb[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    ra[t] = *reinterpret_cast<const float4*>(a0 + 16 * t + 4 * g);
+    rb[t] = *reinterpret_cast<const float4*>(b0 + 16 * t + 4 * g);
+  }
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const float4 x = ra[t % R], y = rb[t % R];
+    if (t + R < NQ) {
+      ra[t % R] = *reinterpret_cast<const float4*>(a0 + 16 * (t + R) + 4 * g);
+      rb[t % R] = *reinterpret_cast<const float4*>(b0 + 16 * (t + R) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
+    f32x4& acc = (t & 1) ? c1 : c0;
+    acc = s_mfma(x.x, y.x, acc);
+    acc = s_mfma(x.y, y.y, acc);
+    acc = s_mfma(x.z, y.z, acc);
+    acc = s_mfma(x.w, y.w, acc);
+  }
+}
+__device__ __forceinline__ void s_wgrad11(const float* a0, const float* b0, int nq, int g, f32x4& c) {
+  f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  int t = 0;
+  for (; t + 16 <= nq; t += 16) s_wgrad11_n<16>(a0 + 16 * t, b0 + 16 * t, g, c, c1);
+  switch (nq - t) {
+#define S_CASE(n) case n: s_wgrad11_n<n>(a0 + 16 * t, b0 + 16 * t, g, c, c1); break;
+    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
+    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
+#undef S_CASE
+    default: break;
+  }
+  c += c1;
+}
 
 // c[bi][bj] += Σ over NQ quads of dZᵀ[n0 + 16bi + j][rows]·Xᵀ[m0 + 16bj + j][rows]
 // (a 2×2 grid of 16×16 MFMA tiles: four independent chains, four float4
@@ -776,99 +791,148 @@ __device__ __forceinline__ void s_wgrad22(const float* a0, const float* a1, cons
   }
 }
 
-// Launch 2.  Workgroups [0, Σ blocks·S): one 32×32 weight block and K-chunk
-// each (actor's first, the chunks of a block adjacent); then kSVecWG for the
-// vector parameters.  SINK: where the weight blocks' sums go — SINK_PART (the
-// chunk partials, reduced by launch 3) or, when both nets have one chunk,
-// P.G.sink.  The vector parameters always go to P.G.sink; with SINK_ADAM
-// (one chunk, Adam) the last workgroup commits the step counts.
-template <int SINK>
-__global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P) {
-  __shared__ float red[kSGW - 1][16][64];
+// One 16·BT-square block of a weight matrix and K-chunk s of S (launch 2):
+// wave w forms the block's BT×BT MFMA tiles over its quarter of the chunk's
+// quads; the waves' sums are added in wave order through LDS, each wave then
+// taking BT² of every lane's elements (f = BT²·w + k → tile f/4, register
+// f%4).  S = 1: into the final sink (Adam with its p / m / v loaded ahead, or
+// the gradient buffer); otherwise the chunk partials of launch 3.
+template <int BT>
+__device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int s, int u, bool adam, bool open_a,
+                                         float (*red)[16][64], const float (*sc)[2]) {
+  constexpr int NT = BT * BT;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const SNet& N = actor ? P.a : P.c;
+  const bool direct = S == 1;
+  const int cb = s_cb(N.I, BT);
+  const bool l1 = u < (16 / BT) * cb;
+  const int uu = l1 ? u : u - (16 / BT) * cb, ncb = l1 ? cb : 16 / BT;
+  const int n0 = 16 * BT * (uu / ncb), m0 = 16 * BT * (uu % ncb);
+  const int M = l1 ? N.I : kSH;
+  const bool act = !adam || !actor || open_a;
+  int en[NT], em[NT];
+  float pp[NT], pm[NT], pv[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const int f = NT * w + k, q = f >> 2, r = f & 3;
+    en[k] = n0 + 16 * (q / BT) + 4 * g + r;
+    em[k] = m0 + 16 * (q % BT) + j;
+    if (direct && adam && act && em[k] < M) {   // Adam's operands, in flight during the gradient
+      const long long i = (l1 ? N.w1 : N.w2) + (long long)en[k] * M + em[k];
+      pp[k] = N.p[i];
+      pm[k] = N.m[i];
+      pv[k] = N.v[i];
+    }
+  }
+  const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
+  const float* dzT = actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT);
+  const float* xT = actor ? (l1 ? P.w.xaT : P.w.h1aT) : (l1 ? P.w.xcT : P.w.h1cT);
+  // the chunk's quads, split over the waves (contiguous, wave order)
+  const int Q = KP / 16, qc = (Q + S - 1) / S, q0 = min(Q, s * qc), q1 = min(Q, q0 + qc);
+  const int qw = (q1 - q0 + kSGW - 1) / kSGW;
+  const int wa = min(q1, q0 + w * qw), wb = min(q1, wa + qw);
+  f32x4 c[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (columns past M are not stored: clamped, their sums discarded)
+  if constexpr (BT == 1) {
+    s_wgrad11(dzT + (size_t)(n0 + j) * KS + 16 * wa, xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, wb - wa, g, c[0]);
+  } else {
+    s_wgrad22(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
+              xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
+              wb - wa, g, c);
+  }
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * q + r][l] = c[q][r];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const int f = NT * w + k;
+    float t = red[0][f][l];
+#pragma unroll
+    for (int v = 1; v < kSGW; ++v) t += red[v][f][l];
+    if (!direct) {
+      float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
+      const int Mp = l1 ? s_mp(N.I) : kSH;
+      part[((size_t)s * kSH + en[k]) * Mp + em[k]] = t;   // (pad columns too)
+    } else if (act && em[k] < M) {
+      const int si = actor ? 0 : 1;
+      const long long i = (l1 ? N.w1 : N.w2) + (long long)en[k] * M + em[k];
+      if (!adam) P.G.g[si][i] = t;
+      else s_adam(N, i, t, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr, pp[k],
+                  pm[k], pv[k]);
+    }
+  }
+}
+
+// Launch 2.  Workgroups [0, Σ blocks·S): one weight block and K-chunk each
+// (s_wblock; the actor's first, the chunks of a block adjacent; 16×16 blocks
+// for a net with long columns (P.G.bt = 1: enough blocks to fill the CUs),
+// 32×32 otherwise (four float4 operands per 16 MFMAs)); then the vector
+// parameters, 16 lanes per element (lane k sums the tile partial rows
+// t ≡ k mod 16 in order, a fixed DPP butterfly adds the lanes), into P.G.sink.
+// With Adam and no launch 3 the last workgroup commits the step counts.
+__global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P, int fin) {
+  __shared__ float red[kSGW][16][64];
   __shared__ float sc[2][2];
   __shared__ bool last;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const int tid = threadIdx.x;
   s_adam_scalars(P, sc, tid);
-  const bool open_a = P.G.sink != SINK_ADAM || s_gate_open(P);
-  __syncthreads();
-  const int nwa = s_nblk(P.a.I) * P.G.S[0], nwc = s_nblk(P.c.I) * P.G.S[1];
+  const bool adam = P.G.sink == SINK_ADAM;
+  const bool open_a = !adam || s_gate_open(P);
+  const int nwa = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0], nwc = s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1];
   const int blk = blockIdx.x;
+  __syncthreads();   // (sc)
   if (blk < nwa + nwc) {
     const bool actor = blk < nwa;
     const int S = P.G.S[actor ? 0 : 1];
     const int T = actor ? blk : blk - nwa;
-    const int s = T % S, u = T / S;
-    const SNet& N = actor ? P.a : P.c;
-    // a closed gate skips the actor's Adam (the partials of SINK_PART are formed
-    // regardless: launch 3 reads the gate)
-    if (SINK != SINK_ADAM || !actor || open_a) {
-      const int mb1 = s_mb1(N.I);
-      const bool l1 = u < 8 * mb1;
-      const int uu = l1 ? u : u - 8 * mb1, ncb = l1 ? mb1 : 8;
-      const int n0 = 32 * (uu / ncb), m0 = 32 * (uu % ncb);
-      const int M = l1 ? N.I : kSH;
-      const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
-      const float* dzT = actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT);
-      const float* xT = actor ? (l1 ? P.w.xaT : P.w.h1aT) : (l1 ? P.w.xcT : P.w.h1cT);
-      // the chunk's quads, split over the waves (contiguous, wave order)
-      const int Q = KP / 16, qc = (Q + S - 1) / S, q0 = min(Q, s * qc), q1 = min(Q, q0 + qc);
-      const int qw = (q1 - q0 + kSGW - 1) / kSGW;
-      const int wa = min(q1, q0 + w * qw), wb = min(q1, wa + qw);
-      const float* a0 = dzT + (size_t)(n0 + j) * KS + 16 * wa;
-      const float* a1 = dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa;
-      // (columns past M are not stored: clamped, their sums discarded)
-      const float* b0 = xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa;
-      const float* b1 = xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa;
-      f32x4 c[4];
+    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, T % S, T / S, adam, open_a, red, sc);
+    else s_wblock<2>(P, actor, S, T % S, T / S, adam, open_a, red, sc);
+  } else {
+    const int e = ((blk - nwa - nwc) * (int)blockDim.x + tid) >> 4, k = tid & 15;
+    bool actor;
+    long long i;
+    const float* col;
+    int cstride, nt, u;
+    if (s_vec_loc(P, e, actor, i, col, cstride, nt, u)) {   // (uniform over the element's 16 lanes)
+      const SNet& N = actor ? P.a : P.c;
+      const bool doit = !adam || !actor || open_a;
+      float p0 = 0.f, m0 = 0.f, v0 = 0.f;
+      if (doit && adam && k == 0) {
+        p0 = N.p[i];
+        m0 = N.m[i];
+        v0 = N.v[i];
+      }
+      float gsum;
+      if (col) {
+        float acc = 0.f;
+        int tt = k;
+        for (; tt + 16 * 7 < nt; tt += 16 * 8) {
+          float v[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      s_wgrad22(a0, a1, b0, b1, wb - wa, g, c);
-      if (w > 0)
+          for (int q = 0; q < 8; ++q) v[q] = col[(size_t)(tt + 16 * q) * cstride];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) red[w - 1][4 * q + r][l] = c[q][r];
-      __syncthreads();
-      if (w == 0) {
-#pragma unroll
-        for (int v = 0; v < kSGW - 1; ++v)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) c[q][r] += red[v][4 * q + r][l];
-        const int Mp = l1 ? 32 * mb1 : kSH;
-        float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int m = m0 + 16 * (q & 1) + j;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + 16 * (q >> 1) + 4 * g + r;
-            if (SINK == SINK_PART) {
-              part[((size_t)s * kSH + n) * Mp + m] = c[q][r];   // (pad columns too: launch 3 skips them)
-            } else if (m < M) {
-              s_sink_w(P, N, actor, SINK, (l1 ? N.w1 : N.w2) + (long long)n * M + m, c[q][r], sc, !l1, n, m);
-            }
-          }
+          for (int q = 0; q < 8; ++q) acc += v[q];
+        }
+        for (; tt < nt; tt += 16) acc += col[(size_t)tt * cstride];
+        gsum = s_row_sum(acc);
+      } else {
+        gsum = P.w.dlogstd[u];
+      }
+      if (doit && k == 0) {
+        if (!adam) {
+          P.G.g[actor ? 0 : 1][i] = gsum;
+        } else {
+          const int si = actor ? 0 : 1;
+          s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, p0, m0, v0);
         }
       }
     }
-  } else {
-    for (int e = (blk - nwa - nwc) * blockDim.x + tid;; e += kSVecWG * blockDim.x) {
-      bool actor;
-      long long i;
-      float gsum;
-      if (!s_vec_elem<false>(P, e, actor, i, gsum)) break;
-      if (P.G.sink == SINK_GRAD) {
-        P.G.g[actor ? 0 : 1][i] = gsum;
-      } else if (!actor || open_a) {
-        const SNet& N = actor ? P.a : P.c;
-        const int si = actor ? 0 : 1;
-        s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, N.p[i], N.m[i], N.v[i]);
-      }
-    }
   }
-  if (SINK != SINK_ADAM) return;
+  if (!fin || !adam) return;
   __syncthreads();
   if (tid == 0) last = atomicAdd(P.w.cnt + 128, 1u) == gridDim.x - 1;
   __syncthreads();
@@ -880,12 +944,12 @@ __global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P) {
 }
 
 // Launch 3, one thread per parameter element: FROM_G = false — the weight
-// matrices' chunk partials summed in chunk order (launch 2 did the vector
-// parameters) into P.G.sink; FROM_G = true (qs_ppo_small_adam, after the rank
+// matrices of the nets with K-chunks (S > 1): the chunk partials summed in
+// chunk order, into P.G.sink; FROM_G = true (qs_ppo_small_adam, after the rank
 // all-reduce) — every parameter's gradient from the gradient buffers ÷ gdiv,
 // into Adam.  Elements: actor W1, W2, critic W1, W2 (row-major, as the
-// parameters), then (FROM_G) the vector parameters.  With Adam the last
-// workgroup commits the step counts.
+// parameters; FROM_G = false: only those of nets with S > 1), then (FROM_G)
+// the vector parameters.  With Adam the last workgroup commits the step counts.
 template <bool FROM_G>
 __global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
   __shared__ float sc[2][2];
@@ -895,8 +959,10 @@ __global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
   const int sink = FROM_G ? SINK_ADAM : P.G.sink;
   const bool open_a = sink != SINK_ADAM || s_gate_open(P);
   __syncthreads();
-  long long e = (long long)blockIdx.x * blockDim.x + tid;
-  const long long nw[4] = {(long long)kSH * P.a.I, (long long)kSH * kSH, (long long)kSH * P.c.I, (long long)kSH * kSH};
+  int e = blockIdx.x * blockDim.x + tid;
+  const bool inc[2] = {FROM_G || P.G.S[0] > 1, FROM_G || P.G.S[1] > 1};
+  const int nw[4] = {inc[0] ? kSH * P.a.I : 0, inc[0] ? kSH * kSH : 0, inc[1] ? kSH * P.c.I : 0,
+                     inc[1] ? kSH * kSH : 0};
   int part = 0;
   while (part < 4 && e >= nw[part]) e -= nw[part++];
   if (part < 4) {
@@ -904,34 +970,40 @@ __global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
     const SNet& N = actor ? P.a : P.c;
     if (sink != SINK_ADAM || !actor || open_a) {
       const int M = l1 ? N.I : kSH;
-      const int n = (int)(e / M), m = (int)(e - (long long)n * M);
+      const int n = e / M, m = e - n * M;
       const long long i = (l1 ? N.w1 : N.w2) + e;
       float gsum;
       if constexpr (FROM_G) {
         gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
       } else {
+        // the S chunk partials, eight loads in flight (clamped: unconditional), added in chunk order
         const int S = P.G.S[actor ? 0 : 1];
-        const int Mp = l1 ? 32 * s_mb1(N.I) : kSH;
+        const int Mp = l1 ? s_mp(N.I) : kSH;
         const float* pp = P.w.wpart[part] + (size_t)n * Mp + m;
         const size_t cs = (size_t)kSH * Mp;
-        float v[kSMaxS];
+        gsum = 0.f;
+        for (int q0 = 0; q0 < S; q0 += 8) {
+          float v[8];
 #pragma unroll
-        for (int q = 0; q < kSMaxS; ++q) v[q] = q < S ? pp[q * cs] : 0.f;
-        gsum = v[0];
+          for (int q = 0; q < 8; ++q) v[q] = pp[(size_t)min(q0 + q, S - 1) * cs];
 #pragma unroll
-        for (int q = 1; q < kSMaxS; ++q)
-          if (q < S) gsum += v[q];
+          for (int q = 0; q < 8; ++q) gsum = (q0 + q == 0) ? v[q] : (q0 + q < S ? gsum + v[q] : gsum);
+        }
       }
-      s_sink_w(P, N, actor, sink, i, gsum, sc, !l1, n, m);
+      const int si = actor ? 0 : 1;
+      if (sink == SINK_GRAD) P.G.g[si][i] = gsum;
+      else s_adam(N, i, gsum, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, n, m, l1 ? N.w1p : nullptr, N.p[i], N.m[i],
+                  N.v[i]);
     }
   } else if (FROM_G) {
     bool actor;
     long long i;
-    float gsum;
-    if (s_vec_elem<true>(P, (int)e, actor, i, gsum) && (!actor || open_a)) {
+    const float* col;
+    int cstride, nt, u;
+    if (s_vec_loc(P, e, actor, i, col, cstride, nt, u) && (!actor || open_a)) {
       const SNet& N = actor ? P.a : P.c;
       const int si = actor ? 0 : 1;
-      s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, N.p[i], N.m[i], N.v[i]);
+      s_adam(N, i, P.G.g[si][i] / P.G.gdiv, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, N.p[i], N.m[i], N.v[i]);
     }
   }
   if (sink != SINK_ADAM) return;
@@ -970,13 +1042,18 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
 
 struct SLayout {
   int nA, nC, KaP, KcP, KaS, KcS;
-  int Sa, Sc;   // K-chunks of the weight gradients per net
+  int Sa, Sc;     // K-chunks of the weight gradients per net
+  int bta, btc;   // their block sides in 16-row tiles
   long long off[20];
   long long bytes;
 };
-// K-chunks for a net's weight gradients: one per kSGQ quads of rows, at most kSMaxS
+// A net's weight-gradient blocks: 16×16 once its columns are long (≥ kSBT1Q
+// quads: the 16×16 blocks' count fills the CUs and each stays MFMA-busy), 32×32
+// below; K-chunks only for 16×16 blocks past kSGQ quads per chunk
+inline int s_bt(long long KP) { return KP / 16 >= kSBT1Q ? 1 : 2; }
 inline int s_chunks(long long KP) {
   const long long q = KP / 16;
+  if (s_bt(KP) != 1) return 1;
   const long long S = (q + kSGQ - 1) / kSGQ;
   return (int)(S < 1 ? 1 : (S > kSMaxS ? kSMaxS : S));
 }
@@ -994,6 +1071,8 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   L.KcS = L.KcP + kSPad;
   L.Sa = Ia > 0 ? s_chunks(L.KaP) : 0;
   L.Sc = s_chunks(L.KcP);
+  L.bta = s_bt(L.KaP);
+  L.btc = s_bt(L.KcP);
   const long long pw = 4LL * kSH;   // bytes of a [256] partial column run
   const long long sz[20] = {
       4LL * Ia * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS,   // xaT h1aT dz2aT dz1aT
@@ -1144,6 +1223,8 @@ static void s_bind(SArgs& P, const qs_mlp256* actor, const qs_mlp256* critic, co
   for (int i = 0; i < 4; ++i) P.w.wpart[i] = (float*)(wb + L.off[16 + i]);
   P.G.S[0] = L.Sa;
   P.G.S[1] = L.Sc;
+  P.G.bt[0] = L.bta;
+  P.G.bt[1] = L.btc;
   P.G.sink = SINK_ADAM;
   P.G.g[0] = P.G.g[1] = nullptr;
   P.G.gdiv = 1.0f;
@@ -1172,13 +1253,14 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
 // Launches 2 (and 3 when a net's weight gradients are split in K-chunks) into P.G.sink
 static void s_launch_grad(const SArgs& P, hipStream_t st) {
   const bool one = P.G.S[0] == 1 && P.G.S[1] == 1;
-  const int grid = s_nblk(P.a.I) * P.G.S[0] + s_nblk(P.c.I) * P.G.S[1] + kSVecWG;
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kSGW), kSReserveG, st, P); };
-  if (!one) go(ppo_small_wgrad_kernel<SINK_PART>);
-  else if (P.G.sink == SINK_GRAD) go(ppo_small_wgrad_kernel<SINK_GRAD>);
-  else go(ppo_small_wgrad_kernel<SINK_ADAM>);
+  const int nvec = (2 * kSH + P.a.A * kSH + 2 * P.a.A) + (3 * kSH + 1);
+  const int vwg = (16 * nvec + 64 * kSGW - 1) / (64 * kSGW);   // 16 lanes per vector element
+  const int grid = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0] + s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1] + vwg;
+  hipLaunchKernelGGL(ppo_small_wgrad_kernel, dim3(grid), dim3(64 * kSGW), kSReserveG, st, P, (int)one);
   if (one) return;
-  const long long nel = (long long)kSH * (P.a.I + P.c.I) + 2LL * kSH * kSH;
+  long long nel = 0;
+  for (int k = 0; k < 2; ++k)
+    if (P.G.S[k] > 1) nel += (long long)kSH * ((k ? P.c.I : P.a.I) + kSH);
   hipLaunchKernelGGL(ppo_small_apply_kernel<false>, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, P);
 }
 

@@ -1447,7 +1447,8 @@ class MAPPOAgent:
                 self._step_minibatch(rollouts, self._g_idx, self._g_acc)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: the RCCL watchdog thread may query earlier collectives' events during the capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(k):
                 self._step_minibatch(rollouts, self._g_perm[i * mb:(i + 1) * mb], self._g_acc)
         for t, v in zip((self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq, self.actor_opt.step,

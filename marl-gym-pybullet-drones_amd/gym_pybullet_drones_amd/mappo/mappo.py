@@ -395,7 +395,8 @@ class MAPPO:
         rollouts.next_obs_slots[0].copy_(self.obs)
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        # thread_local: the RCCL watchdog thread may query earlier collectives' events during the capture
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for t in range(self.rollout_steps):
                 self._rollout_step(rollouts, t)
         torch.cuda.current_stream().wait_stream(s)
