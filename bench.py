@@ -399,6 +399,8 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
     # each (the obs ring cycling through its `slots` buffers inside a graph), so that
     # exactly `steps` run: a window of 484 steps is one replay, not 16 (each graph
     # boundary cost ~9 µs of idle device time between the replays)
+    from gym_pybullet_drones_amd.mappo.agent import drain_collectives
+    drain_collectives()   # N ranks: the fences' collectives retired before the capture (RCCL watchdog)
     gsteps = max(1, min(args.graph_steps, args.steps))
     n_full, rem = divmod(args.steps, gsteps)
     stream = torch.cuda.Stream()
@@ -652,7 +654,8 @@ def allreduce_us(n, reps=10, per_graph=20):
         for _ in range(3):
             dist.all_reduce(buf)
     torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
+    from gym_pybullet_drones_amd.mappo.agent import drain_collectives
+    drain_collectives()   # the warm-up all-reduces retired before the capture (RCCL watchdog)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode="thread_local"):   # (the RCCL watchdog polls from its thread)
         for _ in range(per_graph):

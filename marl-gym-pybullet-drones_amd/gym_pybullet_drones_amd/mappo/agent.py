@@ -22,6 +22,7 @@ MI355X-specific structure:
 import ctypes
 import math
 import os
+import time
 from collections import defaultdict
 
 import torch
@@ -918,6 +919,18 @@ def _dist_world():
     return tdist.get_world_size() if (tdist.is_available() and tdist.is_initialized()) else 1
 
 
+def drain_collectives():
+    """Before a graph capture with a process group up: let the RCCL watchdog
+    retire every eager collective issued so far (warm-up all-reduces, barriers).
+    It polls each pending work's HIP event from its own thread, and an event
+    query whose stream is capturing is refused (hipErrorCapturedEvent /
+    hipErrorStreamCaptureUnsupported), which kills the process.  The watchdog
+    loop runs every 100 ms; the device is drained first so every work is done."""
+    if tdist.is_available() and tdist.is_initialized():
+        torch.cuda.synchronize()
+        time.sleep(0.25)
+
+
 class MAPPOAgent:
     """AG:501-772 with the update on device (flat buffers, gated HIP Adam, optional graph)."""
 
@@ -1446,8 +1459,9 @@ class MAPPOAgent:
             for _ in range(2):
                 self._step_minibatch(rollouts, self._g_idx, self._g_acc)
         torch.cuda.current_stream().wait_stream(s)
+        drain_collectives()
         g = torch.cuda.CUDAGraph()
-        # thread_local: the RCCL watchdog thread may query earlier collectives' events during the capture
+        # thread_local: the RCCL watchdog thread may run during the capture
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(k):
                 self._step_minibatch(rollouts, self._g_perm[i * mb:(i + 1) * mb], self._g_acc)
