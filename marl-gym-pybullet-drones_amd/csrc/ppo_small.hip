@@ -49,6 +49,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "qs_learner.h"
@@ -68,7 +69,7 @@ constexpr int kSMaxI = 640;            // widest input (Spiral's centralized cri
 constexpr int kSNarrowI = 256;         // the forward/backward instance for inputs up to this width (smaller LDS X tile)
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
-constexpr int kSGW = 4;                // waves per weight-gradient workgroup (one 32×32 block and K-chunk)
+constexpr int kSGW = 16;               // waves per weight-gradient workgroup (one weight block and K-chunk)
 constexpr int kSBT1Q = 128;            // quads (16 rows) from which a net's weight gradients take 16×16 blocks
 constexpr int kSGQ = 512;              // quads per K-chunk of 16×16 blocks (longer columns: chunk partials + launch 3)
 constexpr int kSMaxS = 32;             // most K-chunks per net
@@ -78,7 +79,7 @@ constexpr int kSPad = 16;              // floats past the padded rows in a trans
 // packed up to three to a CU while other CUs idle (the grids are one workgroup
 // per CU or fewer); qs_wgrad_t's workgroups two to a CU, the weight-gradient
 // kernel's three.
-constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024, kSReserveG = 40 * 1024;
+constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024, kSReserveG = 0;
 
 #ifdef QS_TILE_STAMPS
 // dev builds only: s_memrealtime (100 MHz) at the tile's phase boundaries,
@@ -702,93 +703,62 @@ __host__ __device__ inline int s_cb(int I, int bt) { return (I + 16 * bt - 1) / 
 __host__ __device__ inline int s_nblk(int I, int bt) { return (16 / bt) * s_cb(I, bt) + (16 / bt) * (16 / bt); }
 __host__ __device__ inline int s_mp(int I) { return 32 * ((I + 31) / 32); }
 
-// c[0] += Σ over NQ quads of dZᵀ[n0 + j][rows]·Xᵀ[m0 + j][rows] (one 16×16 tile;
-// the even and odd quads on two accumulator chains, added at the end), R quads
-// of loads ahead; compile-time NQ
-template <int NQ>
-__device__ __forceinline__ void s_wgrad11_n(const float* a0, const float* b0, int g, f32x4& c0, f32x4& c1) {
-  constexpr int R = NQ < 8 ? NQ : 8;
-  float4 ra[R], rb[R];
-#pragma unroll
-  for (int t = 0; t < R; ++t) {
-    ra[t] = *reinterpret_cast<const float4*>(a0 + 16 * t + 4 * g);
-    rb[t] = *reinterpret_cast<const float4*>(b0 + 16 * t + 4 * g);
-  }
-#pragma unroll
-  for (int t = 0; t < NQ; ++t) {
-    const float4 x = ra[t % R], y = rb[t % R];
-    if (t + R < NQ) {
-      ra[t % R] = *reinterpret_cast<const float4*>(a0 + 16 * (t + R) + 4 * g);
-      rb[t % R] = *reinterpret_cast<const float4*>(b0 + 16 * (t + R) + 4 * g);
+// c[bi·BT + bj] += Σ over the nq quads (16 rows each) of
+// dZᵀ[16bi + j][rows]·Xᵀ[16bj + j][rows] for the BT×BT 16×16 MFMA tiles of a
+// block (rows of a0 / b0 at their first quad; row 16 further: a1 / b1).  A
+// ring of R quads of float4 operands runs continuously over the run-time quad
+// count (unrolled by R, the loads past the end clamped to the last quad and
+// their operands zeroed, so every load is unconditional and the wait counts
+// static); BT = 1 alternates two accumulator chains.
+template <int BT>
+__device__ __forceinline__ void s_wgrad_ring(const float* a0, const float* a1, const float* b0, const float* b1,
+                                             int nq, int g, f32x4 (&c)[BT * BT]) {
+  constexpr int R = BT == 1 ? 8 : 4;
+  constexpr int NO = 2 * BT;   // float4 operands per quad
+  if (nq <= 0) return;
+  float4 ring[R][NO];
+  auto ld = [&](int t, float4 (&o)[NO]) {
+    const int q = 16 * min(t, nq - 1) + 4 * g;
+    o[0] = *reinterpret_cast<const float4*>(a0 + q);
+    o[1] = *reinterpret_cast<const float4*>(b0 + q);
+    if constexpr (BT == 2) {
+      o[2] = *reinterpret_cast<const float4*>(a1 + q);
+      o[3] = *reinterpret_cast<const float4*>(b1 + q);
     }
-    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
-    f32x4& acc = (t & 1) ? c1 : c0;
-    acc = s_mfma(x.x, y.x, acc);
-    acc = s_mfma(x.y, y.y, acc);
-    acc = s_mfma(x.z, y.z, acc);
-    acc = s_mfma(x.w, y.w, acc);
-  }
-}
-__device__ __forceinline__ void s_wgrad11(const float* a0, const float* b0, int nq, int g, f32x4& c) {
+  };
+#pragma unroll
+  for (int k = 0; k < R; ++k) ld(k, ring[k]);
   f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
-  int t = 0;
-  for (; t + 16 <= nq; t += 16) s_wgrad11_n<16>(a0 + 16 * t, b0 + 16 * t, g, c, c1);
-  switch (nq - t) {
-#define S_CASE(n) case n: s_wgrad11_n<n>(a0 + 16 * t, b0 + 16 * t, g, c, c1); break;
-    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
-    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
-#undef S_CASE
-    default: break;
-  }
-  c += c1;
-}
-
-// c[bi][bj] += Σ over NQ quads of dZᵀ[n0 + 16bi + j][rows]·Xᵀ[m0 + 16bj + j][rows]
-// (a 2×2 grid of 16×16 MFMA tiles: four independent chains, four float4
-// operands per 16 MFMAs), R quads of loads ahead; compile-time NQ
-template <int NQ>
-__device__ __forceinline__ void s_wgrad22_n(const float* a0, const float* a1, const float* b0, const float* b1, int g,
-                                            f32x4 (&c)[4]) {
-  constexpr int R = NQ < 4 ? NQ : 4;
-  float4 ra0[R], ra1[R], rb0[R], rb1[R];
+  for (int t = 0; t < nq; t += R) {
 #pragma unroll
-  for (int t = 0; t < R; ++t) {
-    ra0[t] = *reinterpret_cast<const float4*>(a0 + 16 * t + 4 * g);
-    ra1[t] = *reinterpret_cast<const float4*>(a1 + 16 * t + 4 * g);
-    rb0[t] = *reinterpret_cast<const float4*>(b0 + 16 * t + 4 * g);
-    rb1[t] = *reinterpret_cast<const float4*>(b1 + 16 * t + 4 * g);
-  }
+    for (int k = 0; k < R; ++k) {
+      float4 o[NO];
 #pragma unroll
-  for (int t = 0; t < NQ; ++t) {
-    const float4 x0 = ra0[t % R], x1 = ra1[t % R], y0 = rb0[t % R], y1 = rb1[t % R];
-    if (t + R < NQ) {
-      ra0[t % R] = *reinterpret_cast<const float4*>(a0 + 16 * (t + R) + 4 * g);
-      ra1[t % R] = *reinterpret_cast<const float4*>(a1 + 16 * (t + R) + 4 * g);
-      rb0[t % R] = *reinterpret_cast<const float4*>(b0 + 16 * (t + R) + 4 * g);
-      rb1[t % R] = *reinterpret_cast<const float4*>(b1 + 16 * (t + R) + 4 * g);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
-#define S_Q4(E)                        \
-  c[0] = s_mfma(x0.E, y0.E, c[0]);     \
-  c[1] = s_mfma(x0.E, y1.E, c[1]);     \
-  c[2] = s_mfma(x1.E, y0.E, c[2]);     \
-  c[3] = s_mfma(x1.E, y1.E, c[3]);
-    S_Q4(x) S_Q4(y) S_Q4(z) S_Q4(w)
+      for (int u = 0; u < NO; ++u) o[u] = ring[k][u];
+      ld(t + k + R, ring[k]);
+      __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
+      if (t + k >= nq) {   // past the end: a zero contribution (uniform)
+#pragma unroll
+        for (int u = 0; u < NO; u += 2) o[u] = float4{0.f, 0.f, 0.f, 0.f};
+      }
+      if constexpr (BT == 1) {
+        f32x4& acc = (k & 1) ? c1 : c[0];
+        acc = s_mfma(o[0].x, o[1].x, acc);
+        acc = s_mfma(o[0].y, o[1].y, acc);
+        acc = s_mfma(o[0].z, o[1].z, acc);
+        acc = s_mfma(o[0].w, o[1].w, acc);
+      } else {
+#define S_Q4(E)                           \
+  c[0] = s_mfma(o[0].E, o[1].E, c[0]);    \
+  c[1] = s_mfma(o[0].E, o[3].E, c[1]);    \
+  c[2] = s_mfma(o[2].E, o[1].E, c[2]);    \
+  c[3] = s_mfma(o[2].E, o[3].E, c[3]);
+        S_Q4(x) S_Q4(y) S_Q4(z) S_Q4(w)
 #undef S_Q4
+      }
+    }
   }
-}
-// any nq: whole blocks of 16 quads, then the remainder by dispatch
-__device__ __forceinline__ void s_wgrad22(const float* a0, const float* a1, const float* b0, const float* b1, int nq,
-                                          int g, f32x4 (&c)[4]) {
-  int t = 0;
-  for (; t + 16 <= nq; t += 16) s_wgrad22_n<16>(a0 + 16 * t, a1 + 16 * t, b0 + 16 * t, b1 + 16 * t, g, c);
-  switch (nq - t) {
-#define S_CASE(n) case n: s_wgrad22_n<n>(a0 + 16 * t, a1 + 16 * t, b0 + 16 * t, b1 + 16 * t, g, c); break;
-    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
-    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15)
-#undef S_CASE
-    default: break;
-  }
+  if constexpr (BT == 1) c[0] += c1;
 }
 
 // One 16·BT-square block of a weight matrix and K-chunk s of S (launch 2):
@@ -810,19 +780,16 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
   const int n0 = 16 * BT * (uu / ncb), m0 = 16 * BT * (uu % ncb);
   const int M = l1 ? N.I : kSH;
   const bool act = !adam || !actor || open_a;
-  int en[NT], em[NT];
-  float pp[NT], pm[NT], pv[NT];
-#pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const int f = NT * w + k, q = f >> 2, r = f & 3;
-    en[k] = n0 + 16 * (q / BT) + 4 * g + r;
-    em[k] = m0 + 16 * (q % BT) + j;
-    if (direct && adam && act && em[k] < M) {   // Adam's operands, in flight during the gradient
-      const long long i = (l1 ? N.w1 : N.w2) + (long long)en[k] * M + em[k];
-      pp[k] = N.p[i];
-      pm[k] = N.m[i];
-      pv[k] = N.v[i];
-    }
+  // the sink: wave w < 4·NT takes register f = w of every lane (tile f/4, register f%4)
+  const bool fin_w = w < 4 * NT;
+  const int f = w, q = f >> 2, r = f & 3;
+  const int en = n0 + 16 * (q / BT) + 4 * g + r, em = m0 + 16 * (q % BT) + j;
+  const long long ei = (l1 ? N.w1 : N.w2) + (long long)en * M + em;
+  float pp = 0.f, pm = 0.f, pv = 0.f;
+  if (fin_w && direct && adam && act && em < M) {   // Adam's operands, in flight during the gradient
+    pp = N.p[ei];
+    pm = N.m[ei];
+    pv = N.v[ei];
   }
   const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
   const float* dzT = actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT);
@@ -833,37 +800,28 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
   const int wa = min(q1, q0 + w * qw), wb = min(q1, wa + qw);
   f32x4 c[NT];
 #pragma unroll
-  for (int q = 0; q < NT; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NT; ++t) c[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   // (columns past M are not stored: clamped, their sums discarded)
-  if constexpr (BT == 1) {
-    s_wgrad11(dzT + (size_t)(n0 + j) * KS + 16 * wa, xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, wb - wa, g, c[0]);
-  } else {
-    s_wgrad22(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
-              xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
-              wb - wa, g, c);
-  }
+  s_wgrad_ring<BT>(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
+                   xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
+                   wb - wa, g, c);
 #pragma unroll
-  for (int q = 0; q < NT; ++q)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[w][4 * q + r][l] = c[q][r];
+    for (int k = 0; k < 4; ++k) red[w][4 * t + k][l] = c[t][k];
   __syncthreads();
+  if (!fin_w) return;
+  float tot = red[0][f][l];
 #pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const int f = NT * w + k;
-    float t = red[0][f][l];
-#pragma unroll
-    for (int v = 1; v < kSGW; ++v) t += red[v][f][l];
-    if (!direct) {
-      float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
-      const int Mp = l1 ? s_mp(N.I) : kSH;
-      part[((size_t)s * kSH + en[k]) * Mp + em[k]] = t;   // (pad columns too)
-    } else if (act && em[k] < M) {
-      const int si = actor ? 0 : 1;
-      const long long i = (l1 ? N.w1 : N.w2) + (long long)en[k] * M + em[k];
-      if (!adam) P.G.g[si][i] = t;
-      else s_adam(N, i, t, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr, pp[k],
-                  pm[k], pv[k]);
-    }
+  for (int v = 1; v < kSGW; ++v) tot += red[v][f][l];
+  if (!direct) {
+    float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
+    const int Mp = l1 ? s_mp(N.I) : kSH;
+    part[((size_t)s * kSH + en) * Mp + em] = tot;   // (pad columns too)
+  } else if (act && em < M) {
+    const int si = actor ? 0 : 1;
+    if (!adam) P.G.g[si][ei] = tot;
+    else s_adam(N, ei, tot, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en, em, l1 ? N.w1p : nullptr, pp, pm, pv);
   }
 }
 
@@ -1067,8 +1025,13 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   L.KcP = 16 * L.nC;
   // row strides off a power of two: rows 16 KB apart all mapped to one memory
   // channel (the critic's weight gradients ran 10x slower at 4 096 rows)
-  L.KaS = L.KaP ? L.KaP + kSPad : 0;
-  L.KcS = L.KcP + kSPad;
+  static const int pad = [] {   // dev probe: QS_SMALL_PAD overrides the pad (floats, a multiple of 4)
+    const char* e = getenv("QS_SMALL_PAD");
+    const int v = e ? atoi(e) : kSPad;
+    return v >= 0 && v % 4 == 0 ? v : kSPad;
+  }();
+  L.KaS = L.KaP ? L.KaP + pad : 0;
+  L.KcS = L.KcP + pad;
   L.Sa = Ia > 0 ? s_chunks(L.KaP) : 0;
   L.Sc = s_chunks(L.KcP);
   L.bta = s_bt(L.KaP);
