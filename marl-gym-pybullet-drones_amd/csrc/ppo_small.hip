@@ -71,7 +71,8 @@ constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
 constexpr int kSGW = 16;               // waves per weight-gradient workgroup (one weight block and K-chunk)
 constexpr int kSBT1Q = 128;            // quads (16 rows) from which a net's weight gradients take 16×16 blocks
-constexpr int kSGQ = 512;              // quads per K-chunk of 16×16 blocks (longer columns: chunk partials + launch 3)
+constexpr int kSGQW = 16;              // most quads per wave of the weight-gradient kernel (compile-time counts)
+constexpr int kSGQ = kSGQW * 16;       // quads per K-chunk (longer columns: chunk partials + launch 3)
 constexpr int kSMaxS = 32;             // most K-chunks per net
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
 // Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
@@ -703,22 +704,21 @@ __host__ __device__ inline int s_cb(int I, int bt) { return (I + 16 * bt - 1) / 
 __host__ __device__ inline int s_nblk(int I, int bt) { return (16 / bt) * s_cb(I, bt) + (16 / bt) * (16 / bt); }
 __host__ __device__ inline int s_mp(int I) { return 32 * ((I + 31) / 32); }
 
-// c[bi·BT + bj] += Σ over the nq quads (16 rows each) of
+// c[bi·BT + bj] += Σ over NQ quads (16 rows each) of
 // dZᵀ[16bi + j][rows]·Xᵀ[16bj + j][rows] for the BT×BT 16×16 MFMA tiles of a
-// block (rows of a0 / b0 at their first quad; row 16 further: a1 / b1).  A
-// ring of R quads of float4 operands runs continuously over the run-time quad
-// count (unrolled by R, the loads past the end clamped to the last quad and
-// their operands zeroed, so every load is unconditional and the wait counts
-// static); BT = 1 alternates two accumulator chains.
-template <int BT>
-__device__ __forceinline__ void s_wgrad_ring(const float* a0, const float* a1, const float* b0, const float* b1,
-                                             int nq, int g, f32x4 (&c)[BT * BT]) {
-  constexpr int R = BT == 1 ? 8 : 4;
+// block (rows of a0 / b0 at their first quad; row 16 further: a1 / b1).  NQ is
+// a compile-time count (a run-time bound made the compiler wait for every
+// outstanding load at the loop's back edge): the loop unrolls fully, R quads of
+// float4 operands in flight; BT = 1 alternates two accumulator chains.
+template <int BT, int NQ>
+__device__ __forceinline__ void s_wgrad_n(const float* a0, const float* a1, const float* b0, const float* b1, int g,
+                                          f32x4 (&c)[BT * BT]) {
+  constexpr int RM = BT == 1 ? 8 : 4;
+  constexpr int R = NQ < RM ? NQ : RM;
   constexpr int NO = 2 * BT;   // float4 operands per quad
-  if (nq <= 0) return;
   float4 ring[R][NO];
   auto ld = [&](int t, float4 (&o)[NO]) {
-    const int q = 16 * min(t, nq - 1) + 4 * g;
+    const int q = 16 * t + 4 * g;
     o[0] = *reinterpret_cast<const float4*>(a0 + q);
     o[1] = *reinterpret_cast<const float4*>(b0 + q);
     if constexpr (BT == 2) {
@@ -729,36 +729,42 @@ __device__ __forceinline__ void s_wgrad_ring(const float* a0, const float* a1, c
 #pragma unroll
   for (int k = 0; k < R; ++k) ld(k, ring[k]);
   f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < nq; t += R) {
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      float4 o[NO];
+  for (int t = 0; t < NQ; ++t) {
+    float4 o[NO];
 #pragma unroll
-      for (int u = 0; u < NO; ++u) o[u] = ring[k][u];
-      ld(t + k + R, ring[k]);
-      __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
-      if (t + k >= nq) {   // past the end: a zero contribution (uniform)
-#pragma unroll
-        for (int u = 0; u < NO; u += 2) o[u] = float4{0.f, 0.f, 0.f, 0.f};
-      }
-      if constexpr (BT == 1) {
-        f32x4& acc = (k & 1) ? c1 : c[0];
-        acc = s_mfma(o[0].x, o[1].x, acc);
-        acc = s_mfma(o[0].y, o[1].y, acc);
-        acc = s_mfma(o[0].z, o[1].z, acc);
-        acc = s_mfma(o[0].w, o[1].w, acc);
-      } else {
+    for (int u = 0; u < NO; ++u) o[u] = ring[t % R][u];
+    if (t + R < NQ) ld(t + R, ring[t % R]);
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
+    if constexpr (BT == 1) {
+      f32x4& acc = (t & 1) ? c1 : c[0];
+      acc = s_mfma(o[0].x, o[1].x, acc);
+      acc = s_mfma(o[0].y, o[1].y, acc);
+      acc = s_mfma(o[0].z, o[1].z, acc);
+      acc = s_mfma(o[0].w, o[1].w, acc);
+    } else {
 #define S_Q4(E)                           \
   c[0] = s_mfma(o[0].E, o[1].E, c[0]);    \
   c[1] = s_mfma(o[0].E, o[3].E, c[1]);    \
   c[2] = s_mfma(o[2].E, o[1].E, c[2]);    \
   c[3] = s_mfma(o[2].E, o[3].E, c[3]);
-        S_Q4(x) S_Q4(y) S_Q4(z) S_Q4(w)
+      S_Q4(x) S_Q4(y) S_Q4(z) S_Q4(w)
 #undef S_Q4
-      }
     }
   }
   if constexpr (BT == 1) c[0] += c1;
+}
+// nq (0 .. kSGQW) quads by dispatch to the compile-time count
+template <int BT>
+__device__ __forceinline__ void s_wgrad_q(const float* a0, const float* a1, const float* b0, const float* b1, int nq,
+                                          int g, f32x4 (&c)[BT * BT]) {
+  switch (nq) {
+#define S_CASE(n) case n: s_wgrad_n<BT, n>(a0, a1, b0, b1, g, c); break;
+    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
+    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15) S_CASE(16)
+#undef S_CASE
+    default: break;
+  }
 }
 
 // One 16·BT-square block of a weight matrix and K-chunk s of S (launch 2):
@@ -802,9 +808,9 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
 #pragma unroll
   for (int t = 0; t < NT; ++t) c[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   // (columns past M are not stored: clamped, their sums discarded)
-  s_wgrad_ring<BT>(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
-                   xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
-                   wb - wa, g, c);
+  s_wgrad_q<BT>(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
+                xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
+                wb - wa, g, c);
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -1011,7 +1017,6 @@ struct SLayout {
 inline int s_bt(long long KP) { return KP / 16 >= kSBT1Q ? 1 : 2; }
 inline int s_chunks(long long KP) {
   const long long q = KP / 16;
-  if (s_bt(KP) != 1) return 1;
   const long long S = (q + kSGQ - 1) / kSGQ;
   return (int)(S < 1 ? 1 : (S > kSMaxS ? kSMaxS : S));
 }
