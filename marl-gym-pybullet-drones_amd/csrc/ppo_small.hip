@@ -69,9 +69,9 @@ constexpr int kSMaxI = 640;            // widest input (Spiral's centralized cri
 constexpr int kSNarrowI = 256;         // the forward/backward instance for inputs up to this width (smaller LDS X tile)
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
-constexpr int kSGW = 16;               // waves per weight-gradient workgroup (one weight block and K-chunk)
+constexpr int kSGW = 8;                // waves per weight-gradient workgroup (one weight block and K-chunk; two a CU)
 constexpr int kSBT1Q = 128;            // quads (16 rows) from which a net's weight gradients take 16×16 blocks
-constexpr int kSGQW = 16;              // most quads per wave of the weight-gradient kernel (compile-time counts)
+constexpr int kSGQW = 32;              // most quads per wave of the weight-gradient kernel (compile-time runs of <= 16)
 constexpr int kSGQ = kSGQW * 16;       // quads per K-chunk (longer columns: chunk partials + launch 3)
 constexpr int kSMaxS = 32;             // most K-chunks per net
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
@@ -91,8 +91,16 @@ __device__ unsigned long long g_tile_stamps[kStampWG * 8];
   do {                                                                                                          \
     if (threadIdx.x == 0 && blockIdx.x < kStampWG) g_tile_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+__device__ unsigned long long g_wg_stamps[kStampWG * 4];
+#define W_STAMP(k)                                                                                          \
+  do {                                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < kStampWG) g_wg_stamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define S_STAMP(k) \
+  do {             \
+  } while (0)
+#define W_STAMP(k) \
   do {             \
   } while (0)
 #endif
@@ -141,6 +149,8 @@ struct SArgs {
   const double* ret;       // [T·E]
   float scale, clip, ent_coef, kl_thr;
   int gate;
+  int fb_tail;             // 1: the forward/backward launch's last tile of each net sums the loss rows
+                           // (qs_ppo_critic_tiles); 0: launch 2 does (no release fence per tile)
   float* kl_out;
   double* acc;
   SNet a, c;
@@ -570,10 +580,15 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
       for (int q = 0; q < 16; ++q) sacc += ls_w[q][k];
       lp[k] = sacc;
     }
-    __threadfence();
-    const int ntiles = POL ? P.nA : P.nC;
-    last = atomicAdd(W.cnt + (POL ? 0 : 64), 1u) == (unsigned)ntiles - 1;
+    if (P.fb_tail) {
+      // (an agent-scope release per tile: hundreds of tiles' L2 write-backs
+      // serialise — 9 µs a tile at 288 tiles — so launch 2 sums the rows instead)
+      __threadfence();
+      const int ntiles = POL ? P.nA : P.nC;
+      last = atomicAdd(W.cnt + (POL ? 0 : 64), 1u) == (unsigned)ntiles - 1;
+    }
   }
+  if (!P.fb_tail) return;
   __syncthreads();
   S_STAMP(6);
   if (!last || w != 0) return;
@@ -642,6 +657,30 @@ __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, floa
   N.p[i] = p1;
   if (w2t) w2t[(size_t)k * kSH + n] = p1;
   if (w1p) w1p[(size_t)n * s_ip(N.I) + k] = p1;
+}
+
+// Σ over a net's tile loss rows (rows [nt][NL], NL <= 2 + kSMaxA) in a fixed
+// order, by one whole wave: lane q takes tiles q, q + 64, ... in order, then an
+// xor butterfly (every lane ends with the same bits: each level adds the same
+// two operands) — the fb tiles' tail arithmetic, so every workgroup that needs
+// the totals forms identical ones
+__device__ __forceinline__ void s_loss_tot(const double* rows, int nt, int NL, int l, double (&tot)[2 + kSMaxA]) {
+#pragma unroll
+  for (int k = 0; k < 2 + kSMaxA; ++k) tot[k] = 0.0;
+  for (int t = l; t < nt; t += 64)
+#pragma unroll
+    for (int k = 0; k < 2 + kSMaxA; ++k)
+      if (k < NL) tot[k] += rows[(size_t)t * NL + k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 2 + kSMaxA; ++k) tot[k] += __shfl_xor(tot[k], o, 64);
+}
+// The actor's KL gate from the tile loss rows (approx_kl = Σ / K, float32 as the fb tail writes it)
+__device__ __forceinline__ bool s_gate_rows(const SArgs& P, int l, double (&tot)[2 + kSMaxA]) {
+  s_loss_tot(P.w.lossa, P.nA, 2 + P.a.A, l, tot);
+  const float akl = (float)(tot[1] / (double)(P.mb * P.D));
+  return !P.gate || akl <= P.kl_thr;
 }
 
 // Adam's bias corrections of both nets from their step counts (float32 of the
@@ -754,10 +793,11 @@ __device__ __forceinline__ void s_wgrad_n(const float* a0, const float* a1, cons
   }
   if constexpr (BT == 1) c[0] += c1;
 }
-// nq (0 .. kSGQW) quads by dispatch to the compile-time count
+// nq (0 .. kSGQW) quads: runs of 16, then the remainder, by dispatch to the compile-time count
 template <int BT>
 __device__ __forceinline__ void s_wgrad_q(const float* a0, const float* a1, const float* b0, const float* b1, int nq,
                                           int g, f32x4 (&c)[BT * BT]) {
+  for (; nq > 16; nq -= 16, a0 += 256, a1 += 256, b0 += 256, b1 += 256) s_wgrad_n<BT, 16>(a0, a1, b0, b1, g, c);
   switch (nq) {
 #define S_CASE(n) case n: s_wgrad_n<BT, n>(a0, a1, b0, b1, g, c); break;
     S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
@@ -774,25 +814,36 @@ __device__ __forceinline__ void s_wgrad_q(const float* a0, const float* a1, cons
 // f%4).  S = 1: into the final sink (Adam with its p / m / v loaded ahead, or
 // the gradient buffer); otherwise the chunk partials of launch 3.
 template <int BT>
-__device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int s, int u, bool adam, bool open_a,
-                                         float (*red)[16][64], const float (*sc)[2]) {
+__device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int s, int u, bool adam,
+                                         float (*red)[16][64], const float (*sc)[2], bool* sopen) {
   constexpr int NT = BT * BT;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const SNet& N = actor ? P.a : P.c;
   const bool direct = S == 1;
+  // logical block u: W2's G×G grid first, in eight (G/4)×(G/2) sub-grids of
+  // consecutive blocks (one XCD's share after s_xcd_swz: a quarter of dZ2ᵀ's
+  // rows and half of H1ᵀ's stay in that XCD's L2), then W1's blocks
+  constexpr int G = 16 / BT, GT = G * G / 8;
   const int cb = s_cb(N.I, BT);
-  const bool l1 = u < (16 / BT) * cb;
-  const int uu = l1 ? u : u - (16 / BT) * cb, ncb = l1 ? cb : 16 / BT;
-  const int n0 = 16 * BT * (uu / ncb), m0 = 16 * BT * (uu % ncb);
+  const bool l1 = u >= G * G;
+  int n0, m0;
+  if (!l1) {
+    const int tile = u / GT, v = u - tile * GT;
+    n0 = 16 * BT * ((G / 4) * (tile >> 1) + v / (G / 2));
+    m0 = 16 * BT * ((G / 2) * (tile & 1) + v % (G / 2));
+  } else {
+    const int uu = u - G * G;
+    n0 = 16 * BT * (uu / cb);
+    m0 = 16 * BT * (uu % cb);
+  }
   const int M = l1 ? N.I : kSH;
-  const bool act = !adam || !actor || open_a;
   // the sink: wave w < 4·NT takes register f = w of every lane (tile f/4, register f%4)
   const bool fin_w = w < 4 * NT;
   const int f = w, q = f >> 2, r = f & 3;
   const int en = n0 + 16 * (q / BT) + 4 * g + r, em = m0 + 16 * (q % BT) + j;
   const long long ei = (l1 ? N.w1 : N.w2) + (long long)en * M + em;
   float pp = 0.f, pm = 0.f, pv = 0.f;
-  if (fin_w && direct && adam && act && em < M) {   // Adam's operands, in flight during the gradient
+  if (fin_w && direct && adam && em < M) {   // Adam's operands, in flight during the gradient
     pp = N.p[ei];
     pm = N.m[ei];
     pv = N.v[ei];
@@ -811,12 +862,20 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
   s_wgrad_q<BT>(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
                 xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
                 wb - wa, g, c);
+  W_STAMP(1);
+  if (w == 0 && direct && adam && actor) {   // the actor's KL gate (AG:731-734), before the sums are read
+    double tot[2 + kSMaxA];
+    const bool o = s_gate_rows(P, l, tot);
+    if (l == 0) *sopen = o;
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[w][4 * t + k][l] = c[t][k];
   __syncthreads();
+  W_STAMP(2);
   if (!fin_w) return;
+  const bool act = !(direct && adam && actor) || *sopen;
   float tot = red[0][f][l];
 #pragma unroll
   for (int v = 1; v < kSGW; ++v) tot += red[v][f][l];
@@ -831,6 +890,16 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
   }
 }
 
+// Workgroup T of n consecutive ones (the dispatcher deals them to the 8 XCDs
+// round-robin, T mod 8) → logical index: each XCD's workgroups take one
+// contiguous range of logical indices (neighbouring blocks share operand rows
+// in that XCD's L2); the last n mod 8 unchanged
+__device__ __forceinline__ int s_xcd_swz(int T, int n) {
+  const int per = n >> 3;
+  if (per == 0 || T >= 8 * per) return T;
+  return (T & 7) * per + (T >> 3);
+}
+
 // Launch 2.  Workgroups [0, Σ blocks·S): one weight block and K-chunk each
 // (s_wblock; the actor's first, the chunks of a block adjacent; 16×16 blocks
 // for a net with long columns (P.G.bt = 1: enough blocks to fill the CUs),
@@ -838,24 +907,29 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
 // parameters, 16 lanes per element (lane k sums the tile partial rows
 // t ≡ k mod 16 in order, a fixed DPP butterfly adds the lanes), into P.G.sink.
 // With Adam and no launch 3 the last workgroup commits the step counts.
-__global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P, int fin) {
+__global__ void __launch_bounds__(64 * kSGW) __attribute__((amdgpu_waves_per_eu(4)))
+ppo_small_wgrad_kernel(SArgs P, int fin) {
+  // (4 waves a SIMD: two 8-wave workgroups a CU, the grid in one round)
   __shared__ float red[kSGW][16][64];
   __shared__ float sc[2][2];
-  __shared__ bool last;
-  const int tid = threadIdx.x;
+  __shared__ bool last, sopen;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   s_adam_scalars(P, sc, tid);
   const bool adam = P.G.sink == SINK_ADAM;
-  const bool open_a = !adam || s_gate_open(P);
   const int nwa = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0], nwc = s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1];
   const int blk = blockIdx.x;
   __syncthreads();   // (sc)
+  W_STAMP(0);
   if (blk < nwa + nwc) {
     const bool actor = blk < nwa;
     const int S = P.G.S[actor ? 0 : 1];
-    const int T = actor ? blk : blk - nwa;
-    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, T % S, T / S, adam, open_a, red, sc);
-    else s_wblock<2>(P, actor, S, T % S, T / S, adam, open_a, red, sc);
+    const int T = s_xcd_swz(actor ? blk : blk - nwa, actor ? nwa : nwc);
+    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, T % S, T / S, adam, red, sc, &sopen);
+    else s_wblock<2>(P, actor, S, T % S, T / S, adam, red, sc, &sopen);
   } else {
+    // the actor's loss totals (every wave: the gate, logstd's gradient)
+    double tot[2 + kSMaxA];
+    const bool open_a = s_gate_rows(P, l, tot);
     const int e = ((blk - nwa - nwc) * (int)blockDim.x + tid) >> 4, k = tid & 15;
     bool actor;
     long long i;
@@ -865,7 +939,7 @@ __global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P, int
       const SNet& N = actor ? P.a : P.c;
       const bool doit = !adam || !actor || open_a;
       float p0 = 0.f, m0 = 0.f, v0 = 0.f;
-      if (doit && adam && k == 0) {
+      if (adam && k == 0) {
         p0 = N.p[i];
         m0 = N.m[i];
         v0 = N.v[i];
@@ -883,8 +957,8 @@ __global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P, int
         }
         for (; tt < nt; tt += 16) acc += col[(size_t)tt * cstride];
         gsum = s_row_sum(acc);
-      } else {
-        gsum = P.w.dlogstd[u];
+      } else {   // logstd: d(policy)/d logstd from the loss rows − ent_coef (AG:602-640)
+        gsum = (float)tot[2 + u] - P.ent_coef;
       }
       if (doit && k == 0) {
         if (!adam) {
@@ -895,12 +969,40 @@ __global__ void __launch_bounds__(64 * kSGW) ppo_small_wgrad_kernel(SArgs P, int
         }
       }
     }
+    if (blk == nwa + nwc && w == 0) {
+      // the minibatch's loss statistics (the fb tail of ppo_heads_kernel's arithmetic):
+      // approx_kl (the gate's value; the multi-rank exchange averages it), dlogstd, acc
+      double totc[2 + kSMaxA];
+      s_loss_tot(P.w.lossc, P.nC, 1, l, totc);
+      if (l == 0) {
+        const int A = P.a.A;
+        const double K = (double)(P.mb * P.D);
+        const float lc = (float)log(sqrt(2.0 * M_PI));
+        float ent = 0.0f;
+        for (int a = 0; a < A; ++a) {
+          const float lsd = logf(expf(P.a.p[P.a.logstd + a]));
+          ent = a == 0 ? (0.5f + lc) + lsd : ent + ((0.5f + lc) + lsd);
+          P.w.dlogstd[a] = (float)tot[2 + a] - P.ent_coef;
+        }
+        const float akl = (float)(tot[1] / K);
+        *P.kl_out = akl;
+        P.acc[0] += tot[0] / K;
+        P.acc[1] += 0.5 * (totc[0] / (double)P.mb);
+        P.acc[2] += (double)(-ent);
+        P.acc[3] += (double)akl;
+      }
+    }
   }
+  W_STAMP(3);
   if (!fin || !adam) return;
   __syncthreads();
   if (tid == 0) last = atomicAdd(P.w.cnt + 128, 1u) == gridDim.x - 1;
   __syncthreads();
-  if (last && tid == 0) {   // every workgroup read the step counts before arriving
+  if (!last || w != 0) return;
+  // every workgroup read the step counts before arriving
+  double tot[2 + kSMaxA];
+  const bool open_a = s_gate_rows(P, l, tot);
+  if (l == 0) {
     P.w.cnt[128] = 0u;
     if (open_a) *P.a.step = *P.a.step + 1.0f;
     *P.c.step = *P.c.step + 1.0f;
@@ -1149,6 +1251,7 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   P.gate = gate;
   P.kl_out = kl_out;
   P.acc = acc;
+  P.fb_tail = 0;
   s_bind(P, actor, critic, L, work);
   return QS_OK;
 }
@@ -1322,6 +1425,7 @@ int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* 
   P.w.lossc = (double*)(wb + L.off[14]);
   P.w.cnt = (unsigned*)(wb + L.off[15]);
   P.nA = 0;   // critic tiles only
+  P.fb_tail = 1;   // (the last tile adds the value loss to acc[1])
   P.KaP = P.KaS = 0;
   P.KcS = L.KcS;
   s_launch_fb(P, L.nC, (hipStream_t)stream);
@@ -1330,6 +1434,12 @@ int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* 
 }
 
 #ifdef QS_TILE_STAMPS
+int qs_dev_wgrad_stamps(unsigned long long* host, int64_t n) {
+  if (n > (int64_t)kStampWG * 4) n = (int64_t)kStampWG * 4;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? QS_OK
+             : QS_E_HIP;
+}
 int qs_dev_tile_stamps(unsigned long long* host, int64_t n) {
   if (n > (int64_t)kStampWG * 8) n = (int64_t)kStampWG * 8;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tile_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess

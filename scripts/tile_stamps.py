@@ -38,6 +38,16 @@ def dump(label, nwg):
 
 def main():
     torch.cuda.init()
+    if len(sys.argv) > 1:   # per-rank shapes (scripts/learner_mb.py RANK_SHAPES) on the tile path
+        from gym_pybullet_drones_amd.mappo import agent as agent_mod
+        agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
+        for shape in sys.argv[1:]:
+            learner_mb.per_minibatch_us(shape, reps=1, small=True)
+            torch.cuda.synchronize()
+            D, O, A, mb, T, E = learner_mb.SHAPES[shape]
+            nA, nC = (mb * D + 15) // 16, (mb + 15) // 16
+            dump(f"{shape} tile path (actor tiles {nA}, critic tiles {nC})", nA + nC)
+        return
     for name, shape in (("ref small step", "ref"),):
         learner_mb.per_minibatch_us(shape, reps=1, small=True)
         torch.cuda.synchronize()

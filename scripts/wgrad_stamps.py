@@ -1,0 +1,60 @@
+"""Dev: per-workgroup phase timestamps of the tile path's weight-gradient launch
+(ppo_small_wgrad_kernel) from the QS_TILE_STAMPS dev build (s_memrealtime, 100 MHz,
+thread 0): 0 entry (after the Adam scalars), 1 wave 0's contraction done,
+2 the waves' sums reduced, 3 done (sink written).
+  bash scripts/build_dev_step.sh tstamps -DQS_TILE_STAMPS
+  QS_DEV_LIB=marl-gym-pybullet-drones_amd/build/dev/lib_tstamps.so python scripts/wgrad_stamps.py C3/8 ..."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "marl-gym-pybullet-drones_amd"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gym_pybullet_drones_amd import _lib as L  # noqa: E402
+from gym_pybullet_drones_amd.mappo import agent as agent_mod  # noqa: E402
+import learner_mb  # noqa: E402
+
+
+def nblk(I, bt):
+    return (16 // bt) * ((I + 16 * bt - 1) // (16 * bt)) + (16 // bt) ** 2
+
+
+def main():
+    torch.cuda.init()
+    agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
+    for shape in sys.argv[1:] or ["C3/8"]:
+        learner_mb.per_minibatch_us(shape, reps=1, small=True)
+        torch.cuda.synchronize()
+        D, O, A, mb, T, E = learner_mb.SHAPES[shape]
+        Ka, Kc = mb * D, mb
+        bt = lambda K: 1 if (K + 15) // 16 >= 128 else 2
+        S = lambda K: max(1, ((K + 15) // 16 + 255) // 256)   # kSGQ = 8 waves x 32 quads
+        na, nc = nblk(O, bt(Ka)) * S(Ka), nblk(D * O, bt(Kc)) * S(Kc)
+        nvec = (2 * 256 + A * 256 + 2 * A) + (3 * 256 + 1)
+        nv = (16 * nvec + 511) // 512   # kSGW = 8 waves
+        n = na + nc + nv
+        buf = (ctypes.c_ulonglong * (n * 4))()
+        f = L.load().qs_dev_wgrad_stamps
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        assert f(buf, n * 4) == 0
+        s = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.int64)
+        t0 = s[:, 0].min()
+        rel = (s - t0) * 0.01
+        print(f"== {shape}: actor blocks {na} (bt {bt(Ka)}, S {S(Ka)}), critic blocks {nc} (bt {bt(Kc)}), vector WGs {nv}")
+        for name, sl in (("actor", slice(0, na)), ("critic", slice(na, na + nc)), ("vector", slice(na + nc, n))):
+            r = rel[sl]
+            line = f"  {name:6s} entry {np.median(r[:, 0]):6.2f} (max {r[:, 0].max():6.2f})"
+            if name != "vector":
+                line += (f"  contraction {np.median(r[:, 1] - r[:, 0]):6.2f} (max {(r[:, 1] - r[:, 0]).max():6.2f})"
+                         f"  reduce {np.median(r[:, 2] - r[:, 1]):6.2f}  sink {np.median(r[:, 3] - r[:, 2]):6.2f}")
+            line += f"  end {np.median(r[:, 3]):6.2f} (max {r[:, 3].max():6.2f}) us"
+            print(line)
+        ent = np.sort(rel[:, 0])
+        print("  entry quantiles (us):", [round(float(ent[int(q * (n - 1))]), 2) for q in (0, 0.25, 0.5, 0.6, 0.75, 0.9, 1)])
+
+
+if __name__ == "__main__":
+    main()
