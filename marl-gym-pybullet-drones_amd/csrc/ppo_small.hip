@@ -70,6 +70,7 @@ constexpr int kSNarrowI = 256;         // the forward/backward instance for inpu
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
 constexpr int kSGW = 8;                // waves per weight-gradient workgroup (one weight block and K-chunk; two a CU)
+constexpr int kSCUs = 256;              // MI355X compute units (one forward/backward tile each)
 constexpr int kSBT1Q = 128;            // quads (16 rows) from which a net's weight gradients take 16×16 blocks
 constexpr int kSGQW = 32;              // most quads per wave of the weight-gradient kernel (compile-time runs of <= 16)
 constexpr int kSGQ = kSGQW * 16;       // quads per K-chunk (longer columns: chunk partials + launch 3)
@@ -140,6 +141,7 @@ struct SGrad {
 
 struct SArgs {
   int mb, D, nA, nC, KaP, KcP;
+  int rb;                  // 16-row blocks per forward/backward tile
   int KaS, KcS;            // row strides of the transposed activations (KaP / KcP + kSPad)
   const float* X;          // the rollout's obs table [T·E·D][O] (critic rows: [T·E][D·O])
   const long long* idx;    // the minibatch's env-timesteps [mb]
@@ -224,23 +226,39 @@ __device__ __forceinline__ void s_prefill(float4 (&ra)[kSRing], const float* wro
 #pragma unroll
   for (int t = 0; t < (NQ < kSRing ? NQ : kSRing); ++t) ra[t] = s_ldq<VEC>(wrow, t, I, g);
 }
-template <int NQ, bool VEC>
-__device__ __forceinline__ void s_run(float4 (&ra)[kSRing], const float* wrow, int I, const float* brow, int g,
-                                      f32x4& c) {
+// RB row blocks of 16 share each weight quad: z[rb] += its contraction with
+// the activation row brow + rb·bs (LDS).  RB = 1: the even and odd quads on two
+// accumulator chains; RB > 1: the row blocks are the independent chains.
+template <int NQ, bool VEC, int RB>
+__device__ __forceinline__ void s_run(float4 (&ra)[kSRing], const float* wrow, int I, const float* brow, int bs, int g,
+                                      f32x4 (&z)[RB]) {
   f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NQ; ++t) {
     const float4 a = ra[t % kSRing];
     if (t + kSRing < NQ) ra[t % kSRing] = s_ldq<VEC>(wrow, t + kSRing, I, g);
-    const float4 bv = *reinterpret_cast<const float4*>(brow + 16 * t + 4 * g);
+    float4 bv[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) bv[rb] = *reinterpret_cast<const float4*>(brow + rb * bs + 16 * t + 4 * g);
     __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the loads next to their use
-    f32x4& acc = (t & 1) ? c1 : c;
-    acc = s_mfma(a.x, bv.x, acc);
-    acc = s_mfma(a.y, bv.y, acc);
-    acc = s_mfma(a.z, bv.z, acc);
-    acc = s_mfma(a.w, bv.w, acc);
+    if constexpr (RB == 1) {
+      f32x4& acc = (t & 1) ? c1 : z[0];
+      acc = s_mfma(a.x, bv[0].x, acc);
+      acc = s_mfma(a.y, bv[0].y, acc);
+      acc = s_mfma(a.z, bv[0].z, acc);
+      acc = s_mfma(a.w, bv[0].w, acc);
+    } else {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) z[rb] = s_mfma(a.x, bv[rb].x, z[rb]);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) z[rb] = s_mfma(a.y, bv[rb].y, z[rb]);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) z[rb] = s_mfma(a.z, bv[rb].z, z[rb]);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) z[rb] = s_mfma(a.w, bv[rb].w, z[rb]);
+    }
   }
-  c += c1;
+  if constexpr (RB == 1) z[0] += c1;
 }
 // layer 1 over nq = ⌈I/16⌉ quads (1..16): the compile-time count by dispatch
 #define S_NQ_SWITCH(nq, CALL)                                                                       \
@@ -256,30 +274,30 @@ __device__ __forceinline__ void s_run(float4 (&ra)[kSRing], const float* wrow, i
 // phases ahead (s_prefill<min(nq, 16)>); up to 16 quads by one compile-time run,
 // wider inputs (WIDE: up to kSMaxI) in 16-quad blocks that refill the ring at
 // their start, then the remainder
-template <bool VEC, bool WIDE>
-__device__ __forceinline__ void s_layer1(float4 (&ring)[kSRing], const float* wrow, int I, const float* brow, int g,
-                                         int nq, f32x4& z) {
-#define S_RUNL(n) s_run<n, VEC>(ring, wrow, I, brow, g, z)
+template <bool VEC, bool WIDE, int RB>
+__device__ __forceinline__ void s_layer1(float4 (&ring)[kSRing], const float* wrow, int I, const float* brow, int bs,
+                                         int g, int nq, f32x4 (&z)[RB]) {
+#define S_RUNL(n) s_run<n, VEC, RB>(ring, wrow, I, brow, bs, g, z)
   if (!WIDE || nq <= 16) {
     S_NQ_SWITCH(nq, S_RUNL)
     return;
   }
 #undef S_RUNL
   if constexpr (WIDE) {
-    s_run<16, VEC>(ring, wrow, I, brow, g, z);
+    s_run<16, VEC, RB>(ring, wrow, I, brow, bs, g, z);
     int t = 16;
     for (; t + 16 <= nq; t += 16) {
       s_prefill<16, VEC>(ring, wrow + 16 * t, I - 16 * t, g);
-      s_run<16, VEC>(ring, wrow + 16 * t, I - 16 * t, brow + 16 * t, g, z);
+      s_run<16, VEC, RB>(ring, wrow + 16 * t, I - 16 * t, brow + 16 * t, bs, g, z);
     }
     if (t < nq) {
       const float* wr = wrow + 16 * t;
       const float* br = brow + 16 * t;
       const int Ir = I - 16 * t;
-#define S_REM(n)                          \
-  {                                       \
-    s_prefill<n, VEC>(ring, wr, Ir, g);   \
-    s_run<n, VEC>(ring, wr, Ir, br, g, z); \
+#define S_REM(n)                                    \
+  {                                                 \
+    s_prefill<n, VEC>(ring, wr, Ir, g);             \
+    s_run<n, VEC, RB>(ring, wr, Ir, br, bs, g, z);  \
   }
       S_NQ_SWITCH(nq - t, S_REM)
 #undef S_REM
@@ -326,24 +344,28 @@ __device__ __forceinline__ void s_wgrad_acc(const float* arow, const float* brow
 }
 
 // ---------------------------------------------------------------- launch 1
-// One 16-row tile of one net: POL = the actor (policy head over A outputs),
-// otherwise the critic (value head).
-template <int A, bool POL, bool V1, int MAXI>
+// One tile of 16·RB rows of one net: POL = the actor (policy head over A
+// outputs), otherwise the critic (value head).  Lane (g, j) of wave w holds
+// hidden units 16w + 4g .. + 3 of rows r0 + 16·rb + j, rb < RB: each weight quad
+// streamed from L2 feeds RB MFMA groups (RB = 2 once a launch has more tiles
+// than CUs).  xs (the X tile) and dz2s share LDS: xs is dead after layer 1.
+template <int A, bool POL, bool V1, int MAXI, int RB>
 __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, float* xs, float* h1s, float* dz2s,
-                                       float* prm, float (*hp)[16], double (*ls_w)[2 + kSMaxA]) {
+                                       float* prm, float (*hp)[16 * RB], double (*ls_w)[2 + kSMaxA]) {
   static_assert(kSBPW == 1, "one hidden block per wave");
   constexpr int NL = POL ? 2 + A : 1;   // loss sums: policy, approx_kl, d logstd[A] | value
+  constexpr int TR = 16 * RB;           // rows of the tile
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const int I = N.I, XS = s_xs(I), Ip = s_ip(I), nq1 = Ip / 16;
   const int K = POL ? P.mb * P.D : P.mb;
   const int KP = POL ? P.KaS : P.KcS;   // the transposed rows' stride
-  const int r0 = tile * 16;
+  const int r0 = tile * TR;
   const SWork& W = P.w;
   float* xT = POL ? W.xaT : W.xcT;
   float* h1T = POL ? W.h1aT : W.h1cT;
   float* dz2T = POL ? W.dz2aT : W.dz2cT;
   float* dz1T = POL ? W.dz1aT : W.dz1cT;
-  const int b0 = w, h0 = 16 * b0 + 4 * g;   // the wave's hidden block; lane (g, j): units h0 .. h0 + 3 of row j
+  const int b0 = w, h0 = 16 * b0 + 4 * g;   // the wave's hidden block; lane (g, j): units h0 .. h0 + 3
   // layer 1's rows: the padded copy as whole float4 quads when there is one,
   // otherwise the parameter rows with clamped scalar loads
   // (V1: the launch checked that the net has the copy)
@@ -365,37 +387,48 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   }
 #undef S_PRE1
 #undef S_PRE1V
-  // (the wide instance fills layer 2's ring after layer 1: both rings live
-  // across a many-block layer 1 would not fit in the 128 registers of a 16-wave workgroup)
-  if constexpr (MAXI <= kSNarrowI) s_prefill<16, true>(ring2, w2row, kSH, g);
-  const int R = r0 + j;
-  const bool rv = R < K;
-  float hact[A], hlpo = 0.f;
-  double had = 0.0;
-  if constexpr (POL) {
-    const long long ei = rv ? R / P.D : 0;
-    const long long e_idx = rv ? P.idx[ei] : 0;
-    const long long gi = e_idx * P.D + (R - ei * P.D);
+  // (the wide and the two-block instances fill layer 2's ring after layer 1:
+  // both rings live across it would not fit in the 128 registers of a 16-wave workgroup)
+  constexpr bool kEarly2 = MAXI <= kSNarrowI && RB == 1;
+  if constexpr (kEarly2) s_prefill<16, true>(ring2, w2row, kSH, g);
+  bool rv[RB];
+  float hact[RB][A], hlpo[RB];
+  double had[RB];
 #pragma unroll
-    for (int a = 0; a < A; ++a) hact[a] = rv ? P.act[gi * A + a] : 0.f;
-    if (rv) {
-      hlpo = P.logp_old[gi];
-      had = P.adv[e_idx];
+  for (int rb = 0; rb < RB; ++rb) {
+    const int R = r0 + 16 * rb + j;
+    rv[rb] = R < K;
+    hlpo[rb] = 0.f;
+    had[rb] = 0.0;
+    if constexpr (POL) {
+      const long long ei = rv[rb] ? R / P.D : 0;
+      const long long e_idx = rv[rb] ? P.idx[ei] : 0;
+      const long long gi = e_idx * P.D + (R - ei * P.D);
+#pragma unroll
+      for (int a = 0; a < A; ++a) hact[rb][a] = rv[rb] ? P.act[gi * A + a] : 0.f;
+      if (rv[rb]) {
+        hlpo[rb] = P.logp_old[gi];
+        had[rb] = P.adv[e_idx];
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < A; ++a) hact[rb][a] = 0.f;
+      if (rv[rb]) had[rb] = P.ret[P.idx[R]];   // the value head's return
     }
-  } else {
-#pragma unroll
-    for (int a = 0; a < A; ++a) hact[a] = 0.f;
-    if (rv) had = P.ret[P.idx[R]];   // the value head's return
   }
   {
     constexpr int kXU = (16 * MAXI + kSBlock - 1) / kSBlock;
-    float v[kXU];
-    const int rr = tid & 15, Rx = r0 + rr;
-    const long long src = Rx < K ? (POL ? (P.idx[Rx / P.D] * P.D + Rx % P.D) : P.idx[Rx]) * I : -1;
+    float v[RB][kXU];
+    const int rr = tid & 15;
 #pragma unroll
-    for (int u = 0; u < kXU; ++u) {
-      const int k = (tid >> 4) + u * (kSBlock / 16);
-      v[u] = src >= 0 && k < I ? P.X[src + k] : 0.f;
+    for (int rb = 0; rb < RB; ++rb) {
+      const int Rx = r0 + 16 * rb + rr;
+      const long long src = Rx < K ? (POL ? (P.idx[Rx / P.D] * P.D + Rx % P.D) : P.idx[Rx]) * I : -1;
+#pragma unroll
+      for (int u = 0; u < kXU; ++u) {
+        const int k = (tid >> 4) + u * (kSBlock / 16);
+        v[rb][u] = src >= 0 && k < I ? P.X[src + k] : 0.f;
+      }
     }
     // biases and head: prm = [b1 | b2 | W3 (A rows) | b3 | logstd]
     for (int e = tid; e < 2 * kSH + A * kSH + 2 * A; e += kSBlock) {
@@ -408,10 +441,14 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
       prm[e] = pv;
     }
 #pragma unroll
-    for (int u = 0; u < kXU; ++u) {
-      const int k = (tid >> 4) + u * (kSBlock / 16);
-      if (k < Ip) xs[rr * XS + k] = v[u];
-      if (k < I) xT[(size_t)k * KP + Rx] = v[u];
+    for (int rb = 0; rb < RB; ++rb) {
+      const int Rx = r0 + 16 * rb + rr;
+#pragma unroll
+      for (int u = 0; u < kXU; ++u) {
+        const int k = (tid >> 4) + u * (kSBlock / 16);
+        if (k < Ip) xs[(16 * rb + rr) * XS + k] = v[rb][u];
+        if (k < I) xT[(size_t)k * KP + Rx] = v[rb][u];
+      }
     }
   }
   __syncthreads();
@@ -421,163 +458,212 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   const float* sw3 = prm + 2 * kSH;
   const float* sb3 = prm + 2 * kSH + A * kSH;
   const float* slogstd = sb3 + A;
-  // ---- layer 1: Z1ᵀ[h0 + r][row j] in register r of lane (g, j)
-  f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-  s_layer1<V1, (MAXI > kSNarrowI)>(ring1, w1row, V1 ? Ip : I, xs + j * XS, g, nq1, z);
-  if constexpr (MAXI > kSNarrowI) s_prefill<16, true>(ring2, w2row, kSH, g);
-  float h1[4];
+  if (POL && tile == 0 && tid == 0 && !P.fb_tail) {
+    // the policy's entropy from this minibatch's logstd, for launch 2's statistics
+    // (launch 2 updates logstd in place; dlogstd[kSMaxA] keeps the value it reports)
+    const float lc = (float)log(sqrt(2.0 * M_PI));
+    float ent = 0.0f;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) h1[r] = s_tanh(z[r] + sb1[h0 + r]);
-  *reinterpret_cast<float4*>(h1s + j * kSHS + h0) = float4{h1[0], h1[1], h1[2], h1[3]};
+    for (int a = 0; a < A; ++a) {
+      const float lsd = logf(expf(slogstd[a]));
+      ent = a == 0 ? (0.5f + lc) + lsd : ent + ((0.5f + lc) + lsd);
+    }
+    W.dlogstd[kSMaxA] = ent;
+  }
+  // ---- layer 1: Z1ᵀ[h0 + r][row] in register r of lane (g, j)
+  f32x4 z[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) z[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s_layer1<V1, (MAXI > kSNarrowI), RB>(ring1, w1row, V1 ? Ip : I, xs + j * XS, 16 * XS, g, nq1, z);
+  if constexpr (!kEarly2) s_prefill<16, true>(ring2, w2row, kSH, g);
+  float h1[RB][4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h1[rb][r] = s_tanh(z[rb][r] + sb1[h0 + r]);
+    *reinterpret_cast<float4*>(h1s + (16 * rb + j) * kSHS + h0) = float4{h1[rb][0], h1[rb][1], h1[rb][2], h1[rb][3]};
+  }
   __syncthreads();
   S_STAMP(2);
   // ---- layer 2: Z2ᵀ = W2·H1ᵀ (its ring filled at the start); the backward's ring filled behind it
-  z = f32x4{0.f, 0.f, 0.f, 0.f};
-  s_run<16, true>(ring2, w2row, kSH, h1s + j * kSHS, g, z);
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) z[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s_run<16, true, RB>(ring2, w2row, kSH, h1s + j * kSHS, 16 * kSHS, g, z);
   s_prefill<16, true>(ring1, w2trow, kSH, g);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) h1T[(size_t)(h0 + r) * KP + r0 + j] = h1[r];   // (after the loads above)
-  float h2[4], hs[A];
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-  for (int a = 0; a < A; ++a) hs[a] = 0.f;
+    for (int r = 0; r < 4; ++r) h1T[(size_t)(h0 + r) * KP + r0 + 16 * rb + j] = h1[rb][r];   // (after the loads above)
+  float h2[RB][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    h2[r] = s_tanh(z[r] + sb2[h0 + r]);
+  for (int rb = 0; rb < RB; ++rb) {
+    float hs[A];
 #pragma unroll
-    for (int a = 0; a < A; ++a) hs[a] += h2[r] * sw3[a * kSH + h0 + r];
-  }
-  // the head: the wave's partial dot of row j (lane groups g added), then the waves in order
+    for (int a = 0; a < A; ++a) hs[a] = 0.f;
 #pragma unroll
-  for (int a = 0; a < A; ++a) {
-    float t = hs[a] + __shfl_xor(hs[a], 16, 64);
-    t = t + __shfl_xor(t, 32, 64);
-    if (g == 0) hp[w * A + a][j] = t;
+    for (int r = 0; r < 4; ++r) {
+      h2[rb][r] = s_tanh(z[rb][r] + sb2[h0 + r]);
+#pragma unroll
+      for (int a = 0; a < A; ++a) hs[a] += h2[rb][r] * sw3[a * kSH + h0 + r];
+    }
+    // the head: the wave's partial dot of the row (lane groups g added), then the waves in order
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      float t = hs[a] + __shfl_xor(hs[a], 16, 64);
+      t = t + __shfl_xor(t, 32, 64);
+      if (g == 0) hp[w * A + a][16 * rb + j] = t;
+    }
   }
   __syncthreads();
   S_STAMP(3);
-  float mu[A];
-#pragma unroll
-  for (int a = 0; a < A; ++a) {
-    float t = hp[a][j];
-#pragma unroll
-    for (int v = 1; v < kSW; ++v) t += hp[v * A + a][j];
-    mu[a] = t + sb3[a];
-  }
-  // ---- the loss head of row j (every wave forms it; wave 0, lane group 0 counts it)
-  float dout[A];
-  double ls[NL];
-#pragma unroll
-  for (int k = 0; k < NL; ++k) ls[k] = 0.0;
-  if constexpr (POL) {
-    // compute_policy_loss (AG:602-640) and its gradient: ppo_heads_kernel's arithmetic
-    float sd[A], lsd[A], var2[A];
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      sd[a] = expf(slogstd[a]);
-      lsd[a] = logf(sd[a]);
-      var2[a] = 2.0f * (sd[a] * sd[a]);
-    }
-    const float lc = (float)log(sqrt(2.0 * M_PI));
-    const float lo = 1.0f - P.clip, hi = 1.0f + P.clip;
-    const double G = -1.0 / (double)K;
-    float t1[A], logp = 0.0f;
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      const float m = mu[a] * P.scale;
-      t1[a] = hact[a] - m;
-      const float t4 = (float)((double)(-(t1[a] * t1[a])) / (double)var2[a]);
-      const float lp = (t4 - lsd[a]) - lc;
-      logp = a == 0 ? lp : logp + lp;
-    }
-    const float lpo = hlpo;
-    const float ratio = expf(logp - lpo);
-    const double ad = had;
-    const float rc = fminf(fmaxf(ratio, lo), hi);
-    const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
-    const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
-    const double g2 = s2 < s1 ? G : (s1 == s2 ? G / 2 : 0.0);
-    float gr = (float)(g1 * ad);
-    if (ratio >= lo && ratio <= hi) gr = gr + (float)(g2 * ad);
-    const float gl = gr * ratio;
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      const float gt3 = (float)((double)gl / (double)var2[a]);
-      const float gt1 = -gt3 * 2.0f * t1[a];
-      dout[a] = rv ? -gt1 * P.scale : 0.f;
-      if (rv) ls[2 + a] = (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
-    }
-    if (rv) {
-      ls[0] = -(s1 < s2 ? s1 : s2);
-      ls[1] = (double)(lpo - logp);
-    }
-  } else {
-    // compute_value_loss (AG:642-683, centralized, unclipped): qs_value_head's arithmetic
-    if (rv) {
-      const double rt = had;
-      double rs = 0;
-      for (int d = 0; d < P.D; ++d) rs += rt;
-      const double diff = (double)mu[0] - rs / (double)P.D;
-      ls[0] = diff * diff;
-      dout[0] = (float)(diff / (double)P.mb);
-    } else {
-      dout[0] = 0.f;
-    }
-  }
-  // ---- dZ2 = (dout·W3) ⊙ (1 − H2²); the tile's b2 / W3 / b3 partial rows (row sums over j)
+  // ---- per row block: the loss head of the row (every wave forms it; wave 0,
+  // lane group 0 records its loss terms), dZ2 = (dout·W3) ⊙ (1 − H2²) and the
+  // tile's b2 / W3 / b3 partial rows (row sums over j, the row blocks in order)
   float* pa = (POL ? W.partAa : W.partAc) + (size_t)tile * (kSH + A * kSH + A);
   float* pb = (POL ? W.partBa : W.partBc) + (size_t)tile * kSH;
-  float d4[4];
+  float d4[RB][4], sbp[4], swp[A][4], sdo[A];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int h = h0 + r;
-    float gg = 0.f;
-#pragma unroll
-    for (int a = 0; a < A; ++a) gg += dout[a] * sw3[a * kSH + h];
-    const float hv = h2[r];
-    d4[r] = gg * (1.f - hv * hv);
-    const float sb = s_row_sum(d4[r]);
-    if (j == 0) pa[h] = sb;
+  for (int rb = 0; rb < RB; ++rb) {
+    float mu[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      const float sw = s_row_sum(dout[a] * hv);
-      if (j == 0) pa[kSH + a * kSH + h] = sw;
+      float t = hp[a][16 * rb + j];
+#pragma unroll
+      for (int v = 1; v < kSW; ++v) t += hp[v * A + a][16 * rb + j];
+      mu[a] = t + sb3[a];
     }
-  }
-  *reinterpret_cast<float4*>(dz2s + j * kSHS + h0) = float4{d4[0], d4[1], d4[2], d4[3]};
-  S_STAMP(4);
-  if (w == 0)
+    float dout[A];
+    double ls[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) ls[k] = 0.0;
+    if constexpr (POL) {
+      // compute_policy_loss (AG:602-640) and its gradient: ppo_heads_kernel's arithmetic
+      float sd[A], lsd[A], var2[A];
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        sd[a] = expf(slogstd[a]);
+        lsd[a] = logf(sd[a]);
+        var2[a] = 2.0f * (sd[a] * sd[a]);
+      }
+      const float lc = (float)log(sqrt(2.0 * M_PI));
+      const float lo = 1.0f - P.clip, hi = 1.0f + P.clip;
+      const double G = -1.0 / (double)K;
+      float t1[A], logp = 0.0f;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const float m = mu[a] * P.scale;
+        t1[a] = hact[rb][a] - m;
+        const float t4 = (float)((double)(-(t1[a] * t1[a])) / (double)var2[a]);
+        const float lp = (t4 - lsd[a]) - lc;
+        logp = a == 0 ? lp : logp + lp;
+      }
+      const float lpo = hlpo[rb];
+      const float ratio = expf(logp - lpo);
+      const double ad = had[rb];
+      const float rc = fminf(fmaxf(ratio, lo), hi);
+      const double s1 = (double)ratio * ad, s2 = (double)rc * ad;
+      const double g1 = s1 < s2 ? G : (s1 == s2 ? G / 2 : 0.0);
+      const double g2 = s2 < s1 ? G : (s1 == s2 ? G / 2 : 0.0);
+      float gr = (float)(g1 * ad);
+      if (ratio >= lo && ratio <= hi) gr = gr + (float)(g2 * ad);
+      const float gl = gr * ratio;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const float gt3 = (float)((double)gl / (double)var2[a]);
+        const float gt1 = -gt3 * 2.0f * t1[a];
+        dout[a] = rv[rb] ? -gt1 * P.scale : 0.f;
+        if (rv[rb]) ls[2 + a] = (double)gl * ((double)(t1[a] * t1[a]) / ((double)sd[a] * sd[a]) - 1.0);
+      }
+      if (rv[rb]) {
+        ls[0] = -(s1 < s2 ? s1 : s2);
+        ls[1] = (double)(lpo - logp);
+      }
+    } else {
+      // compute_value_loss (AG:642-683, centralized, unclipped): qs_value_head's arithmetic
+      if (rv[rb]) {
+        const double rt = had[rb];
+        double rs = 0;
+        for (int d = 0; d < P.D; ++d) rs += rt;
+        const double diff = (double)mu[0] - rs / (double)P.D;
+        ls[0] = diff * diff;
+        dout[0] = (float)(diff / (double)P.mb);
+      } else {
+        dout[0] = 0.f;
+      }
+    }
+    if (w == 0 && g == 0)
+#pragma unroll
+      for (int k = 0; k < NL; ++k) ls_w[16 * rb + j][k] = ls[k];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = h0 + r;
+      float gg = 0.f;
+#pragma unroll
+      for (int a = 0; a < A; ++a) gg += dout[a] * sw3[a * kSH + h];
+      const float hv = h2[rb][r];
+      d4[rb][r] = gg * (1.f - hv * hv);
+      const float sb = s_row_sum(d4[rb][r]);
+      sbp[r] = rb == 0 ? sb : sbp[r] + sb;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const float sw = s_row_sum(dout[a] * hv);
+        swp[a][r] = rb == 0 ? sw : swp[a][r] + sw;
+      }
+    }
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const float t = s_row_sum(dout[a]);
-      if (l == 0) pa[kSH + A * kSH + a] = t;
+      sdo[a] = rb == 0 ? t : sdo[a] + t;
     }
+  }
+  if (j == 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pa[h0 + r] = sbp[r];
+#pragma unroll
+      for (int a = 0; a < A; ++a) pa[kSH + a * kSH + h0 + r] = swp[a][r];
+    }
+  if (w == 0 && l == 0)
+#pragma unroll
+    for (int a = 0; a < A; ++a) pa[kSH + A * kSH + a] = sdo[a];
+  // (dz2s aliases xs: every wave's layer-1 reads of it precede two barriers)
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+    *reinterpret_cast<float4*>(dz2s + (16 * rb + j) * kSHS + h0) = float4{d4[rb][0], d4[rb][1], d4[rb][2], d4[rb][3]};
+  S_STAMP(4);
   __syncthreads();
   // ---- dH1ᵀ = W2ᵀ·dZ2ᵀ (rows of the transposed copy; ring filled during the head), dZ1 = dH1 ⊙ (1 − H1²)
-  z = f32x4{0.f, 0.f, 0.f, 0.f};
-  s_run<16, true>(ring1, w2trow, kSH, dz2s + j * kSHS, g, z);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) dz2T[(size_t)(h0 + r) * KP + R] = d4[r];
+  for (int rb = 0; rb < RB; ++rb) z[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s_run<16, true, RB>(ring1, w2trow, kSH, dz2s + j * kSHS, 16 * kSHS, g, z);
+  float sbq[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float u = h1[r];
-    const float d = z[r] * (1.f - u * u);
-    dz1T[(size_t)(h0 + r) * KP + R] = d;
-    const float sb = s_row_sum(d);
-    if (j == 0) pb[h0 + r] = sb;
+  for (int rb = 0; rb < RB; ++rb) {
+    const int R = r0 + 16 * rb + j;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dz2T[(size_t)(h0 + r) * KP + R] = d4[rb][r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float u = h1[rb][r];
+      const float d = z[rb][r] * (1.f - u * u);
+      dz1T[(size_t)(h0 + r) * KP + R] = d;
+      const float sb = s_row_sum(d);
+      sbq[r] = rb == 0 ? sb : sbq[r] + sb;
+    }
   }
-  // ---- the tile's loss sums (wave 0, rows in order), then the net's last tile
-  if (w == 0 && g == 0)
+  if (j == 0)
 #pragma unroll
-    for (int k = 0; k < NL; ++k) ls_w[j][k] = ls[k];
-  __syncthreads();
+    for (int r = 0; r < 4; ++r) pb[h0 + r] = sbq[r];
+  __syncthreads();   // (ls_w)
   S_STAMP(5);
+  // ---- the tile's loss sums (rows in order), then (fb_tail) the net's last tile
   __shared__ bool last;
   if (tid == 0) {
     double* lp = POL ? W.lossa + (size_t)tile * NL : W.lossc + tile;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
       double sacc = 0.0;
-      for (int q = 0; q < 16; ++q) sacc += ls_w[q][k];
+      for (int q = 0; q < TR; ++q) sacc += ls_w[q][k];
       lp[k] = sacc;
     }
     if (P.fb_tail) {
@@ -630,16 +716,16 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   }
 }
 
-template <int A, bool V1, int MAXI>
+template <int A, bool V1, int MAXI, int RB>
 __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
-  __shared__ float xs[16 * s_xs(MAXI)];
-  __shared__ float h1s[16 * kSHS];
-  __shared__ float dz2s[16 * kSHS];
-  __shared__ float hp[kSW * kSMaxA][16];
-  __shared__ double ls_w[16][2 + kSMaxA];
+  constexpr int XSZ = 16 * RB * s_xs(MAXI), DSZ = 16 * RB * kSHS;
+  __shared__ float xsd[XSZ > DSZ ? XSZ : DSZ];   // the X tile, then dZ2 (dead / not yet live in turn)
+  __shared__ float h1s[16 * RB * kSHS];
+  __shared__ float hp[kSW * kSMaxA][16 * RB];
+  __shared__ double ls_w[16 * RB][2 + kSMaxA];
   __shared__ float prm[2 * kSH + kSMaxA * kSH + 2 * kSMaxA];
-  if ((int)blockIdx.x < P.nA) s_tile<A, true, V1, MAXI>(P, P.a, blockIdx.x, xs, h1s, dz2s, prm, hp, ls_w);
-  else s_tile<1, false, V1, MAXI>(P, P.c, blockIdx.x - P.nA, xs, h1s, dz2s, prm, hp, ls_w);
+  if ((int)blockIdx.x < P.nA) s_tile<A, true, V1, MAXI, RB>(P, P.a, blockIdx.x, xsd, h1s, xsd, prm, hp, ls_w);
+  else s_tile<1, false, V1, MAXI, RB>(P, P.c, blockIdx.x - P.nA, xsd, h1s, xsd, prm, hp, ls_w);
 }
 
 // ---------------------------------------------------------------- launches 2 and 3
@@ -837,16 +923,23 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
     m0 = 16 * BT * (uu % cb);
   }
   const int M = l1 ? N.I : kSH;
-  // the sink: wave w < 4·NT takes register f = w of every lane (tile f/4, register f%4)
-  const bool fin_w = w < 4 * NT;
-  const int f = w, q = f >> 2, r = f & 3;
-  const int en = n0 + 16 * (q / BT) + 4 * g + r, em = m0 + 16 * (q % BT) + j;
-  const long long ei = (l1 ? N.w1 : N.w2) + (long long)en * M + em;
-  float pp = 0.f, pm = 0.f, pv = 0.f;
-  if (fin_w && direct && adam && em < M) {   // Adam's operands, in flight during the gradient
-    pp = N.p[ei];
-    pm = N.m[ei];
-    pv = N.v[ei];
+  // the sink: register slot f = w + kSGW·k of every lane (tile f/4, register f%4), f < 4·NT
+  constexpr int NF = (4 * NT + kSGW - 1) / kSGW;   // slots per wave
+  int en[NF], em[NF];
+  long long ei[NF];
+  float pp[NF], pm[NF], pv[NF];
+#pragma unroll
+  for (int k = 0; k < NF; ++k) {
+    const int f = w + kSGW * k, q = f >> 2, r = f & 3;
+    en[k] = n0 + 16 * (q / BT) + 4 * g + r;
+    em[k] = m0 + 16 * (q % BT) + j;
+    ei[k] = (l1 ? N.w1 : N.w2) + (long long)en[k] * M + em[k];
+    pp[k] = pm[k] = pv[k] = 0.f;
+    if (f < 4 * NT && direct && adam && em[k] < M) {   // Adam's operands, in flight during the gradient
+      pp[k] = N.p[ei[k]];
+      pm[k] = N.m[ei[k]];
+      pv[k] = N.v[ei[k]];
+    }
   }
   const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
   const float* dzT = actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT);
@@ -874,19 +967,24 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
     for (int k = 0; k < 4; ++k) red[w][4 * t + k][l] = c[t][k];
   __syncthreads();
   W_STAMP(2);
-  if (!fin_w) return;
   const bool act = !(direct && adam && actor) || *sopen;
-  float tot = red[0][f][l];
 #pragma unroll
-  for (int v = 1; v < kSGW; ++v) tot += red[v][f][l];
-  if (!direct) {
-    float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
-    const int Mp = l1 ? s_mp(N.I) : kSH;
-    part[((size_t)s * kSH + en) * Mp + em] = tot;   // (pad columns too)
-  } else if (act && em < M) {
-    const int si = actor ? 0 : 1;
-    if (!adam) P.G.g[si][ei] = tot;
-    else s_adam(N, ei, tot, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en, em, l1 ? N.w1p : nullptr, pp, pm, pv);
+  for (int k = 0; k < NF; ++k) {
+    const int f = w + kSGW * k;
+    if (f >= 4 * NT) break;
+    float tot = red[0][f][l];
+#pragma unroll
+    for (int v = 1; v < kSGW; ++v) tot += red[v][f][l];
+    if (!direct) {
+      float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
+      const int Mp = l1 ? s_mp(N.I) : kSH;
+      part[((size_t)s * kSH + en[k]) * Mp + em[k]] = tot;   // (pad columns too)
+    } else if (act && em[k] < M) {
+      const int si = actor ? 0 : 1;
+      if (!adam) P.G.g[si][ei[k]] = tot;
+      else s_adam(N, ei[k], tot, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr,
+                  pp[k], pm[k], pv[k]);
+    }
   }
 }
 
@@ -977,13 +1075,8 @@ ppo_small_wgrad_kernel(SArgs P, int fin) {
       if (l == 0) {
         const int A = P.a.A;
         const double K = (double)(P.mb * P.D);
-        const float lc = (float)log(sqrt(2.0 * M_PI));
-        float ent = 0.0f;
-        for (int a = 0; a < A; ++a) {
-          const float lsd = logf(expf(P.a.p[P.a.logstd + a]));
-          ent = a == 0 ? (0.5f + lc) + lsd : ent + ((0.5f + lc) + lsd);
-          P.w.dlogstd[a] = (float)tot[2 + a] - P.ent_coef;
-        }
+        const float ent = P.w.dlogstd[kSMaxA];   // (launch 1's tile 0: the logstd before this launch's Adam)
+        for (int a = 0; a < A; ++a) P.w.dlogstd[a] = (float)tot[2 + a] - P.ent_coef;
         const float akl = (float)(tot[1] / K);
         *P.kl_out = akl;
         P.acc[0] += tot[0] / K;
@@ -1107,6 +1200,7 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
 }
 
 struct SLayout {
+  int rb;         // 16-row blocks per forward/backward tile
   int nA, nC, KaP, KcP, KaS, KcS;
   int Sa, Sc;     // K-chunks of the weight gradients per net
   int bta, btc;   // their block sides in 16-row tiles
@@ -1126,10 +1220,14 @@ inline int s_chunks(long long KP) {
 SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   SLayout L;
   const long long Ka = Ia > 0 ? (long long)mb * D : 0, Kc = mb;
-  L.nA = (int)((Ka + 15) / 16);
-  L.nC = (int)((Kc + 15) / 16);
-  L.KaP = 16 * L.nA;
-  L.KcP = 16 * L.nC;
+  // 32-row tiles once 16-row ones would not fit in one round of the CUs (the
+  // two-block tile does twice the MFMA work for about 1.2x the latency)
+  // (one-output actors only: wider heads' per-row state spills out of the 128 registers)
+  L.rb = (Ia > 0 && A == 1 && (Ka + 15) / 16 + (Kc + 15) / 16 > kSCUs) ? 2 : 1;
+  L.nA = (int)((Ka + 16 * L.rb - 1) / (16 * L.rb));
+  L.nC = (int)((Kc + 16 * L.rb - 1) / (16 * L.rb));
+  L.KaP = 16 * L.rb * L.nA;
+  L.KcP = 16 * L.rb * L.nC;
   // row strides off a power of two: rows 16 KB apart all mapped to one memory
   // channel (the critic's weight gradients ran 10x slower at 4 096 rows)
   static const int pad = [] {   // dev probe: QS_SMALL_PAD overrides the pad (floats, a multiple of 4)
@@ -1149,7 +1247,7 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
       4LL * Ic * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS,   // xcT h1cT dz2cT dz1cT
       4LL * L.nA * (kSH + A * kSH + A), 4LL * L.nA * kSH,                           // partAa partBa
       4LL * L.nC * (2 * kSH + 1), 4LL * L.nC * kSH,                                 // partAc partBc
-      4LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192,                    // dlogstd lossa lossc cnt
+      8LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192,                    // dlogstd (+ entropy) lossa lossc cnt
       pw * L.Sa * 32 * ((Ia + 31) / 32), pw * L.Sa * kSH,                           // K-chunk partials: actor W1 W2
       pw * L.Sc * 32 * ((Ic + 31) / 32), pw * L.Sc * kSH};                          //                  critic W1 W2
   long long o = 0;
@@ -1232,6 +1330,7 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   L = s_layout(mb, D, actor->in, critic->in, A);
   P.mb = mb;
   P.D = D;
+  P.rb = L.rb;
   P.nA = L.nA;
   P.nC = L.nC;
   P.KaP = L.KaP;
@@ -1306,19 +1405,29 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
   // the wide instance (a 640-input LDS X tile) only when a net needs it
   const bool v1 = P.c.w1p && (P.nA == 0 || P.a.w1p);
   const bool wide = P.c.I > kSNarrowI || (P.nA > 0 && P.a.I > kSNarrowI);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kSBlock), kSReserveFB, st, P); };
-  // (the wide instance reads layer 1 from the padded copies only: s_args
+  // (the two-block and the wide two-block tiles use more than 80 KB of LDS: one a CU without a reserve)
+  auto go = [&](auto kern, int reserve) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kSBlock), reserve, st, P); };
+  // (the wide instances read layer 1 from the padded copies only: s_args
   // refuses a net wider than kSNarrowI without one)
-#define S_FB(AA)                                                                                   \
-  (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI>)                                               \
-        : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI>) : go(ppo_small_fb_kernel<AA, false, kSNarrowI>)))
-  switch (P.a.A) {
+#define S_FB(AA)                                                                                                     \
+  (P.rb == 2 ? (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2>, 0)                                                \
+                     : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 2>, 0)                                       \
+                           : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 2>, 0)))                                    \
+             : (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 1>, kSReserveFB)                                      \
+                     : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 1>, kSReserveFB)                             \
+                           : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 1>, kSReserveFB))))
+#define S_FB1(AA)                                                                                    \
+  (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 1>, kSReserveFB)                                 \
+        : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 1>, kSReserveFB)                        \
+              : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 1>, kSReserveFB)))
+  switch (P.a.A) {   // (two-block tiles: one-output actors, s_layout)
     case 1: S_FB(1); break;
-    case 2: S_FB(2); break;
-    case 3: S_FB(3); break;
-    default: S_FB(4); break;
+    case 2: S_FB1(2); break;
+    case 3: S_FB1(3); break;
+    default: S_FB1(4); break;
   }
 #undef S_FB
+#undef S_FB1
 }
 
 // Launches 2 (and 3 when a net's weight gradients are split in K-chunks) into P.G.sink
@@ -1426,7 +1535,10 @@ int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* 
   P.w.cnt = (unsigned*)(wb + L.off[15]);
   P.nA = 0;   // critic tiles only
   P.fb_tail = 1;   // (the last tile adds the value loss to acc[1])
+  P.rb = L.rb;     // (1: the critic-only layout)
+  P.nC = L.nC;
   P.KaP = P.KaS = 0;
+  P.KcP = L.KcP;
   P.KcS = L.KcS;
   s_launch_fb(P, L.nC, (hipStream_t)stream);
   hipError_t e = hipGetLastError();

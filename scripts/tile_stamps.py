@@ -45,8 +45,9 @@ def main():
             learner_mb.per_minibatch_us(shape, reps=1, small=True)
             torch.cuda.synchronize()
             D, O, A, mb, T, E = learner_mb.SHAPES[shape]
-            nA, nC = (mb * D + 15) // 16, (mb + 15) // 16
-            dump(f"{shape} tile path (actor tiles {nA}, critic tiles {nC})", nA + nC)
+            rb = 2 if (A == 1 and (mb * D + 15) // 16 + (mb + 15) // 16 > 256) else 1
+            nA, nC = (mb * D + 16 * rb - 1) // (16 * rb), (mb + 16 * rb - 1) // (16 * rb)
+            dump(f"{shape} tile path ({16 * rb}-row tiles) (actor tiles {nA}, critic tiles {nC})", nA + nC)
         return
     for name, shape in (("ref small step", "ref"),):
         learner_mb.per_minibatch_us(shape, reps=1, small=True)
