@@ -455,7 +455,10 @@ class _F16Work(_M3Work):
 # qs_ppo_small_adam) takes minibatches of at most this many actor rows (mb·D,
 # at most QS_PPO_SMALL_MAX_ROWS); larger ones run the split-K path
 # (_iteration_direct)
-_SMALL_MAX_ROWS = 2048
+# (measured per minibatch through the exchange path, profiles/r05_rank_shapes.txt: the
+# tile path at 4 096 / 5 120 / 8 192 actor rows 73 / 120 / 120-133 µs against the direct
+# iteration's 317 / 193 / 158-226 µs; at 16 384 rows 185 against 163)
+_SMALL_MAX_ROWS = 8192
 _SMALL_MAX_IN = 640   # widest net input the tile kernels take (Spiral's 595-wide critic)
 
 
