@@ -746,6 +746,11 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
+    # stdout carries the one JSON line: whatever the libraries print there (RCCL's
+    # version banner at its first communicator) goes to stderr instead
+    out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ranks = Ranks(dry=args.dry_run)
     world, rank = ranks.world, ranks.rank
     if args.dry_run:
@@ -758,7 +763,7 @@ def main():
                 "dry_run": {"pid": os.getpid(), "ppid": os.getppid(), "pppid": _ppid(os.getppid()),
                             "backend": "gloo" if world > 1 else None},
                 "legs": [{"kind": k, "name": n, "scaling": sc, "envs_per_rank": e, "mini_batch_per_rank": m}
-                         for k, n, sc, e, m in leg_plan(args, world)]}), flush=True)
+                         for k, n, sc, e, m in leg_plan(args, world)]}), file=out, flush=True)
         ranks.close()
         return
     E, D = args.envs, args.drones
@@ -865,7 +870,7 @@ def main():
         if world > 1:
             line["mappo_strong"] = mappo_strong or None
             line["configs_strong"] = configs_strong or None
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     ranks.close()
 
 
