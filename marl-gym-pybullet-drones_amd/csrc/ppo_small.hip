@@ -71,9 +71,13 @@ constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
 constexpr int kSGW = 8;                // waves per weight-gradient workgroup (one weight block and K-chunk; two a CU)
 constexpr int kSCUs = 256;              // MI355X compute units (one forward/backward tile each)
-constexpr int kSBT1Q = 128;            // quads (16 rows) from which a net's weight gradients take 16×16 blocks
+constexpr int kSBT1Q = 1 << 30;        // quads (16 rows) from which a net's weight gradients would take 16×16 blocks
+                                       // (never: 32×32 blocks and K-chunks move half the operand bytes per MFMA)
 constexpr int kSGQW = 32;              // most quads per wave of the weight-gradient kernel (compile-time runs of <= 16)
-constexpr int kSGQ = kSGQW * 16;       // quads per K-chunk (longer columns: chunk partials + launch 3)
+constexpr int kSGQ = 64;               // quads per K-chunk (1 024 rows, 8 a wave): longer columns in chunks whose
+                                       // last-arriving workgroup sums the block's partials
+constexpr int kSBlkCnt = 2048;         // arrival counters of the chunked weight blocks (both nets)
+static_assert(kSGQ / kSGW <= kSGQW, "a wave's share of a K-chunk must fit s_wgrad_q's runs");
 constexpr int kSMaxS = 32;             // most K-chunks per net
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
 // Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
@@ -125,7 +129,8 @@ struct SWork {   // workspace views (qs_ppo_small_work_bytes)
   float *xaT, *h1aT, *dz2aT, *dz1aT, *xcT, *h1cT, *dz2cT, *dz1cT;
   float *partAa, *partBa, *partAc, *partBc, *dlogstd;
   double *lossa, *lossc;
-  unsigned* cnt;   // [0] actor tiles, [64] critic tiles, [128] weight-gradient workgroups, [160] apply workgroups
+  unsigned* cnt;   // [0] actor tiles, [64] critic tiles, [128] weight-gradient workgroups, [160] apply workgroups,
+                   // [256 + block] chunk arrivals of a chunked weight block
   float* wpart[4];   // K-chunk partials [S][256][Mp] of actor W1, actor W2, critic W1, critic W2 (Mp: M padded to 32)
 };
 
@@ -741,6 +746,9 @@ __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, floa
   const float denom = sqrtf(v1) / bc2s + N.eps;
   const float p1 = p - (N.lr / bc1) * (m1 / denom);
   N.p[i] = p1;
+#ifdef QS_X_NO_W2T
+  w2t = nullptr;   // dev probe: the transposed copy's scattered stores skipped (results wrong)
+#endif
   if (w2t) w2t[(size_t)k * kSH + n] = p1;
   if (w1p) w1p[(size_t)n * s_ip(N.I) + k] = p1;
 }
@@ -901,7 +909,8 @@ __device__ __forceinline__ void s_wgrad_q(const float* a0, const float* a1, cons
 // the gradient buffer); otherwise the chunk partials of launch 3.
 template <int BT>
 __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int s, int u, bool adam,
-                                         float (*red)[16][64], const float (*sc)[2], bool* sopen) {
+                                         float (*red)[16][64], const float (*sc)[2], bool* sopen, bool* slast,
+                                         int bid) {
   constexpr int NT = BT * BT;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const SNet& N = actor ? P.a : P.c;
@@ -956,7 +965,7 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
                 xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
                 wb - wa, g, c);
   W_STAMP(1);
-  if (w == 0 && direct && adam && actor) {   // the actor's KL gate (AG:731-734), before the sums are read
+  if (w == 0 && adam && actor) {   // the actor's KL gate (AG:731-734), before the sums are read
     double tot[2 + kSMaxA];
     const bool o = s_gate_rows(P, l, tot);
     if (l == 0) *sopen = o;
@@ -967,24 +976,58 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
     for (int k = 0; k < 4; ++k) red[w][4 * t + k][l] = c[t][k];
   __syncthreads();
   W_STAMP(2);
-  const bool act = !(direct && adam && actor) || *sopen;
+  const bool act = !(adam && actor) || *sopen;
+  const int si = actor ? 0 : 1;
+  float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
+  const int Mp = l1 ? s_mp(N.I) : kSH;
+  float tot[NF];
 #pragma unroll
   for (int k = 0; k < NF; ++k) {
     const int f = w + kSGW * k;
     if (f >= 4 * NT) break;
-    float tot = red[0][f][l];
+    tot[k] = red[0][f][l];
 #pragma unroll
-    for (int v = 1; v < kSGW; ++v) tot += red[v][f][l];
+    for (int v = 1; v < kSGW; ++v) tot[k] += red[v][f][l];
     if (!direct) {
-      float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
-      const int Mp = l1 ? s_mp(N.I) : kSH;
-      part[((size_t)s * kSH + en[k]) * Mp + em[k]] = tot;   // (pad columns too)
+      part[((size_t)s * kSH + en[k]) * Mp + em[k]] = tot[k];   // (pad columns too)
     } else if (act && em[k] < M) {
-      const int si = actor ? 0 : 1;
-      if (!adam) P.G.g[si][ei[k]] = tot;
-      else s_adam(N, ei[k], tot, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr,
+      if (!adam) P.G.g[si][ei[k]] = tot[k];
+      else s_adam(N, ei[k], tot[k], sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr,
                   pp[k], pm[k], pv[k]);
     }
+  }
+  if (direct) return;
+  // K-chunks: the block's last-arriving workgroup sums its S partials in chunk
+  // order (an agent-scope release of the partials before the arrival count, an
+  // acquire after it) and sinks them — no further launch
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    const bool lst = atomicAdd(P.w.cnt + 256 + bid, 1u) == (unsigned)S - 1;
+    *slast = lst;
+    if (lst) P.w.cnt[256 + bid] = 0u;
+  }
+  __syncthreads();
+  if (!*slast) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+  for (int k = 0; k < NF; ++k) {
+    const int f = w + kSGW * k;
+    if (f >= 4 * NT) break;
+    if (!(act && em[k] < M)) continue;
+    const float* pk = part + (size_t)en[k] * Mp + em[k];
+    const size_t cs = (size_t)kSH * Mp;
+    float g = 0.f;
+    for (int q0 = 0; q0 < S; q0 += 8) {   // eight chunks' loads in flight (clamped: unconditional), added in order
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = pk[(size_t)min(q0 + q, S - 1) * cs];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g = (q0 + q == 0) ? v[q] : (q0 + q < S ? g + v[q] : g);
+    }
+    if (!adam) P.G.g[si][ei[k]] = g;
+    else s_adam(N, ei[k], g, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr,
+                N.p[ei[k]], N.m[ei[k]], N.v[ei[k]]);
   }
 }
 
@@ -1010,7 +1053,7 @@ ppo_small_wgrad_kernel(SArgs P, int fin) {
   // (4 waves a SIMD: two 8-wave workgroups a CU, the grid in one round)
   __shared__ float red[kSGW][16][64];
   __shared__ float sc[2][2];
-  __shared__ bool last, sopen;
+  __shared__ bool last, sopen, slast;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   s_adam_scalars(P, sc, tid);
   const bool adam = P.G.sink == SINK_ADAM;
@@ -1022,8 +1065,9 @@ ppo_small_wgrad_kernel(SArgs P, int fin) {
     const bool actor = blk < nwa;
     const int S = P.G.S[actor ? 0 : 1];
     const int T = s_xcd_swz(actor ? blk : blk - nwa, actor ? nwa : nwc);
-    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, T % S, T / S, adam, red, sc, &sopen);
-    else s_wblock<2>(P, actor, S, T % S, T / S, adam, red, sc, &sopen);
+    const int bid = (actor ? 0 : s_nblk(P.a.I, P.G.bt[0])) + T / S;   // (arrival counter of the chunked block)
+    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, T % S, T / S, adam, red, sc, &sopen, &slast, bid);
+    else s_wblock<2>(P, actor, S, T % S, T / S, adam, red, sc, &sopen, &slast, bid);
   } else {
     // the actor's loss totals (every wave: the gate, logstd's gradient)
     double tot[2 + kSMaxA];
@@ -1247,7 +1291,7 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
       4LL * Ic * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS,   // xcT h1cT dz2cT dz1cT
       4LL * L.nA * (kSH + A * kSH + A), 4LL * L.nA * kSH,                           // partAa partBa
       4LL * L.nC * (2 * kSH + 1), 4LL * L.nC * kSH,                                 // partAc partBc
-      8LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * 192,                    // dlogstd (+ entropy) lossa lossc cnt
+      8LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * (256 + kSBlkCnt),      // dlogstd (+ entropy) lossa lossc cnt
       pw * L.Sa * 32 * ((Ia + 31) / 32), pw * L.Sa * kSH,                           // K-chunk partials: actor W1 W2
       pw * L.Sc * 32 * ((Ic + 31) / 32), pw * L.Sc * kSH};                          //                  critic W1 W2
   long long o = 0;
@@ -1432,7 +1476,7 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
 
 // Launches 2 (and 3 when a net's weight gradients are split in K-chunks) into P.G.sink
 static void s_launch_grad(const SArgs& P, hipStream_t st) {
-  const bool one = P.G.S[0] == 1 && P.G.S[1] == 1;
+  const bool one = true;   // (chunked blocks are summed by their last-arriving workgroup)
   const int nvec = (2 * kSH + P.a.A * kSH + 2 * P.a.A) + (3 * kSH + 1);
   const int vwg = (16 * nvec + 64 * kSGW - 1) / (64 * kSGW);   // 16 lanes per vector element
   const int grid = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0] + s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1] + vwg;

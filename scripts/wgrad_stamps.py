@@ -30,8 +30,8 @@ def main():
         torch.cuda.synchronize()
         D, O, A, mb, T, E = learner_mb.SHAPES[shape]
         Ka, Kc = mb * D, mb
-        bt = lambda K: 1 if (K + 15) // 16 >= 128 else 2
-        S = lambda K: max(1, ((K + 15) // 16 + 255) // 256)   # kSGQ = 8 waves x 32 quads
+        bt = lambda K: 2   # (32x32 blocks, kSBT1Q)
+        S = lambda K: max(1, ((K + 15) // 16 + 63) // 64)   # kSGQ = 64 quads per chunk
         na, nc = nblk(O, bt(Ka)) * S(Ka), nblk(D * O, bt(Kc)) * S(Kc)
         nvec = (2 * 256 + A * 256 + 2 * A) + (3 * 256 + 1)
         nv = (16 * nvec + 511) // 512   # kSGW = 8 waves
