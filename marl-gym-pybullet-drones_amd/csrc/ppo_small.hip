@@ -69,14 +69,14 @@ constexpr int kSMaxI = 640;            // widest input (Spiral's centralized cri
 constexpr int kSNarrowI = 256;         // the forward/backward instance for inputs up to this width (smaller LDS X tile)
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
-constexpr int kSGW = 8;                // waves per weight-gradient workgroup (one weight block and K-chunk; two a CU)
+constexpr int kSGW = 4;                // waves per weight-gradient workgroup (one weight block and K-chunk; four a CU)
 constexpr int kSCUs = 256;              // MI355X compute units (one forward/backward tile each)
 constexpr int kSBT1Q = 1 << 30;        // quads (16 rows) from which a net's weight gradients would take 16×16 blocks
                                        // (never: 32×32 blocks and K-chunks move half the operand bytes per MFMA)
 constexpr int kSGQW = 32;              // most quads per wave of the weight-gradient kernel (compile-time runs of <= 16)
-constexpr int kSGQ = 64;               // quads per K-chunk (1 024 rows, 8 a wave): longer columns in chunks whose
-                                       // last-arriving workgroup sums the block's partials
-constexpr int kSBlkCnt = 2048;         // arrival counters of the chunked weight blocks (both nets)
+constexpr int kSGQ = 64;               // quads per K-chunk (1 024 rows, 16 a wave): longer columns in chunk
+                                       // partials, summed by launch 3
+constexpr int kSBlkCnt = 0;            // (no per-block arrival counters)
 static_assert(kSGQ / kSGW <= kSGQW, "a wave's share of a K-chunk must fit s_wgrad_q's runs");
 constexpr int kSMaxS = 32;             // most K-chunks per net
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
@@ -142,6 +142,7 @@ struct SGrad {
   int sink;          // the final sink: SINK_ADAM (one rank) or SINK_GRAD (this rank's gradient, for the all-reduce)
   float* g[2];       // SINK_GRAD / qs_ppo_small_adam: the nets' gradient buffers (flat, the params' layout)
   float gdiv;        // qs_ppo_small_adam: the all-reduced sums ÷ gdiv (the world size), approx_kl too
+  int dev_skip;      // dev builds: bit 0 skips the actor's weight blocks, bit 1 the critic's, bit 2 the vectors
 };
 
 struct SArgs {
@@ -909,8 +910,7 @@ __device__ __forceinline__ void s_wgrad_q(const float* a0, const float* a1, cons
 // the gradient buffer); otherwise the chunk partials of launch 3.
 template <int BT>
 __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int s, int u, bool adam,
-                                         float (*red)[16][64], const float (*sc)[2], bool* sopen, bool* slast,
-                                         int bid) {
+                                         float (*red)[16][64], const float (*sc)[2], bool* sopen) {
   constexpr int NT = BT * BT;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
   const SNet& N = actor ? P.a : P.c;
@@ -996,39 +996,9 @@ __device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int 
                   pp[k], pm[k], pv[k]);
     }
   }
-  if (direct) return;
-  // K-chunks: the block's last-arriving workgroup sums its S partials in chunk
-  // order (an agent-scope release of the partials before the arrival count, an
-  // acquire after it) and sinks them — no further launch
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    const bool lst = atomicAdd(P.w.cnt + 256 + bid, 1u) == (unsigned)S - 1;
-    *slast = lst;
-    if (lst) P.w.cnt[256 + bid] = 0u;
-  }
-  __syncthreads();
-  if (!*slast) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#pragma unroll
-  for (int k = 0; k < NF; ++k) {
-    const int f = w + kSGW * k;
-    if (f >= 4 * NT) break;
-    if (!(act && em[k] < M)) continue;
-    const float* pk = part + (size_t)en[k] * Mp + em[k];
-    const size_t cs = (size_t)kSH * Mp;
-    float g = 0.f;
-    for (int q0 = 0; q0 < S; q0 += 8) {   // eight chunks' loads in flight (clamped: unconditional), added in order
-      float v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = pk[(size_t)min(q0 + q, S - 1) * cs];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) g = (q0 + q == 0) ? v[q] : (q0 + q < S ? g + v[q] : g);
-    }
-    if (!adam) P.G.g[si][ei[k]] = g;
-    else s_adam(N, ei[k], g, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr,
-                N.p[ei[k]], N.m[ei[k]], N.v[ei[k]]);
-  }
+  // (K-chunks: launch 3 sums the partials.  Summing them here, in the block's
+  // last-arriving workgroup, needed an agent-scope release per workgroup before
+  // its arrival count: +18 µs at C3/8, the L2 write-backs serialising)
 }
 
 // Workgroup T of n consecutive ones (the dispatcher deals them to the 8 XCDs
@@ -1050,10 +1020,10 @@ __device__ __forceinline__ int s_xcd_swz(int T, int n) {
 // With Adam and no launch 3 the last workgroup commits the step counts.
 __global__ void __launch_bounds__(64 * kSGW) __attribute__((amdgpu_waves_per_eu(4)))
 ppo_small_wgrad_kernel(SArgs P, int fin) {
-  // (4 waves a SIMD: two 8-wave workgroups a CU, the grid in one round)
+  // (4 waves a SIMD: four 4-wave workgroups a CU, the grid in one round)
   __shared__ float red[kSGW][16][64];
   __shared__ float sc[2][2];
-  __shared__ bool last, sopen, slast;
+  __shared__ bool last, sopen;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   s_adam_scalars(P, sc, tid);
   const bool adam = P.G.sink == SINK_ADAM;
@@ -1061,13 +1031,20 @@ ppo_small_wgrad_kernel(SArgs P, int fin) {
   const int blk = blockIdx.x;
   __syncthreads();   // (sc)
   W_STAMP(0);
+#ifdef QS_DEV_BUILD
+  if ((P.G.dev_skip & 1) && blk < nwa) return;
+  if ((P.G.dev_skip & 2) && blk >= nwa && blk < nwa + nwc) return;
+  if ((P.G.dev_skip & 4) && blk >= nwa + nwc) return;
+#endif
   if (blk < nwa + nwc) {
     const bool actor = blk < nwa;
     const int S = P.G.S[actor ? 0 : 1];
+    // logical index, K-chunk major: an XCD's contiguous share of them (s_xcd_swz) is one
+    // or two chunks' rows of the operands
     const int T = s_xcd_swz(actor ? blk : blk - nwa, actor ? nwa : nwc);
-    const int bid = (actor ? 0 : s_nblk(P.a.I, P.G.bt[0])) + T / S;   // (arrival counter of the chunked block)
-    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, T % S, T / S, adam, red, sc, &sopen, &slast, bid);
-    else s_wblock<2>(P, actor, S, T % S, T / S, adam, red, sc, &sopen, &slast, bid);
+    const int nb = (actor ? nwa : nwc) / S, s = T / nb, u = T - s * nb;
+    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, s, u, adam, red, sc, &sopen);
+    else s_wblock<2>(P, actor, S, s, u, adam, red, sc, &sopen);
   } else {
     // the actor's loss totals (every wave: the gate, logstd's gradient)
     double tot[2 + kSMaxA];
@@ -1158,56 +1135,65 @@ __global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
   __shared__ float sc[2][2];
   __shared__ bool last;
   const int tid = threadIdx.x;
-  s_adam_scalars(P, sc, tid);
   const int sink = FROM_G ? SINK_ADAM : P.G.sink;
-  const bool open_a = sink != SINK_ADAM || s_gate_open(P);
-  __syncthreads();
+  // the element, its gradient and Adam operands first (in flight across the scalars' barrier)
   int e = blockIdx.x * blockDim.x + tid;
   const bool inc[2] = {FROM_G || P.G.S[0] > 1, FROM_G || P.G.S[1] > 1};
   const int nw[4] = {inc[0] ? kSH * P.a.I : 0, inc[0] ? kSH * kSH : 0, inc[1] ? kSH * P.c.I : 0,
                      inc[1] ? kSH * kSH : 0};
   int part = 0;
   while (part < 4 && e >= nw[part]) e -= nw[part++];
+  bool actor = part < 2, l1 = (part & 1) == 0, have = false;
+  long long i = 0;
+  int n = 0, m = 0;
+  float gsum = 0.f, p0 = 0.f, m0 = 0.f, v0 = 0.f;
   if (part < 4) {
-    const bool actor = part < 2, l1 = (part & 1) == 0;
     const SNet& N = actor ? P.a : P.c;
-    if (sink != SINK_ADAM || !actor || open_a) {
-      const int M = l1 ? N.I : kSH;
-      const int n = e / M, m = e - n * M;
-      const long long i = (l1 ? N.w1 : N.w2) + e;
-      float gsum;
-      if constexpr (FROM_G) {
-        gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
-      } else {
-        // the S chunk partials, eight loads in flight (clamped: unconditional), added in chunk order
-        const int S = P.G.S[actor ? 0 : 1];
-        const int Mp = l1 ? s_mp(N.I) : kSH;
-        const float* pp = P.w.wpart[part] + (size_t)n * Mp + m;
-        const size_t cs = (size_t)kSH * Mp;
-        gsum = 0.f;
-        for (int q0 = 0; q0 < S; q0 += 8) {
-          float v[8];
+    const int M = l1 ? N.I : kSH;
+    n = e / M;
+    m = e - n * M;
+    i = (l1 ? N.w1 : N.w2) + e;
+    have = true;
+    if constexpr (FROM_G) {
+      gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
+    } else {
+      // the S chunk partials, eight loads in flight (clamped: unconditional), added in chunk order
+      const int S = P.G.S[actor ? 0 : 1];
+      const int Mp = l1 ? s_mp(N.I) : kSH;
+      const float* pp = P.w.wpart[part] + (size_t)n * Mp + m;
+      const size_t cs = (size_t)kSH * Mp;
+      for (int q0 = 0; q0 < S; q0 += 8) {
+        float v[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = pp[(size_t)min(q0 + q, S - 1) * cs];
+        for (int q = 0; q < 8; ++q) v[q] = pp[(size_t)min(q0 + q, S - 1) * cs];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) gsum = (q0 + q == 0) ? v[q] : (q0 + q < S ? gsum + v[q] : gsum);
-        }
+        for (int q = 0; q < 8; ++q) gsum = (q0 + q == 0) ? v[q] : (q0 + q < S ? gsum + v[q] : gsum);
       }
-      const int si = actor ? 0 : 1;
-      if (sink == SINK_GRAD) P.G.g[si][i] = gsum;
-      else s_adam(N, i, gsum, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, n, m, l1 ? N.w1p : nullptr, N.p[i], N.m[i],
-                  N.v[i]);
     }
   } else if (FROM_G) {
-    bool actor;
-    long long i;
     const float* col;
     int cstride, nt, u;
-    if (s_vec_loc(P, e, actor, i, col, cstride, nt, u) && (!actor || open_a)) {
-      const SNet& N = actor ? P.a : P.c;
-      const int si = actor ? 0 : 1;
-      s_adam(N, i, P.G.g[si][i] / P.G.gdiv, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, N.p[i], N.m[i], N.v[i]);
+    if (s_vec_loc(P, e, actor, i, col, cstride, nt, u)) {
+      have = true;
+      l1 = false;
+      gsum = P.G.g[actor ? 0 : 1][i] / P.G.gdiv;
     }
+  }
+  const SNet& N = actor ? P.a : P.c;
+  if (have && sink == SINK_ADAM) {
+    p0 = N.p[i];
+    m0 = N.m[i];
+    v0 = N.v[i];
+  }
+  s_adam_scalars(P, sc, tid);
+  const bool open_a = sink != SINK_ADAM || s_gate_open(P);
+  __syncthreads();
+  if (have && (sink != SINK_ADAM || !actor || open_a)) {
+    const int si = actor ? 0 : 1;
+    const bool w2 = part < 4 && !l1;
+    if (sink == SINK_GRAD) P.G.g[si][i] = gsum;
+    else s_adam(N, i, gsum, sc[si][0], sc[si][1], w2 ? N.w2t : nullptr, n, m, part < 4 && l1 ? N.w1p : nullptr, p0, m0,
+                v0);
   }
   if (sink != SINK_ADAM) return;
   __syncthreads();
@@ -1257,7 +1243,16 @@ struct SLayout {
 inline int s_bt(long long KP) { return KP / 16 >= kSBT1Q ? 1 : 2; }
 inline int s_chunks(long long KP) {
   const long long q = KP / 16;
-  const long long S = (q + kSGQ - 1) / kSGQ;
+#ifdef QS_DEV_BUILD
+  static const int gq = [] {   // dev probe: QS_SMALL_GQ quads per K-chunk (a multiple of 16, <= kSGW·kSGQW)
+    const char* e = getenv("QS_SMALL_GQ");
+    const int v = e ? atoi(e) : kSGQ;
+    return v >= 16 && v <= kSGW * kSGQW && v % 16 == 0 ? v : kSGQ;
+  }();
+#else
+  constexpr int gq = kSGQ;
+#endif
+  const long long S = (q + gq - 1) / gq;
   return (int)(S < 1 ? 1 : (S > kSMaxS ? kSMaxS : S));
 }
 // Ia = 0: the critic's tiles only (qs_ppo_critic_tiles), no actor buffers
@@ -1475,8 +1470,17 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
 }
 
 // Launches 2 (and 3 when a net's weight gradients are split in K-chunks) into P.G.sink
-static void s_launch_grad(const SArgs& P, hipStream_t st) {
-  const bool one = true;   // (chunked blocks are summed by their last-arriving workgroup)
+static void s_launch_grad(SArgs P, hipStream_t st) {
+#ifdef QS_DEV_BUILD
+  static const int skip = [] {
+    const char* e = getenv("QS_WG_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  P.G.dev_skip = skip;
+#else
+  P.G.dev_skip = 0;
+#endif
+  const bool one = P.G.S[0] == 1 && P.G.S[1] == 1;
   const int nvec = (2 * kSH + P.a.A * kSH + 2 * P.a.A) + (3 * kSH + 1);
   const int vwg = (16 * nvec + 64 * kSGW - 1) / (64 * kSGW);   // 16 lanes per vector element
   const int grid = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0] + s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1] + vwg;

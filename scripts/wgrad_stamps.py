@@ -34,7 +34,7 @@ def main():
         S = lambda K: max(1, ((K + 15) // 16 + 63) // 64)   # kSGQ = 64 quads per chunk
         na, nc = nblk(O, bt(Ka)) * S(Ka), nblk(D * O, bt(Kc)) * S(Kc)
         nvec = (2 * 256 + A * 256 + 2 * A) + (3 * 256 + 1)
-        nv = (16 * nvec + 511) // 512   # kSGW = 8 waves
+        nv = (16 * nvec + 255) // 256   # kSGW = 4 waves
         n = na + nc + nv
         buf = (ctypes.c_ulonglong * (n * 4))()
         f = L.load().qs_dev_wgrad_stamps
