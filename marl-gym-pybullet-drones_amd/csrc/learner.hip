@@ -1850,34 +1850,44 @@ __host__ __device__ constexpr int m3w_lds_floats(int Ip) {
   return 32 * (Ip + 1) > kM3Steps2 * 64 ? 32 * (Ip + 1) : kM3Steps2 * 64;
 }
 
-__device__ __forceinline__ void m3w_share(float* xs, const float* mine, float* all, int w) {
+// The exchange of the waves' activation blocks: wave w's 16 values of lane
+// (c, h) are B-operand steps 16w .. 16w + 15 of the 256-deep contraction, kept
+// in LDS as one float4 per k-quad and lane (k-quad q = steps 4q .. 4q + 3 at
+// xs4[q·64 + lane]) — each lane's four operands of a quad in one ds_read_b128,
+// consecutive lanes on consecutive 16 B.  (Held in 128 registers per lane, they
+// put the 8-wave kernels at 210 VGPRs: one workgroup per CU, its staging and
+// barriers never overlapped by another's MFMAs.)
+__device__ __forceinline__ void m3w_share(float4* xs4, const float* mine, int w) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) xs[(w * 16 + i) * 64 + lane] = mine[i];
+  for (int i = 0; i < 4; ++i)
+    xs4[(4 * w + i) * 64 + lane] = make_float4(mine[4 * i], mine[4 * i + 1], mine[4 * i + 2], mine[4 * i + 3]);
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kM3Steps2; ++k) all[k] = xs[k * 64 + lane];
 }
 
 // Σ_k over the 128 MFMA steps of block blk of a [8 blk][32 q][64][4] packed
-// matrix (W2p or W2Tp) with the B operand in registers.  A wave's block is
-// private to it, so it streams straight from L2 into a ring of eight float4
-// (eight k-quads = 32 MFMAs ahead), no LDS.
-__device__ __forceinline__ f32x16 m3w_contract(const float4* __restrict__ mat, int blk, const float* bv) {
-  const float4* p = mat + (size_t)blk * 32 * 64 + (threadIdx.x & 63);
+// matrix (W2p or W2Tp), the B operand from the LDS exchange (m3w_share) one
+// k-quad ahead.  A wave's block is private to it, so it streams straight from
+// L2 into a ring of eight float4 (eight k-quads = 32 MFMAs ahead), no LDS.
+__device__ __forceinline__ f32x16 m3w_contract(const float4* __restrict__ mat, int blk, const float4* xs4) {
+  const int lane = threadIdx.x & 63;
+  const float4* p = mat + (size_t)blk * 32 * 64 + lane;
+  const float4* b = xs4 + lane;
   float4 ring[8];
 #pragma unroll
-  for (int b = 0; b < 8; ++b) ring[b] = p[b * 64];
+  for (int u = 0; u < 8; ++u) ring[u] = p[u * 64];
+  float4 bn = b[0];
   f32x16 z = f32x16{};
 #pragma unroll
   for (int q = 0; q < 32; ++q) {
-    const float4 wv = ring[q & 7];
+    const float4 wv = ring[q & 7], bv = bn;
     if (q + 8 < 32) ring[q & 7] = p[(q + 8) * 64];
-    __builtin_amdgcn_sched_barrier(0);   // keep the load eight k-quads ahead (the scheduler would sink it)
-    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, bv[4 * q + 0], z, 0, 0, 0);
-    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, bv[4 * q + 1], z, 0, 0, 0);
-    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, bv[4 * q + 2], z, 0, 0, 0);
-    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, bv[4 * q + 3], z, 0, 0, 0);
+    if (q + 1 < 32) bn = b[(q + 1) * 64];
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead (the scheduler would sink them)
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, bv.x, z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, bv.y, z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, bv.z, z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, bv.w, z, 0, 0, 0);
   }
   return z;
 }
@@ -1905,7 +1915,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
                                                               const long long* __restrict__ rows,
                                                               float* __restrict__ Xg, int G, M3ValueHead vh) {
   // LDS: the X tile during layer 1, then the H1ᵀ exchange
-  extern __shared__ float lds[];   // m3w_lds_floats(Ip)
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // m3w_lds_floats(Ip)
   __shared__ float hp[kM3WWaves][A][64];
   float* xs = lds;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
@@ -1973,16 +1983,17 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
     }
   }
   __syncthreads();   // the X tile is dead: the LDS is reused below
-  float mine[16], hb[kM3Steps2];
+  float mine[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int m = 32 * w + m3_row(i, h);
     mine[i] = m3_tanh(acc[i] + b1[m]);
     m3_st(h1r, roff + (unsigned)m * kstride, mine[i]);
   }
-  m3w_share(xs, mine, hb, w);
+  float4* const xs4 = reinterpret_cast<float4*>(xs);
+  m3w_share(xs4, mine, w);
   // layer 2, block w: Z2ᵀ[w] = W2[w]·H1ᵀ
-  const f32x16 z = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip)), w, hb);
+  const f32x16 z = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip)), w, xs4);
   float hs[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) hs[a] = 0.f;
@@ -2046,7 +2057,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
 }
 
 template <int A>
-__global__ void __launch_bounds__(kM3WBlock) mlp3w_bwd_kernel(long long K, const float* __restrict__ dout,
+__global__ void __launch_bounds__(kM3WBlock) __attribute__((amdgpu_waves_per_eu(A <= 2 ? 4 : 1))) mlp3w_bwd_kernel(long long K, const float* __restrict__ dout,
                                                               const float* __restrict__ H1T,
                                                               const float* __restrict__ H2T,
                                                               const float* __restrict__ pack, int Ip,
@@ -2054,7 +2065,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_bwd_kernel(long long K, const
                                                               float* __restrict__ dZ1T, float* __restrict__ partA,
                                                               float* __restrict__ partB) {
   constexpr int N = kM3N, PA = N + A * N + A;
-  __shared__ float xs[kM3Steps2 * 64];
+  __shared__ __attribute__((aligned(16))) float xs[kM3Steps2 * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   const long long r = (long long)blockIdx.x * 32 + c;
   const bool rv = r < K;
@@ -2099,10 +2110,10 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_bwd_kernel(long long K, const
 #pragma unroll
     for (int a = 0; a < A; ++a) pa[N + a * N + m] = sdw[a];
   }
-  float zb[kM3Steps2];
-  m3w_share(xs, mine, zb, w);
+  float4* const xs4 = reinterpret_cast<float4*>(xs);
+  m3w_share(xs4, mine, w);
   // dH1ᵀ block w = (W2ᵀ)[w]·dZ2ᵀ; dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²)
-  const f32x16 d = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip) + m3_w2_floats()), w, zb);
+  const f32x16 d = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip) + m3_w2_floats()), w, xs4);
   float z1[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -2393,6 +2404,18 @@ int qs_mlp_sum_partials_multi(int32_t n, const int32_t* G, const int64_t* P, con
 // with scripts/mlp3_fwd_probe.py: K 65 536 × I 72 116.5 µs vs 133.6 wide,
 // K 40 960 × I 119 127.4 vs 96.7)
 static bool m3_wide(int64_t K, int32_t I) { return K < 16384 || I > (K >= 65536 ? 72 : 64); }
+// The forward's choice (it leaves no partials, so it need not follow the
+// backward's tiles): the 8-wave kernel at every shape since its exchange moved
+// to LDS (101 VGPRs, two workgroups per CU) — C3 / C4 / C5 rollout 180 / 82 /
+// 111 µs against the 4-wave kernel's 186 / 127 / 115 (scripts/mlp3_fwd_probe.py).
+static bool m3_wide_fwd(int64_t K, int32_t I) {
+#ifdef QS_M3_FORCE_WIDE   // dev probe: every forward on the 8-wave (1) or the 4-wave (0) kernels
+  return QS_M3_FORCE_WIDE || (void(K), void(I), false);
+#else
+  (void)K; (void)I;
+  return true;
+#endif
+}
 int32_t qs_mlp3_tiles(int64_t K, int32_t I) { return (int32_t)(m3_wide(K, I) ? (K + 31) / 32 : (K + 127) / 128); }   // partial rows
 
 int64_t qs_mlp3_pack_floats(int32_t I) {
@@ -2418,7 +2441,7 @@ static int mlp3_fwd_launch(int64_t K, int32_t I, int32_t N, int32_t A, const flo
     return fail(QS_E_INVALID, std::string(name) + ": bad argument (N must be 256, 1 <= A <= 4, I <= 1024)");
   if (G < 1 || (G > 1 && Xg)) return fail(QS_E_INVALID, std::string(name) + ": bad group size");
   // the row-gathering form with a gathered copy (G = 1) is the 8-wave kernel's
-  const bool wide = (rows && G == 1) || m3_wide(K, I);
+  const bool wide = (rows && G == 1) || m3_wide_fwd(K, I);
   if (vh.dv && (!wide || A != 1)) return fail(QS_E_INVALID, std::string(name) + ": the value head needs the 8-wave kernel and A = 1");
   const unsigned grid = (unsigned)(wide ? (K + 31) / 32 : qs_mlp3_tiles(K, I));
   const unsigned lds = wide ? (unsigned)(m3w_lds_floats((I + 31) & ~31) * sizeof(float)) : 0u;

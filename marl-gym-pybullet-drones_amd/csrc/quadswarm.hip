@@ -144,7 +144,7 @@ struct qs_handle {
   int* err = nullptr;
   unsigned long long* stamps = nullptr;   // dev-only (QS_STAMPS)
   int* rq = nullptr;            // deferred reset-search queue (header + one 128-B record per env), MultiHover layouts that can reject
-  int32_t* rpre = nullptr;      // [E] next chunk of each env's precomputed reset search
+  int32_t* rpre = nullptr;      // [E] each env's precomputed next-episode reset search (qs::kPreFound)
   bool reject_free = false;     // MultiHover layout whose reset draws can never be rejected
   int num_cu = 256;             // compute units of the device (LDS residency plan)
   qs::LogWork* logw = nullptr;  // qs_episode_log's device scratch
@@ -234,21 +234,10 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   if (!ok) return fail(QS_E_INVALID, "launch: bad act_type");
   HIP_TRY(hipGetLastError());
   if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none)
-    // Workgroups claim chunks of the queued envs' tries dynamically; the grid is
-    // sized from E so a small shard does not pay 1024 empty workgroups every step.
-#ifdef QS_DEV_BUILD
-    static const int cap = [] {   // dev knob QS_RESET_GRID: the search grid's workgroup cap
-      const char* v = getenv("QS_RESET_GRID");
-      const int c = v ? atoi(v) : 0;
-      return c >= 64 && c <= 16384 ? c : 1024;
-    }();
-#else
-    constexpr int cap = 1024;
-#endif
-    // kQueueWG workgroups for the queue, then one per env for the precomputed
-    // resets
-    const int rgrid = P.reset_pre ? qs::kQueueWG + std::min(4 * cap, P.E)
-                                  : std::min(cap, std::max(64, P.E * 4));
+    // Workgroups claim chunks of the queued envs' tries dynamically; kQueueWG
+    // workgroups for the queue, then one per env (up to 4 096, grid-strided
+    // beyond) for the precomputed resets
+    const int rgrid = qs::kQueueWG + std::min(4096, P.E);
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }

@@ -54,9 +54,9 @@ namespace qs {
 constexpr int kBlock = 64;
 // Per-env record, kEnvRec int32 words: the QS_ENV_FIELDS counters (words 0-3,
 // QS_E_* order), the episode return as f64 (words 4-5), the number of episodes
-// this env has logged (word 6, kEnvLogWord), the precomputed reset of its next
-// episode (word 7, kEnvPreWord: bit 31 set, episode & 0x7f in bits 24-30, the
-// first accepted MultiHover reset try in bits 0-23; reset_search_kernel).  32 B per env
+// this env has logged (word 6, kEnvLogWord), word 7 spare (zero; the
+// precomputed resets live in their own array, Params::reset_pre, which the
+// step kernel only reads, so no search need race the record's store).  32 B per env
 // make a wave's envs (D = 8) one 256-B span, loaded and stored whole: written
 // field by field, [field][E] arrays took partial-line writes.
 constexpr int kEnvRec = 8;
@@ -65,6 +65,13 @@ constexpr int kEnvLogWord = 6;
 constexpr int kEnvPreWord = 7;
 constexpr uint32_t kMaxResetTries = 1u << 24;
 constexpr int kResetNoneDev = 0x7f7f7f7f;   // deferred reset search: "no accepted try yet"
+// reset_pre[e]: the precomputed search for episode ep of env e (written only by
+// reset_precompute in reset_search_kernel).  Bits 24-30 hold ep & 0x7f (the tag: a word whose tag
+// is not the episode being entered is void, so nothing need clear it when the
+// env resets); bit 31 set: bits 0-23 are ep's first accepted try; clear: bits
+// 0-23 count the 256-try chunks (tries 0 .. 256·c − 1) already rejected.
+constexpr uint32_t kPreFound = 0x80000000u;
+__device__ __forceinline__ bool pre_tag_is(int32_t w, uint32_t ep) { return (((uint32_t)w >> 24) & 0x7fu) == (ep & 0x7fu); }
 // deferred reset search queue (reset_search_kernel): 128-B lines of int32
 // words in `reset_queue` — line 0 {count, envs written}, line 1 + slot {claim
 // word (u64: chunks claimed | best try << 32), env id, gang}
@@ -244,7 +251,7 @@ template <class T> struct Params {
   int* err;               // [1] reset search overflow flag
   int* reset_queue;       // deferred MultiHover reset searches (reset_search_kernel's records); or NULL
   int reject_free;        // MultiHover layout whose reset draws can never be rejected: try 0 is the reset
-  int32_t* reset_pre;     // [E] next chunk of each env's precomputed next-episode reset search; or NULL
+  int32_t* reset_pre;     // [E] each env's precomputed next-episode reset search (kPre* encoding); or NULL
   int stage_rows;         // obs rows staged in LDS per pass
   unsigned long long* stamps;   // dev builds only (QS_STAMPS_BUILD)
   // per-step I/O
@@ -747,10 +754,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   int32_t total = (int32_t)c23.x, ep_len = (int32_t)c23.y;
   const double ep_ret0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvRetWord * 4, 0));
   const v2u_t c67 = __builtin_amdgcn_raw_buffer_load_b64(env_r, (int)ev, kEnvLogWord * 4, 0);
-  const int32_t log_n0 = (int32_t)c67.x, pre0 = (int32_t)c67.y;
-  // the precomputed search's progress (256-try chunks all rejected), so a queued
-  // env's search starts past them; a null buffer reads 0 (num_records 0)
-  const int32_t pre_c = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
+  const int32_t log_n0 = (int32_t)c67.x;
+  // the precomputed search (kPreFound encoding): the next episode's try, or the
+  // chunks it has rejected so far, so a queued env's search starts past them; a
+  // null buffer reads 0 (num_records 0)
+  const int32_t pre0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
       rsrc(P.reset_pre, P.reset_pre ? E * 4u : 0u), valid ? (int)(e * 4u) : (int)kOOB, 0, 0);
   issue_fence();
   T pos[3], q[4], vel[3], w[3], lrpm[4], pid[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tgt[3] = {0, 0, 0};
@@ -1505,10 +1513,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         if (do_reset && !qs_dev::kNoResetDraw)
           reset_candidate(P, orig, d, 0u, genv, (uint32_t)episode, init[0], init[1], init[2]);
       } else {
-        // The next episode's first accepted try, when reset_search_kernel has
-        // found it ahead of time (word 7 of the env record, for this episode)
+        // The next episode's first accepted try, when reset_search_kernel's
+        // precompute has found it ahead of time (reset_pre, tagged with this episode)
         const bool pre_ok = P.reset_pre && P.mode != MODE_RESET_ALL && do_reset && pre0 < 0 &&
-                            ((pre0 >> 24) & 0x7f) == (episode & 0x7f);
+                            pre_tag_is(pre0, (uint32_t)episode);
         if (pre_ok) reset_candidate(P, orig, d, (uint32_t)pre0 & 0xffffffu, genv, (uint32_t)episode, init[0], init[1], init[2]);
         // Phase 1: every other group tries index 0 for its own env.
         if (tid < P.EPB) { s.reject[tid] = 0; s.win_try[tid] = 0; }
@@ -1534,6 +1542,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
             // claim word {chunks claimed, best try none}, env id, gang 0.  The
             // precomputed search rejected tries [0, 256·pre_c): the claims start at
             // the chunk (tries 1 + 256k … 256k + 256) that holds try 256·pre_c
+            const int pre_c = pre0 >= 0 && pre_tag_is(pre0, (uint32_t)episode) ? (pre0 & 0xffffff) : 0;
             const int k0 = pre_c > 0 ? pre_c - 1 : 0;
             *reinterpret_cast<int4*>(P.reset_queue + kRqLine * (1 + slot)) =
                 make_int4(k0, kResetNoneDev, (int)(blockIdx.x * P.EPB + lenv), 0);
@@ -1639,9 +1648,9 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     r[QS_E_STEP_COUNTER] = step_counter; r[QS_E_EPISODE] = episode; r[QS_E_TOTAL_STEPS] = total;
     r[QS_E_EP_LEN] = ep_len_out;
     r[kEnvRetWord] = (int32_t)(unsigned)rb; r[kEnvRetWord + 1] = (int32_t)(unsigned)(rb >> 32);
-    // a reset consumes the precomputed try (the next search starts over)
-    r[kEnvLogWord] = log_n; r[kEnvPreWord] = do_reset ? 0 : pre0;
-    if (P.reset_pre && do_reset) P.reset_pre[e] = 0;
+    // (a reset voids the precomputed word by its tag: the next search is for
+    // the episode after this one)
+    r[kEnvLogWord] = log_n; r[kEnvPreWord] = 0;
   }
   __syncthreads();
   {
@@ -1708,18 +1717,103 @@ __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
   atomicMin(w, ((unsigned long long)(unsigned)t << 32) | 0x7fffffffull);
 }
 
+// One chunk of an env's tries, [base, base + kResetChunk), one per thread:
+// returns the smallest accepted try of the chunk (kResetNone if none;
+// workgroup-uniform) — with the chunks taken in order, the sequential loop's
+// first accepted try.  Drones 0-1 and their pair test first; the tries that
+// pass it (18.6 % for C2's layout) are compacted into the first lanes (their
+// two draws kept in LDS) and draw drones 2.. there, so a try the first pair
+// rejects costs two Philox draws instead of D: every wave kept drawing all D
+// while any of its 64 tries was alive, which is nearly always.  The accept
+// test is the same conjunction of z and pair tests in either order.  claim_in
+// (thread 0's value) comes back to every thread in *claim_out after the
+// chunk, for the queue loop's claim issued one chunk ahead.
+template <class T> struct ResetLds {
+  T p[kResetChunk][6];   // the compacted tries' drone 0-1 positions
+  int t[kResetChunk];
+  int cnt, win;
+  unsigned long long claim;
+};
+template <class T>
+__device__ int reset_chunk(const Params<T>& P, const T (&orig)[kResetMaxD][3], uint32_t base, uint32_t genv,
+                           uint32_t ep, ResetLds<T>& L, unsigned long long claim_in = 0,
+                           unsigned long long* claim_out = nullptr) {
+  const int D = P.D, tid = threadIdx.x;
+  const uint32_t t = base + (uint32_t)tid;
+  if (tid == 0) { L.cnt = 0; L.win = kResetNone; }
+  bool ok = t < kMaxResetTries;
+  T a[3] = {T(0), T(0), T(0)}, b[3] = {T(0), T(0), T(0)};
+  if (ok) {
+    reset_candidate(P, orig[0], 0, t, genv, ep, a[0], a[1], a[2]);
+    if (a[2] < T(0.1)) ok = false;
+  }
+  if (D > 1 && ok) {
+    reset_candidate(P, orig[1], 1, t, genv, ep, b[0], b[1], b[2]);
+    if (b[2] < T(0.1) || too_close(a[0], a[1], a[2], b[0], b[1], b[2])) ok = false;
+  }
+  __syncthreads();   // L.cnt / L.win initialised
+  if (D <= 2) {
+    if (ok) atomicMin(&L.win, (int)t);
+  } else {
+    // wave-aggregated slots: one LDS add per wave, the lanes' ranks from mbcnt
+    const unsigned long long m = __ballot(ok);
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    int wb = 0;
+    if ((tid & 63) == 0 && m) wb = atomicAdd(&L.cnt, __popcll(m));
+    wb = __shfl(wb, 0);
+    if (ok) {
+      const int s = wb + lane;
+      L.t[s] = (int)t;
+      L.p[s][0] = a[0]; L.p[s][1] = a[1]; L.p[s][2] = a[2];
+      L.p[s][3] = b[0]; L.p[s][4] = b[1]; L.p[s][5] = b[2];
+    }
+    __syncthreads();
+    if (tid < L.cnt) {
+      const uint32_t tt = (uint32_t)L.t[tid];
+      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
+      px[0] = L.p[tid][0]; py[0] = L.p[tid][1]; pz[0] = L.p[tid][2];
+      px[1] = L.p[tid][3]; py[1] = L.p[tid][4]; pz[1] = L.p[tid][5];
+      bool ok2 = true;
+#pragma unroll
+      for (int d = 2; d < kResetMaxD; ++d) {
+        if (d < D && ok2) {
+          reset_candidate(P, orig[d], d, tt, genv, ep, px[d], py[d], pz[d]);
+          if (pz[d] < T(0.1)) ok2 = false;
+#pragma unroll
+          for (int i = 0; i < d; ++i)
+            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok2 = false;
+        }
+      }
+      if (ok2) atomicMin(&L.win, (int)tt);
+    }
+  }
+  if (tid == 0) L.claim = claim_in;
+  __syncthreads();
+  const int w = L.win;
+  if (claim_out) *claim_out = L.claim;
+  __syncthreads();   // L is rewritten by the next chunk
+  return w;
+}
+
 // The precomputed resets: an env's next-episode reset draw depends only on
 // (seed, env, episode), so the search for it need not wait for the reset.
-// One workgroup per env (the launch's workgroups past the first kQueueWG):
-// each launch it tests kPreChunks chunks of 256 tries (tries 256·c + t, try 0
-// included) of its env when word 7 of the env record holds no try for the
-// next episode, continuing at chunk reset_pre[e]; the first accepted try goes
-// into word 7, and the step kernel that resets the env into that episode uses
-// it instead of testing try 0 — the first accepted try of MH:83-102, as the
-// queue search finds it.  No atomics.  An env that resets before its search
-// ends takes the step kernel's own path (try 0, then the queue, whose claims
-// start past the chunks tested here).  (One wave per env, 64 tries a step:
-// the serial Philox chain of a lone wave made 8 steps cost 25 µs a launch.)
+// The search launch's workgroups past the queue's, grid-strided over the
+// envs, one workgroup at a time: an env whose
+// reset_pre word holds no try for its next episode gets kPreChunks chunks of
+// 256 tries (chunk c: tries 256·c + t, try 0 included), continuing at the
+// word's chunk count when its tag is that episode's; the first accepted try
+// goes into the word with kPreFound, and the step kernel that resets the env
+// into that episode draws it instead of testing try 0 — the first accepted
+// try of MH:83-102, as the queue search finds it.  No atomics, and nothing
+// for the step to clear: a reset voids the word by its tag (the search for the
+// episode after it starts at chunk 0), so a precompute running beside the step
+// could not race it either (measured as a parallel graph branch on a second
+// stream: no overlap — 28.1 against 28.8 µs per C2 step serial).
+// An env that resets before
+// its search ends takes the step kernel's own path (try 0, then the queue,
+// whose claims start past the chunks tested here).  (One wave per env, 64
+// tries a step: the serial Philox chain of a lone wave made 8 steps cost
+// 25 µs a launch.)
 #ifndef QS_PRE_CHUNKS
 #define QS_PRE_CHUNKS 2
 #endif
@@ -1727,69 +1821,62 @@ __device__ __forceinline__ void rq_publish(unsigned long long* w, int t) {
 #define QS_QUEUE_WG 256
 #endif
 constexpr int kPreChunks = QS_PRE_CHUNKS;
-constexpr int kQueueWG = QS_QUEUE_WG;   // workgroups of the search launch that serve the queue (the rest precompute)
+constexpr int kQueueWG = QS_QUEUE_WG;   // workgroups of the queue search launch
+
 template <class T>
-__device__ void reset_precompute(const Params<T>& P, const T (&orig)[kResetMaxD][3], int first, int stride) {
-  __shared__ int s_pw;
-  const int D = P.D, tid = threadIdx.x;
-  for (int e = first; e < P.E; e += stride) {   // workgroup-uniform
-    int32_t* const rec = P.env + (size_t)e * kEnvRec;
-    // the record's two halves and the chunk counter in one round trip
-    const int4 r0 = *reinterpret_cast<const int4*>(rec), r1 = *reinterpret_cast<const int4*>(rec + 4);
-    int c = P.reset_pre[e];
-    if (r1.w < 0) continue;   // word 7: found already
-    const uint32_t ep = (uint32_t)r0.y + 1u, genv = (uint32_t)(P.env_offset + e);   // r0.y: QS_E_EPISODE
-    for (int k = 0; k < kPreChunks; ++k, ++c) {
-      if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
-      const uint32_t t = (uint32_t)c * kResetChunk + (uint32_t)tid;
-      bool ok = true;
-      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
+__device__ __forceinline__ void reset_orig(const Params<T>& P, T (&orig)[kResetMaxD][3]) {
 #pragma unroll
-      for (int d = 0; d < kResetMaxD; ++d) {
-        if (d < D && ok) {
-          reset_candidate(P, orig[d], d, t, genv, ep, px[d], py[d], pz[d]);
-          if (pz[d] < T(0.1)) ok = false;
+  for (int d = 0; d < kResetMaxD; ++d)
 #pragma unroll
-          for (int i = 0; i < d; ++i)
-            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
-        }
-      }
-      if (tid == 0) s_pw = kResetNone;
-      __syncthreads();
-      if (ok) atomicMin(&s_pw, (int)t);
-      __syncthreads();
-      const int w = s_pw;
-      __syncthreads();
-      if (w != kResetNone) {
-        if (tid == 0) rec[kEnvPreWord] = (int32_t)(0x80000000u | ((ep & 0x7fu) << 24) | (uint32_t)w);
-        c = -1;
-        break;
-      }
-    }
-    if (tid == 0 && c >= 0) P.reset_pre[e] = c;
-  }
+    for (int k = 0; k < 3; ++k) orig[d][k] = d < P.D ? P.orig_xyz[d * 3 + k] : T(0);
 }
 
 template <class T>
+__device__ void reset_precompute(const Params<T>& P, ResetLds<T>& L, int first, int stride) {
+  const int tid = threadIdx.x;
+  T orig[kResetMaxD][3];
+  reset_orig(P, orig);
+  for (int e = first; e < P.E; e += stride) {   // workgroup-uniform
+    const uint32_t ep = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE] + 1u;
+    const int32_t w0 = P.reset_pre[e];
+    const bool mine = pre_tag_is(w0, ep);   // else void: ep's search starts at chunk 0
+    if (mine && w0 < 0) continue;           // found already
+    int c = mine ? (w0 & 0xffffff) : 0;
+    const uint32_t genv = (uint32_t)(P.env_offset + e), tag = (ep & 0x7fu) << 24;
+    int found = kResetNone;
+    for (int k = 0; k < kPreChunks; ++k, ++c) {
+      if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
+      found = reset_chunk(P, orig, (uint32_t)c * kResetChunk, genv, ep, L);
+      if (found != kResetNone) break;
+    }
+    if (tid == 0)
+      P.reset_pre[e] = (int32_t)(found != kResetNone ? kPreFound | tag | (uint32_t)found : tag | (uint32_t)c);
+  }
+}
+
+// The search launch: its first kQueueWG workgroups serve the queue (G of
+// them), the others precompute (with reset_pre), so neither waits for the other.
+template <class T>
 __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) {
+  __shared__ ResetLds<T> L;
   __shared__ unsigned long long s_claim;
-  __shared__ int s_win, s_fin;
+  __shared__ int s_fin;
+  const int G = P.reset_pre ? min((int)gridDim.x, kQueueWG) : (int)gridDim.x;
+  if ((int)blockIdx.x >= G) {
+    reset_precompute(P, L, (int)blockIdx.x - G, (int)gridDim.x - G);
+    return;
+  }
   int* const rq = P.reset_queue;
   const int n = rq[0];
   const int D = P.D;
   const int tid = threadIdx.x;
+  if (n == 0) return;   // nothing queued: the usual step
   T orig[kResetMaxD][3];
-#pragma unroll
-  for (int d = 0; d < kResetMaxD; ++d)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) orig[d][k] = d < D ? P.orig_xyz[d * 3 + k] : T(0);
-  const int home = n > 0 ? (int)(blockIdx.x % (unsigned)n) : 0;
-  // With the precomputed resets the first kQueueWG workgroups serve the queue
-  // and the others precompute (so neither waits for the other).  More envs than
-  // queue workgroups (a reset of every env): workgroup b takes envs b, b + G,
-  // b + 2G, … in turn.
-  const int G = P.reset_pre ? min((int)gridDim.x, kQueueWG) : (int)gridDim.x;
-  int idx = n > 0 && (int)blockIdx.x < min(G, n * kResetGang) ? home : -1;   // nothing queued: the usual step
+  reset_orig(P, orig);
+  const int home = (int)(blockIdx.x % (unsigned)n);
+  // More envs than queue workgroups (a reset of every env): workgroup b takes
+  // envs b, b + G, b + 2G, … in turn.
+  int idx = (int)blockIdx.x < min(G, n * kResetGang) ? home : -1;
   QS_RS_BEGIN();
   while (idx >= 0) {
     int* const r = rq + kRqLine * (1 + idx);
@@ -1817,27 +1904,7 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
       if (base >= (long long)kMaxResetTries) break;
       unsigned long long cw_next = 0;
       if (tid == 0) cw_next = rq_claim(cwp);   // one chunk ahead: used after this chunk's tries
-      const uint32_t t = (uint32_t)base + (uint32_t)tid;
-      bool ok = t < kMaxResetTries;
-      T px[kResetMaxD], py[kResetMaxD], pz[kResetMaxD];
-#pragma unroll
-      for (int d = 0; d < kResetMaxD; ++d) {
-        if (d < D && ok) {
-          reset_candidate(P, orig[d], d, t, genv, episode, px[d], py[d], pz[d]);
-          if (pz[d] < T(0.1)) ok = false;
-#pragma unroll
-          for (int i = 0; i < d; ++i)
-            if (too_close(px[i], py[i], pz[i], px[d], py[d], pz[d])) ok = false;
-        }
-      }
-      if (tid == 0) s_win = kResetNone;
-      __syncthreads();
-      if (ok) atomicMin(&s_win, (int)t);
-      if (tid == 0) s_claim = cw_next;
-      __syncthreads();
-      const int w = s_win;
-      cw = s_claim;
-      __syncthreads();   // s_win / s_claim are rewritten next chunk
+      const int w = reset_chunk(P, orig, (uint32_t)base, genv, episode, L, cw_next, &cw);
       if (w != kResetNone) {
         found = w;       // the claim ahead is above w: the loop test leaves
         if (tid == 0) rq_publish(cwp, w);
@@ -1885,11 +1952,11 @@ __global__ void __launch_bounds__(kResetBlock) reset_search_kernel(Params<T> P) 
         if (atomicAdd(&rq[1], 1) == n - 1) { rq[0] = 0; rq[1] = 0; }
       }
     }
+    __syncthreads();   // s_fin / s_claim are rewritten by the next slot
     idx = idx + G < n ? idx + G : -1;
     QS_RS_PICK();
   }
   QS_RS_END(n);
-  if (P.reset_pre && (int)blockIdx.x >= G) reset_precompute(P, orig, (int)blockIdx.x - G, (int)gridDim.x - G);
 }
 
 }  // namespace qs
