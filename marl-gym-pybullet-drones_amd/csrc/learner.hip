@@ -1892,6 +1892,48 @@ __device__ __forceinline__ f32x16 m3w_contract(const float4* __restrict__ mat, i
   return z;
 }
 
+// The register-held exchange (round 4): every lane holds the 128 B-operand
+// steps of the contraction.  Kept for the backward, where the LDS exchange
+// measured slower beside the fused actor (the C3 update: the critic's 8-wave
+// backward shares the CUs with the actor chain's kernels); dev builds select
+// either per kernel (QS_M3W_FWD_REGS / QS_M3W_BWD_LDS).
+__device__ __forceinline__ void m3w_share_regs(float* xs, const float* mine, float* all, int w) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xs[(w * 16 + i) * 64 + lane] = mine[i];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kM3Steps2; ++k) all[k] = xs[k * 64 + lane];
+}
+__device__ __forceinline__ f32x16 m3w_contract_regs(const float4* __restrict__ mat, int blk, const float* bv) {
+  const float4* p = mat + (size_t)blk * 32 * 64 + (threadIdx.x & 63);
+  float4 ring[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) ring[b] = p[b * 64];
+  f32x16 z = f32x16{};
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const float4 wv = ring[q & 7];
+    if (q + 8 < 32) ring[q & 7] = p[(q + 8) * 64];
+    __builtin_amdgcn_sched_barrier(0);   // keep the load eight k-quads ahead (the scheduler would sink it)
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.x, bv[4 * q + 0], z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.y, bv[4 * q + 1], z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.z, bv[4 * q + 2], z, 0, 0, 0);
+    z = __builtin_amdgcn_mfma_f32_32x32x2f32(wv.w, bv[4 * q + 3], z, 0, 0, 0);
+  }
+  return z;
+}
+#ifdef QS_M3W_FWD_REGS
+constexpr bool kM3wFwdLds = false;
+#else
+constexpr bool kM3wFwdLds = true;
+#endif
+#ifdef QS_M3W_BWD_LDS
+constexpr bool kM3wBwdLds = true;
+#else
+constexpr bool kM3wBwdLds = false;
+#endif
+
 // The centralized critic's value head folded into its forward (qs_mlp3_fwd_rows_value):
 // compute_value_loss (AG:642-683) per row as qs_value_head does it, its loss sum
 // from the last workgroup.  dv == NULL: the plain forward.
@@ -1990,10 +2032,17 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
     mine[i] = m3_tanh(acc[i] + b1[m]);
     m3_st(h1r, roff + (unsigned)m * kstride, mine[i]);
   }
-  float4* const xs4 = reinterpret_cast<float4*>(xs);
-  m3w_share(xs4, mine, w);
   // layer 2, block w: Z2ᵀ[w] = W2[w]·H1ᵀ
-  const f32x16 z = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip)), w, xs4);
+  f32x16 z;
+  if constexpr (kM3wFwdLds) {
+    float4* const xs4 = reinterpret_cast<float4*>(xs);
+    m3w_share(xs4, mine, w);
+    z = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip)), w, xs4);
+  } else {
+    float hb[kM3Steps2];
+    m3w_share_regs(xs, mine, hb, w);
+    z = m3w_contract_regs(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip)), w, hb);
+  }
   float hs[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) hs[a] = 0.f;
@@ -2057,7 +2106,7 @@ __global__ void __launch_bounds__(kM3WBlock) mlp3w_fwd_kernel(long long K, int I
 }
 
 template <int A>
-__global__ void __launch_bounds__(kM3WBlock) __attribute__((amdgpu_waves_per_eu(A <= 2 ? 4 : 1))) mlp3w_bwd_kernel(long long K, const float* __restrict__ dout,
+__global__ void __launch_bounds__(kM3WBlock) __attribute__((amdgpu_waves_per_eu(kM3wBwdLds && A <= 2 ? 4 : 1))) mlp3w_bwd_kernel(long long K, const float* __restrict__ dout,
                                                               const float* __restrict__ H1T,
                                                               const float* __restrict__ H2T,
                                                               const float* __restrict__ pack, int Ip,
@@ -2110,10 +2159,18 @@ __global__ void __launch_bounds__(kM3WBlock) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int a = 0; a < A; ++a) pa[N + a * N + m] = sdw[a];
   }
-  float4* const xs4 = reinterpret_cast<float4*>(xs);
-  m3w_share(xs4, mine, w);
   // dH1ᵀ block w = (W2ᵀ)[w]·dZ2ᵀ; dZ1ᵀ = dH1ᵀ ⊙ (1 − H1ᵀ²)
-  const f32x16 d = m3w_contract(reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip) + m3_w2_floats()), w, xs4);
+  const float4* const w2t = reinterpret_cast<const float4*>(pack + m3_w1p_floats(Ip) + m3_w2_floats());
+  f32x16 d;
+  if constexpr (kM3wBwdLds) {
+    float4* const xs4 = reinterpret_cast<float4*>(xs);
+    m3w_share(xs4, mine, w);
+    d = m3w_contract(w2t, w, xs4);
+  } else {
+    float zb[kM3Steps2];
+    m3w_share_regs(xs, mine, zb, w);
+    d = m3w_contract_regs(w2t, w, zb);
+  }
   float z1[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
