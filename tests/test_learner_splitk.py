@@ -129,7 +129,8 @@ def test_group_rows_forward_bit_identical(envsteps, D, din, A):
     """qs_mlp3_fwd_group_rows (batch row r = table row rows[r // D]·D + r % D, the
     actor's minibatch read from the rollout table) against qs_mlp3_fwd on the
     gathered rows: the same kernel arithmetic, so identical bits (outputs and the
-    saved activations); 4-wave kernel at 32 768 rows, 8-wave kernel below."""
+    saved activations); the 8-wave kernel at every size (the forward's choice
+    since round 5)."""
     from gym_pybullet_drones_amd.mappo.agent import _M3Work
     torch.manual_seed(3)
     net = MLP(din, A, [256, 256], act='tanh').cuda()
