@@ -235,9 +235,9 @@ template <class T> static int launch(qs_handle* h, qs::Params<T>& P, hipStream_t
   HIP_TRY(hipGetLastError());
   if (P.reset_queue) {   // the envs whose try 0 was rejected (usually none)
     // Workgroups claim chunks of the queued envs' tries dynamically; kQueueWG
-    // workgroups for the queue, then one per env (up to 4 096, grid-strided
-    // beyond) for the precomputed resets
-    const int rgrid = qs::kQueueWG + std::min(4096, P.E);
+    // workgroups for the queue, then one per kPreEnvs envs (up to 4 096 envs,
+    // grid-strided beyond) for the precomputed resets
+    const int rgrid = qs::kQueueWG + std::min(4096 / qs::kPreEnvs, (P.E + qs::kPreEnvs - 1) / qs::kPreEnvs);
     hipLaunchKernelGGL(qs::reset_search_kernel<T>, dim3(rgrid), dim3(qs::kResetBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
   }

@@ -1822,6 +1822,10 @@ __device__ int reset_chunk(const Params<T>& P, const T (&orig)[kResetMaxD][3], u
 #endif
 constexpr int kPreChunks = QS_PRE_CHUNKS;
 constexpr int kQueueWG = QS_QUEUE_WG;   // workgroups of the queue search launch
+#ifndef QS_PRE_ENVS
+#define QS_PRE_ENVS 1   // measured: 2 / 4 envs per workgroup made C2 23.5 / 26.9 µs per step (1: 22.2)
+#endif
+constexpr int kPreEnvs = QS_PRE_ENVS;   // envs per precompute workgroup
 
 template <class T>
 __device__ __forceinline__ void reset_orig(const Params<T>& P, T (&orig)[kResetMaxD][3]) {
@@ -1836,21 +1840,34 @@ __device__ void reset_precompute(const Params<T>& P, ResetLds<T>& L, int first, 
   const int tid = threadIdx.x;
   T orig[kResetMaxD][3];
   reset_orig(P, orig);
-  for (int e = first; e < P.E; e += stride) {   // workgroup-uniform
-    const uint32_t ep = (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE] + 1u;
-    const int32_t w0 = P.reset_pre[e];
-    const bool mine = pre_tag_is(w0, ep);   // else void: ep's search starts at chunk 0
-    if (mine && w0 < 0) continue;           // found already
-    int c = mine ? (w0 & 0xffffff) : 0;
-    const uint32_t genv = (uint32_t)(P.env_offset + e), tag = (ep & 0x7fu) << 24;
-    int found = kResetNone;
-    for (int k = 0; k < kPreChunks; ++k, ++c) {
-      if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
-      found = reset_chunk(P, orig, (uint32_t)c * kResetChunk, genv, ep, L);
-      if (found != kResetNone) break;
+  // kPreEnvs envs per workgroup (first + j·stride), their episode and word
+  // loaded together (one env per workgroup measured fastest: the launch is
+  // bound by its slowest workgroup's chunks, not by the dispatch)
+  for (int e0 = first; e0 < P.E; e0 += stride * kPreEnvs) {   // workgroup-uniform
+    uint32_t ep[kPreEnvs];
+    int32_t w0[kPreEnvs];
+#pragma unroll
+    for (int j = 0; j < kPreEnvs; ++j) {
+      const int e = e0 + j * stride;
+      ep[j] = e < P.E ? (uint32_t)P.env[(size_t)e * kEnvRec + QS_E_EPISODE] + 1u : 0u;
+      w0[j] = e < P.E ? P.reset_pre[e] : 0;
     }
-    if (tid == 0)
-      P.reset_pre[e] = (int32_t)(found != kResetNone ? kPreFound | tag | (uint32_t)found : tag | (uint32_t)c);
+#pragma unroll
+    for (int j = 0; j < kPreEnvs; ++j) {
+      const int e = e0 + j * stride;
+      const bool mine = pre_tag_is(w0[j], ep[j]);   // else void: the search starts at chunk 0
+      if (e >= P.E || (mine && w0[j] < 0)) continue;   // found already
+      int c = mine ? (w0[j] & 0xffffff) : 0;
+      const uint32_t genv = (uint32_t)(P.env_offset + e), tag = (ep[j] & 0x7fu) << 24;
+      int found = kResetNone;
+      for (int k = 0; k < kPreChunks; ++k, ++c) {
+        if ((uint32_t)c * kResetChunk >= kMaxResetTries) break;   // none below the cap: the step's own path flags it
+        found = reset_chunk(P, orig, (uint32_t)c * kResetChunk, genv, ep[j], L);
+        if (found != kResetNone) break;
+      }
+      if (tid == 0)
+        P.reset_pre[e] = (int32_t)(found != kResetNone ? kPreFound | tag | (uint32_t)found : tag | (uint32_t)c);
+    }
   }
 }
 
