@@ -260,6 +260,12 @@ def main():
                   dict(critic_tiles=False, critic_after_actor=True)):
             us, path = per_minibatch_us("C4", **v)
             print(f"C4  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+    if "ct" in which:   # the critic on the tile launch (qs_ppo_critic_tiles) vs the 8-wave kernels, interleaved
+        for shape in ("C3", "C4"):
+            for v in (dict(critic_tiles=False), dict(critic_tiles=True), dict(critic_tiles=False),
+                      dict(critic_tiles=True)):
+                us, path = per_minibatch_us(shape, **v)
+                print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "ablate" in which:
         ablate()
     if "ablate4" in which:
