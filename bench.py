@@ -602,7 +602,9 @@ def mappo_leg(args, ranks, T, cfg=None, rank_shape=None):
         learner_path = ("qs_ppo_small_grads + all-reduce + qs_ppo_small_adam" if (world > 1 or rank_shape) else
                         "qs_ppo_small_step (16-row tiles, 2-3 launches per minibatch)")
     else:
-        learner_path = ("qs_mlp3f_actor + bmm dW2" if fused_actor else "qs_mlp3 actor") + (
+        fold = fused_actor and getattr(m.agent._ws_actor, "pw1f", None) is not None
+        learner_path = (("qs_mlp3f_actor_w1 (dW1 folded) + bmm dW2" if fold else "qs_mlp3f_actor + bmm dW2")
+                        if fused_actor else "qs_mlp3 actor") + (
             " | critic qs_ppo_critic_tiles + qs_wgrad_t" if type(getattr(m.agent, "_ws_critic", None)).__name__
             == "_CriticTiles" else " | critic qs_mlp3w + GEMMs")
     exchange = int(m.agent._reduce_buf.numel())   # [critic grads | actor grads | approx_kl] floats

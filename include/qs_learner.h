@@ -208,6 +208,15 @@ int qs_mlp3f_actor(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, c
                    float action_scale, const float* act, const float* logp_old, const double* adv, float clip,
                    float ent_coef, float* Xa, float* H1T, float* dZ2T, float* dZ1T, float* partA, float* partB,
                    float* dlogstd, float* kl_out, double* acc, void* work, float* mean_out, void* stream);
+/* qs_mlp3f_actor with dW1 folded in (round 5): part_w1 [qs_mlp3f_tiles(K)][256][I]
+ * receives each workgroup's Σ over its 128 rows of dZ1ᵀ·X (their fixed-order sum
+ * is the W1 gradient: qs_mlp_sum_adam); dZ1T may then be NULL (not stored). */
+int qs_mlp3f_actor_w1(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, const int64_t* idx, const float* pack,
+                      const float* b1, const float* b2, const float* W3, const float* b3, const float* logstd,
+                      float action_scale, const float* act, const float* logp_old, const double* adv, float clip,
+                      float ent_coef, float* Xa, float* H1T, float* dZ2T, float* dZ1T, float* partA, float* partB,
+                      float* dlogstd, float* kl_out, double* acc, void* work, float* mean_out, float* part_w1,
+                      void* stream);
 
 /* The value half of qs_ppo_heads (compute_value_loss AG:642-683, centralized,
  * unclipped): dv[i] = (v[i] − mean_d ret)/mb and acc[1] += 0.5·mean_i (v −

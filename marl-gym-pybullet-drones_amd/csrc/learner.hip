@@ -1145,7 +1145,7 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
     float ent_coef, float* __restrict__ Xa, float* __restrict__ H1T, float* __restrict__ dZ2T,
     float* __restrict__ dZ1T, float* __restrict__ partA, float* __restrict__ partB, double* __restrict__ lossp,
     float* __restrict__ dlogstd, float* __restrict__ kl_out, double* __restrict__ acc, unsigned* __restrict__ count,
-    float* __restrict__ mean_out) {
+    float* __restrict__ mean_out, float* __restrict__ partW1) {
   constexpr int N = kM3N, PA = f_pa(A), NL = 2 + A;   // loss sums: policy, approx_kl, d logstd[A]
   extern __shared__ float4 f_lds[];
   float* lf = reinterpret_cast<float*>(f_lds);
@@ -1167,7 +1167,8 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
   const long long ei = rv ? row / D : 0;
   const float* xrow = X + (rv ? (idx[ei] * D + (row - ei * D)) * (long long)I : 0);
   const size_t hbytes = (size_t)K * N * 4;
-  const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), z2r = m3_rsrc(dZ2T, hbytes), z1r = m3_rsrc(dZ1T, hbytes);
+  const __amdgpu_buffer_rsrc_t h1r = m3_rsrc(H1T, hbytes), z2r = m3_rsrc(dZ2T, hbytes),
+                               z1r = m3_rsrc(dZ1T, dZ1T ? hbytes : 0);   // NULL with partW1: no dZ1 stores
   // H1, dZ2, dZ1 are row-major [K][256]: a lane's block of four hidden units is 16 contiguous bytes
   const unsigned voff = rv ? (unsigned)((row * N + 4 * g) * 4) : kM3OOB;
   // One continuous chunk stream over the whole pack (W1f | W2f | W2b): chunk c + 2
@@ -1451,6 +1452,66 @@ __global__ void __launch_bounds__(kFBlock) mlp3f_actor_kernel(
 #pragma unroll
     for (int v = 1; v < kFWaves; ++v) s += spb[v * N + t];
     partB[(size_t)blockIdx.x * N + t] = s;
+  }
+  if (partW1) {   // kernel-uniform
+    // ---- dW1 = dZ1ᵀ·X over the workgroup's 128 rows, from the
+    // dZ1 still in registers: no dZ1 stores, no separate 27-column GEMM beside
+    // dW2.  The LDS is free once the partial rows above are read: the X tile
+    // [128][Ip + 16] (staged from this workgroup's own Xa rows), then dZ1 one
+    // 128-unit half at a time [128][144]; wave w contracts m-block w of the half
+    // against every k-block, 4 rows per 16x16x4 step (A: dZ1[row][m], B:
+    // X[row][k]); strides ≡ 16 mod 64 put the four rows of a read on distinct banks.
+    constexpr int DZS = 144;
+    const int XS = Ip + 16, KB = Ip / 16;   // KB <= kFMaxIp / 16 = 8
+    float* const dzs = lf;                  // [128][DZS]
+    float* const xs = lf + 128 * DZS;       // [128][XS]
+    const long long r0 = (long long)blockIdx.x * kFWaves * 16;
+    __syncthreads();   // spa / spb read
+    for (int t = tid; t < 128 * Ip; t += kFBlock) {
+      const int rr = t / Ip, k = t - rr * Ip;
+      xs[rr * XS + k] = (r0 + rr < K && k < I) ? Xa[(r0 + rr) * I + k] : 0.f;
+    }
+    const int rq = l >> 4, cq = l & 15;
+    float* const pw = partW1 + (size_t)blockIdx.x * N * I;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int bb = 0; bb < 8; ++bb)
+        *reinterpret_cast<float4*>(dzs + (w * 16 + j) * DZS + 16 * bb + 4 * g) =
+            make_float4(h1[8 * p + bb][0], h1[8 * p + bb][1], h1[8 * p + bb][2], h1[8 * p + bb][3]);
+      __syncthreads();
+      f32x4 a4[kFMaxIp / 16];
+#pragma unroll
+      for (int kb = 0; kb < kFMaxIp / 16; ++kb) a4[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // one step's operands read ahead of its MFMAs (unrolled further, the
+      // compiler hoisted every read and spilled the kernel's registers)
+      float av = dzs[rq * DZS + 16 * w + cq], xv[kFMaxIp / 16];
+#pragma unroll
+      for (int kb = 0; kb < kFMaxIp / 16; ++kb) xv[kb] = kb < KB ? xs[rq * XS + 16 * kb + cq] : 0.f;
+#pragma unroll 1
+      for (int s4 = 0; s4 < 32; ++s4) {
+        const int rn = 4 * (s4 + 1 < 32 ? s4 + 1 : s4) + rq;
+        const float an = dzs[rn * DZS + 16 * w + cq];
+        float xn[kFMaxIp / 16];
+#pragma unroll
+        for (int kb = 0; kb < kFMaxIp / 16; ++kb) xn[kb] = kb < KB ? xs[rn * XS + 16 * kb + cq] : 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kb = 0; kb < kFMaxIp / 16; ++kb)
+          if (kb < KB) a4[kb] = mfma16(av, xv[kb], a4[kb]);
+        av = an;
+#pragma unroll
+        for (int kb = 0; kb < kFMaxIp / 16; ++kb) xv[kb] = xn[kb];
+      }
+#pragma unroll
+      for (int kb = 0; kb < kFMaxIp / 16; ++kb) {
+        const int k = 16 * kb + cq;
+        if (kb < KB && k < I)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pw[(size_t)(128 * p + 16 * w + 4 * rq + r) * I + k] = a4[kb][r];
+      }
+      __syncthreads();   // dzs is rewritten by the next half
+    }
   }
   if (tid == 0) {
 #pragma unroll
@@ -2746,19 +2807,33 @@ int qs_mlp3f_actor(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, c
                    float action_scale, const float* act, const float* logp_old, const double* adv, float clip,
                    float ent_coef, float* Xa, float* H1T, float* dZ2T, float* dZ1T, float* partA, float* partB,
                    float* dlogstd, float* kl_out, double* acc, void* work, float* mean_out, void* stream) {
+  if (!dZ1T) return fail(QS_E_INVALID, "qs_mlp3f_actor: dZ1T is NULL (qs_mlp3f_actor_w1 folds dW1 instead)");
+  return qs_mlp3f_actor_w1(K, I, D, A, X, idx, pack, b1, b2, W3, b3, logstd, action_scale, act, logp_old, adv, clip,
+                           ent_coef, Xa, H1T, dZ2T, dZ1T, partA, partB, dlogstd, kl_out, acc, work, mean_out, nullptr,
+                           stream);
+}
+
+int qs_mlp3f_actor_w1(int64_t K, int32_t I, int32_t D, int32_t A, const float* X, const int64_t* idx, const float* pack,
+                      const float* b1, const float* b2, const float* W3, const float* b3, const float* logstd,
+                      float action_scale, const float* act, const float* logp_old, const double* adv, float clip,
+                      float ent_coef, float* Xa, float* H1T, float* dZ2T, float* dZ1T, float* partA, float* partB,
+                      float* dlogstd, float* kl_out, double* acc, void* work, float* mean_out, float* part_w1,
+                      void* stream) {
   if (K <= 0 || D <= 0 || K % D || K * kM3N * 4 >= (int64_t(1) << 31) || I <= 0 || f16_ip(I) > kFMaxIp || A < 1 ||
       A > kMaxA || !X || !idx || !pack || !b1 || !b2 || !W3 || !b3 || !logstd || !act || !logp_old || !adv || !Xa ||
-      !H1T || !dZ2T || !dZ1T || !partA || !partB || !dlogstd || !kl_out || !acc || !work)
+      !H1T || !dZ2T || (!dZ1T && !part_w1) || !partA || !partB || !dlogstd || !kl_out || !acc || !work)
     return fail(QS_E_INVALID, "qs_mlp3f_actor: bad argument (K a multiple of D, K·1024 < 2^31, I <= 128, 1 <= A <= 4)");
   const unsigned grid = (unsigned)qs_mlp3f_tiles(K);
   unsigned* count = (unsigned*)work;
   double* lossp = (double*)((char*)work + 64);
+  // the folded dW1's LDS: dZ1 half [128][144] + the X tile [128][Ip + 16]
+  const int w1_lds = part_w1 ? 128 * 144 + 128 * (f16_ip(I) + 16) : 0;
   auto go = [&](auto kern, int AA) {
-    const int lds = f_lds_floats(AA) * (int)sizeof(float);
+    const int lds = std::max(f_lds_floats(AA), w1_lds) * (int)sizeof(float);
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kFBlock), (unsigned)lds, (hipStream_t)stream, (long long)K, (int)I, (int)D,
                        X, (const long long*)idx, pack, b1, b2, W3, b3, logstd, action_scale, act, logp_old, adv, clip,
-                       ent_coef, Xa, H1T, dZ2T, dZ1T, partA, partB, lossp, dlogstd, kl_out, acc, count, mean_out);
+                       ent_coef, Xa, H1T, dZ2T, dZ1T, partA, partB, lossp, dlogstd, kl_out, acc, count, mean_out, part_w1);
   };
   switch (A) {
     case 1: go(mlp3f_actor_kernel<1>, 1); break;

@@ -66,7 +66,7 @@ EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get
            "qs_mlp_sum_partials_multi", "qs_adam_step", "qs_mlp3_tiles", "qs_mlp3_pack_floats",
            "qs_mlp3_pack", "qs_mlp3_fwd", "qs_mlp3_fwd_rows", "qs_mlp3_fwd_group_rows", "qs_mlp3_bwd", "qs_mlp_wgrad", "qs_mlp_wgrad_chunks", "qs_adam_multi",
            "qs_adam_multi_pack", "qs_mlp_sum_adam", "qs_mlp_sum_adam_work_bytes", "qs_mlp3f_tiles", "qs_mlp3f_pack_floats", "qs_mlp3f_work_bytes",
-           "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
+           "qs_mlp3f_pack", "qs_mlp3f_actor", "qs_mlp3f_actor_w1", "qs_value_head", "qs_mlp_wgrad_x_chunks", "qs_mlp_wgrad_x",
            "qs_wgrad_rm", "qs_learner_last_error", "qs_rms_work_bytes", "qs_rms_update", "qs_rms_normalize",
            "qs_rms_last_error", "qs_mlp3_value_work_bytes", "qs_mlp3_fwd_rows_value", "qs_policy_sample", "qs_rollout_record", "qs_rollout_last_error", "qs_ppo_small_work_bytes", "qs_ppo_small_step", "qs_ppo_small_last_error",
            "qs_ppo_small_layout", "qs_ppo_critic_tiles", "qs_wgrad_t", "qs_ppo_small_grads", "qs_ppo_small_adam")
@@ -157,6 +157,8 @@ def load():
     L.qs_mlp3f_pack.argtypes = [ctypes.c_int32, vp, vp, vp, vp]
     L.qs_mlp3f_actor.argtypes = ([i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 8 + [f32] + [vp] * 3
                                  + [f32, f32] + [vp] * 12)
+    L.qs_mlp3f_actor_w1.argtypes = ([i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [vp] * 8 + [f32] + [vp] * 3
+                                    + [f32, f32] + [vp] * 13)
     L.qs_value_head.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 7
     L.qs_mlp_wgrad_x_chunks.argtypes = [i64, ctypes.c_int32]
     L.qs_mlp_wgrad_x.argtypes = [i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32, vp, vp, vp]

@@ -366,6 +366,10 @@ class _F16Work(_M3Work):
     rows and reduction tasks as _M3Work.backward."""
 
     w1_stream = True   # dW1 on a third stream beside dW2 (False: after it, one stream)
+    # dW1 inside the fused launch (qs_mlp3f_actor_w1, opt-in): measured slower — C3 235–242 vs
+    # 220–222 µs per minibatch, C4 276 vs 245–248 (the epilogue lengthens the launch every
+    # other kernel of the minibatch waits on; DESIGN §9f); default: the split-K GEMMs
+    fold_w1 = False
 
     def __init__(self, mlp, K, device):
         f0, f1, f2 = mlp.fcs
@@ -388,7 +392,9 @@ class _F16Work(_M3Work):
         self.C2 = self.C1 = 0
         self.S2, self.S1 = _splitk_chunks(K, m2), _splitk_chunks(K, m1)
         self.pw2 = torch.empty((self.S2, 256, 256), **f32) if self.S2 > 1 else None
-        self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 else None
+        self.pw1 = torch.empty((self.S1, 256, self.I), **f32) if self.S1 > 1 and not self.fold_w1 else None
+        # folded dW1: one [256][I] partial per 128-row workgroup (dZ1 is then never stored)
+        self.pw1f = torch.empty((G, 256, self.I), **f32) if self.fold_w1 else None
 
     def repack(self):
         f0, f1, _ = self.mlp.fcs
@@ -416,19 +422,24 @@ class _F16Work(_M3Work):
         forks work onto another stream behind it)."""
         f0, f1, f2 = self.mlp.fcs
         logstd = actor.logstd
-        L.check(L.load().qs_mlp3f_actor(
+        fold = self.pw1f is not None
+        L.check(L.load().qs_mlp3f_actor_w1(
             self.K, self.I, D, self.A, L.ptr(table), L.ptr(idx), L.ptr(self.pack), L.ptr(f0.bias), L.ptr(f1.bias),
             L.ptr(f2.weight), L.ptr(f2.bias), L.ptr(logstd), float(actor.action_scale), L.ptr(rollouts.act),
             L.ptr(rollouts.logp), L.ptr(rollouts.adv_env), float(clip), float(ent_coef), L.ptr(self.xa),
-            L.ptr(self.h1), L.ptr(self.dz2), L.ptr(self.dz1), L.ptr(self.part_a), L.ptr(self.part_b),
-            L.ptr(logstd.grad), L.ptr(kl), L.ptr(acc), L.ptr(self.work), L.ptr(self.mean), _stream()),
-            "qs_mlp3f_actor")
+            L.ptr(self.h1), L.ptr(self.dz2), None if fold else L.ptr(self.dz1), L.ptr(self.part_a),
+            L.ptr(self.part_b), L.ptr(logstd.grad), L.ptr(kl), L.ptr(acc), L.ptr(self.work), L.ptr(self.mean),
+            L.ptr(self.pw1f), _stream()),
+            "qs_mlp3f_actor_w1")
         N, A = 256, self.A
         tasks.append((self.G, self.part_a.shape[1], self.part_a, f1.bias.grad, N, f2.weight.grad, A * N, f2.bias.grad))
         tasks.append((self.G, N, self.part_b, f0.bias.grad, N, None, 0, None))
         if after_actor is not None:
             after_actor()
-        if self.w1_stream:
+        if fold:
+            w2 = self._splitk_rm(f1.weight.grad, self.dz2, self.h1, self.pw2, self.S2)   # dW2 = dZ2ᵀ·H1
+            w1 = (self.G, N * self.I, self.pw1f, f0.weight.grad, N * self.I, None, 0, None)
+        elif self.w1_stream:
             # dW1's small GEMMs (a few dozen workgroups each) beside dW2's on a third
             # stream; joined before the caller's reductions
             cur = torch.cuda.current_stream()

@@ -148,7 +148,7 @@ def ablate(shape="C3"):
     noop = lambda *a: 0
     M3, F16, FB = agent_mod._M3Work, agent_mod._F16Work, agent_mod.FlatBuffers
     pieces = {
-        "actor kernel": [(lib, "qs_mlp3f_actor", noop)],
+        "actor kernel": [(lib, "qs_mlp3f_actor", noop), (lib, "qs_mlp3f_actor_w1", noop)],
         "actor dW2": [(F16, "_splitk_rm", lambda self, dst, dy, x, part, S:
                        None if dst is self.mlp.fcs[1].weight.grad else ORIG_RM(self, dst, dy, x, part, S))],
         "actor dW1": [(F16, "_splitk_rm", lambda self, dst, dy, x, part, S:
@@ -249,6 +249,13 @@ def main():
                 us, path = per_minibatch_us(shape)
                 print(f"{shape}  w1_stream={w1s!s:48s} {us:8.1f} us/minibatch  [{path}]", flush=True)
         agent_mod._F16Work.w1_stream = True
+    if "fold" in which:   # dW1 folded into the fused actor vs the split-K GEMMs (default), interleaved
+        for shape in ("C3", "C4"):
+            for f in (True, False, True, False):
+                agent_mod._F16Work.fold_w1 = f
+                us, path = per_minibatch_us(shape)
+                print(f"{shape}  fold_w1={f!s:50s} {us:8.1f} us/minibatch  [{path}]", flush=True)
+        agent_mod._F16Work.fold_w1 = False
     if "vh" in which:   # the critic's value head folded into its forward vs the separate launch, interleaved
         for shape in ("C3", "C4"):
             for v in (dict(), dict(fused_value_head=True), dict(), dict(fused_value_head=True), dict()):

@@ -118,3 +118,74 @@ def test_wgrad_rm_matches_fp64(K, N, M, C):
     assert torch.equal(part, again)
     # shapes the kernel does not take are refused
     assert lib.qs_wgrad_rm(K, 96, M, L.ptr(A), L.ptr(B), C, L.ptr(part), stream) != 0
+
+
+@pytest.mark.parametrize("mb,D,I,A", [(4096, 8, 27, 1), (96, 3, 27, 1), (37, 5, 72, 2), (2560, 5, 119, 4)])
+def test_folded_dw1_matches_fp64(mb, D, I, A):
+    """qs_mlp3f_actor_w1 (dW1 = dZ1ᵀ·X folded into the fused launch, VERDICT r04
+    item 2): each workgroup's [256][I] partial against an fp64 matmul of the
+    unfolded launch's dZ1 and Xa over the workgroup's 128 rows, their sum against
+    autograd's W1 gradient; every other output bit-identical to qs_mlp3f_actor's."""
+    import ctypes
+    from gym_pybullet_drones_amd import _lib as L
+    lib = L.load()
+    dev = "cuda"
+    net = _net(I, A, 4)
+    logstd = nn.Parameter(torch.full((A,), -0.5, device=dev))
+    TE = 2 * mb + 3
+    g = torch.Generator(device=dev).manual_seed(7)
+    table = torch.randn(TE, D, I, device=dev, generator=g)
+    act = torch.randn(TE, D, A, device=dev, generator=g)
+    adv = torch.randn(TE, device=dev, dtype=torch.float64, generator=g)
+    idx = torch.randperm(TE, device=dev, generator=g)[:mb]
+    x = table[idx].reshape(mb * D, I)
+    with torch.no_grad():
+        d0 = torch.distributions.Normal(net(x), logstd.exp())
+        lp0 = d0.log_prob(act[idx].reshape(-1, A)).sum(-1) + 0.05 * torch.randn(mb * D, device=dev, generator=g)
+    logp_old = torch.zeros(TE, D, device=dev)
+    logp_old[idx] = lp0.reshape(mb, D)
+    clip, ent = 0.2, 0.01
+    K = mb * D
+    mean = net(x)
+    dist = torch.distributions.Normal(mean, logstd.exp())
+    logp = dist.log_prob(act[idx].reshape(-1, A)).sum(-1, keepdim=True)
+    ratio = torch.exp(logp - logp_old[idx].reshape(-1, 1))
+    a_ = adv[idx].repeat_interleave(D).reshape(-1, 1)
+    pl = -torch.min(ratio * a_, torch.clamp(ratio, 1 - clip, 1 + clip) * a_).mean()
+    (pl + ent * (-dist.entropy().sum(-1).mean())).backward()
+    f32 = dict(device=dev, dtype=torch.float32)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    pack = torch.empty(int(lib.qs_mlp3f_pack_floats(I)), **f32)
+    L.check(lib.qs_mlp3f_pack(I, L.ptr(net[0].weight), L.ptr(net[2].weight), L.ptr(pack), stream), "qs_mlp3f_pack")
+    G = int(lib.qs_mlp3f_tiles(K))
+    outs = []
+    for fold in (False, True):
+        o = dict(xa=torch.full((K, I), np.nan, **f32), H1=torch.full((K, 256), np.nan, **f32),
+                 dZ2=torch.full((K, 256), np.nan, **f32), dZ1=torch.full((K, 256), np.nan, **f32),
+                 pA=torch.empty((G, 256 * (1 + A) + A), **f32), pB=torch.empty((G, 256), **f32),
+                 dls=torch.empty(A, **f32), kl=torch.empty(1, **f32), acc=torch.zeros(4, dtype=torch.float64, device=dev),
+                 pw1=torch.full((G, 256, I), np.nan, **f32) if fold else None)
+        work = torch.zeros(int(lib.qs_mlp3f_work_bytes(K)), dtype=torch.uint8, device=dev)
+        L.check(lib.qs_mlp3f_actor_w1(K, I, D, A, L.ptr(table), L.ptr(idx), L.ptr(pack), L.ptr(net[0].bias),
+                                      L.ptr(net[2].bias), L.ptr(net[4].weight), L.ptr(net[4].bias), L.ptr(logstd), 1.0,
+                                      L.ptr(act), L.ptr(logp_old), L.ptr(adv), clip, ent, L.ptr(o["xa"]), L.ptr(o["H1"]),
+                                      L.ptr(o["dZ2"]), None if fold else L.ptr(o["dZ1"]), L.ptr(o["pA"]), L.ptr(o["pB"]),
+                                      L.ptr(o["dls"]), L.ptr(o["kl"]), L.ptr(o["acc"]), L.ptr(work), None,
+                                      L.ptr(o["pw1"]), stream), "qs_mlp3f_actor_w1")
+        torch.cuda.synchronize()
+        outs.append(o)
+    ref, got = outs
+    for k in ("xa", "H1", "dZ2", "pA", "pB", "dls", "kl", "acc"):
+        assert torch.equal(ref[k], got[k]), k
+    assert torch.isnan(got["dZ1"]).all()   # not stored when folded
+    # per workgroup (128 rows): the fp64 contraction of the unfolded launch's dZ1 and Xa
+    rows = torch.arange(G * 128, device=dev).clamp(max=K - 1)
+    valid = (torch.arange(G * 128, device=dev) < K).double().view(G, 128, 1)
+    dz = ref["dZ1"].double()[rows].view(G, 128, 256) * valid
+    xa = ref["xa"].double()[rows].view(G, 128, I) * valid
+    want = torch.bmm(dz.transpose(1, 2), xa)
+    sc = float(want.abs().max())
+    torch.testing.assert_close(got["pw1"].double(), want, rtol=0, atol=1e-5 * sc)
+    total = got["pw1"].double().sum(0).float()
+    s0 = float(net[0].weight.grad.abs().max())
+    torch.testing.assert_close(total, net[0].weight.grad, rtol=1e-3, atol=1e-4 * s0)
