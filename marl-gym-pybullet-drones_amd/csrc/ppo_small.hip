@@ -1252,7 +1252,11 @@ inline int s_chunks(long long KP) {
 #else
   constexpr int gq = kSGQ;
 #endif
-  const long long S = (q + gq - 1) / gq;
+  long long S = (q + gq - 1) / gq;
+  // a remainder of at most gq/8 quads joins the other chunks (48-row tiles pad
+  // 1 024 critic rows to 1 056: a second chunk sent the critic through launch 3,
+  // 8 → 15 µs at C3/4)
+  if (S > 1 && q - (S - 1) * gq <= gq / 8) --S;
   return (int)(S < 1 ? 1 : (S > kSMaxS ? kSMaxS : S));
 }
 // Ia = 0: the critic's tiles only (qs_ppo_critic_tiles), no actor buffers
@@ -1262,7 +1266,11 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   // 32-row tiles once 16-row ones would not fit in one round of the CUs (the
   // two-block tile does twice the MFMA work for about 1.2x the latency)
   // (one-output actors only: wider heads' per-row state spills out of the 128 registers)
-  L.rb = (Ia > 0 && A == 1 && (Ka + 15) / 16 + (Kc + 15) / 16 > kSCUs) ? 2 : 1;
+  // 48-row tiles (narrow nets, the padded W1 copies) once 32-row ones would not
+  // fit either: C3 at G = 4 (8 192 actor rows) ran its 288 two-block tiles in
+  // two rounds (72 µs)
+  const long long t16 = (Ka + 15) / 16 + (Kc + 15) / 16, t32 = (Ka + 31) / 32 + (Kc + 31) / 32;
+  L.rb = (Ia > 0 && A == 1 && t16 > kSCUs) ? (t32 > kSCUs && Ia <= kSNarrowI && Ic <= kSNarrowI ? 3 : 2) : 1;
   L.nA = (int)((Ka + 16 * L.rb - 1) / (16 * L.rb));
   L.nC = (int)((Kc + 16 * L.rb - 1) / (16 * L.rb));
   L.KaP = 16 * L.rb * L.nA;
@@ -1367,6 +1375,8 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   if ((long long)mb * D * kSH >= (1LL << 31))
     return sfail(QS_E_INVALID, std::string(name) + ": minibatch too large for 32-bit activation offsets");
   L = s_layout(mb, D, actor->in, critic->in, A);
+  if (need_actor && L.rb == 3 && (!critic->w1p || !actor->w1p))   // (the critic-only launch lays out its own tiles)
+    return sfail(QS_E_INVALID, std::string(name) + ": minibatches past 256 two-block tiles need the padded W1 copies (w1p)");
   P.mb = mb;
   P.D = D;
   P.rb = L.rb;
@@ -1449,7 +1459,8 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
   // (the wide instances read layer 1 from the padded copies only: s_args
   // refuses a net wider than kSNarrowI without one)
 #define S_FB(AA)                                                                                                     \
-  (P.rb == 2 ? (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2>, 0)                                                \
+  (P.rb == 3 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3>, 0) :   /* (narrow nets with w1p: s_layout, s_args) */ \
+  P.rb == 2 ? (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2>, 0)                                                \
                      : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 2>, 0)                                       \
                            : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 2>, 0)))                                    \
              : (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 1>, kSReserveFB)                                      \
