@@ -147,7 +147,7 @@ struct SGrad {
 
 struct SArgs {
   int mb, D, nA, nC, KaP, KcP;
-  int rb;                  // 16-row blocks per forward/backward tile
+  int rb, rbc;             // 16-row blocks per forward/backward tile: the actor's, the critic's
   int KaS, KcS;            // row strides of the transposed activations (KaP / KcP + kSPad)
   const float* X;          // the rollout's obs table [T·E·D][O] (critic rows: [T·E][D·O])
   const long long* idx;    // the minibatch's env-timesteps [mb]
@@ -722,16 +722,24 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
   }
 }
 
-template <int A, bool V1, int MAXI, int RB>
+// RB: the actor's row blocks per tile; RBC: the critic's (its tiles are the
+// launch's slowest — 216 inputs staged and contracted — so they stay at 16 rows
+// while the actor's grow, when the CUs hold both)
+template <int A, bool V1, int MAXI, int RB, int RBC = RB>
 __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
-  constexpr int XSZ = 16 * RB * s_xs(MAXI), DSZ = 16 * RB * kSHS;
+  constexpr int RM = RB > RBC ? RB : RBC;
+  constexpr int XSZ = 16 * RM * s_xs(MAXI), DSZ = 16 * RM * kSHS;
   __shared__ float xsd[XSZ > DSZ ? XSZ : DSZ];   // the X tile, then dZ2 (dead / not yet live in turn)
-  __shared__ float h1s[16 * RB * kSHS];
-  __shared__ float hp[kSW * kSMaxA][16 * RB];
-  __shared__ double ls_w[16 * RB][2 + kSMaxA];
+  __shared__ float h1s[16 * RM * kSHS];
+  __shared__ float hp[kSW * kSMaxA][16 * RM];
+  __shared__ double ls_w[16 * RM][2 + kSMaxA];
   __shared__ float prm[2 * kSH + kSMaxA * kSH + 2 * kSMaxA];
-  if ((int)blockIdx.x < P.nA) s_tile<A, true, V1, MAXI, RB>(P, P.a, blockIdx.x, xsd, h1s, xsd, prm, hp, ls_w);
-  else s_tile<1, false, V1, MAXI, RB>(P, P.c, blockIdx.x - P.nA, xsd, h1s, xsd, prm, hp, ls_w);
+  if ((int)blockIdx.x < P.nA)
+    s_tile<A, true, V1, MAXI, RB>(P, P.a, blockIdx.x, xsd, h1s, xsd, prm, reinterpret_cast<float (*)[16 * RB]>(hp),
+                                  ls_w);
+  else
+    s_tile<1, false, V1, MAXI, RBC>(P, P.c, blockIdx.x - P.nA, xsd, h1s, xsd, prm,
+                                    reinterpret_cast<float (*)[16 * RBC]>(hp), ls_w);
 }
 
 // ---------------------------------------------------------------- launches 2 and 3
@@ -1230,7 +1238,7 @@ __global__ void __launch_bounds__(64 * kSAW) wgrad_t_kernel(int N, int M, int KP
 }
 
 struct SLayout {
-  int rb;         // 16-row blocks per forward/backward tile
+  int rb, rbc;    // 16-row blocks per forward/backward tile: the actor's, the critic's
   int nA, nC, KaP, KcP, KaS, KcS;
   int Sa, Sc;     // K-chunks of the weight gradients per net
   int bta, btc;   // their block sides in 16-row tiles
@@ -1272,9 +1280,13 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   const long long t16 = (Ka + 15) / 16 + (Kc + 15) / 16, t32 = (Ka + 31) / 32 + (Kc + 31) / 32;
   L.rb = (Ia > 0 && A == 1 && t16 > kSCUs) ? (t32 > kSCUs && Ia <= kSNarrowI && Ic <= kSNarrowI ? 3 : 2) : 1;
   L.nA = (int)((Ka + 16 * L.rb - 1) / (16 * L.rb));
-  L.nC = (int)((Kc + 16 * L.rb - 1) / (16 * L.rb));
+  // the critic's tiles at 16 rows while both nets' tiles still fit one round:
+  // they are the launch's slowest (C3/8: 37.8 µs at 32 rows against the
+  // actor's 30.6, phase stamps)
+  L.rbc = (L.rb > 1 && L.nA + (Kc + 15) / 16 <= kSCUs) ? 1 : L.rb;
+  L.nC = (int)((Kc + 16 * L.rbc - 1) / (16 * L.rbc));
   L.KaP = 16 * L.rb * L.nA;
-  L.KcP = 16 * L.rb * L.nC;
+  L.KcP = 16 * L.rbc * L.nC;
   // row strides off a power of two: rows 16 KB apart all mapped to one memory
   // channel (the critic's weight gradients ran 10x slower at 4 096 rows)
   static const int pad = [] {   // dev probe: QS_SMALL_PAD overrides the pad (floats, a multiple of 4)
@@ -1380,6 +1392,7 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   P.mb = mb;
   P.D = D;
   P.rb = L.rb;
+  P.rbc = L.rbc;
   P.nA = L.nA;
   P.nC = L.nC;
   P.KaP = L.KaP;
@@ -1459,10 +1472,14 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
   // (the wide instances read layer 1 from the padded copies only: s_args
   // refuses a net wider than kSNarrowI without one)
 #define S_FB(AA)                                                                                                     \
-  (P.rb == 3 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3>, 0) :   /* (narrow nets with w1p: s_layout, s_args) */ \
-  P.rb == 2 ? (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2>, 0)                                                \
-                     : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 2>, 0)                                       \
-                           : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 2>, 0)))                                    \
+  (P.rb == 3 ? (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3, 1>, 0)   /* (narrow nets with w1p) */     \
+                           : go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3, 3>, 0)) :                                  \
+  P.rb == 2 ? (wide ? (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2, 1>, 0)                                \
+                                  : go(ppo_small_fb_kernel<AA, true, kSMaxI, 2, 2>, 0))                                \
+                     : (v1 ? (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 2, 1>, 0)                       \
+                                         : go(ppo_small_fb_kernel<AA, true, kSNarrowI, 2, 2>, 0))                      \
+                           : (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, false, kSNarrowI, 2, 1>, 0)                      \
+                                         : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 2, 2>, 0))))                   \
              : (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 1>, kSReserveFB)                                      \
                      : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 1>, kSReserveFB)                             \
                            : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 1>, kSReserveFB))))
@@ -1595,6 +1612,7 @@ int qs_ppo_critic_tiles(int32_t mb, int32_t D, const float* obs, const int64_t* 
   P.nA = 0;   // critic tiles only
   P.fb_tail = 1;   // (the last tile adds the value loss to acc[1])
   P.rb = L.rb;     // (1: the critic-only layout)
+  P.rbc = L.rbc;
   P.nC = L.nC;
   P.KaP = P.KaS = 0;
   P.KcP = L.KcP;

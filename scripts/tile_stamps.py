@@ -18,7 +18,7 @@ from gym_pybullet_drones_amd import _lib as L  # noqa: E402
 import learner_mb  # noqa: E402
 
 
-def dump(label, nwg):
+def dump(label, nwg, nA=None):
     lib = L.load()
     buf = (ctypes.c_ulonglong * (nwg * 8))()
     f = lib.qs_dev_tile_stamps
@@ -32,6 +32,12 @@ def dump(label, nwg):
     for k in range(1, 7):
         d = rel[:, k] - rel[:, k - 1]
         print(f"  {names[k - 1]:>12s} -> {names[k]:<12s} median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+    if nA is not None and 0 < nA < nwg:   # the actor's and the critic's tiles apart
+        for nm, sl in (("actor", slice(0, nA)), ("critic", slice(nA, nwg))):
+            r = rel[sl]   # (stamp 5, dH1 done: the tiles' last phase since the per-tile tail moved to launch 2)
+            ph = "  ".join(f"{np.median(r[:, k] - r[:, k - 1]):6.2f}" for k in range(1, 6))
+            print(f"  {nm:>6s} tiles: phases 1-5 median [{ph}] us; entry .. dH1 max {np.max(r[:, 5] - r[:, 0]):7.2f} us; "
+                  f"last {r[:, 5].max():.2f} us")
     last = rel[:, 7][s[:, 7] > 0]
     print(f"  arrivals end {rel[:, 6].max():.2f} us; last tile done at {last.max() if len(last) else float('nan'):.2f} us")
 
@@ -45,9 +51,12 @@ def main():
             learner_mb.per_minibatch_us(shape, reps=1, small=True)
             torch.cuda.synchronize()
             D, O, A, mb, T, E = learner_mb.SHAPES[shape]
-            rb = 2 if (A == 1 and (mb * D + 15) // 16 + (mb + 15) // 16 > 256) else 1
-            nA, nC = (mb * D + 16 * rb - 1) // (16 * rb), (mb + 16 * rb - 1) // (16 * rb)
-            dump(f"{shape} tile path ({16 * rb}-row tiles) (actor tiles {nA}, critic tiles {nC})", nA + nC)
+            t16, t32 = (mb * D + 15) // 16 + (mb + 15) // 16, (mb * D + 31) // 32 + (mb + 31) // 32
+            rb = (3 if t32 > 256 and O <= 256 and D * O <= 256 else 2) if (A == 1 and t16 > 256) else 1
+            nA = (mb * D + 16 * rb - 1) // (16 * rb)
+            rbc = 1 if rb > 1 and nA + (mb + 15) // 16 <= 256 else rb   # (ppo_small.hip s_layout)
+            nC = (mb + 16 * rbc - 1) // (16 * rbc)
+            dump(f"{shape} tile path ({16 * rb}/{16 * rbc}-row tiles) (actor tiles {nA}, critic tiles {nC})", nA + nC, nA)
         return
     for name, shape in (("ref small step", "ref"),):
         learner_mb.per_minibatch_us(shape, reps=1, small=True)
