@@ -725,17 +725,20 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
 // RB: the actor's row blocks per tile; RBC: the critic's (its tiles are the
 // launch's slowest — 216 inputs staged and contracted — so they stay at 16 rows
 // while the actor's grow, when the CUs hold both)
-template <int A, bool V1, int MAXI, int RB, int RBC = RB>
+// MAXA: the actor's input bound (a narrow actor beside a wide critic: its
+// 48-row X tile sized for its own width)
+template <int A, bool V1, int MAXI, int RB, int RBC = RB, int MAXA = MAXI>
 __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
   constexpr int RM = RB > RBC ? RB : RBC;
-  constexpr int XSZ = 16 * RM * s_xs(MAXI), DSZ = 16 * RM * kSHS;
+  constexpr int XA = 16 * RB * s_xs(MAXA), XC = 16 * RBC * s_xs(MAXI);
+  constexpr int XSZ = XA > XC ? XA : XC, DSZ = 16 * RM * kSHS;
   __shared__ float xsd[XSZ > DSZ ? XSZ : DSZ];   // the X tile, then dZ2 (dead / not yet live in turn)
   __shared__ float h1s[16 * RM * kSHS];
   __shared__ float hp[kSW * kSMaxA][16 * RM];
   __shared__ double ls_w[16 * RM][2 + kSMaxA];
   __shared__ float prm[2 * kSH + kSMaxA * kSH + 2 * kSMaxA];
   if ((int)blockIdx.x < P.nA)
-    s_tile<A, true, V1, MAXI, RB>(P, P.a, blockIdx.x, xsd, h1s, xsd, prm, reinterpret_cast<float (*)[16 * RB]>(hp),
+    s_tile<A, true, V1, MAXA, RB>(P, P.a, blockIdx.x, xsd, h1s, xsd, prm, reinterpret_cast<float (*)[16 * RB]>(hp),
                                   ls_w);
   else
     s_tile<1, false, V1, MAXI, RBC>(P, P.c, blockIdx.x - P.nA, xsd, h1s, xsd, prm,
@@ -1277,8 +1280,13 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   // 48-row tiles (narrow nets, the padded W1 copies) once 32-row ones would not
   // fit either: C3 at G = 4 (8 192 actor rows) ran its 288 two-block tiles in
   // two rounds (72 µs)
+  // (a wide critic only beside them at 16 rows: C5/8's 432-input critic)
   const long long t16 = (Ka + 15) / 16 + (Kc + 15) / 16, t32 = (Ka + 31) / 32 + (Kc + 31) / 32;
-  L.rb = (Ia > 0 && A == 1 && t16 > kSCUs) ? (t32 > kSCUs && Ia <= kSNarrowI && Ic <= kSNarrowI ? 3 : 2) : 1;
+  L.rb = 1;
+  if (Ia > 0 && A == 1 && t16 > kSCUs) {
+    L.rb = 2;
+    if (t32 > kSCUs && Ia <= kSNarrowI && (Ic <= kSNarrowI || (Ka + 47) / 48 + (Kc + 15) / 16 <= kSCUs)) L.rb = 3;
+  }
   L.nA = (int)((Ka + 16 * L.rb - 1) / (16 * L.rb));
   // the critic's tiles at 16 rows while both nets' tiles still fit one round:
   // they are the launch's slowest (C3/8: 37.8 µs at 32 rows against the
@@ -1472,8 +1480,9 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
   // (the wide instances read layer 1 from the padded copies only: s_args
   // refuses a net wider than kSNarrowI without one)
 #define S_FB(AA)                                                                                                     \
-  (P.rb == 3 ? (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3, 1>, 0)   /* (narrow nets with w1p) */     \
-                           : go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3, 3>, 0)) :                                  \
+  (P.rb == 3 ? (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 3, 1, kSNarrowI>, 0)   /* (narrow actor, w1p) */      \
+                : P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3, 1>, 0)                                     \
+                             : go(ppo_small_fb_kernel<AA, true, kSNarrowI, 3, 3>, 0)) :                                  \
   P.rb == 2 ? (wide ? (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2, 1>, 0)                                \
                                   : go(ppo_small_fb_kernel<AA, true, kSMaxI, 2, 2>, 0))                                \
                      : (v1 ? (P.rbc == 1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 2, 1>, 0)                       \
