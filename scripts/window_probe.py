@@ -70,6 +70,24 @@ print(f"replay + sync                      {med(lambda: (g.replay(), torch.cuda.
 print(f"replay + stream sync               {med(lambda: (g.replay(), cur.synchronize())):8.1f} us")
 print(f"events + replay + 2 sync (bench)   {med(events_window):8.1f} us")
 print(f"replay + event sync                {med(lambda: (ev_end.record(cur) if g.replay() is None else None, ev_end.synchronize())):8.1f} us")
+def spin_window():   # the end of the window noticed by polling the last event, then the device sync
+    b = torch.cuda.Event()
+    g.replay()
+    b.record(cur)
+    while not b.query():
+        pass
+    torch.cuda.synchronize()
+
+
+print(f"replay + spin on event + sync      {med(spin_window):8.1f} us")
+try:   # the graph launched straight through the HIP runtime (torch's replay bookkeeping skipped)
+    import ctypes
+    hip = ctypes.CDLL([l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l][0])
+    ex = ctypes.c_void_p(g.raw_cuda_graph_exec())
+    st = ctypes.c_void_p(cur.cuda_stream)
+    print(f"hipGraphLaunch + sync              {med(lambda: (hip.hipGraphLaunch(ex, st), torch.cuda.synchronize())):8.1f} us")
+except Exception as e:   # (older torch: no raw_cuda_graph_exec)
+    print("hipGraphLaunch probe skipped:", e)
 med(kernel_us)
 print(f"event-timed graph                  {statistics.median(ev):8.1f} us  ({statistics.median(ev) / K:.2f} us/step)")
 sw.close()
