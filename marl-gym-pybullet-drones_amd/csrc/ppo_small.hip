@@ -1286,6 +1286,10 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   if (Ia > 0 && A == 1 && t16 > kSCUs) {
     L.rb = 2;
     if (t32 > kSCUs && Ia <= kSNarrowI && (Ic <= kSNarrowI || (Ka + 47) / 48 + (Kc + 15) / 16 <= kSCUs)) L.rb = 3;
+  } else if (Ia > 0 && A > 1 && t16 > kSCUs && Ia <= kSNarrowI && (Ka + 31) / 32 + (Kc + 15) / 16 <= kSCUs) {
+    // wider heads at 32 rows: the tile spills 70 registers, and still beats two
+    // rounds of 16-row tiles (C4/4: 128 → 112 µs per minibatch)
+    L.rb = 2;
   }
   L.nA = (int)((Ka + 16 * L.rb - 1) / (16 * L.rb));
   // the critic's tiles at 16 rows while both nets' tiles still fit one round:
@@ -1395,7 +1399,9 @@ static int s_args(int32_t mb, int32_t D, const float* obs, const int64_t* idx, c
   if ((long long)mb * D * kSH >= (1LL << 31))
     return sfail(QS_E_INVALID, std::string(name) + ": minibatch too large for 32-bit activation offsets");
   L = s_layout(mb, D, actor->in, critic->in, A);
-  if (need_actor && L.rb == 3 && (!critic->w1p || !actor->w1p))   // (the critic-only launch lays out its own tiles)
+  // (the three-block tiles and the wider heads' two-block ones read layer 1 from
+  // the padded copies only; the critic-only launch lays out its own tiles)
+  if (need_actor && (L.rb == 3 || (L.rb == 2 && A > 1)) && (!critic->w1p || !actor->w1p))
     return sfail(QS_E_INVALID, std::string(name) + ": minibatches past 256 two-block tiles need the padded W1 copies (w1p)");
   P.mb = mb;
   P.D = D;
@@ -1493,7 +1499,8 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
                      : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 1>, kSReserveFB)                             \
                            : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 1>, kSReserveFB))))
 #define S_FB1(AA)                                                                                    \
-  (wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 1>, kSReserveFB)                                 \
+  (P.rb == 2 ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 2, 1, kSNarrowI>, 0) :                       \
+  wide ? go(ppo_small_fb_kernel<AA, true, kSMaxI, 1>, kSReserveFB)                                 \
         : (v1 ? go(ppo_small_fb_kernel<AA, true, kSNarrowI, 1>, kSReserveFB)                        \
               : go(ppo_small_fb_kernel<AA, false, kSNarrowI, 1>, kSReserveFB)))
   switch (P.a.A) {   // (two-block tiles: one-output actors, s_layout)

@@ -53,7 +53,9 @@ def main():
             D, O, A, mb, T, E = learner_mb.SHAPES[shape]
             t16, t32 = (mb * D + 15) // 16 + (mb + 15) // 16, (mb * D + 31) // 32 + (mb + 31) // 32
             rb = (3 if t32 > 256 and O <= 256 and (D * O <= 256 or (mb * D + 47) // 48 + (mb + 15) // 16 <= 256)
-                  else 2) if (A == 1 and t16 > 256) else 1   # (ppo_small.hip s_layout)
+                  else 2) if (A == 1 and t16 > 256) else (
+                2 if A > 1 and t16 > 256 and O <= 256 and (mb * D + 31) // 32 + (mb + 15) // 16 <= 256 else 1)
+            # (ppo_small.hip s_layout)
             nA = (mb * D + 16 * rb - 1) // (16 * rb)
             rbc = 1 if rb > 1 and nA + (mb + 15) // 16 <= 256 else rb   # (ppo_small.hip s_layout)
             nC = (mb + 16 * rbc - 1) // (16 * rbc)

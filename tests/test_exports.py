@@ -104,6 +104,6 @@ def test_tile_layouts_at_the_per_rank_shapes():
     assert lay(1024, 8, 27, 216, 1) == dict(nA=171, nC=64, KaP=8208, KcP=1024, Sa=8, Sc=1)
     # C5 at G = 8: a narrow actor at 48 rows beside the 432-wide critic at 16
     assert lay(512, 16, 27, 432, 1) == dict(nA=171, nC=32, KaP=8208, KcP=512, Sa=8, Sc=1)
-    # C4 at G = 4: four-output actors keep 16-row tiles (their head's per-row state)
+    # C4 at G = 4: the four-output actor at 32 rows beside the 595-wide critic at 16 (one round)
     d = lay(1024, 5, 119, 595, 4)
-    assert (d["nA"], d["nC"], d["KaP"], d["KcP"]) == (320, 64, 5120, 1024)
+    assert (d["nA"], d["nC"], d["KaP"], d["KcP"]) == (160, 64, 5120, 1024)

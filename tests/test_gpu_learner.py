@@ -309,7 +309,7 @@ def test_direct_update_fused_actor_four_outputs(graphs):
 @pytest.mark.parametrize("E,T,D,A,O", [(8, 8, 8, 1, 27), (32, 8, 8, 1, 27), (5, 6, 8, 1, 27), (16, 4, 5, 4, 27),
                                        (3, 2, 16, 1, 27), (64, 16, 8, 1, 27), (32, 8, 16, 1, 27),
                                        (16, 8, 5, 4, 119), (4, 4, 8, 4, 72), (128, 16, 8, 1, 27),
-                                       (64, 16, 16, 1, 27), (256, 16, 8, 1, 27)])
+                                       (64, 16, 16, 1, 27), (128, 16, 5, 4, 119), (256, 16, 8, 1, 27)])
 @pytest.mark.parametrize("graphs", [False, True])
 def test_small_update_matches_autograd(graphs, E, T, D, A, O, monkeypatch):
     """The tile path (qs_ppo_small_step: two launches per minibatch, three
@@ -323,7 +323,8 @@ def test_small_update_matches_autograd(graphs, E, T, D, A, O, monkeypatch):
     (32, 8, 16): C5's drones, a 432-wide critic on 128 rows and 2 048 actor rows;
     (128, 16, 8): 8 192 actor rows (C3 at G = 4: 48-row actor tiles, 16-row
     critic tiles, one round of the CUs); (64, 16, 16): C5 at G = 8, 8 192 actor
-    rows beside a 432-wide critic at 16 rows; (256, 16, 8): 16 384 actor rows (C3 at G = 2: 48-row tiles in
+    rows beside a 432-wide critic at 16 rows; (128, 16, 5, 4, 119): C4 at G = 4
+    (5 120 four-output actor rows, a 595-wide critic); (256, 16, 8): 16 384 actor rows (C3 at G = 2: 48-row tiles in
     two rounds, the actor's weight gradients in K-chunks summed by launch 3);
     (16, 8, 5, 4, 119): Spiral's obs, a 595-wide critic; (4, 4, 8, 4, 72): a
     576-wide critic (C3 with VEL actions), past 640 nothing."""
