@@ -247,7 +247,7 @@ def _ppid(pid):
         return int(f.read().rsplit(")", 1)[1].split()[1])
 
 
-def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dyn", aux=()):
+def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dyn", aux=(), extra22=False):
     """The oracle (C++ restatement of the reference step, fp64) timed on this host's
     cores at the reference's 176 envs (README.md:38-39: 22 workers x 8 envs) on the
     same task, D, action type and physics as a GPU leg (BASELINE.md:36): a bounded
@@ -256,11 +256,14 @@ def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dy
     import qs_oracle
     D = D or args.drones
     act = act or args.act
-    # the reference topology: 22 workers x 8 envs (README.md:38-39, BASELINE.md:35-37),
-    # 22 OpenMP threads whatever OMP_NUM_THREADS says (num_threads(22) in the oracle's
-    # loop); host_cpu() records the CPUs this process may use and the quota, and
-    # whether 22 threads oversubscribe them
-    threads = CPU_WORKERS
+    # the reference topology: 22 workers x 8 envs (README.md:38-39, BASELINE.md:35-37)
+    # on at most the CPUs this process may use: min(22, affinity CPUs, the cgroup
+    # quota) OpenMP threads (22 threads on a 16-CPU quota were
+    # throttled, which understated the CPU path); `extra22` also times 22 threads
+    # oversubscribed, as a labelled extra
+    host = host_cpu()
+    threads = max(1, min(CPU_WORKERS, host["nproc"] or CPU_WORKERS,
+                         int(host["cpu_quota"]) if host["cpu_quota"] else CPU_WORKERS))
     E = 176
     ophys, oaux = ("pyb", ("dw",)) if physics == "pyb_dw" else (physics, tuple(aux))
     kw = dict(initial_xyzs=grid_layout(D)) if task == "multihover" and D >= 6 else {}
@@ -279,15 +282,26 @@ def cpu_baseline(args, seconds, task="multihover", D=None, act=None, physics="dy
         steps += chunk
         # next chunk: double, but no longer than the rest of the budget at the last chunk's rate
         chunk = max(1, min(2 * chunk, int((seconds - dt) / max(dc / chunk, 1e-9)) + 1))
+    out22 = None
+    if extra22 and threads < CPU_WORKERS:   # the 22-worker topology oversubscribed (labelled extra)
+        s22, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 3:
+            sim.run_random(8, CPU_WORKERS)
+            s22 += 8
+        out22 = {"value": E * D * s22 / (time.perf_counter() - t0), "threads": CPU_WORKERS,
+                 "note": "22 OpenMP threads on fewer CPUs (oversubscribed): not the baseline"}
     sim.close()
-    host = host_cpu()
     host["threads"] = threads
     host["oversubscribed"] = threads > min(host["nproc"] or threads, host["cpu_quota"] or threads)
-    return {"value": E * D * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
-            "host": host,
-            "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {task} {E} envs x "
-                      f"{D} drones, {act}, {physics}{'+' + '+'.join(aux) if aux else ''}, {steps} random-policy "
-                      f"ctrl steps, OpenMP {threads} threads, {dt:.1f} s"}
+    out = {"value": E * D * steps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+           "host": host,
+           "sample": f"C++ oracle (CPU restatement of the reference step, fp64, not PyBullet), {task} {E} envs x "
+                     f"{D} drones ({CPU_WORKERS} reference workers' envs), {act}, "
+                     f"{physics}{'+' + '+'.join(aux) if aux else ''}, {steps} random-policy "
+                     f"ctrl steps, OpenMP {threads} threads (this process's CPU share), {dt:.1f} s"}
+    if out22:
+        out["oversubscribed_22"] = out22
+    return out
 
 
 def host_cpu():
@@ -403,8 +417,7 @@ def sim_leg(args, ranks, physics="dyn", task="multihover", E=None, D=None, act=N
     # each (the obs ring cycling through its `slots` buffers inside a graph), so that
     # exactly `steps` run: a window of 484 steps is one replay, not 16 (each graph
     # boundary cost ~9 µs of idle device time between the replays)
-    from gym_pybullet_drones_amd.mappo.agent import drain_collectives
-    drain_collectives()   # N ranks: the fences' collectives retired before the capture (RCCL watchdog)
+    # (no collective inside the window's graph: the fences' eager barriers stay on the default group)
     gsteps = max(1, min(args.graph_steps, args.steps))
     n_full, rem = divmod(args.steps, gsteps)
     stream = torch.cuda.Stream()
@@ -670,12 +683,12 @@ def allreduce_us(n, reps=10, per_graph=20):
         for _ in range(3):
             dist.all_reduce(buf)
     torch.cuda.current_stream().wait_stream(s)
-    from gym_pybullet_drones_amd.mappo.agent import drain_collectives
-    drain_collectives()   # the warm-up all-reduces retired before the capture (RCCL watchdog)
+    from gym_pybullet_drones_amd.mappo.collectives import capture_collectives, collective_group
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):   # (the RCCL watchdog polls from its thread)
+    # the captured all-reduces on the capture group, as the update graph issues them (mappo/collectives.py)
+    with capture_collectives(), torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(per_graph):
-            dist.all_reduce(buf)
+            dist.all_reduce(buf, group=collective_group())
     g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -852,7 +865,7 @@ def main():
                 configs[name]["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds / 4, c["task"], c["drones"],
                                                              c["act"], c["physics"], c["aux"])
     if rank == 0:
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args, args.cpu_seconds)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args, args.cpu_seconds, extra22=True)
         traffic, traffic_src = pmc_traffic(E, D, args.act)
         line = {
             "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": steps,

@@ -337,8 +337,8 @@ const char* qs_rollout_last_error(void);
  * weight-gradient GEMMs / qs_mlp_sum_adam there: the actor's forward, policy
  * loss head (AG:602-640) and backward and the critic's forward, value head
  * (AG:642-683) and backward in 16-row tiles, then every weight gradient
- * summed over the whole minibatch (32×32 blocks, K-chunks past 1 024 rows
- * summed in chunk order) and applied by Adam in place (the actor's step gated
+ * summed over the whole minibatch (64×64 tiles staged through LDS, K-chunks
+ * summed in chunk order by a third launch) and applied by Adam in place (the actor's step gated
  * on approx_kl <= kl_thr when gate != 0, AG:731-734; the critic's always,
  * AG:757-760).  Both nets are 256-wide tanh MLPs (nn.Linear layout, row-major
  * [out][in], at most 640 inputs) inside flat parameter / Adam buffers; w2t is a
@@ -348,7 +348,9 @@ const char* qs_rollout_last_error(void);
  * logp_old [T·E·D], adv / ret [T·E] (float64).  Writes kl_out[0] = approx_kl
  * and acc[0..3] += policy, value, entropy loss, approx_kl, as qs_ppo_heads.
  * work: qs_ppo_small_work_bytes(mb, D, actor in, critic in, A) bytes, zeroed
- * once (the launches leave their counters zero). */
+ * once (the weight gradients read the transposed activations' zero padding;
+ * launch 1 also stores the minibatch's Adam bias corrections there, formed
+ * from the step counts before this minibatch's step commits them). */
 #define QS_PPO_SMALL_MAX_ROWS 16384   /* mb·D at most */
 typedef struct qs_mlp256 {
   float* params;       /* flat parameter buffer of the net (FlatBuffers)     */
@@ -376,7 +378,8 @@ int qs_ppo_small_step(int32_t mb, int32_t D, const float* obs, const int64_t* id
  * then applies Adam from the sums ÷ grad_div (the world size; the actor gated
  * on the summed approx_kl ÷ grad_div <= kl_thr when gate != 0) and keeps the
  * W2ᵀ / padded W1 copies current.  One rank (grad_div 1) gives
- * qs_ppo_small_step's bits.  work: the same workspace (its counters). */
+ * qs_ppo_small_step's bits.  work: the same workspace, as the preceding
+ * qs_ppo_small_grads left it (its Adam bias corrections). */
 int qs_ppo_small_grads(int32_t mb, int32_t D, const float* obs, const int64_t* idx, const float* act,
                        const float* logp_old, const double* adv, const double* ret, float action_scale, float clip,
                        float ent_coef, const qs_mlp256* actor, const qs_mlp256* critic, float* grad_a, float* grad_c,
@@ -387,7 +390,7 @@ int qs_ppo_small_adam(int32_t mb, int32_t D, const qs_mlp256* actor, const qs_ml
 const char* qs_ppo_small_last_error(void);
 /* The workspace's parts (off[QS_PPO_SMALL_LAYOUT_N]): off[0..15] byte offsets
  * of xaT, h1aT, dz2aT, dz1aT, xcT, h1cT, dz2cT, dz1cT (transposed [width][rows
- * padded to 16]), partAa, partBa, partAc, partBc (per-tile partial rows
+ * padded to 64, + 16]), partAa, partBa, partAc, partBc (per-tile partial rows
  * [tile][256 + 256·A + A] = Σ dZ2 | Σ dout·H2 | Σ dout, and [tile][256] = Σ dZ1),
  * dlogstd, the loss partials, the counters; off[16..19] = actor tiles, critic
  * tiles, padded actor rows, padded critic rows; off[20] = bytes; off[21..22] =

@@ -36,7 +36,8 @@
 //     partials.  Four more workgroups reduce the vector parameters (biases,
 //     head, logstd) from the tile partials.
 //  3. ppo_small_apply_kernel (S > 1 only): the chunk partials summed in chunk
-//     order into the same sinks; the last workgroup commits the step counts.
+//     order into the same sinks; one thread commits the step counts (launch 1
+//     formed the bias corrections from them, so nothing waits for the others).
 // Multi-rank: qs_ppo_small_grads runs 1–3 with the gradient
 // buffers as the sink (this rank's minibatch mean); the caller all-reduces
 // [critic grads | actor grads | approx_kl]; qs_ppo_small_adam is launch 3's
@@ -69,23 +70,18 @@ constexpr int kSMaxI = 640;            // widest input (Spiral's centralized cri
 constexpr int kSNarrowI = 256;         // the forward/backward instance for inputs up to this width (smaller LDS X tile)
 constexpr int kSMaxA = 4;
 constexpr int kSAW = 4;                // waves (16×16 tiles) per workgroup of qs_wgrad_t
-constexpr int kSGW = 4;                // waves per weight-gradient workgroup (one weight block and K-chunk; four a CU)
+constexpr int kSGW = 4;                // waves per weight-gradient workgroup (one 64×64 tile and K-chunk)
 constexpr int kSCUs = 256;              // MI355X compute units (one forward/backward tile each)
-constexpr int kSBT1Q = 1 << 30;        // quads (16 rows) from which a net's weight gradients would take 16×16 blocks
-                                       // (never: 32×32 blocks and K-chunks move half the operand bytes per MFMA)
-constexpr int kSGQW = 32;              // most quads per wave of the weight-gradient kernel (compile-time runs of <= 16)
-constexpr int kSGQ = 64;               // quads per K-chunk (1 024 rows, 16 a wave): longer columns in chunk
-                                       // partials, summed by launch 3
 constexpr int kSBlkCnt = 0;            // (no per-block arrival counters)
-static_assert(kSGQ / kSGW <= kSGQW, "a wave's share of a K-chunk must fit s_wgrad_q's runs");
 constexpr int kSMaxS = 32;             // most K-chunks per net
 constexpr int kSPad = 16;              // floats past the padded rows in a transposed activation row
+constexpr int kSScOff = 8;             // the bias corrections' slot in the dlogstd block (SWork::dlogstd)
 // Dynamic LDS reserved (unused) so the dispatcher spreads the workgroups: a
 // forward/backward tile uses ~53 KB (the narrow instance) and would otherwise be
 // packed up to three to a CU while other CUs idle (the grids are one workgroup
 // per CU or fewer); qs_wgrad_t's workgroups two to a CU, the weight-gradient
 // kernel's three.
-constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024, kSReserveG = 0;
+constexpr int kSReserveFB = 32 * 1024, kSReserveW = 72 * 1024;
 
 #ifdef QS_TILE_STAMPS
 // dev builds only: s_memrealtime (100 MHz) at the tile's phase boundaries,
@@ -127,10 +123,11 @@ struct SNet {   // one 256-wide tanh MLP inside its flat Adam buffers (qs_mlp256
 
 struct SWork {   // workspace views (qs_ppo_small_work_bytes)
   float *xaT, *h1aT, *dz2aT, *dz1aT, *xcT, *h1cT, *dz2cT, *dz1cT;
-  float *partAa, *partBa, *partAc, *partBc, *dlogstd;
+  float *partAa, *partBa, *partAc, *partBc;
+  float* dlogstd;   // [0, kSMaxA) d logstd, [kSMaxA] the entropy, [kSScOff, +4) Adam's bias corrections
+                    // (actor bc1, sqrt bc2, critic bc1, sqrt bc2) for this minibatch's step
   double *lossa, *lossc;
-  unsigned* cnt;   // [0] actor tiles, [64] critic tiles, [128] weight-gradient workgroups, [160] apply workgroups,
-                   // [256 + block] chunk arrivals of a chunked weight block
+  unsigned* cnt;   // [0] actor tiles, [64] critic tiles (qs_ppo_critic_tiles' last-tile sums)
   float* wpart[4];   // K-chunk partials [S][256][Mp] of actor W1, actor W2, critic W1, critic W2 (Mp: M padded to 32)
 };
 
@@ -138,11 +135,10 @@ struct SWork {   // workspace views (qs_ppo_small_work_bytes)
 enum { SINK_PART = 0, SINK_ADAM = 1, SINK_GRAD = 2 };
 struct SGrad {
   int S[2];          // K-chunks per net (actor, critic)
-  int bt[2];         // weight-gradient block side per net, in 16-row tiles (1: 16×16, 2: 32×32)
+  int spc[2];        // 64-row steps per K-chunk
   int sink;          // the final sink: SINK_ADAM (one rank) or SINK_GRAD (this rank's gradient, for the all-reduce)
   float* g[2];       // SINK_GRAD / qs_ppo_small_adam: the nets' gradient buffers (flat, the params' layout)
   float gdiv;        // qs_ppo_small_adam: the all-reduced sums ÷ gdiv (the world size), approx_kl too
-  int dev_skip;      // dev builds: bit 0 skips the actor's weight blocks, bit 1 the critic's, bit 2 the vectors
 };
 
 struct SArgs {
@@ -727,8 +723,24 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
 // while the actor's grow, when the CUs hold both)
 // MAXA: the actor's input bound (a narrow actor beside a wide critic: its
 // 48-row X tile sized for its own width)
+// Adam's bias corrections of a net for its next step (float32 of the float64
+// powers, as learner.hip): bc1 = 1 − β1^t, sqrt(bc2) = sqrt(1 − β2^t), t = step + 1
+__device__ __forceinline__ void s_bias_corr(const SNet& N, float* out) {
+  const unsigned t = (unsigned)(*N.step) + 1u;
+  out[0] = (float)(1.0 - s_powi((double)N.beta1, t));
+  out[1] = (float)sqrt(1.0 - s_powi((double)N.beta2, t));
+}
+
 template <int A, bool V1, int MAXI, int RB, int RBC = RB, int MAXA = MAXI>
 __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
+  // The minibatch's bias corrections, from the step counts before any launch of
+  // it changes them: the Adam launches read these, so the one thread that
+  // commits a step count there needs no arrival count of the other workgroups
+  // (a 700-workgroup fan-in on one counter cost ~9 µs)
+  if (!P.fb_tail && blockIdx.x == 0 && threadIdx.x == 0) {
+    s_bias_corr(P.a, P.w.dlogstd + kSScOff);
+    s_bias_corr(P.c, P.w.dlogstd + kSScOff + 2);
+  }
   constexpr int RM = RB > RBC ? RB : RBC;
   constexpr int XA = 16 * RB * s_xs(MAXA), XC = 16 * RBC * s_xs(MAXI);
   constexpr int XSZ = XA > XC ? XA : XC, DSZ = 16 * RM * kSHS;
@@ -789,15 +801,18 @@ __device__ __forceinline__ bool s_gate_rows(const SArgs& P, int l, double (&tot)
   return !P.gate || akl <= P.kl_thr;
 }
 
-// Adam's bias corrections of both nets from their step counts (float32 of the
-// float64 powers, as learner.hip), and whether the actor's KL gate is open
-__device__ __forceinline__ void s_adam_scalars(const SArgs& P, float (&sc)[2][2], int tid) {
-  if (tid < 2) {
-    const SNet& N = tid == 0 ? P.a : P.c;
-    const unsigned t = (unsigned)(*N.step) + 1u;
-    sc[tid][0] = (float)(1.0 - s_powi((double)N.beta1, t));
-    sc[tid][1] = (float)sqrt(1.0 - s_powi((double)N.beta2, t));
-  }
+// Adam's bias corrections of both nets, as launch 1 formed them from the step
+// counts (s_bias_corr): nothing in launches 2 / 3 reads a step count, so the
+// one thread that commits them needs no arrival count
+__device__ __forceinline__ void s_adam_scalars(const SArgs& P, float (*sc)[2], int tid) {
+  if (tid < 4) sc[tid >> 1][tid & 1] = P.w.dlogstd[kSScOff + tid];
+}
+// The step counts' commit (torch.optim.Adam's state['step'] += 1): the critic
+// always, the actor when its KL gate is open (AG:731-760); one thread of one
+// workgroup, after launch 1 read them
+__device__ __forceinline__ void s_commit_steps(const SArgs& P, bool open_a) {
+  if (open_a) *P.a.step = *P.a.step + 1.0f;
+  *P.c.step = *P.c.step + 1.0f;
 }
 __device__ __forceinline__ bool s_gate_open(const SArgs& P) {
   return !P.gate || *P.kl_out / P.G.gdiv <= P.kl_thr;
@@ -841,297 +856,308 @@ __device__ __forceinline__ bool s_vec_loc(const SArgs& P, int e, bool& actor, lo
   return true;
 }
 
-// A weight matrix's 32×32 blocks: W1 [256][I] (⌈I/32⌉ column blocks) then W2
-// [256][256]; nblk(N) blocks per net
-// 16·BT-square blocks of W1 [256][I] (⌈I/(16·BT)⌉ column blocks) then W2 [256][256]:
-// s_nblk(I, BT) blocks per net; the chunk partials' rows are s_mp(I) wide for either BT
-__host__ __device__ inline int s_cb(int I, int bt) { return (I + 16 * bt - 1) / (16 * bt); }
-__host__ __device__ inline int s_nblk(int I, int bt) { return (16 / bt) * s_cb(I, bt) + (16 / bt) * (16 / bt); }
-__host__ __device__ inline int s_mp(int I) { return 32 * ((I + 31) / 32); }
+// ---------------------------------------------------------------- launch 2: weight gradients
+// dW1 = dZ1ᵀ·X and dW2 = dZ2ᵀ·H1 of both nets from the transposed activations
+// launch 1 wrote ([rows][K], K contiguous: C[n][m] = Σ_k A[n][k]·B[m][k]).  One
+// 4-wave workgroup per 64×64 output tile and K-chunk (a run of 64-row steps):
+// each wave owns a 32×32 quadrant (2×2 MFMA tiles, four accumulator chains),
+// the tile's two 64-row operand panels are staged global → LDS by
+// global_load_lds (16 B a lane) into a four-stage ring, three stages in flight
+// while the fourth is read (counted vmcnt + raw s_barrier: the loads stay in
+// flight across the barrier; with three stages a step took ~1.6 µs against
+// ~0.85 of MFMA work: the loads' latency was not covered).  The four waves share every staged byte, so L2
+// serves each operand row once per 64 outputs (the 32×32 blocks of round 5,
+// a wave per K-quarter, read every operand byte 8× over: 0.20 of the MFMA peak).
+// One chunk per tile (S = 1): the gradient goes straight into its sink (Adam
+// in place, or the gradient buffer); otherwise the chunk partials of launch 3.
+constexpr int kGT = 64;                   // output tile side (n and m)
+constexpr int kGBK = 64;                  // K-rows per LDS stage (four quads)
+constexpr int kGNS = 4;                   // stages in the LDS ring (three in flight while one is read)
+constexpr int kGPanel = kGT * kGBK;       // floats of one operand's stage image (16 KB)
+constexpr int kGLdsBytes = kGNS * 2 * kGPanel * 4 + 64;   // (+ the Adam scalars and the gate flag)
 
-// c[bi·BT + bj] += Σ over NQ quads (16 rows each) of
-// dZᵀ[16bi + j][rows]·Xᵀ[16bj + j][rows] for the BT×BT 16×16 MFMA tiles of a
-// block (rows of a0 / b0 at their first quad; row 16 further: a1 / b1).  NQ is
-// a compile-time count (a run-time bound made the compiler wait for every
-// outstanding load at the loop's back edge): the loop unrolls fully, R quads of
-// float4 operands in flight; BT = 1 alternates two accumulator chains.
-template <int BT, int NQ>
-__device__ __forceinline__ void s_wgrad_n(const float* a0, const float* a1, const float* b0, const float* b1, int g,
-                                          f32x4 (&c)[BT * BT]) {
-  constexpr int RM = BT == 1 ? 8 : 4;
-  constexpr int R = NQ < RM ? NQ : RM;
-  constexpr int NO = 2 * BT;   // float4 operands per quad
-  float4 ring[R][NO];
-  auto ld = [&](int t, float4 (&o)[NO]) {
-    const int q = 16 * t + 4 * g;
-    o[0] = *reinterpret_cast<const float4*>(a0 + q);
-    o[1] = *reinterpret_cast<const float4*>(b0 + q);
-    if constexpr (BT == 2) {
-      o[2] = *reinterpret_cast<const float4*>(a1 + q);
-      o[3] = *reinterpret_cast<const float4*>(b1 + q);
-    }
+__host__ __device__ inline int s_gcb(int I) { return (I + kGT - 1) / kGT; }     // W1's column tiles
+__host__ __device__ inline int s_gtiles(int I) { return 16 + 4 * s_gcb(I); }    // W2's 4×4, then W1's 4×cb
+__host__ __device__ inline int s_mp(int I) { return 32 * ((I + 31) / 32); }     // a chunk partial's row width
+
+// global_load_lds_dwordx4 by inline asm: the compiler neither counts it nor, not
+// knowing which LDS bytes it writes, drains it with vmcnt(0) before every ds_read
+// of the ring (the builtin's form did: the stages in flight were waited for at
+// each step).  The ring's waits are the counted ones in the kernel.  m0: the
+// wave-uniform LDS byte address (lane l writes m0 + 16·l).
+__device__ __forceinline__ void s_glds16(const float* gsrc, unsigned m0v) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(m0v)
+               : "memory");
+}
+// A stage image of one operand: tile rows 0..63 of a transposed activation, K-columns
+// k0 .. k0+63, as [row][64] with the 16-B pieces XOR-swizzled (piece p of row r at
+// position p ^ (r & 15): a 16-lane float4 read of one piece of 16 consecutive rows
+// covers all 64 banks).  The LDS destination of an LDS-DMA load is lane-linear, so
+// the swizzle is on the source: instruction q fills rows 4q .. 4q+3, wave w issues
+// q = 4w .. 4w+3; src[i] is lane l's row / piece of instruction 4w + i (rows past
+// the operand's last clamped to it, their products discarded), m0: the image's
+// LDS byte address of instruction 4w.
+__device__ __forceinline__ void s_gstage(const float* const (&src)[4], int k0, unsigned m0) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s_glds16(src[i] + k0, m0 + 1024u * i);
+}
+__device__ __forceinline__ void s_gsrc(const float* base, int KS, int rmax, int w, int l, const float* (&src)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * (4 * w + i) + (l >> 4), p = l & 15;
+    src[i] = base + (size_t)min(r, rmax) * KS + 4 * (p ^ (r & 15));
+  }
+}
+// The wave's quadrant over one stage's four quads: c[2·rb + cb] += A rows 32wn + 16rb + j ×
+// B rows 32wm + 16cb + j, κ = 16t + 4g + e (lane (g, j) reads piece 4t + g of its row).
+// mid(): issued once the first quad's operand reads are (the next stage's loads:
+// their issue then overlaps those reads' latency instead of delaying them).
+template <class MID>
+__device__ __forceinline__ void s_gquads(const float* la, const float* lb, int wn, int wm, int g, int j,
+                                         f32x4 (&c)[4], MID mid) {
+  float4 a[4][2], b[4][2];
+  auto rd = [&](int t) {
+#if defined(QS_WG_X) && (QS_WG_X & 2)
+    // dev probe: no LDS reads (register operands)
+    a[t][0] = a[t][1] = b[t][0] = b[t][1] = make_float4(la[0] + t, 1.f, 2.f, 3.f);
+    return;
+#endif
+    const int ph = 4 * ((4 * t + g) ^ j);
+    a[t][0] = *reinterpret_cast<const float4*>(la + (32 * wn + j) * kGBK + ph);
+    a[t][1] = *reinterpret_cast<const float4*>(la + (32 * wn + 16 + j) * kGBK + ph);
+    b[t][0] = *reinterpret_cast<const float4*>(lb + (32 * wm + j) * kGBK + ph);
+    b[t][1] = *reinterpret_cast<const float4*>(lb + (32 * wm + 16 + j) * kGBK + ph);
   };
+  rd(0);
+  mid();
 #pragma unroll
-  for (int k = 0; k < R; ++k) ld(k, ring[k]);
-  f32x4 c1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 1; t < 4; ++t) rd(t);
 #pragma unroll
-  for (int t = 0; t < NQ; ++t) {
-    float4 o[NO];
-#pragma unroll
-    for (int u = 0; u < NO; ++u) o[u] = ring[t % R][u];
-    if (t + R < NQ) ld(t + R, ring[t % R]);
-    __builtin_amdgcn_sched_barrier(0);   // keep the loads R quads ahead
-    if constexpr (BT == 1) {
-      f32x4& acc = (t & 1) ? c1 : c[0];
-      acc = s_mfma(o[0].x, o[1].x, acc);
-      acc = s_mfma(o[0].y, o[1].y, acc);
-      acc = s_mfma(o[0].z, o[1].z, acc);
-      acc = s_mfma(o[0].w, o[1].w, acc);
-    } else {
-#define S_Q4(E)                           \
-  c[0] = s_mfma(o[0].E, o[1].E, c[0]);    \
-  c[1] = s_mfma(o[0].E, o[3].E, c[1]);    \
-  c[2] = s_mfma(o[2].E, o[1].E, c[2]);    \
-  c[3] = s_mfma(o[2].E, o[3].E, c[3]);
-      S_Q4(x) S_Q4(y) S_Q4(z) S_Q4(w)
-#undef S_Q4
-    }
+  for (int t = 0; t < 4; ++t) {
+#define S_GQ(E)                                  \
+  c[0] = s_mfma(a[t][0].E, b[t][0].E, c[0]);     \
+  c[1] = s_mfma(a[t][0].E, b[t][1].E, c[1]);     \
+  c[2] = s_mfma(a[t][1].E, b[t][0].E, c[2]);     \
+  c[3] = s_mfma(a[t][1].E, b[t][1].E, c[3]);
+    S_GQ(x) S_GQ(y) S_GQ(z) S_GQ(w)
+#undef S_GQ
   }
-  if constexpr (BT == 1) c[0] += c1;
-}
-// nq (0 .. kSGQW) quads: runs of 16, then the remainder, by dispatch to the compile-time count
-template <int BT>
-__device__ __forceinline__ void s_wgrad_q(const float* a0, const float* a1, const float* b0, const float* b1, int nq,
-                                          int g, f32x4 (&c)[BT * BT]) {
-  for (; nq > 16; nq -= 16, a0 += 256, a1 += 256, b0 += 256, b1 += 256) s_wgrad_n<BT, 16>(a0, a1, b0, b1, g, c);
-  switch (nq) {
-#define S_CASE(n) case n: s_wgrad_n<BT, n>(a0, a1, b0, b1, g, c); break;
-    S_CASE(1) S_CASE(2) S_CASE(3) S_CASE(4) S_CASE(5) S_CASE(6) S_CASE(7) S_CASE(8)
-    S_CASE(9) S_CASE(10) S_CASE(11) S_CASE(12) S_CASE(13) S_CASE(14) S_CASE(15) S_CASE(16)
-#undef S_CASE
-    default: break;
-  }
-}
-
-// One 16·BT-square block of a weight matrix and K-chunk s of S (launch 2):
-// wave w forms the block's BT×BT MFMA tiles over its quarter of the chunk's
-// quads; the waves' sums are added in wave order through LDS, each wave then
-// taking BT² of every lane's elements (f = BT²·w + k → tile f/4, register
-// f%4).  S = 1: into the final sink (Adam with its p / m / v loaded ahead, or
-// the gradient buffer); otherwise the chunk partials of launch 3.
-template <int BT>
-__device__ __forceinline__ void s_wblock(const SArgs& P, bool actor, int S, int s, int u, bool adam,
-                                         float (*red)[16][64], const float (*sc)[2], bool* sopen) {
-  constexpr int NT = BT * BT;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
-  const SNet& N = actor ? P.a : P.c;
-  const bool direct = S == 1;
-  // logical block u: W2's G×G grid first, in eight (G/4)×(G/2) sub-grids of
-  // consecutive blocks (one XCD's share after s_xcd_swz: a quarter of dZ2ᵀ's
-  // rows and half of H1ᵀ's stay in that XCD's L2), then W1's blocks
-  constexpr int G = 16 / BT, GT = G * G / 8;
-  const int cb = s_cb(N.I, BT);
-  const bool l1 = u >= G * G;
-  int n0, m0;
-  if (!l1) {
-    const int tile = u / GT, v = u - tile * GT;
-    n0 = 16 * BT * ((G / 4) * (tile >> 1) + v / (G / 2));
-    m0 = 16 * BT * ((G / 2) * (tile & 1) + v % (G / 2));
-  } else {
-    const int uu = u - G * G;
-    n0 = 16 * BT * (uu / cb);
-    m0 = 16 * BT * (uu % cb);
-  }
-  const int M = l1 ? N.I : kSH;
-  // the sink: register slot f = w + kSGW·k of every lane (tile f/4, register f%4), f < 4·NT
-  constexpr int NF = (4 * NT + kSGW - 1) / kSGW;   // slots per wave
-  int en[NF], em[NF];
-  long long ei[NF];
-  float pp[NF], pm[NF], pv[NF];
-#pragma unroll
-  for (int k = 0; k < NF; ++k) {
-    const int f = w + kSGW * k, q = f >> 2, r = f & 3;
-    en[k] = n0 + 16 * (q / BT) + 4 * g + r;
-    em[k] = m0 + 16 * (q % BT) + j;
-    ei[k] = (l1 ? N.w1 : N.w2) + (long long)en[k] * M + em[k];
-    pp[k] = pm[k] = pv[k] = 0.f;
-    if (f < 4 * NT && direct && adam && em[k] < M) {   // Adam's operands, in flight during the gradient
-      pp[k] = N.p[ei[k]];
-      pm[k] = N.m[ei[k]];
-      pv[k] = N.v[ei[k]];
-    }
-  }
-  const int KP = actor ? P.KaP : P.KcP, KS = actor ? P.KaS : P.KcS;
-  const float* dzT = actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT);
-  const float* xT = actor ? (l1 ? P.w.xaT : P.w.h1aT) : (l1 ? P.w.xcT : P.w.h1cT);
-  // the chunk's quads, split over the waves (contiguous, wave order)
-  const int Q = KP / 16, qc = (Q + S - 1) / S, q0 = min(Q, s * qc), q1 = min(Q, q0 + qc);
-  const int qw = (q1 - q0 + kSGW - 1) / kSGW;
-  const int wa = min(q1, q0 + w * qw), wb = min(q1, wa + qw);
-  f32x4 c[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) c[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // (columns past M are not stored: clamped, their sums discarded)
-  s_wgrad_q<BT>(dzT + (size_t)(n0 + j) * KS + 16 * wa, dzT + (size_t)(n0 + 16 + j) * KS + 16 * wa,
-                xT + (size_t)min(m0 + j, M - 1) * KS + 16 * wa, xT + (size_t)min(m0 + 16 + j, M - 1) * KS + 16 * wa,
-                wb - wa, g, c);
-  W_STAMP(1);
-  if (w == 0 && adam && actor) {   // the actor's KL gate (AG:731-734), before the sums are read
-    double tot[2 + kSMaxA];
-    const bool o = s_gate_rows(P, l, tot);
-    if (l == 0) *sopen = o;
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) red[w][4 * t + k][l] = c[t][k];
-  __syncthreads();
-  W_STAMP(2);
-  const bool act = !(adam && actor) || *sopen;
-  const int si = actor ? 0 : 1;
-  float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
-  const int Mp = l1 ? s_mp(N.I) : kSH;
-  float tot[NF];
-#pragma unroll
-  for (int k = 0; k < NF; ++k) {
-    const int f = w + kSGW * k;
-    if (f >= 4 * NT) break;
-    tot[k] = red[0][f][l];
-#pragma unroll
-    for (int v = 1; v < kSGW; ++v) tot[k] += red[v][f][l];
-    if (!direct) {
-      part[((size_t)s * kSH + en[k]) * Mp + em[k]] = tot[k];   // (pad columns too)
-    } else if (act && em[k] < M) {
-      if (!adam) P.G.g[si][ei[k]] = tot[k];
-      else s_adam(N, ei[k], tot[k], sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en[k], em[k], l1 ? N.w1p : nullptr,
-                  pp[k], pm[k], pv[k]);
-    }
-  }
-  // (K-chunks: launch 3 sums the partials.  Summing them here, in the block's
-  // last-arriving workgroup, needed an agent-scope release per workgroup before
-  // its arrival count: +18 µs at C3/8, the L2 write-backs serialising)
 }
 
 // Workgroup T of n consecutive ones (the dispatcher deals them to the 8 XCDs
 // round-robin, T mod 8) → logical index: each XCD's workgroups take one
-// contiguous range of logical indices (neighbouring blocks share operand rows
-// in that XCD's L2); the last n mod 8 unchanged
+// contiguous range of logical indices (the tiles of one K-chunk share its
+// operand rows in that XCD's L2); the last n mod 8 unchanged
 __device__ __forceinline__ int s_xcd_swz(int T, int n) {
   const int per = n >> 3;
   if (per == 0 || T >= 8 * per) return T;
   return (T & 7) * per + (T >> 3);
 }
 
-// Launch 2.  Workgroups [0, Σ blocks·S): one weight block and K-chunk each
-// (s_wblock; the actor's first, the chunks of a block adjacent; 16×16 blocks
-// for a net with long columns (P.G.bt = 1: enough blocks to fill the CUs),
-// 32×32 otherwise (four float4 operands per 16 MFMAs)); then the vector
-// parameters, 16 lanes per element (lane k sums the tile partial rows
-// t ≡ k mod 16 in order, a fixed DPP butterfly adds the lanes), into P.G.sink.
-// With Adam and no launch 3 the last workgroup commits the step counts.
-__global__ void __launch_bounds__(64 * kSGW) __attribute__((amdgpu_waves_per_eu(4)))
-ppo_small_wgrad_kernel(SArgs P, int fin) {
-  // (4 waves a SIMD: four 4-wave workgroups a CU, the grid in one round)
-  __shared__ float red[kSGW][16][64];
-  __shared__ float sc[2][2];
-  __shared__ bool last, sopen;
+// The vector parameters' workgroup vb of launch 2 (b1, b2, W3, b3 of both nets,
+// the actor's logstd), 16 lanes per element: lane k sums the tile partial rows
+// t ≡ k mod 16 in order, a fixed DPP butterfly adds the lanes, into P.G.sink.
+// Workgroup 0's wave 0 also records the minibatch's loss statistics and (fin:
+// no launch 3 follows, Adam) commits the step counts.
+__device__ __forceinline__ void s_vec_wg(const SArgs& P, int vb, bool adam, bool fin, const float (*sc)[2]) {
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  s_adam_scalars(P, sc, tid);
-  const bool adam = P.G.sink == SINK_ADAM;
-  const int nwa = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0], nwc = s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1];
-  const int blk = blockIdx.x;
-  __syncthreads();   // (sc)
-  W_STAMP(0);
-#ifdef QS_DEV_BUILD
-  if ((P.G.dev_skip & 1) && blk < nwa) return;
-  if ((P.G.dev_skip & 2) && blk >= nwa && blk < nwa + nwc) return;
-  if ((P.G.dev_skip & 4) && blk >= nwa + nwc) return;
-#endif
-  if (blk < nwa + nwc) {
-    const bool actor = blk < nwa;
-    const int S = P.G.S[actor ? 0 : 1];
-    // logical index, K-chunk major: an XCD's contiguous share of them (s_xcd_swz) is one
-    // or two chunks' rows of the operands
-    const int T = s_xcd_swz(actor ? blk : blk - nwa, actor ? nwa : nwc);
-    const int nb = (actor ? nwa : nwc) / S, s = T / nb, u = T - s * nb;
-    if (P.G.bt[actor ? 0 : 1] == 1) s_wblock<1>(P, actor, S, s, u, adam, red, sc, &sopen);
-    else s_wblock<2>(P, actor, S, s, u, adam, red, sc, &sopen);
-  } else {
-    // the actor's loss totals (every wave: the gate, logstd's gradient)
-    double tot[2 + kSMaxA];
-    const bool open_a = s_gate_rows(P, l, tot);
-    const int e = ((blk - nwa - nwc) * (int)blockDim.x + tid) >> 4, k = tid & 15;
-    bool actor;
-    long long i;
-    const float* col;
-    int cstride, nt, u;
-    if (s_vec_loc(P, e, actor, i, col, cstride, nt, u)) {   // (uniform over the element's 16 lanes)
-      const SNet& N = actor ? P.a : P.c;
-      const bool doit = !adam || !actor || open_a;
-      float p0 = 0.f, m0 = 0.f, v0 = 0.f;
-      if (adam && k == 0) {
-        p0 = N.p[i];
-        m0 = N.m[i];
-        v0 = N.v[i];
-      }
-      float gsum;
-      if (col) {
-        float acc = 0.f;
-        int tt = k;
-        for (; tt + 16 * 7 < nt; tt += 16 * 8) {
-          float v[8];
+  // the actor's loss totals (every wave: the gate, logstd's gradient)
+  double tot[2 + kSMaxA];
+  const bool open_a = s_gate_rows(P, l, tot);
+  const int e = (vb * (int)blockDim.x + tid) >> 4, k = tid & 15;
+  bool actor;
+  long long i;
+  const float* col;
+  int cstride, nt, u;
+  if (s_vec_loc(P, e, actor, i, col, cstride, nt, u)) {   // (uniform over the element's 16 lanes)
+    const SNet& N = actor ? P.a : P.c;
+    const bool doit = !adam || !actor || open_a;
+    float p0 = 0.f, m0 = 0.f, v0 = 0.f;
+    if (adam && k == 0) {
+      p0 = N.p[i];
+      m0 = N.m[i];
+      v0 = N.v[i];
+    }
+    float gsum;
+    if (col) {
+      float acc = 0.f;
+      int tt = k;
+      for (; tt + 16 * 7 < nt; tt += 16 * 8) {
+        float v[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = col[(size_t)(tt + 16 * q) * cstride];
+        for (int q = 0; q < 8; ++q) v[q] = col[(size_t)(tt + 16 * q) * cstride];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc += v[q];
-        }
-        for (; tt < nt; tt += 16) acc += col[(size_t)tt * cstride];
-        gsum = s_row_sum(acc);
-      } else {   // logstd: d(policy)/d logstd from the loss rows − ent_coef (AG:602-640)
-        gsum = (float)tot[2 + u] - P.ent_coef;
+        for (int q = 0; q < 8; ++q) acc += v[q];
       }
-      if (doit && k == 0) {
-        if (!adam) {
-          P.G.g[actor ? 0 : 1][i] = gsum;
-        } else {
-          const int si = actor ? 0 : 1;
-          s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, p0, m0, v0);
-        }
+      for (; tt < nt; tt += 16) acc += col[(size_t)tt * cstride];
+      gsum = s_row_sum(acc);
+    } else {   // logstd: d(policy)/d logstd from the loss rows − ent_coef (AG:602-640)
+      gsum = (float)tot[2 + u] - P.ent_coef;
+    }
+    if (doit && k == 0) {
+      if (!adam) {
+        P.G.g[actor ? 0 : 1][i] = gsum;
+      } else {
+        const int si = actor ? 0 : 1;
+        s_adam(N, i, gsum, sc[si][0], sc[si][1], nullptr, 0, 0, nullptr, p0, m0, v0);
       }
     }
-    if (blk == nwa + nwc && w == 0) {
-      // the minibatch's loss statistics (the fb tail of ppo_heads_kernel's arithmetic):
-      // approx_kl (the gate's value; the multi-rank exchange averages it), dlogstd, acc
-      double totc[2 + kSMaxA];
-      s_loss_tot(P.w.lossc, P.nC, 1, l, totc);
-      if (l == 0) {
-        const int A = P.a.A;
-        const double K = (double)(P.mb * P.D);
-        const float ent = P.w.dlogstd[kSMaxA];   // (launch 1's tile 0: the logstd before this launch's Adam)
-        for (int a = 0; a < A; ++a) P.w.dlogstd[a] = (float)tot[2 + a] - P.ent_coef;
-        const float akl = (float)(tot[1] / K);
-        *P.kl_out = akl;
-        P.acc[0] += tot[0] / K;
-        P.acc[1] += 0.5 * (totc[0] / (double)P.mb);
-        P.acc[2] += (double)(-ent);
-        P.acc[3] += (double)akl;
-      }
+  }
+  if (vb == 0 && w == 0) {
+    // the minibatch's loss statistics (the fb tail of ppo_heads_kernel's arithmetic):
+    // approx_kl (the gate's value; the multi-rank exchange averages it), dlogstd, acc
+    double totc[2 + kSMaxA];
+    s_loss_tot(P.w.lossc, P.nC, 1, l, totc);
+    if (l == 0) {
+      const int A = P.a.A;
+      const double K = (double)(P.mb * P.D);
+      const float ent = P.w.dlogstd[kSMaxA];   // (launch 1's tile 0: the logstd before this launch's Adam)
+      for (int a = 0; a < A; ++a) P.w.dlogstd[a] = (float)tot[2 + a] - P.ent_coef;
+      const float akl = (float)(tot[1] / K);
+      *P.kl_out = akl;
+      P.acc[0] += tot[0] / K;
+      P.acc[1] += 0.5 * (totc[0] / (double)P.mb);
+      P.acc[2] += (double)(-ent);
+      P.acc[3] += (double)akl;
+      // no launch 3: the step counts (nothing in this launch reads them)
+      if (fin && adam) s_commit_steps(P, open_a);
+    }
+  }
+}
+
+// Launch 2.  Workgroups [0, Σ tiles·S): one 64×64 tile of a weight matrix and
+// one K-chunk each (the actor's first; within a net chunk-major, so an XCD's
+// share of them (s_xcd_swz) is one chunk's operand rows); then the vector
+// parameters (s_vec_wg).  fin: no launch 3 follows (every net in one chunk).
+__global__ void __launch_bounds__(256) ppo_small_wgrad_kernel(SArgs P, int fin) {
+  // ONE dynamic LDS array (a second __shared__ object beside the LDS-DMA ring can
+  // make the compiler drain every load before each stage's reads)
+  extern __shared__ __attribute__((aligned(16))) float s_lds[];
+  float (*sc)[2] = reinterpret_cast<float (*)[2]>(s_lds + kGNS * 2 * kGPanel);
+  int* sopen = reinterpret_cast<int*>(s_lds + kGNS * 2 * kGPanel + 4);
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const bool adam = P.G.sink == SINK_ADAM;
+  const int ua = s_gtiles(P.a.I) * P.G.S[0], uc = s_gtiles(P.c.I) * P.G.S[1];
+  const int blk = blockIdx.x;
+  s_adam_scalars(P, sc, tid);
+  W_STAMP(0);
+  if (blk >= ua + uc) {
+    __syncthreads();   // (sc)
+    s_vec_wg(P, blk - ua - uc, adam, fin, sc);
+    W_STAMP(3);
+    return;
+  }
+  const bool actor = blk < ua;
+  // (by value: through a reference into the kernel arguments every Adam element
+  // reloaded the net's pointers and scalars behind the stores — ~5 µs of sink)
+  const SNet N = actor ? P.a : P.c;
+  const int si = actor ? 0 : 1, S = P.G.S[si], spc = P.G.spc[si], nt = s_gtiles(N.I);
+  const int T = s_xcd_swz(actor ? blk : blk - ua, actor ? ua : uc);
+  const int s = T / nt, t = T - s * nt;
+  const bool l1 = t >= 16;
+  int n0, m0;
+  if (!l1) {
+    n0 = kGT * (t >> 2);
+    m0 = kGT * (t & 3);
+  } else {
+    const int tt = t - 16, cb = s_gcb(N.I);
+    n0 = kGT * (tt / cb);
+    m0 = kGT * (tt % cb);
+  }
+  const int M = l1 ? N.I : kSH;
+  const int KS = actor ? P.KaS : P.KcS;
+  const int nsteps = ((actor ? P.KaP : P.KcP) + kGBK - 1) / kGBK;
+  const int st0 = s * spc, ns = min(nsteps, st0 + spc) - st0;
+  const float* Ab = (actor ? (l1 ? P.w.dz1aT : P.w.dz2aT) : (l1 ? P.w.dz1cT : P.w.dz2cT)) + (size_t)n0 * KS;
+  const float* Bb = (actor ? (l1 ? P.w.xaT : P.w.h1aT) : (l1 ? P.w.xcT : P.w.h1cT)) + (size_t)m0 * KS;
+  const int bmax = min(kGT - 1, M - 1 - m0);
+  const int wn = w >> 1, wm = w & 1;
+  const bool live = kGT / 2 * wm < M - m0;   // the wave's 32 columns hold some of the matrix's
+  const bool direct = S == 1;
+  // the sink's elements: slot f = 4q + r, tile q = 2rb + cb, register r
+  long long ei[16];
+  float pp[16], pm[16], pv[16];
+#pragma unroll
+  for (int f = 0; f < 16; ++f) {
+    const int q = f >> 2, r = f & 3;
+    const int en = n0 + 32 * wn + 16 * (q >> 1) + 4 * g + r, em = m0 + 32 * wm + 16 * (q & 1) + j;
+    ei[f] = (l1 ? N.w1 : N.w2) + (long long)en * M + em;
+    pp[f] = pm[f] = pv[f] = 0.f;
+    if (direct && adam && em < M) {   // Adam's operands, in flight during the contraction
+      pp[f] = N.p[ei[f]];
+      pm[f] = N.m[ei[f]];
+      pv[f] = N.v[ei[f]];
+    }
+  }
+  f32x4 c[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the ring: stage i in image i mod kGNS; stages i + 1 .. i + kGNS − 1 in flight while i is read
+  const float* asrc[4];
+  const float* bsrc[4];
+  s_gsrc(Ab, KS, kGT - 1, w, l, asrc);
+  s_gsrc(Bb, KS, bmax, w, l, bsrc);
+  const unsigned wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) float*)s_lds + 4096u * wu;
+  auto stage = [&](int k) {   // stage k (a step of the chunk) into image k mod kGNS
+#if defined(QS_WG_X) && (QS_WG_X & 1)
+    return;   // dev probe: no operand loads (the contraction reads stale LDS)
+#endif
+    const unsigned m0 = lds0 + (unsigned)((k % kGNS) * 2 * kGPanel * 4);
+    s_gstage(asrc, kGBK * (st0 + k), m0);
+    s_gstage(bsrc, kGBK * (st0 + k), m0 + kGPanel * 4);
+  };
+  for (int k = 0; k < kGNS - 1 && k < ns; ++k) stage(k);
+  static_assert(kGNS == 4, "the counted waits below assume at most two stages after the one read");
+  for (int i = 0; i < ns; ++i) {
+    // this wave's eight loads of stage i landed (the later stages' may stay in
+    // flight: eight loads a stage), then every wave's: the barrier
+    const int ahead = min(kGNS - 2, ns - 1 - i);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const float* img = s_lds + (i % kGNS) * 2 * kGPanel;
+    // stage i + kGNS − 1 goes into the image every wave finished reading in step i − 1
+    auto next = [&]() {
+      if (i + kGNS - 1 < ns) stage(i + kGNS - 1);
+    };
+    // (every wave contracts, a dead quadrant too: a branch around the MFMAs made the
+    // compiler copy the accumulators between AGPRs and VGPRs every step)
+    s_gquads(img, img + kGPanel, wn, wm, g, j, c, next);
+  }
+  W_STAMP(1);
+  __syncthreads();   // (sc; no LDS-DMA in flight)
+  if (w == 0 && direct && adam && actor) {   // the actor's KL gate (AG:731-734)
+    double tot[2 + kSMaxA];
+    const bool o = s_gate_rows(P, l, tot);
+    if (l == 0) *sopen = o;
+  }
+  __syncthreads();
+  W_STAMP(2);
+  if (!live) return;
+  const bool act = !(adam && actor) || *sopen;
+  float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
+  const int Mp = l1 ? s_mp(N.I) : kSH;
+#pragma unroll
+  for (int f = 0; f < 16; ++f) {
+    const int q = f >> 2, r = f & 3;
+    const int en = n0 + 32 * wn + 16 * (q >> 1) + 4 * g + r, em = m0 + 32 * wm + 16 * (q & 1) + j;
+    if (em >= M) continue;
+    const float v = c[q][r];
+    if (!direct) {
+      part[((size_t)s * kSH + en) * Mp + em] = v;
+    } else if (act) {
+      if (!adam) P.G.g[si][ei[f]] = v;
+      else s_adam(N, ei[f], v, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en, em, l1 ? N.w1p : nullptr, pp[f],
+                  pm[f], pv[f]);
     }
   }
   W_STAMP(3);
-  if (!fin || !adam) return;
-  __syncthreads();
-  if (tid == 0) last = atomicAdd(P.w.cnt + 128, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last || w != 0) return;
-  // every workgroup read the step counts before arriving
-  double tot[2 + kSMaxA];
-  const bool open_a = s_gate_rows(P, l, tot);
-  if (l == 0) {
-    P.w.cnt[128] = 0u;
-    if (open_a) *P.a.step = *P.a.step + 1.0f;
-    *P.c.step = *P.c.step + 1.0f;
-  }
 }
 
 // Launch 3, one thread per parameter element: FROM_G = false — the weight
@@ -1140,11 +1166,10 @@ ppo_small_wgrad_kernel(SArgs P, int fin) {
 // all-reduce) — every parameter's gradient from the gradient buffers ÷ gdiv,
 // into Adam.  Elements: actor W1, W2, critic W1, W2 (row-major, as the
 // parameters; FROM_G = false: only those of nets with S > 1), then (FROM_G)
-// the vector parameters.  With Adam the last workgroup commits the step counts.
+// the vector parameters.  With Adam one thread commits the step counts.
 template <bool FROM_G>
 __global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
   __shared__ float sc[2][2];
-  __shared__ bool last;
   const int tid = threadIdx.x;
   const int sink = FROM_G ? SINK_ADAM : P.G.sink;
   // the element, its gradient and Adam operands first (in flight across the scalars' barrier)
@@ -1206,15 +1231,8 @@ __global__ void __launch_bounds__(256) ppo_small_apply_kernel(SArgs P) {
     else s_adam(N, i, gsum, sc[si][0], sc[si][1], w2 ? N.w2t : nullptr, n, m, part < 4 && l1 ? N.w1p : nullptr, p0, m0,
                 v0);
   }
-  if (sink != SINK_ADAM) return;
-  __syncthreads();
-  if (tid == 0) last = atomicAdd(P.w.cnt + 160, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (last && tid == 0) {
-    P.w.cnt[160] = 0u;
-    if (open_a) *P.a.step = *P.a.step + 1.0f;
-    *P.c.step = *P.c.step + 1.0f;
-  }
+  // the step counts, by one thread (nothing in this launch reads them)
+  if (sink == SINK_ADAM && blockIdx.x == 0 && tid == 0) s_commit_steps(P, open_a);
 }
 
 // Split-K weight gradient from transposed activations: partial[s][n][m] =
@@ -1244,31 +1262,41 @@ struct SLayout {
   int rb, rbc;    // 16-row blocks per forward/backward tile: the actor's, the critic's
   int nA, nC, KaP, KcP, KaS, KcS;
   int Sa, Sc;     // K-chunks of the weight gradients per net
-  int bta, btc;   // their block sides in 16-row tiles
+  int spca, spcc; // their 64-row steps per chunk
   long long off[20];
   long long bytes;
 };
-// A net's weight-gradient blocks: 16×16 once its columns are long (≥ kSBT1Q
-// quads: the 16×16 blocks' count fills the CUs and each stays MFMA-busy), 32×32
-// below; K-chunks only for 16×16 blocks past kSGQ quads per chunk
-inline int s_bt(long long KP) { return KP / 16 >= kSBT1Q ? 1 : 2; }
-inline int s_chunks(long long KP) {
-  const long long q = KP / 16;
-#ifdef QS_DEV_BUILD
-  static const int gq = [] {   // dev probe: QS_SMALL_GQ quads per K-chunk (a multiple of 16, <= kSGW·kSGQW)
-    const char* e = getenv("QS_SMALL_GQ");
-    const int v = e ? atoi(e) : kSGQ;
-    return v >= 16 && v <= kSGW * kSGQW && v % 16 == 0 ? v : kSGQ;
-  }();
-#else
-  constexpr int gq = kSGQ;
-#endif
-  long long S = (q + gq - 1) / gq;
-  // a remainder of at most gq/8 quads joins the other chunks (48-row tiles pad
-  // 1 024 critic rows to 1 056: a second chunk sent the critic through launch 3,
-  // 8 → 15 µs at C3/4)
-  if (S > 1 && q - (S - 1) * gq <= gq / 8) --S;
-  return (int)(S < 1 ? 1 : (S > kSMaxS ? kSMaxS : S));
+// The weight gradients' K-chunks of both nets (launch 2): steps of 64 rows,
+// spc per chunk.  A 64×64 tile and chunk is one workgroup on one CU for about
+// spc × 2 048 MFMA cycles (~0.85 µs a step) plus ~1.5 steps of fill (the first
+// stages' latency), so the launch takes about (rounds of the CUs) × (the
+// longest chunk + 1.5); each chunk adds ~0.3 MB of partials that launch 3
+// reads back (~0.2 step), and one chunk per net needs no launch 3 (~6 steps
+// with its boundary).  The cheapest (Sa, Sc) by that estimate.
+inline void s_chunks(int Ia, int Ic, long long KaP, long long KcP, SLayout& L) {
+  const int na = Ia > 0 ? (int)((KaP + kGBK - 1) / kGBK) : 0, nc = (int)((KcP + kGBK - 1) / kGBK);
+  const int ta = Ia > 0 ? s_gtiles(Ia) : 0, tc = s_gtiles(Ic);
+  double best = 1e30;
+  L.Sa = Ia > 0 ? 1 : 0;
+  L.Sc = 1;
+  for (int pa = 1; pa <= (na > 0 ? na : 1); ++pa) {        // steps per actor chunk
+    const int Sa = na > 0 ? (na + pa - 1) / pa : 0;
+    if (Sa > kSMaxS) continue;
+    for (int pc = 1; pc <= nc; ++pc) {
+      const int Sc = (nc + pc - 1) / pc;
+      if (Sc > kSMaxS) continue;
+      const int units = ta * Sa + tc * Sc, rounds = (units + kSCUs - 1) / kSCUs;
+      const int longest = std::max(na > 0 ? pa : 0, pc);
+      const double cost = rounds * (longest + 1.5) + 0.2 * (Sa + Sc) + ((Sa > 1 || Sc > 1) ? 6.0 : 0.0);
+      if (cost < best - 1e-9) {
+        best = cost;
+        L.Sa = Sa;
+        L.Sc = Sc;
+        L.spca = pa;
+        L.spcc = pc;
+      }
+    }
+  }
 }
 // Ia = 0: the critic's tiles only (qs_ppo_critic_tiles), no actor buffers
 SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
@@ -1301,24 +1329,27 @@ SLayout s_layout(int mb, int D, int Ia, int Ic, int A) {
   L.KcP = 16 * L.rbc * L.nC;
   // row strides off a power of two: rows 16 KB apart all mapped to one memory
   // channel (the critic's weight gradients ran 10x slower at 4 096 rows)
+#ifdef QS_DEV_BUILD
   static const int pad = [] {   // dev probe: QS_SMALL_PAD overrides the pad (floats, a multiple of 4)
     const char* e = getenv("QS_SMALL_PAD");
     const int v = e ? atoi(e) : kSPad;
     return v >= 0 && v % 4 == 0 ? v : kSPad;
   }();
-  L.KaS = L.KaP ? L.KaP + pad : 0;
-  L.KcS = L.KcP + pad;
-  L.Sa = Ia > 0 ? s_chunks(L.KaP) : 0;
-  L.Sc = s_chunks(L.KcP);
-  L.bta = s_bt(L.KaP);
-  L.btc = s_bt(L.KcP);
+#else
+  constexpr int pad = kSPad;
+#endif
+  // (launch 2 reads whole 64-row steps: the columns up to the next multiple of
+  // 64 stay zero — nothing writes them, the caller zeroes the workspace)
+  L.KaS = L.KaP ? (L.KaP + kGBK - 1) / kGBK * kGBK + pad : 0;
+  L.KcS = (L.KcP + kGBK - 1) / kGBK * kGBK + pad;
+  s_chunks(Ia, Ic, L.KaP, L.KcP, L);
   const long long pw = 4LL * kSH;   // bytes of a [256] partial column run
   const long long sz[20] = {
       4LL * Ia * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS, 4LL * kSH * L.KaS,   // xaT h1aT dz2aT dz1aT
       4LL * Ic * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS, 4LL * kSH * L.KcS,   // xcT h1cT dz2cT dz1cT
       4LL * L.nA * (kSH + A * kSH + A), 4LL * L.nA * kSH,                           // partAa partBa
       4LL * L.nC * (2 * kSH + 1), 4LL * L.nC * kSH,                                 // partAc partBc
-      8LL * kSMaxA, 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * (256 + kSBlkCnt),      // dlogstd (+ entropy) lossa lossc cnt
+      4LL * (kSScOff + 4), 8LL * L.nA * (2 + A), 8LL * L.nC, 4LL * (256 + kSBlkCnt),   // dlogstd (+ entropy, bias corr.) lossa lossc cnt
       pw * L.Sa * 32 * ((Ia + 31) / 32), pw * L.Sa * kSH,                           // K-chunk partials: actor W1 W2
       pw * L.Sc * 32 * ((Ic + 31) / 32), pw * L.Sc * kSH};                          //                  critic W1 W2
   long long o = 0;
@@ -1469,8 +1500,8 @@ static void s_bind(SArgs& P, const qs_mlp256* actor, const qs_mlp256* critic, co
   for (int i = 0; i < 4; ++i) P.w.wpart[i] = (float*)(wb + L.off[16 + i]);
   P.G.S[0] = L.Sa;
   P.G.S[1] = L.Sc;
-  P.G.bt[0] = L.bta;
-  P.G.bt[1] = L.btc;
+  P.G.spc[0] = L.spca;
+  P.G.spc[1] = L.spcc;
   P.G.sink = SINK_ADAM;
   P.G.g[0] = P.G.g[1] = nullptr;
   P.G.gdiv = 1.0f;
@@ -1514,21 +1545,16 @@ static void s_launch_fb(const SArgs& P, int grid, hipStream_t st) {
 }
 
 // Launches 2 (and 3 when a net's weight gradients are split in K-chunks) into P.G.sink
-static void s_launch_grad(SArgs P, hipStream_t st) {
-#ifdef QS_DEV_BUILD
-  static const int skip = [] {
-    const char* e = getenv("QS_WG_SKIP");
-    return e ? atoi(e) : 0;
-  }();
-  P.G.dev_skip = skip;
-#else
-  P.G.dev_skip = 0;
-#endif
-  const bool one = P.G.S[0] == 1 && P.G.S[1] == 1;
+static void s_launch_grad(const SArgs& P, hipStream_t st) {
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)ppo_small_wgrad_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kGLdsBytes),
+                            true);
+  (void)attr;
+  const bool one = P.G.S[0] <= 1 && P.G.S[1] == 1;
   const int nvec = (2 * kSH + P.a.A * kSH + 2 * P.a.A) + (3 * kSH + 1);
   const int vwg = (16 * nvec + 64 * kSGW - 1) / (64 * kSGW);   // 16 lanes per vector element
-  const int grid = s_nblk(P.a.I, P.G.bt[0]) * P.G.S[0] + s_nblk(P.c.I, P.G.bt[1]) * P.G.S[1] + vwg;
-  hipLaunchKernelGGL(ppo_small_wgrad_kernel, dim3(grid), dim3(64 * kSGW), kSReserveG, st, P, (int)one);
+  const int grid = s_gtiles(P.a.I) * P.G.S[0] + s_gtiles(P.c.I) * P.G.S[1] + vwg;
+  hipLaunchKernelGGL(ppo_small_wgrad_kernel, dim3(grid), dim3(64 * kSGW), kGLdsBytes, st, P, (int)one);
   if (one) return;
   long long nel = 0;
   for (int k = 0; k < 2; ++k)

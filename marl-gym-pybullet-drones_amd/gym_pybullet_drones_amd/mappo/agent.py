@@ -22,7 +22,6 @@ MI355X-specific structure:
 import ctypes
 import math
 import os
-import time
 from collections import defaultdict
 
 import torch
@@ -31,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib as L
+from .collectives import capture_collectives, collective_group  # noqa: F401  (re-exported)
 
 
 def get_activation(name):
@@ -933,18 +933,6 @@ def _dist_world():
     return tdist.get_world_size() if (tdist.is_available() and tdist.is_initialized()) else 1
 
 
-def drain_collectives():
-    """Before a graph capture with a process group up: let the RCCL watchdog
-    retire every eager collective issued so far (warm-up all-reduces, barriers).
-    It polls each pending work's HIP event from its own thread, and an event
-    query whose stream is capturing is refused (hipErrorCapturedEvent /
-    hipErrorStreamCaptureUnsupported), which kills the process.  The watchdog
-    loop runs every 100 ms; the device is drained first so every work is done."""
-    if tdist.is_available() and tdist.is_initialized():
-        torch.cuda.synchronize()
-        time.sleep(0.25)
-
-
 class MAPPOAgent:
     """AG:501-772 with the update on device (flat buffers, gated HIP Adam, optional graph)."""
 
@@ -964,6 +952,7 @@ class MAPPOAgent:
         # graph too (RCCL collectives are graph-capturable); False: eager iterations
         self.graph_collectives = kwargs.get('graph_collectives', True)
         self._force_allreduce = False   # tests: take the all-reduce path with one rank
+        self._kl_div = 1   # what the approx_kl slot holds ÷ the mean (the tile path's exchange: the ranks' sum)
         self.fused_heads = fused_heads   # qs_ppo_heads (False: the loss heads as plain torch ops)
         self.direct = kwargs.get('direct', True)   # the fused MLP kernels without autograd (_iteration_direct)
         # the direct iteration's actor on qs_mlp3f_actor (forward + loss head + backward in one launch)
@@ -1373,10 +1362,11 @@ class MAPPOAgent:
             L.check(lib.qs_ppo_small_step(*head, gate, thr, ctypes.byref(na), ctypes.byref(nc), L.ptr(self._kl),
                                           L.ptr(acc), L.ptr(self._sm_work), st), "qs_ppo_small_step")
             return
+        self._kl_div = world   # (the all-reduced approx_kl slot is the ranks' sum: _actor_gate_open)
         L.check(lib.qs_ppo_small_grads(*head, ctypes.byref(na), ctypes.byref(nc), L.ptr(self.actor_opt.grad),
                                        L.ptr(self.critic_opt.grad), L.ptr(self._kl), L.ptr(acc), L.ptr(self._sm_work),
                                        st), "qs_ppo_small_grads")
-        tdist.all_reduce(self._reduce_buf)   # one collective: the sums of [critic | actor | approx_kl]
+        tdist.all_reduce(self._reduce_buf, group=collective_group())   # one collective: [critic | actor | approx_kl]
         L.check(lib.qs_ppo_small_adam(mb, D, ctypes.byref(na), ctypes.byref(nc), L.ptr(self.actor_opt.grad),
                                       L.ptr(self.critic_opt.grad), float(world), gate, thr, L.ptr(self._kl),
                                       L.ptr(self._sm_work), st), "qs_ppo_small_adam")
@@ -1412,20 +1402,22 @@ class MAPPOAgent:
         rank evaluates the same KL gate on the same value.  Runs on any device
         (tests/test_distributed_cpu.py drives it on CPU tensors with gloo)."""
         if world > 1 or self._force_allreduce:
-            tdist.all_reduce(self._reduce_buf)
+            tdist.all_reduce(self._reduce_buf, group=collective_group())
             self._reduce_buf.div_(world)
 
     def _exchange_bucket(self, bucket, world):
         """One bucket of the direct iteration's exchange (critic gradients, or actor
         gradients + approx_kl): all-reduce (sum) and divide by the world size on
         the current stream — the same values as the one-piece `_exchange`."""
-        tdist.all_reduce(bucket)
+        tdist.all_reduce(bucket, group=collective_group())
         bucket.div_(world)
 
     def _actor_gate_open(self):
         """AG:731-734: the actor steps only if approx_kl <= 1.5·target_kl (a device
         tensor; the HIP Adam reads it on the device, this is the host view)."""
-        return self.target_kl <= 0 or bool(self._kl.item() <= 1.5 * self.target_kl)
+        # (after the tile path's exchange the slot holds the ranks' SUM: qs_ppo_small_adam
+        # divides it on the device, this host view by _kl_div)
+        return self.target_kl <= 0 or bool(self._kl.item() / self._kl_div <= 1.5 * self.target_kl)
 
     def _optimizer_steps(self):
         """Actor Adam gated by the KL value on the device, critic Adam always
@@ -1439,6 +1431,7 @@ class MAPPOAgent:
         self._optimizer_steps()
 
     def _step_minibatch(self, rollouts, idx, acc):
+        self._kl_div = 1
         if self.fused_heads and self._fused_heads_ok(rollouts):
             if self._small_ok(rollouts, idx.shape[0]):
                 self._iteration_small(rollouts, idx, acc)
@@ -1473,10 +1466,10 @@ class MAPPOAgent:
             for _ in range(2):
                 self._step_minibatch(rollouts, self._g_idx, self._g_acc)
         torch.cuda.current_stream().wait_stream(s)
-        drain_collectives()
         g = torch.cuda.CUDAGraph()
-        # thread_local: the RCCL watchdog thread may run during the capture
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        # thread_local: the RCCL watchdog thread may run during the capture; the
+        # captured all-reduces on their own group (capture_collectives)
+        with capture_collectives(), torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(k):
                 self._step_minibatch(rollouts, self._g_perm[i * mb:(i + 1) * mb], self._g_acc)
         for t, v in zip((self.actor_opt.flat, self.actor_opt.exp_avg, self.actor_opt.exp_avg_sq, self.actor_opt.step,

@@ -40,7 +40,7 @@ import torch.distributed as tdist
 from .. import _lib as L
 from ..utils.enums import ActionType, Physics
 from ..vec_env import SwarmVecEnv, VecRecordEpisodeStatistics
-from .agent import drain_collectives, MAPPOAgent
+from .agent import capture_collectives, MAPPOAgent
 from .buffer import MAPPOBuffer, normalize_advantages
 from .config import MAPPO_CONFIG
 from .normalization import BaseNormalizer, MeanStdNormalizer, RewardStdNormalizer
@@ -395,8 +395,8 @@ class MAPPO:
         rollouts.next_obs_slots[0].copy_(self.obs)
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        drain_collectives()   # (the watchdog must not poll an eager collective's event during the capture)
-        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        # (the normaliser's captured all-reduces on their own group: capture_collectives)
+        with capture_collectives(), torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for t in range(self.rollout_steps):
                 self._rollout_step(rollouts, t)
         torch.cuda.current_stream().wait_stream(s)

@@ -233,6 +233,14 @@ def main():
                 print(f"{shape}  {str(v):55s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "ranks" in which:
         ranks()
+    if "tiles" in which:   # the tile path alone at the per-rank shapes (QS_SHAPES): exchange path, fused step
+        world1()
+        agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
+        tag = os.path.basename(os.environ.get("QS_DEV_LIB", "default"))
+        for shape in os.environ.get("QS_SHAPES", " ".join(RANK_SHAPES)).split():
+            for v in (dict(small=True, force=True), dict(small=True, force=False)):
+                us, path = per_minibatch_us(shape, **v)
+                print(f"{tag:>12s} {shape:5s} {str(v):36s} {us:8.1f} us/minibatch  [{path}]", flush=True)
     for w in which:   # "shape:NAME[:direct]": one shape's tile (or direct) path alone, e.g. under a kernel trace
         if w.startswith("shape:"):
             _, name, *rest = w.split(":")

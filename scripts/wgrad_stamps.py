@@ -1,7 +1,7 @@
 """Dev: per-workgroup phase timestamps of the tile path's weight-gradient launch
 (ppo_small_wgrad_kernel) from the QS_TILE_STAMPS dev build (s_memrealtime, 100 MHz,
-thread 0): 0 entry (after the Adam scalars), 1 wave 0's contraction done,
-2 the waves' sums reduced, 3 done (sink written).
+thread 0): 0 entry, 1 wave 0's contraction done (the LDS ring drained),
+2 the KL gate read, 3 done (sink written).
   bash scripts/build_dev_step.sh tstamps -DQS_TILE_STAMPS
   QS_DEV_LIB=marl-gym-pybullet-drones_amd/build/dev/lib_tstamps.so python scripts/wgrad_stamps.py C3/8 ..."""
 import ctypes
@@ -18,8 +18,8 @@ from gym_pybullet_drones_amd.mappo import agent as agent_mod  # noqa: E402
 import learner_mb  # noqa: E402
 
 
-def nblk(I, bt):
-    return (16 // bt) * ((I + 16 * bt - 1) // (16 * bt)) + (16 // bt) ** 2
+def gtiles(I):   # 64×64 tiles per net: W2's 4×4, then W1's 4×⌈I/64⌉ (ppo_small.hip s_gtiles)
+    return 16 + 4 * ((I + 63) // 64)
 
 
 def main():
@@ -29,10 +29,10 @@ def main():
         learner_mb.per_minibatch_us(shape, reps=1, small=True)
         torch.cuda.synchronize()
         D, O, A, mb, T, E = learner_mb.SHAPES[shape]
-        Ka, Kc = mb * D, mb
-        bt = lambda K: 2   # (32x32 blocks, kSBT1Q)
-        S = lambda K: max(1, ((K + 15) // 16 + 63) // 64)   # kSGQ = 64 quads per chunk
-        na, nc = nblk(O, bt(Ka)) * S(Ka), nblk(D * O, bt(Kc)) * S(Kc)
+        off = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
+        assert L.load().qs_ppo_small_layout(mb, D, O, D * O, A, off) == 0
+        Sa, Sc = off[27], off[28]
+        na, nc = gtiles(O) * Sa, gtiles(D * O) * Sc
         nvec = (2 * 256 + A * 256 + 2 * A) + (3 * 256 + 1)
         nv = (16 * nvec + 255) // 256   # kSGW = 4 waves
         n = na + nc + nv
@@ -43,13 +43,13 @@ def main():
         s = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.int64)
         t0 = s[:, 0].min()
         rel = (s - t0) * 0.01
-        print(f"== {shape}: actor blocks {na} (bt {bt(Ka)}, S {S(Ka)}), critic blocks {nc} (bt {bt(Kc)}), vector WGs {nv}")
+        print(f"== {shape}: actor tile-chunks {na} (S {Sa}), critic tile-chunks {nc} (S {Sc}), vector WGs {nv}")
         for name, sl in (("actor", slice(0, na)), ("critic", slice(na, na + nc)), ("vector", slice(na + nc, n))):
             r = rel[sl]
             line = f"  {name:6s} entry {np.median(r[:, 0]):6.2f} (max {r[:, 0].max():6.2f})"
             if name != "vector":
                 line += (f"  contraction {np.median(r[:, 1] - r[:, 0]):6.2f} (max {(r[:, 1] - r[:, 0]).max():6.2f})"
-                         f"  reduce {np.median(r[:, 2] - r[:, 1]):6.2f}  sink {np.median(r[:, 3] - r[:, 2]):6.2f}")
+                         f"  gate {np.median(r[:, 2] - r[:, 1]):6.2f}  sink {np.median(r[:, 3] - r[:, 2]):6.2f}")
             line += f"  end {np.median(r[:, 3]):6.2f} (max {r[:, 3].max():6.2f}) us"
             print(line)
         ent = np.sort(rel[:, 0])

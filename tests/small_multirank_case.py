@@ -8,8 +8,15 @@ O, A = 27, 1
 EPOCHS, MB_PER_EPOCH = 2, 2
 
 
-def build(E, T, D, rank=0, world=1):
-    """Agent + this rank's MAPPOBuffer (envs [rank·E/world, (rank+1)·E/world))."""
+# the KL gate closed far from its threshold: logp_old shifted by +KL_SHIFT makes every
+# minibatch's approx_kl ≈ KL_SHIFT (the actor never steps, so it stays there) against
+# a threshold of 1.5·GATE_TARGET_KL
+KL_SHIFT, GATE_TARGET_KL = 0.05, 1e-4
+
+
+def build(E, T, D, rank=0, world=1, gate_closed=False):
+    """Agent + this rank's MAPPOBuffer (envs [rank·E/world, (rank+1)·E/world)).
+    gate_closed: the actor's KL gate shut on every minibatch (AG:731-734)."""
     from gym_pybullet_drones_amd.mappo import agent as agent_mod
     from gym_pybullet_drones_amd.mappo.agent import MAPPOAgent
     from gym_pybullet_drones_amd.mappo.buffer import MAPPOBuffer
@@ -23,7 +30,8 @@ def build(E, T, D, rank=0, world=1):
     # ranks' and the single rank's row-sum orders could branch differently; the gated
     # branch has its own tests in tests/test_gpu_learner.py)
     agent = MAPPOAgent(obs_space, act_space, hidden_dim=256, opt_epochs=EPOCHS, mini_batch_size=1,
-                       entropy_coef=0.005, target_kl=1e9, use_graphs=False, device="cuda", small=True)
+                       entropy_coef=0.005, target_kl=GATE_TARGET_KL if gate_closed else 1e9, use_graphs=False,
+                       device="cuda", small=True)
     g = torch.Generator().manual_seed(2)
     obs = torch.randn((T, E, D, O), generator=g)
     act = torch.randn((T, E, D, A), generator=g)
@@ -37,7 +45,8 @@ def build(E, T, D, rank=0, world=1):
     buf.act.copy_(act[:, sl])
     with torch.no_grad():
         d = agent.ac.actor.dist(buf.obs.reshape(-1, O))
-        buf.logp.copy_(d.log_prob(buf.act.reshape(-1, A)).reshape(T, El, D, 1) + noise[:, sl].cuda())
+        buf.logp.copy_(d.log_prob(buf.act.reshape(-1, A)).reshape(T, El, D, 1) + noise[:, sl].cuda()
+                       + (KL_SHIFT if gate_closed else 0.0))
     buf.ret_env.copy_(ret[:, sl])
     buf.adv_env.copy_(adv[:, sl])
     buf.t, buf.full = 0, True

@@ -8,7 +8,7 @@ all-reduce → qs_ppo_small_adam) over its local minibatches; the parameters,
 Adam moments and step counts it ends with are saved for the parent to compare
 with one rank stepping the union of the ranks' minibatches.
 
-usage: small_multirank_worker.py RANK WORLD PORT OUT E T D MB
+usage: small_multirank_worker.py RANK WORLD PORT OUT E T D MB [GATE_CLOSED]
 """
 import os
 import sys
@@ -24,11 +24,12 @@ import torch.distributed as dist  # noqa: E402
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     E, T, D, MB = (int(x) for x in sys.argv[5:9])
+    gate_closed = len(sys.argv) > 9 and sys.argv[9] == "1"
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         import small_multirank_case as case
-        agent, buf = case.build(E, T, D, rank=rank, world=world)
+        agent, buf = case.build(E, T, D, rank=rank, world=world, gate_closed=gate_closed)
         assert dist.get_world_size() == world
         acc = torch.zeros(4, dtype=torch.float64, device="cuda")
         for idx in case.local_minibatches(E // world, T, MB // world):

@@ -87,7 +87,7 @@ def test_tile_layouts_at_the_per_rank_shapes():
     at SURVEY §8(e)'s per-rank shapes — 16-row tiles while both nets fit one
     round of the 256 CUs, then 32- and 48-row actor tiles with the critic's kept
     at 16 rows while they still fit, and the weight gradients'
-    K-chunks (1 024 rows, a remainder of at most 1/8 chunk joining the others)."""
+    K-chunks (64×64 tiles in 64-row steps, s_chunks' launch estimate)."""
     from gym_pybullet_drones_amd import _lib as L
     lib = L.load()
     off = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
@@ -99,11 +99,11 @@ def test_tile_layouts_at_the_per_rank_shapes():
     # the reference's learner shape: 256 actor rows, 32 critic rows, 16-row tiles
     assert lay(32, 8, 27, 216, 1) == dict(nA=16, nC=2, KaP=256, KcP=32, Sa=1, Sc=1)
     # C3 at G = 8: 288 16-row tiles would take two rounds: 32-row actor tiles, 16-row critic tiles
-    assert lay(512, 8, 27, 216, 1) == dict(nA=128, nC=32, KaP=4096, KcP=512, Sa=4, Sc=1)
-    # C3 at G = 4: 48-row actor tiles (171, padded to 8 208 rows: 9 chunks' worth, the last 1 quad → 8)
-    assert lay(1024, 8, 27, 216, 1) == dict(nA=171, nC=64, KaP=8208, KcP=1024, Sa=8, Sc=1)
+    assert lay(512, 8, 27, 216, 1) == dict(nA=128, nC=32, KaP=4096, KcP=512, Sa=8, Sc=1)
+    # C3 at G = 4: 48-row actor tiles (171, padded to 8 208 rows)
+    assert lay(1024, 8, 27, 216, 1) == dict(nA=171, nC=64, KaP=8208, KcP=1024, Sa=9, Sc=2)
     # C5 at G = 8: a narrow actor at 48 rows beside the 432-wide critic at 16
-    assert lay(512, 16, 27, 432, 1) == dict(nA=171, nC=32, KaP=8208, KcP=512, Sa=8, Sc=1)
+    assert lay(512, 16, 27, 432, 1) == dict(nA=171, nC=32, KaP=8208, KcP=512, Sa=10, Sc=1)
     # C4 at G = 4: the four-output actor at 32 rows beside the 595-wide critic at 16 (one round)
     d = lay(1024, 5, 119, 595, 4)
     assert (d["nA"], d["nC"], d["KaP"], d["KcP"]) == (160, 64, 5120, 1024)
