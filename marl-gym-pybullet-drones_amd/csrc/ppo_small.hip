@@ -50,6 +50,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -477,6 +478,9 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) z[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
   s_layer1<V1, (MAXI > kSNarrowI), RB>(ring1, w1row, V1 ? Ip : I, xs + j * XS, 16 * XS, g, nq1, z);
+#ifdef QS_TILE_STAMPS2
+  S_STAMP(6);   // (dev: layer 1's MFMAs issued)
+#endif
   if constexpr (!kEarly2) s_prefill<16, true>(ring2, w2row, kSH, g);
   float h1[RB][4];
 #pragma unroll
@@ -485,6 +489,9 @@ __device__ __forceinline__ void s_tile(const SArgs& P, const SNet& N, int tile, 
     for (int r = 0; r < 4; ++r) h1[rb][r] = s_tanh(z[rb][r] + sb1[h0 + r]);
     *reinterpret_cast<float4*>(h1s + (16 * rb + j) * kSHS + h0) = float4{h1[rb][0], h1[rb][1], h1[rb][2], h1[rb][3]};
   }
+#ifdef QS_TILE_STAMPS2
+  S_STAMP(7);   // (dev: H1 formed and stored)
+#endif
   __syncthreads();
   S_STAMP(2);
   // ---- layer 2: Z2ᵀ = W2·H1ᵀ (its ring filled at the start); the backward's ring filled behind it
@@ -760,15 +767,21 @@ __global__ void __launch_bounds__(kSBlock) ppo_small_fb_kernel(SArgs P) {
 // ---------------------------------------------------------------- launches 2 and 3
 // p / m / v of element i loaded by the caller ahead of the gradient (their
 // latency hides behind the gradient's loads)
+// torch.optim.Adam's element update (amsgrad=False, weight_decay=0: learner.hip's
+// adam_elem) as values: p1, m1, v1 from gradient g and p, m, v
+__device__ __forceinline__ void s_adam_v(const SNet& N, float g, float bc1, float bc2s, float p, float m, float v,
+                                         float& p1, float& m1, float& v1) {
+  m1 = m + (1.0f - N.beta1) * (g - m);
+  v1 = v * N.beta2 + (1.0f - N.beta2) * g * g;
+  const float denom = sqrtf(v1) / bc2s + N.eps;
+  p1 = p - (N.lr / bc1) * (m1 / denom);
+}
 __device__ __forceinline__ void s_adam(const SNet& N, long long i, float g, float bc1, float bc2s, float* w2t,
                                        int n, int k, float* w1p, float p, float m, float v) {
-  // torch.optim.Adam (amsgrad=False, weight_decay=0): learner.hip's adam_elem
-  const float m1 = m + (1.0f - N.beta1) * (g - m);
-  const float v1 = v * N.beta2 + (1.0f - N.beta2) * g * g;
+  float p1, m1, v1;
+  s_adam_v(N, g, bc1, bc2s, p, m, v, p1, m1, v1);
   N.m[i] = m1;
   N.v[i] = v1;
-  const float denom = sqrtf(v1) / bc2s + N.eps;
-  const float p1 = p - (N.lr / bc1) * (m1 / denom);
   N.p[i] = p1;
 #ifdef QS_X_NO_W2T
   w2t = nullptr;   // dev probe: the transposed copy's scattered stores skipped (results wrong)
@@ -964,26 +977,23 @@ __device__ __forceinline__ int s_xcd_swz(int T, int n) {
 // no launch 3 follows, Adam) commits the step counts.
 __device__ __forceinline__ void s_vec_wg(const SArgs& P, int vb, bool adam, bool fin, const float (*sc)[2]) {
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  // the actor's loss totals (every wave: the gate, logstd's gradient)
-  double tot[2 + kSMaxA];
-  const bool open_a = s_gate_rows(P, l, tot);
   const int e = (vb * (int)blockDim.x + tid) >> 4, k = tid & 15;
-  bool actor;
-  long long i;
-  const float* col;
-  int cstride, nt, u;
-  if (s_vec_loc(P, e, actor, i, col, cstride, nt, u)) {   // (uniform over the element's 16 lanes)
+  bool actor = false;
+  long long i = 0;
+  const float* col = nullptr;
+  int cstride = 0, nt = 0, u = 0;
+  const bool have = s_vec_loc(P, e, actor, i, col, cstride, nt, u);   // (uniform over the element's 16 lanes)
+  // the element's partial rows and Adam operands first: their latency runs under
+  // the loss totals' loads and butterflies (the gate), not after them
+  float acc = 0.f, p0 = 0.f, m0 = 0.f, v0 = 0.f;
+  if (have) {
     const SNet& N = actor ? P.a : P.c;
-    const bool doit = !adam || !actor || open_a;
-    float p0 = 0.f, m0 = 0.f, v0 = 0.f;
     if (adam && k == 0) {
       p0 = N.p[i];
       m0 = N.m[i];
       v0 = N.v[i];
     }
-    float gsum;
     if (col) {
-      float acc = 0.f;
       int tt = k;
       for (; tt + 16 * 7 < nt; tt += 16 * 8) {
         float v[8];
@@ -993,10 +1003,16 @@ __device__ __forceinline__ void s_vec_wg(const SArgs& P, int vb, bool adam, bool
         for (int q = 0; q < 8; ++q) acc += v[q];
       }
       for (; tt < nt; tt += 16) acc += col[(size_t)tt * cstride];
-      gsum = s_row_sum(acc);
-    } else {   // logstd: d(policy)/d logstd from the loss rows − ent_coef (AG:602-640)
-      gsum = (float)tot[2 + u] - P.ent_coef;
     }
+  }
+  // the actor's loss totals (every wave: the gate, logstd's gradient)
+  double tot[2 + kSMaxA];
+  const bool open_a = s_gate_rows(P, l, tot);
+  if (have) {
+    const SNet& N = actor ? P.a : P.c;
+    const bool doit = !adam || !actor || open_a;
+    // logstd: d(policy)/d logstd from the loss rows − ent_coef (AG:602-640)
+    const float gsum = col ? s_row_sum(acc) : (float)tot[2 + u] - P.ent_coef;
     if (doit && k == 0) {
       if (!adam) {
         P.G.g[actor ? 0 : 1][i] = gsum;
@@ -1077,19 +1093,23 @@ __global__ void __launch_bounds__(256) ppo_small_wgrad_kernel(SArgs P, int fin) 
   const int wn = w >> 1, wm = w & 1;
   const bool live = kGT / 2 * wm < M - m0;   // the wave's 32 columns hold some of the matrix's
   const bool direct = S == 1;
-  // the sink's elements: slot f = 4q + r, tile q = 2rb + cb, register r
-  long long ei[16];
-  float pp[16], pm[16], pv[16];
+  // The sink takes the wave's 32×32 quadrant row-contiguous (through LDS after the
+  // contraction): lane l owns rows 32wn + (l >> 3) + 8u (u < 4) at columns
+  // 32wm + 4(l & 7) .. + 3, so every store (and Adam's loads) is one float4 —
+  // when the matrix's rows are float4-aligned (M a multiple of 4 and a 16-B
+  // aligned offset; otherwise element by element).
+  const long long wo = l1 ? N.w1 : N.w2;
+  const bool vec4 = (M & 3) == 0 && (wo & 3) == 0;
+  const int mq = m0 + 32 * wm + 4 * (l & 7);   // the lane's first column
+  float4 pp[4], pm[4], pv[4];
 #pragma unroll
-  for (int f = 0; f < 16; ++f) {
-    const int q = f >> 2, r = f & 3;
-    const int en = n0 + 32 * wn + 16 * (q >> 1) + 4 * g + r, em = m0 + 32 * wm + 16 * (q & 1) + j;
-    ei[f] = (l1 ? N.w1 : N.w2) + (long long)en * M + em;
-    pp[f] = pm[f] = pv[f] = 0.f;
-    if (direct && adam && em < M) {   // Adam's operands, in flight during the contraction
-      pp[f] = N.p[ei[f]];
-      pm[f] = N.m[ei[f]];
-      pv[f] = N.v[ei[f]];
+  for (int u = 0; u < 4; ++u) {
+    pp[u] = pm[u] = pv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (direct && adam && vec4 && mq < M) {   // Adam's operands, in flight during the contraction
+      const long long e0 = wo + (long long)(n0 + 32 * wn + (l >> 3) + 8 * u) * M + mq;
+      pp[u] = *reinterpret_cast<const float4*>(N.p + e0);
+      pm[u] = *reinterpret_cast<const float4*>(N.m + e0);
+      pv[u] = *reinterpret_cast<const float4*>(N.v + e0);
     }
   }
   f32x4 c[4];
@@ -1139,22 +1159,65 @@ __global__ void __launch_bounds__(256) ppo_small_wgrad_kernel(SArgs P, int fin) 
   }
   __syncthreads();
   W_STAMP(2);
-  if (!live) return;
   const bool act = !(adam && actor) || *sopen;
   float* part = P.w.wpart[(actor ? 0 : 2) + (l1 ? 0 : 1)];
   const int Mp = l1 ? s_mp(N.I) : kSH;
+  // the quadrant into LDS ([32][36]: 16-B aligned rows), then read back row-contiguous
+  float* qd = s_lds + w * (32 * 36);
 #pragma unroll
   for (int f = 0; f < 16; ++f) {
     const int q = f >> 2, r = f & 3;
-    const int en = n0 + 32 * wn + 16 * (q >> 1) + 4 * g + r, em = m0 + 32 * wm + 16 * (q & 1) + j;
-    if (em >= M) continue;
-    const float v = c[q][r];
+    qd[(16 * (q >> 1) + 4 * g + r) * 36 + 16 * (q & 1) + j] = c[q][r];
+  }
+  // (the wave reads only its own quadrant: its LDS writes and reads are in order)
+  if (!live) return;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int nl = (l >> 3) + 8 * u, en = n0 + 32 * wn + nl;
+    const float4 v = *reinterpret_cast<const float4*>(qd + nl * 36 + 4 * (l & 7));
+    const float vv[4] = {v.x, v.y, v.z, v.w};
     if (!direct) {
-      part[((size_t)s * kSH + en) * Mp + em] = v;
-    } else if (act) {
-      if (!adam) P.G.g[si][ei[f]] = v;
-      else s_adam(N, ei[f], v, sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en, em, l1 ? N.w1p : nullptr, pp[f],
-                  pm[f], pv[f]);
+      if (vec4) {
+        if (mq < M) *reinterpret_cast<float4*>(part + ((size_t)s * kSH + en) * Mp + mq) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (mq + e < M) part[((size_t)s * kSH + en) * Mp + mq + e] = vv[e];
+      }
+      continue;
+    }
+    if (!act) continue;
+    const long long e0 = wo + (long long)en * M + mq;
+    if (!adam) {
+      if (vec4) {
+        if (mq < M) *reinterpret_cast<float4*>(P.G.g[si] + e0) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (mq + e < M) P.G.g[si][e0 + e] = vv[e];
+      }
+    } else if (vec4) {
+      if (mq >= M) continue;
+      const float p4[4] = {pp[u].x, pp[u].y, pp[u].z, pp[u].w}, m4[4] = {pm[u].x, pm[u].y, pm[u].z, pm[u].w},
+                  v4[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
+      float np[4], nm[4], nv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s_adam_v(N, vv[e], sc[si][0], sc[si][1], p4[e], m4[e], v4[e], np[e], nm[e], nv[e]);
+      *reinterpret_cast<float4*>(N.p + e0) = make_float4(np[0], np[1], np[2], np[3]);
+      *reinterpret_cast<float4*>(N.m + e0) = make_float4(nm[0], nm[1], nm[2], nm[3]);
+      *reinterpret_cast<float4*>(N.v + e0) = make_float4(nv[0], nv[1], nv[2], nv[3]);
+      if (!l1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) N.w2t[(size_t)(mq + e) * kSH + en] = np[e];
+      } else if (N.w1p) {
+        *reinterpret_cast<float4*>(N.w1p + (size_t)en * s_ip(N.I) + mq) = make_float4(np[0], np[1], np[2], np[3]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (mq + e < M)
+          s_adam(N, e0 + e, vv[e], sc[si][0], sc[si][1], l1 ? nullptr : N.w2t, en, mq + e, l1 ? N.w1p : nullptr,
+                 N.p[e0 + e], N.m[e0 + e], N.v[e0 + e]);
     }
   }
   W_STAMP(3);
@@ -1275,6 +1338,19 @@ struct SLayout {
 // with its boundary).  The cheapest (Sa, Sc) by that estimate.
 inline void s_chunks(int Ia, int Ic, long long KaP, long long KcP, SLayout& L) {
   const int na = Ia > 0 ? (int)((KaP + kGBK - 1) / kGBK) : 0, nc = (int)((KcP + kGBK - 1) / kGBK);
+#ifdef QS_DEV_BUILD
+  // dev probe: QS_WG_SPC="a,c" fixes the steps per chunk of the actor / critic
+  if (const char* e = getenv("QS_WG_SPC")) {
+    int pa = 0, pc = 0;
+    if (sscanf(e, "%d,%d", &pa, &pc) == 2 && pa > 0 && pc > 0) {
+      L.spca = pa;
+      L.spcc = pc;
+      L.Sa = na > 0 ? (na + pa - 1) / pa : 0;
+      L.Sc = (nc + pc - 1) / pc;
+      if (L.Sa <= kSMaxS && L.Sc <= kSMaxS) return;
+    }
+  }
+#endif
   const int ta = Ia > 0 ? s_gtiles(Ia) : 0, tc = s_gtiles(Ic);
   double best = 1e30;
   L.Sa = Ia > 0 ? 1 : 0;

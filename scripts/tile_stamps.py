@@ -38,6 +38,12 @@ def dump(label, nwg, nA=None):
             ph = "  ".join(f"{np.median(r[:, k] - r[:, k - 1]):6.2f}" for k in range(1, 6))
             print(f"  {nm:>6s} tiles: phases 1-5 median [{ph}] us; entry .. dH1 max {np.max(r[:, 5] - r[:, 0]):7.2f} us; "
                   f"last {r[:, 5].max():.2f} us")
+    if os.environ.get("QS_STAMPS2"):   # the QS_TILE_STAMPS2 build: 6 = layer 1 issued, 7 = H1 stored
+        for nm, sl in (("actor", slice(0, nA)), ("critic", slice(nA, nwg))) if nA else (("all", slice(0, nwg)),):
+            r = rel[sl]
+            print(f"  {nm:>6s} layer 1: staged -> MFMAs issued {np.median(r[:, 6] - r[:, 1]):6.2f}  -> H1 stored "
+                  f"{np.median(r[:, 7] - r[:, 6]):6.2f}  -> barrier {np.median(r[:, 2] - r[:, 7]):6.2f} us")
+        return
     last = rel[:, 7][s[:, 7] > 0]
     print(f"  arrivals end {rel[:, 6].max():.2f} us; last tile done at {last.max() if len(last) else float('nan'):.2f} us")
 
