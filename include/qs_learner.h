@@ -397,9 +397,10 @@ const char* qs_ppo_small_last_error(void);
  * the row strides of the actor's / critic's transposed buffers; off[23..26] =
  * byte offsets of the weight gradients' K-chunk partials [S][256][M padded to
  * 32] (actor W1, W2, critic W1, W2); off[27..28] = the actor's / critic's
- * K-chunks S.  Ia = 0: the critic-only layout of qs_ppo_critic_tiles. */
+ * K-chunks S.  Ia = 0: the critic-only layout of qs_ppo_critic_tiles.  Writes
+ * min(n_off, QS_PPO_SMALL_LAYOUT_N) entries (never past the caller's array). */
 #define QS_PPO_SMALL_LAYOUT_N 29
-int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off);
+int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off, int32_t n_off);
 /* The critic half of qs_ppo_small_step's first launch at any minibatch size:
  * the critic's forward, value head (AG:642-683, acc[1] += value loss) and
  * backward in 16-row tiles over every CU, writing the transposed activations

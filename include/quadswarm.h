@@ -49,7 +49,8 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 2   /* 2: qs_episode_log reports the records it wrote */
+#define QS_ABI_VERSION 3   /* 2: qs_episode_log reports the records it wrote; 3: qs_ppo_small_layout takes
+                              the caller's entry count */
 
 /* ---- status codes ------------------------------------------------------ */
 #define QS_OK 0

@@ -1447,21 +1447,23 @@ int64_t qs_ppo_small_work_bytes(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, i
   return s_layout(mb, D, Ia, Ic, A).bytes;
 }
 
-int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off) {
-  if (mb <= 0 || D <= 0 || Ia < 0 || Ic <= 0 || A < 1 || A > kSMaxA || !off)
+int qs_ppo_small_layout(int32_t mb, int32_t D, int32_t Ia, int32_t Ic, int32_t A, int64_t* off, int32_t n_off) {
+  if (mb <= 0 || D <= 0 || Ia < 0 || Ic <= 0 || A < 1 || A > kSMaxA || !off || n_off < 1)
     return sfail(QS_E_INVALID, "qs_ppo_small_layout: bad argument");
   const SLayout L = s_layout(mb, D, Ia, Ic, A);
-  for (int i = 0; i < 16; ++i) off[i] = L.off[i];
-  off[16] = L.nA;
-  off[17] = L.nC;
-  off[18] = L.KaP;
-  off[19] = L.KcP;
-  off[20] = L.bytes;
-  off[21] = L.KaS;
-  off[22] = L.KcS;
-  for (int i = 0; i < 4; ++i) off[23 + i] = L.off[16 + i];
-  off[27] = L.Sa;
-  off[28] = L.Sc;
+  int64_t v[QS_PPO_SMALL_LAYOUT_N];
+  for (int i = 0; i < 16; ++i) v[i] = L.off[i];
+  v[16] = L.nA;
+  v[17] = L.nC;
+  v[18] = L.KaP;
+  v[19] = L.KcP;
+  v[20] = L.bytes;
+  v[21] = L.KaS;
+  v[22] = L.KcS;
+  for (int i = 0; i < 4; ++i) v[23 + i] = L.off[16 + i];
+  v[27] = L.Sa;
+  v[28] = L.Sc;
+  for (int i = 0; i < QS_PPO_SMALL_LAYOUT_N && i < n_off; ++i) off[i] = v[i];   // (never past the caller's array)
   return QS_OK;
 }
 

@@ -57,7 +57,7 @@ class QsStepOut(ctypes.Structure):
 EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq", "<i8")])
 
 # Every symbol include/quadswarm.h declares (tests check the .so exports them).
-ABI_VERSION = 2   # include/quadswarm.h QS_ABI_VERSION
+ABI_VERSION = 3   # include/quadswarm.h QS_ABI_VERSION
 EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
            "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
            # include/qs_learner.h
@@ -172,7 +172,7 @@ def load():
     L.qs_rollout_record.argtypes = [i64] + [vp] * 7
     L.qs_ppo_small_last_error.restype = ctypes.c_char_p
     L.qs_ppo_small_work_bytes.argtypes = [ctypes.c_int32] * 5
-    L.qs_ppo_small_layout.argtypes = [ctypes.c_int32] * 5 + [vp]
+    L.qs_ppo_small_layout.argtypes = [ctypes.c_int32] * 5 + [vp, ctypes.c_int32]
     L.qs_ppo_critic_tiles.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp, vp, ctypes.POINTER(QsMlp256), vp, vp, vp]
     L.qs_wgrad_t.argtypes = [i64, i64, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp]
     L.qs_ppo_small_step.argtypes = ([ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [f32, f32, f32, ctypes.c_int32, f32]

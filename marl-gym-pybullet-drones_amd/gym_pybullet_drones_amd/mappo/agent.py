@@ -512,7 +512,7 @@ class _CriticTiles:
         f0, f1, f2 = mlp.fcs
         self.mlp, self.mb, self.D, self.I = mlp, mb, D, f0.in_features
         off = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
-        L.check(lib.qs_ppo_small_layout(mb, D, 0, self.I, 1, off), "qs_ppo_small_layout")
+        L.check(lib.qs_ppo_small_layout(mb, D, 0, self.I, 1, off, len(off)), "qs_ppo_small_layout")
         self.nC, KcP, ld = int(off[17]), int(off[19]), int(off[22])
         dev = agent.device
         self.work = torch.zeros(int(off[20]), dtype=torch.uint8, device=dev)

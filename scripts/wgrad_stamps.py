@@ -30,7 +30,7 @@ def main():
         torch.cuda.synchronize()
         D, O, A, mb, T, E = learner_mb.SHAPES[shape]
         off = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
-        assert L.load().qs_ppo_small_layout(mb, D, O, D * O, A, off) == 0
+        assert L.load().qs_ppo_small_layout(mb, D, O, D * O, A, off, len(off)) == 0
         Sa, Sc = off[27], off[28]
         na, nc = gtiles(O) * Sa, gtiles(D * O) * Sc
         nvec = (2 * 256 + A * 256 + 2 * A) + (3 * 256 + 1)

@@ -21,7 +21,7 @@ def test_quadswarm_exports_every_declared_symbol():
         assert hasattr(lib, n), n
     assert set(names) <= set(_lib.EXPORTS)
     lib.qs_abi_version.restype = ctypes.c_int
-    assert lib.qs_abi_version() == 2
+    assert lib.qs_abi_version() == 3
 
 
 def test_create_rejects_bad_spec_without_gpu_work():
@@ -93,7 +93,7 @@ def test_tile_layouts_at_the_per_rank_shapes():
     off = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
 
     def lay(mb, D, Ia, Ic, A):
-        assert lib.qs_ppo_small_layout(mb, D, Ia, Ic, A, off) == 0
+        assert lib.qs_ppo_small_layout(mb, D, Ia, Ic, A, off, len(off)) == 0
         return dict(nA=off[16], nC=off[17], KaP=off[18], KcP=off[19], Sa=off[27], Sc=off[28])
 
     # the reference's learner shape: 256 actor rows, 32 critic rows, 16-row tiles
@@ -107,3 +107,17 @@ def test_tile_layouts_at_the_per_rank_shapes():
     # C4 at G = 4: the four-output actor at 32 rows beside the 595-wide critic at 16 (one round)
     d = lay(1024, 5, 119, 595, 4)
     assert (d["nA"], d["nC"], d["KaP"], d["KcP"]) == (160, 64, 5120, 1024)
+
+
+def test_small_layout_writes_only_the_callers_entries():
+    """qs_ppo_small_layout writes min(n_off, QS_PPO_SMALL_LAYOUT_N)
+    entries — a caller sized for fewer (an older contract) is never overrun."""
+    from gym_pybullet_drones_amd import _lib as L
+    lib = L.load()
+    buf = (ctypes.c_int64 * 40)(*([-7] * 40))
+    assert lib.qs_ppo_small_layout(512, 8, 27, 216, 1, buf, 23) == 0
+    assert all(buf[i] != -7 for i in range(23)) and all(buf[i] == -7 for i in range(23, 40))
+    full = (ctypes.c_int64 * L.QS_PPO_SMALL_LAYOUT_N)()
+    assert lib.qs_ppo_small_layout(512, 8, 27, 216, 1, full, len(full)) == 0
+    assert list(buf[:23]) == list(full[:23])
+    assert lib.qs_ppo_small_layout(512, 8, 27, 216, 1, full, 0) != 0   # no room: refused
