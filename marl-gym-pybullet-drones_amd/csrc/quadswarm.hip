@@ -166,7 +166,10 @@ struct qs_handle {
 #ifndef QS_EPB_HALVINGS
 #define QS_EPB_HALVINGS 0   // measured: one halving made Spiral C4 11.6 -> 18.2 µs; dev builds probe it
 #endif
-static constexpr int kEpbWaves = 2;
+#ifndef QS_EPB_WAVES
+#define QS_EPB_WAVES 2   // (dev builds: the waves per SIMD below which a halving applies)
+#endif
+static constexpr int kEpbWaves = QS_EPB_WAVES;
 static int envs_per_wave(const qs_handle* h) {
   const int E = h->spec.num_envs, simds = 4 * h->num_cu;
   int epb = qs::kBlock / h->spec.num_drones;

@@ -686,8 +686,11 @@ template <int K> __device__ __forceinline__ void dw16_pair(float px, float py, f
 __device__ __forceinline__ float downwash16(float px, float py, float pz) {
   float f1 = 0.f, f2 = 0.f, f3 = 0.f, f4 = 0.f;
   dw16_pair<1>(px, py, pz, f1); dw16_pair<2>(px, py, pz, f2); dw16_pair<3>(px, py, pz, f3);
-  dw16_pair<4>(px, py, pz, f4); dw16_pair<5>(px, py, pz, f1); dw16_pair<6>(px, py, pz, f2);
+  dw16_pair<4>(px, py, pz, f4);
+#ifndef QS_DW_HALF   // (dev probe: half the pair terms, the cost of a two-lanes-per-drone split's half)
+  dw16_pair<5>(px, py, pz, f1); dw16_pair<6>(px, py, pz, f2);
   dw16_pair<7>(px, py, pz, f3); dw16_pair<8>(px, py, pz, f4);
+#endif
   return (f1 + f2) + (f3 + f4);
 }
 
