@@ -681,7 +681,7 @@ def allreduce_us(n, reps=10, per_graph=20):
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         for _ in range(3):
-            dist.all_reduce(buf)
+            dist.all_reduce(buf, async_op=True).wait()   # (eager: the event on the group's own stream)
     torch.cuda.current_stream().wait_stream(s)
     from gym_pybullet_drones_amd.mappo.collectives import capture_collectives, collective_group
     g = torch.cuda.CUDAGraph()

@@ -30,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib as L
+from . import collectives
 from .collectives import capture_collectives, collective_group  # noqa: F401  (re-exported)
 
 
@@ -1007,8 +1008,8 @@ class MAPPOAgent:
         self._adam_work = torch.zeros(nw, dtype=torch.int32, device=self.device)
         self._adam_work_c = torch.zeros(nw, dtype=torch.int32, device=self.device)
         if _dist_world() > 1:   # identical initial weights on every rank
-            tdist.broadcast(self.actor_opt.flat, 0)
-            tdist.broadcast(self.critic_opt.flat, 0)
+            collectives.broadcast(self.actor_opt.flat, 0)
+            collectives.broadcast(self.critic_opt.flat, 0)
         self._opt_ready = True
         self._graph = None
 
@@ -1366,7 +1367,7 @@ class MAPPOAgent:
         L.check(lib.qs_ppo_small_grads(*head, ctypes.byref(na), ctypes.byref(nc), L.ptr(self.actor_opt.grad),
                                        L.ptr(self.critic_opt.grad), L.ptr(self._kl), L.ptr(acc), L.ptr(self._sm_work),
                                        st), "qs_ppo_small_grads")
-        tdist.all_reduce(self._reduce_buf, group=collective_group())   # one collective: [critic | actor | approx_kl]
+        collectives.all_reduce(self._reduce_buf)   # one collective: [critic | actor | approx_kl]
         L.check(lib.qs_ppo_small_adam(mb, D, ctypes.byref(na), ctypes.byref(nc), L.ptr(self.actor_opt.grad),
                                       L.ptr(self.critic_opt.grad), float(world), gate, thr, L.ptr(self._kl),
                                       L.ptr(self._sm_work), st), "qs_ppo_small_adam")
@@ -1402,14 +1403,14 @@ class MAPPOAgent:
         rank evaluates the same KL gate on the same value.  Runs on any device
         (tests/test_distributed_cpu.py drives it on CPU tensors with gloo)."""
         if world > 1 or self._force_allreduce:
-            tdist.all_reduce(self._reduce_buf, group=collective_group())
+            collectives.all_reduce(self._reduce_buf)
             self._reduce_buf.div_(world)
 
     def _exchange_bucket(self, bucket, world):
         """One bucket of the direct iteration's exchange (critic gradients, or actor
         gradients + approx_kl): all-reduce (sum) and divide by the world size on
         the current stream — the same values as the one-piece `_exchange`."""
-        tdist.all_reduce(bucket, group=collective_group())
+        collectives.all_reduce(bucket)
         bucket.div_(world)
 
     def _actor_gate_open(self):

@@ -20,7 +20,7 @@ import torch
 import torch.distributed as tdist
 
 from .. import _lib as L
-from .collectives import collective_group
+from . import collectives
 
 
 def _stream():
@@ -57,7 +57,7 @@ def normalize_advantages(advs, epsilon=1e-8):
         x = advs.to(torch.float64)
         s = torch.stack([x.sum(), (x * x).sum(), torch.tensor(float(x.numel()), dtype=torch.float64,
                                                                 device=x.device)])
-        tdist.all_reduce(s, group=collective_group())
+        collectives.all_reduce(s)
         n = s[2]
         mean = s[0] / n
         var = (s[1] - n * mean * mean) / (n - 1)

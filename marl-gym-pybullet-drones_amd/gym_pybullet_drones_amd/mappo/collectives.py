@@ -1,9 +1,19 @@
 """Process groups for the learner's collectives.
 
-Collectives captured in HIP graphs (the update's gradient all-reduce, the
-rollout's normaliser moments) run on a process group of their own, so the
-RCCL watchdog never polls an eager collective's event while a capture is open
-(capture_collectives); eager collectives stay on the default group.
+The RCCL watchdog thread of a process group polls the HIP end event of every
+eager collective it has not yet retired (a ~100 ms loop); a poll of an event
+last recorded in a stream that is capturing aborts the process
+(hipErrorCapturedEvent).  Two rules keep every such poll off capturing streams,
+with no timing assumption:
+* collectives captured in HIP graphs (the update's gradient all-reduce, the
+  rollout's normaliser moments) run on a process group of their own
+  (capture_collectives): captured works are never enqueued to a watchdog, and
+  that group never runs an eager collective;
+* eager collectives (all_reduce / broadcast below) are issued async and waited
+  for: their events are recorded on the default group's internal stream, which
+  no capture ever joins — not on the caller's current stream, which may be a
+  pooled side stream that a later capture reuses (a synchronous collective
+  records its event there; the round-6 bench aborted so).
 """
 import contextlib
 
@@ -50,3 +60,18 @@ def capture_collectives():
         yield
     finally:
         _capturing -= 1
+
+
+def all_reduce(t):
+    """Sum-all-reduce of t as the learner issues it: inside a capture on the
+    capture group (captured), otherwise async on the default group and waited
+    for (see the module docstring)."""
+    if _capturing:
+        tdist.all_reduce(t, group=collective_group())
+    else:
+        tdist.all_reduce(t, async_op=True).wait()
+
+
+def broadcast(t, src=0):
+    """Eager broadcast from rank src (async + wait: the event on the group's own stream)."""
+    tdist.broadcast(t, src, async_op=True).wait()

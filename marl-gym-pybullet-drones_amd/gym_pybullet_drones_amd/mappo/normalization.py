@@ -18,7 +18,7 @@ import torch
 import torch.distributed as tdist
 
 from .. import _lib as L
-from .collectives import collective_group
+from . import collectives
 
 
 def _dist_on():
@@ -58,7 +58,7 @@ class RunningMeanStd:
         s2 = (x * x).sum(0)
         if _dist_on():
             buf = torch.cat([s1.reshape(-1), s2.reshape(-1), torch.full((1,), n, dtype=torch.float64, device=x.device)])
-            tdist.all_reduce(buf, group=collective_group())
+            collectives.all_reduce(buf)
             k = s1.numel()
             s1, s2, n = buf[:k].view_as(s1), buf[k:2 * k].view_as(s2), buf[2 * k]
             batch_mean = s1 / n
@@ -84,7 +84,7 @@ class RunningMeanStd:
             return
         buf = torch.empty(2 * C + 1, dtype=torch.float64, device=x.device)
         L.check(lib.qs_rms_update(R, C, L.ptr(x), None, None, None, L.ptr(buf), L.ptr(work), st), "qs_rms_update")
-        tdist.all_reduce(buf, group=collective_group())
+        collectives.all_reduce(buf)
         shape = self.mean.shape
         s1, s2, n = buf[:C].view(shape), buf[C:2 * C].view(shape), buf[2 * C]
         batch_mean = s1 / n

@@ -1,10 +1,15 @@
 """Dev probe: graph captures of the update (its all-reduce
 captured) right after eager all-reduces on a world-1 RCCL group, no sleep.
 
-  python scripts/capture_probe.py capture N   # captured all-reduce on the capture group (the product path)
-  python scripts/capture_probe.py default N   # the same on the default group (round 5's hazard, no drain)
+  python scripts/capture_probe.py capture N   # the product path (mappo/collectives.py)
+  python scripts/capture_probe.py default N   # synchronous eager all-reduces and the captured one on the
+                                              # default group (round 5's hazard, without its drain)
 
-Prints one line per capture; an abort of the process is the hazard."""
+Before each capture, eager all-reduces run with the graphs' default capture
+stream current (the stream the next capture uses: a synchronous collective
+records its end event on the current stream).  Prints one line per capture;
+an abort of the process (hipErrorCapturedEvent from the RCCL watchdog) is the
+hazard."""
 import os
 import socket
 import sys
@@ -30,9 +35,8 @@ def main():
         port = s.getsockname()[1]
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
-    if mode == "default":   # the captured all-reduce back on the default group
-        collectives.collective_group = lambda: None
-        agent_mod.collective_group = lambda: None
+    if mode == "default":   # every all-reduce synchronous on the default group
+        collectives.all_reduce = lambda t: dist.all_reduce(t)
     agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
     D, O, A, T, E = 8, 27, 1, 16, 512
     osp, asp = Box(-np.inf * np.ones((D, O)), np.inf * np.ones((D, O))), Box(-np.ones((D, A)), np.ones((D, A)))
@@ -44,9 +48,12 @@ def main():
         t.normal_()
     buf.t, buf.full = 0, True
     x = torch.ones(1 << 16, device="cuda")
+    agent._capture(buf, 1)   # (creates the graphs' default capture stream)
+    cs = torch.cuda.graph.default_capture_stream
     for i in range(n):
-        for _ in range(4):
-            dist.all_reduce(x)
+        with torch.cuda.stream(cs):
+            for _ in range(4):
+                collectives.all_reduce(x)
         t0 = time.perf_counter()
         agent._capture(buf, int(os.environ.get("QS_CAPTURE_K", "400")))   # a capture window of K minibatch iterations (~70 ms at 400)
         agent._graph.replay()

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 5 closing evidence on one box: the whole -m gpu suite, smoke(), the
+# Round 6 closing evidence on one box: the whole -m gpu suite, smoke(), the
 # default bench line; each step under its own limit, stopping at the first
 # failure.  STEPS selects a subset ("tests smoke bench").
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 for s in ${STEPS:-tests smoke bench}; do
   case $s in
     tests)
