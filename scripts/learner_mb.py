@@ -241,12 +241,16 @@ def main():
             for v in (dict(small=True, force=True), dict(small=True, force=False)):
                 us, path = per_minibatch_us(shape, **v)
                 print(f"{tag:>12s} {shape:5s} {str(v):36s} {us:8.1f} us/minibatch  [{path}]", flush=True)
-    for w in which:   # "shape:NAME[:direct]": one shape's tile (or direct) path alone, e.g. under a kernel trace
-        if w.startswith("shape:"):
+    for w in which:   # "shape:NAME[:direct|:force]": one shape's tile (or direct) path alone, e.g. under a
+        if w.startswith("shape:"):   # kernel trace; force: the tile path's exchange launches (world-1 RCCL group)
             _, name, *rest = w.split(":")
             agent_mod._SMALL_MAX_ROWS = L.QS_PPO_SMALL_MAX_ROWS
-            us, path = per_minibatch_us(name, small=not rest)
-            print(f"{name:5s} {'direct' if rest else 'tile'} {us:8.1f} us/minibatch  [{path}]", flush=True)
+            force = rest == ["force"]
+            if force:
+                world1()
+            us, path = per_minibatch_us(name, small=rest != ["direct"], force=force)
+            mode = "direct" if rest == ["direct"] else ("tile+exchange" if force else "tile")
+            print(f"{name:5s} {mode} {us:8.1f} us/minibatch  [{path}]", flush=True)
     if "one" in which:   # the default C3 iteration alone (for a kernel trace: scripts/learner_timeline.py)
         us, path = per_minibatch_us("C3")
         print(f"C3  default {us:8.1f} us/minibatch  [{path}]", flush=True)
