@@ -49,8 +49,8 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 3   /* 2: qs_episode_log reports the records it wrote; 3: qs_ppo_small_layout takes
-                              the caller's entry count */
+#define QS_ABI_VERSION 4   /* 2: qs_episode_log reports the records it wrote; 3: qs_ppo_small_layout takes
+                              the caller's entry count; 4: QS_FLAG_CF2P */
 
 /* ---- status codes ------------------------------------------------------ */
 #define QS_OK 0
@@ -99,6 +99,11 @@ typedef enum {            /* Physics (enums.py:13-21)                      */
                                     (MultiHoverAviary.py:83-102) inside the
                                     step kernel, no deferred search launch
                                     (the validation form of the deferred one) */
+#define QS_FLAG_CF2P 4u  /* DroneModel.CF2P, the + configuration (cf2p.urdf:
+                                    inertia and prop links on the axes;
+                                    BaseAviary.py:852-853 torques,
+                                    DSLPIDControl.py:54-60 mixer); default
+                                    DroneModel.CF2X */
 
 typedef struct qs_spec {
   int32_t task;          /* qs_task                                        */

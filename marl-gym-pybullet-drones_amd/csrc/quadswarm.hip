@@ -264,6 +264,11 @@ static int check_consts() {
   const double max_thrust = 4 * C.KF * max_rpm * max_rpm;
   const double gnd_clip = 0.25 * C.PROP_RADIUS * std::sqrt((15 * max_rpm * max_rpm * C.KF * C.GND_EFF_COEFF) / max_thrust);
   if (!ok || K::GND_CLIP != gnd_clip) return fail(QS_E_INVALID, "qs_create: CF2X device constants disagree with the URDF derivation");
+  // CF2P (QS_FLAG_CF2P): cf2p.urdf:12 inertia, props on the body axes at L (cf2p.urdf:42-79)
+  using MP = qs::Model<true>;
+  const bool okp = MP::IXX == 2.3951e-5 && MP::IYY == 2.3951e-5 && MP::IZZ == 3.2347e-5 && MP::PX[0] == C.L &&
+                   MP::PY[1] == C.L && MP::PX[2] == -C.L && MP::PY[3] == -C.L && MP::PX[1] == 0 && MP::PY[0] == 0;
+  if (!okp) return fail(QS_E_INVALID, "qs_create: CF2P device constants disagree with cf2p.urdf");
   return QS_OK;
 }
 
@@ -280,7 +285,8 @@ int qs_create(const qs_spec* spec, int device, qs_handle** out) {
   if (s.num_envs < 1) return fail(QS_E_INVALID, "qs_create: num_envs must be >= 1");
   if (s.physics != QS_PHYS_DYN && s.physics != QS_PHYS_PYB) return fail(QS_E_INVALID, "qs_create: bad physics");
   if (s.aux_forces & ~7u) return fail(QS_E_INVALID, "qs_create: bad aux_forces");
-  if (s.flags & ~(QS_FLAG_NO_AUTORESET | QS_FLAG_INKERNEL_RESET_SEARCH)) return fail(QS_E_INVALID, "qs_create: bad flags");
+  if (s.flags & ~(QS_FLAG_NO_AUTORESET | QS_FLAG_INKERNEL_RESET_SEARCH | QS_FLAG_CF2P))
+    return fail(QS_E_INVALID, "qs_create: bad flags");
   if (s.pyb_freq <= 0 || s.ctrl_freq <= 0 || s.pyb_freq % s.ctrl_freq)
     return fail(QS_E_INVALID, "qs_create: pyb_freq is not divisible by env_freq");  // BaseAviary.py:79-80
   if (s.ctrl_freq < 2) return fail(QS_E_INVALID, "qs_create: ctrl_freq must be >= 2 (action history length ctrl_freq//2)");

@@ -103,6 +103,21 @@ constexpr double DW1 = 2267.18, DW2 = 0.16, DW3 = -0.11;
 // damping (linear = angular = 0.04) and the collision cylinder (cf2x.urdf:32-35).
 constexpr double kPropX[4] = {0.028, -0.028, -0.028, 0.028}, kPropY[4] = {-0.028, -0.028, 0.028, 0.028};
 constexpr double kPybDamping = 0.04, kCylR = 0.06, kCylHalfLen = 0.0125;
+// The drone model (QS_FLAG_CF2P selects DroneModel.CF2P, the + configuration):
+// cf2p.urdf differs from cf2x.urdf only in the inertia (cf2p.urdf:12) and the
+// prop links, on the body axes at L (cf2p.urdf:42-79); the torques
+// (BaseAviary.py:849-853) and the DSL PID mixer (DSLPIDControl.py:48-60) follow.
+template <bool CF2P> struct Model {
+  static constexpr double IXX = cf2x::IXX, IYY = cf2x::IYY, IZZ = cf2x::IZZ;
+  static constexpr double PX[4] = {kPropX[0], kPropX[1], kPropX[2], kPropX[3]};
+  static constexpr double PY[4] = {kPropY[0], kPropY[1], kPropY[2], kPropY[3]};
+  static constexpr double MIX[4][3] = {{-.5, -.5, -1}, {-.5, .5, 1}, {.5, .5, -1}, {.5, -.5, 1}};
+};
+template <> struct Model<true> {
+  static constexpr double IXX = 2.3951e-5, IYY = 2.3951e-5, IZZ = 3.2347e-5;
+  static constexpr double PX[4] = {cf2x::L, 0, -cf2x::L, 0}, PY[4] = {0, cf2x::L, 0, -cf2x::L};
+  static constexpr double MIX[4][3] = {{0, -1, -1}, {+1, 0, 1}, {0, 1, -1}, {-1, 0, 1}};
+};
 
 // Compile-time shape of an action type (BaseRLAviary.py:262-277).
 template <int ACT> struct Act {
@@ -309,7 +324,7 @@ template <class T> __device__ __forceinline__ void quat_to_rpy(const T q[4], T r
 // DSLPIDControl.computeControl (DSLPIDControl.py:82-259), one drone.
 // pid: int_pos[3], int_rpy[3], last_rpy[3] (updated in place); rpy = the
 // current attitude (computed once by the caller, DSLPIDControl.py:240).
-template <class T>
+template <class T, bool CF2P = false>
 __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T pos[3], const T q[4], const T vel[3],
                                         const T rpy[3], const T tpos[3], T tyaw, const T tvel[3], T rpm[4]) {
   if constexpr (qs_dev::kNoCompute) {
@@ -368,8 +383,12 @@ __device__ __forceinline__ void dsl_pid(T ctrl_dt, T ctrl_hz, T pid[9], const T 
   T tq[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) tq[i] = clampv(-PT[i] * rot_e[i] + DT[i] * rate_e[i] + IT[i] * pid[3 + i], T(-3200), T(3200));
-  // CF2X mixer (DSLPIDControl.py:48-53)
-  const T MX[4][3] = {{T(-.5), T(-.5), T(-1)}, {T(-.5), T(.5), T(1)}, {T(.5), T(.5), T(-1)}, {T(.5), T(-.5), T(1)}};
+  // the mixer (DSLPIDControl.py:48-60)
+  using MD = Model<CF2P>;
+  const T MX[4][3] = {{T(MD::MIX[0][0]), T(MD::MIX[0][1]), T(MD::MIX[0][2])},
+                      {T(MD::MIX[1][0]), T(MD::MIX[1][1]), T(MD::MIX[1][2])},
+                      {T(MD::MIX[2][0]), T(MD::MIX[2][1]), T(MD::MIX[2][2])},
+                      {T(MD::MIX[3][0]), T(MD::MIX[3][1]), T(MD::MIX[3][2])}};
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     T pwm = thrust + (MX[m][0] * tq[0] + MX[m][1] * tq[1] + MX[m][2] * tq[2]);
@@ -707,10 +726,13 @@ __device__ __forceinline__ float downwash16(float px, float py, float pz) {
 // downwash forces (the common P.aux == 0 case: a run-time force branch inside
 // the unrolled substeps cost 0.65 µs of the 10.5 µs C3 launch); 1 = downwash
 // only (C5's PYB_DW), kept on the fp32 fast substep; 2 = any combination
-// through the general substep (the P.aux bits decide at run time).
+// through the general substep (the P.aux bits decide at run time); 3 = the
+// same for DroneModel.CF2P (QS_FLAG_CF2P).
 template <class T, int TASK, int ACT, int CF, int PHYS, int AUXM>
 __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
   using F = M<T>;
+  constexpr bool kP = AUXM == 3;   // DroneModel.CF2P
+  using MD = Model<kP>;
   constexpr int A = Act<ACT>::A;
   constexpr bool kPid = Act<ACT>::pid;
   constexpr bool kHover = TASK == QS_TASK_MULTIHOVER;
@@ -901,7 +923,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         if (!qs_dev::kNoCompute) quat_to_rpy(q, rpy);   // DSLPIDControl.py:240 (and the VEL target yaw, BRL:221)
         if constexpr (ACT == QS_ACT_ONE_D_PID) {
           T tp[3] = {pos[0], pos[1], pos[2] + T(0.1) * T(act[0])};
-          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
+          dsl_pid<T, kP>(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, tp, T(0), z3, rpm);
         } else if constexpr (ACT == QS_ACT_VEL) {
           T v0 = T(act[0]), v1 = T(act[1]), v2 = T(act[2]);
           T n = F::sqrt_(v0 * v0 + v1 * v1 + v2 * v2);
@@ -909,14 +931,14 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           if (n != T(0)) { u0 = v0 / n; u1 = v1 / n; u2 = v2 / n; }
           T sp = T(cf2x::SPEED_LIMIT) * F::abs_(T(act[3]));
           T tv[3] = {sp * u0, sp * u1, sp * u2};
-          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, pos, rpy[2], tv, rpm);
+          dsl_pid<T, kP>(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, pos, rpy[2], tv, rpm);
         } else {   // QS_ACT_PID: _calculateNextStep (BaseAviary.py:1108-1150)
           T dir[3] = {T(act[0]) - pos[0], T(act[1]) - pos[1], T(act[2]) - pos[2]};
           T dist = F::sqrt_(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
           T np_[3];
           if (dist <= T(1)) { np_[0] = T(act[0]); np_[1] = T(act[1]); np_[2] = T(act[2]); }
           else { for (int i = 0; i < 3; ++i) np_[i] = pos[i] + (dir[i] / dist) * T(1); }
-          dsl_pid(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, np_, T(0), z3, rpm);
+          dsl_pid<T, kP>(P.ctrl_dt, P.ctrl_hz, pid, pos, q, vel, rpy, np_, T(0), z3, rpm);
         }
       }
     }
@@ -943,11 +965,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     for (int m = 0; m < 4; ++m) { f[m] = rpm[m] * rpm[m] * T(cf2x::KF); zt[m] = rpm[m] * rpm[m] * T(cf2x::KM); }
     const T thrust_z = ((f[0] + f[1]) + f[2]) + f[3];
     const T tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];
-    const T tx = -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
-    const T ty = (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
-    // PYB: the four prop forces act at their links' COMs (assets/cf2x.urdf:42-79)
-    const T pbx = (((T(kPropY[0]) * f[0]) + T(kPropY[1]) * f[1]) + T(kPropY[2]) * f[2]) + T(kPropY[3]) * f[3];
-    const T pby = (((-T(kPropX[0]) * f[0]) + -T(kPropX[1]) * f[1]) + -T(kPropX[2]) * f[2]) + -T(kPropX[3]) * f[3];
+    // BaseAviary.py:849-850 (CF2X), 852-853 (CF2P)
+    const T tx = kP ? (f[1] - f[3]) * T(cf2x::L) : -(((f[0] + f[1]) - f[2]) - f[3]) * T(cf2x::L_SQRT2);
+    const T ty = kP ? (-f[0] + f[2]) * T(cf2x::L) : (((-f[0] + f[1]) + f[2]) - f[3]) * T(cf2x::L_SQRT2);
+    // PYB: the four prop forces act at their links' COMs (assets/cf2x.urdf:42-79, cf2p.urdf:42-79)
+    const T pbx = (((T(MD::PY[0]) * f[0]) + T(MD::PY[1]) * f[1]) + T(MD::PY[2]) * f[2]) + T(MD::PY[3]) * f[3];
+    const T pby = (((-T(MD::PX[0]) * f[0]) + -T(MD::PX[1]) * f[1]) + -T(MD::PX[2]) * f[2]) + -T(MD::PX[3]) * f[3];
     const T dt = P.dt;
     // The exp-map update preserves |q| (cos²θ + sin²θ = 1), so in fp32 Bullet's
     // s = 2/|q|² (getMatrixFromQuaternion) is formed once per control step; it
@@ -1006,7 +1029,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
     // gyroscopic term reduced with IXX == IYY, and the PYB world-frame exp map
     // applied as the equivalent right product q ⊗ exp(ω_body dt/2) (R(q)ω = q ω q*).
     // Same mathematics as the general path below; fp32 rounding only.
-    constexpr bool kFastSub = sizeof(T) == 4 && AUXM != 2 && CF != 0;
+    constexpr bool kFastSub = sizeof(T) == 4 && AUXM < 2 && CF != 0;
     // _downwash (BaseAviary.py:798-811) for the fast substep: the body-z force of the
     // drones above, from the neighbours' substep-start positions.  D = 16 through
     // DPP (downwash16); otherwise one float4 per drone in LDS, four neighbours in
@@ -1173,8 +1196,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
           quat_to_rpy(q, srpy);
           quat_to_rot(q, R);
           if (F::abs_(srpy[0]) < T(M_PI / 2) && F::abs_(srpy[1]) < T(M_PI / 2)) {
-            const T PX[4] = {T(kPropX[0]), T(kPropX[1]), T(kPropX[2]), T(kPropX[3])};
-            const T PY[4] = {T(kPropY[0]), T(kPropY[1]), T(kPropY[2]), T(kPropY[3])};
+            const T PX[4] = {T(MD::PX[0]), T(MD::PX[1]), T(MD::PX[2]), T(MD::PX[3])};
+            const T PY[4] = {T(MD::PY[0]), T(MD::PY[1]), T(MD::PY[2]), T(MD::PY[3])};
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
               T h = pos[2] + (R[6] * PX[m] + R[7] * PY[m]);
@@ -1227,12 +1250,12 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
         const T vd = k + k * F::sqrt_(vel[0] * vel[0] + vel[1] * vel[1] + vel[2] * vel[2]);
         const T a0 = F::divc(fw0, cf2x::M) - vd * vel[0], a1 = F::divc(fw1, cf2x::M) - vd * vel[1];
         const T a2 = F::divc(fw2, cf2x::M) - vd * vel[2];
-        T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
+        T Jw0 = T(MD::IXX) * w[0], Jw1 = T(MD::IYY) * w[1], Jw2 = T(MD::IZZ) * w[2];
         T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
         const T wdm = k + k * F::sqrt_(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        T wd0 = T(1.0 / cf2x::IXX) * (((pbx + txe) - c0) - wdm * Jw0);
-        T wd1 = T(1.0 / cf2x::IYY) * (((pby + tye) - c1) - wdm * Jw1);
-        T wd2 = T(1.0 / cf2x::IZZ) * ((tz - c2) - wdm * Jw2);
+        T wd0 = T(1.0 / MD::IXX) * (((pbx + txe) - c0) - wdm * Jw0);
+        T wd1 = T(1.0 / MD::IYY) * (((pby + tye) - c1) - wdm * Jw1);
+        T wd2 = T(1.0 / MD::IZZ) * ((tz - c2) - wdm * Jw2);
         vel[0] = vel[0] + dt * a0;
         vel[1] = vel[1] + dt * a1;
         vel[2] = vel[2] + dt * a2;
@@ -1284,10 +1307,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(Params<T> P) {
       } else {
         // _dynamics (BaseAviary.py:836-877)
         T fw0 = R2 * zb + fwx, fw1 = R5 * zb + fwy, fw2 = (R8 * zb - T(cf2x::GRAVITY)) + fwz;
-        T Jw0 = T(cf2x::IXX) * w[0], Jw1 = T(cf2x::IYY) * w[1], Jw2 = T(cf2x::IZZ) * w[2];
+        T Jw0 = T(MD::IXX) * w[0], Jw1 = T(MD::IYY) * w[1], Jw2 = T(MD::IZZ) * w[2];
         T c0 = w[1] * Jw2 - w[2] * Jw1, c1 = w[2] * Jw0 - w[0] * Jw2, c2 = w[0] * Jw1 - w[1] * Jw0;
-        T wd0 = T(1.0 / cf2x::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / cf2x::IYY) * ((ty + tye) - c1);
-        T wd2 = T(1.0 / cf2x::IZZ) * (tz - c2);
+        T wd0 = T(1.0 / MD::IXX) * ((tx + txe) - c0), wd1 = T(1.0 / MD::IYY) * ((ty + tye) - c1);
+        T wd2 = T(1.0 / MD::IZZ) * (tz - c2);
         vel[0] = vel[0] + dt * F::divc(fw0, cf2x::M);
         vel[1] = vel[1] + dt * F::divc(fw1, cf2x::M);
         vel[2] = vel[2] + dt * F::divc(fw2, cf2x::M);

@@ -14,6 +14,11 @@ template <class T, int TASK, int ACT> static void launch_one(int grid, size_t ld
   // no extra forces / downwash only / general force set (step_kernel AUXM)
   const int auxm = P.aux == 0 ? 0 : (P.aux == QS_AUX_DW ? 1 : 2);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, st, P); };
+  if (P.flags & QS_FLAG_CF2P) {   // DroneModel.CF2P: the general substep (AUXM 3), run-time frequency
+    if (phys == QS_PHYS_DYN) go(step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN, 3>);
+    else go(step_kernel<T, TASK, ACT, 0, QS_PHYS_PYB, 3>);
+    return;
+  }
   if (phys == QS_PHYS_DYN) {
     if (!cf) go(step_kernel<T, TASK, ACT, 0, QS_PHYS_DYN, 2>);
     else if (auxm == 0) go(step_kernel<T, TASK, ACT, kCF, QS_PHYS_DYN, 0>);

@@ -22,6 +22,7 @@ AGENT_FIELDS, ENV_FIELDS = 29, 4
 STATE_AGENT, STATE_ENV, STATE_HISTORY, STATE_EP_RETURN = 0, 1, 2, 3
 FLAG_NO_AUTORESET = 1
 FLAG_INKERNEL_RESET_SEARCH = 2
+FLAG_CF2P = 4   # DroneModel.CF2P (include/quadswarm.h QS_FLAG_CF2P)
 REASON_CRASH, REASON_FLIP, REASON_OOB, REASON_ZRANGE = 1, 2, 4, 8
 
 # agent field offsets (include/quadswarm.h)
@@ -57,7 +58,7 @@ class QsStepOut(ctypes.Structure):
 EPISODE_DTYPE = np.dtype([("ret", "<f8"), ("len", "<i4"), ("env", "<i4"), ("seq", "<i8")])
 
 # Every symbol include/quadswarm.h declares (tests check the .so exports them).
-ABI_VERSION = 3   # include/quadswarm.h QS_ABI_VERSION
+ABI_VERSION = 4   # include/quadswarm.h QS_ABI_VERSION
 EXPORTS = ("qs_create", "qs_destroy", "qs_last_error", "qs_abi_version", "qs_get_dims", "qs_reset",
            "qs_reset_envs", "qs_step", "qs_state_io", "qs_episode_log", "qs_reset_error", "qs_calib_copy",
            # include/qs_learner.h

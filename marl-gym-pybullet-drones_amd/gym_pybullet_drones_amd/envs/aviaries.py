@@ -51,7 +51,7 @@ class _SingleEnvAviary:
         self.EPISODE_LEN_SEC = self.swarm.episode_len_sec
         self._started = False
         self._vec_spec = dict(task=self.TASK, num_drones=num_drones, act=ActionType(act), physics=Physics(physics),
-                              pyb_freq=pyb_freq, ctrl_freq=ctrl_freq, precision=precision,
+                              pyb_freq=pyb_freq, ctrl_freq=ctrl_freq, precision=precision, drone_model=self.DRONE_MODEL,
                               initial_xyzs=None if initial_xyzs is None else np.asarray(initial_xyzs, np.float64),
                               **task_kw)
         self.swarm.reset(0)

@@ -65,7 +65,8 @@ def _as_enum(x, enum):
 
 
 class QuadSwarm:
-    """Batch of `num_envs` envs of `num_drones` CF2X drones on one GPU."""
+    """Batch of `num_envs` envs of `num_drones` drones (DroneModel.CF2X, the
+    MAPPO tasks' model, or CF2P) on one GPU."""
 
     def __init__(self, task="multihover", num_envs=1, num_drones=2, act=ActionType.RPM, physics=Physics.DYN,
                  pyb_freq=240, ctrl_freq=None, precision=4, device=None, env_offset=0, initial_xyzs=None,
@@ -82,8 +83,11 @@ class QuadSwarm:
         act = _as_enum(act, ActionType)
         physics = _as_enum(physics, Physics)
         drone_model = _as_enum(drone_model, DroneModel)
-        if drone_model != DroneModel.CF2X:
-            raise NotImplementedError("only DroneModel.CF2X is implemented (the MAPPO tasks' model)")
+        # CF2X and CF2P: the models DSLPIDControl accepts (DSLPIDControl.py:34-36);
+        # CF2P's inertia, props, torques and mixer ride on QS_FLAG_CF2P
+        if drone_model not in (DroneModel.CF2X, DroneModel.CF2P):
+            raise NotImplementedError("DroneModel.CF2X and CF2P are implemented (RACE has no DSL PID, "
+                                      "DSLPIDControl.py:34-36)")
         if any(a not in _AUX_NAMES for a in aux):
             raise ValueError(f"unknown aux force model in {aux!r} (gnd, drag, dw)")
         if not torch.cuda.is_available():
@@ -108,7 +112,8 @@ class QuadSwarm:
         spec.pyb_freq = int(pyb_freq)
         spec.ctrl_freq = int(ctrl_freq)
         spec.precision = int(precision)
-        spec.flags = (0 if autoreset else L.FLAG_NO_AUTORESET) | (L.FLAG_INKERNEL_RESET_SEARCH if inkernel_reset_search else 0)
+        spec.flags = ((0 if autoreset else L.FLAG_NO_AUTORESET) | (L.FLAG_INKERNEL_RESET_SEARCH if inkernel_reset_search else 0)
+                      | (L.FLAG_CF2P if drone_model == DroneModel.CF2P else 0))
         spec.env_offset = int(env_offset)
         spec.episode_len_sec = float(episode_len_sec)
         self._xyz_keep = None
@@ -122,7 +127,7 @@ class QuadSwarm:
         for i in range(3):
             spec.target_center[i] = float(target_center[i])
         self.spec = spec
-        self.act_type, self.physics = act, physics
+        self.act_type, self.physics, self.drone_model = act, physics, drone_model
         self._h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             L.check(self.lib.qs_create(ctypes.byref(spec), self.device.index, ctypes.byref(self._h)), "qs_create")

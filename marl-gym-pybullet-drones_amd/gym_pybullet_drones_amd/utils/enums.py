@@ -3,7 +3,7 @@ from enum import Enum
 
 
 class DroneModel(Enum):
-    """Drone models (only CF2X has a DSL PID and a DYN torque model here)."""
+    """Drone models (CF2X and CF2P: the two with a DSL PID, DSLPIDControl.py:34-36)."""
     CF2X = "cf2x"
     CF2P = "cf2p"
     RACE = "racer"

@@ -81,6 +81,10 @@ struct Consts {
   double GRAVITY, HOVER_RPM, MAX_RPM, MAX_THRUST, GND_EFF_H_CLIP;
   // prop link COM offsets (cf2x.urdf:42-79) — where LINK_FRAME forces act
   double PROP_XY[4][2] = {{0.028, -0.028}, {-0.028, -0.028}, {-0.028, 0.028}, {0.028, 0.028}};
+  // DroneModel.CF2P (QS_FLAG_CF2P): cf2p.urdf differs from cf2x.urdf only in the
+  // inertia (cf2p.urdf:12) and the prop links, on the body axes at L (cf2p.urdf:42-79)
+  double IXX_P = 2.3951e-5, IYY_P = 2.3951e-5, IZZ_P = 3.2347e-5;
+  double PROP_XY_P[4][2] = {{0.0397, 0}, {0, 0.0397}, {-0.0397, 0}, {0, -0.0397}};
   Consts() {
     GRAVITY = G * M;                                           // BA:117
     HOVER_RPM = std::sqrt(GRAVITY / (4 * KF));                 // BA:118
@@ -97,6 +101,7 @@ const double P_FOR[3] = {.4, .4, 1.25}, I_FOR[3] = {.05, .05, .05}, D_FOR[3] = {
 const double P_TOR[3] = {70000., 70000., 60000.}, I_TOR[3] = {.0, .0, 500.}, D_TOR[3] = {20000., 20000., 12000.};
 const double PWM2RPM_SCALE = 0.2685, PWM2RPM_CONST = 4070.3, MIN_PWM = 20000, MAX_PWM = 65535;
 const double MIXER[4][3] = {{-.5, -.5, -1}, {-.5, .5, 1}, {.5, .5, -1}, {.5, -.5, 1}};
+const double MIXER_P[4][3] = {{0, -1, -1}, {+1, 0, 1}, {0, 1, -1}, {-1, 0, 1}};   // CF2P (DSLPIDControl.py:54-60)
 
 template <class R> inline R clip(R x, R lo, R hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
@@ -155,6 +160,9 @@ template <class R> struct Params {
   R KF, KM, M, GRAVITY_DYN, Jd[3], Jinv[3], L_SQRT2, HOVER_RPM, SPEED_LIMIT;
   R G_PID;  // BaseControl.GRAVITY = g*m (BaseControl.py:35)
   R DRAG[3], GND_COEFF, PROP_R, GND_CLIP, DW1, DW2, DW3, PROP_XY[4][2];
+  bool cf2p;       // DroneModel.CF2P: its torques (BA:852-853), inertia, props and mixer
+  R L;             // arm length (the CF2P torques)
+  R MIX[4][3];     // DSLPIDControl.MIXER_MATRIX (PID:48-60)
   R sp_R, sp_OMEGA, sp_VZ, sp_center[3];
   std::vector<R> orig_xyz;  // [D][3] ORIGINAL_INIT_XYZS (MH:78-79) / INIT_XYZS
 };
@@ -214,7 +222,7 @@ void dsl_pid_compute_control(const Params<R>& P, Drone<R>& d, const R cur_pos[3]
   for (int i = 0; i < 3; ++i)
     tq[i] = clip<R>(-R(P_TOR[i]) * rot_e[i] + R(D_TOR[i]) * rates_e[i] + R(I_TOR[i]) * d.int_rpy[i], R(-3200), R(3200));
   for (int m = 0; m < 4; ++m) {
-    R pwm = thrust + (R(MIXER[m][0]) * tq[0] + R(MIXER[m][1]) * tq[1] + R(MIXER[m][2]) * tq[2]);
+    R pwm = thrust + (P.MIX[m][0] * tq[0] + P.MIX[m][1] * tq[1] + P.MIX[m][2] * tq[2]);
     pwm = clip<R>(pwm, R(MIN_PWM), R(MAX_PWM));
     rpm[m] = R(PWM2RPM_SCALE) * pwm + R(PWM2RPM_CONST);
   }
@@ -334,8 +342,14 @@ void dynamics(const Params<R>& P, Drone<R>& d, const R rpm[4], const Snap<R>* sn
   for (int i = 0; i < 3; ++i) fw[i] += fw_extra[i];
   R z_torque = ((-zt[0] + zt[1]) - zt[2]) + zt[3];
   // CF2X (BA:849-851)
-  R x_torque = -(((f[0] + f[1]) - f[2]) - f[3]) * P.L_SQRT2 + tx_extra;
-  R y_torque = (((-f[0] + f[1]) + f[2]) - f[3]) * P.L_SQRT2 + ty_extra;
+  R x_torque, y_torque;
+  if (P.cf2p) {   // BaseAviary.py:852-853
+    x_torque = (f[1] - f[3]) * P.L + tx_extra;
+    y_torque = (-f[0] + f[2]) * P.L + ty_extra;
+  } else {        // BaseAviary.py:849-850
+    x_torque = -(((f[0] + f[1]) - f[2]) - f[3]) * P.L_SQRT2 + tx_extra;
+    y_torque = (((-f[0] + f[1]) + f[2]) - f[3]) * P.L_SQRT2 + ty_extra;
+  }
   R w[3] = {d.rpy_rates[0], d.rpy_rates[1], d.rpy_rates[2]};
   R Jw[3] = {P.Jd[0] * w[0], P.Jd[1] * w[1], P.Jd[2] * w[2]};
   R wxJw[3];
@@ -950,8 +964,13 @@ template <class R> int make_params(const qs_spec* s, Params<R>& P) {
   P.dt = R(1.0 / s->pyb_freq); P.ctrl_dt = R(1.0 / s->ctrl_freq);
   P.ep_len_sec = R(s->episode_len_sec);
   P.KF = R(C.KF); P.KM = R(C.KM); P.M = R(C.M); P.GRAVITY_DYN = R(C.GRAVITY);
-  P.Jd[0] = R(C.IXX); P.Jd[1] = R(C.IYY); P.Jd[2] = R(C.IZZ);
-  P.Jinv[0] = R(1.0 / C.IXX); P.Jinv[1] = R(1.0 / C.IYY); P.Jinv[2] = R(1.0 / C.IZZ);
+  P.cf2p = (s->flags & QS_FLAG_CF2P) != 0;
+  const double IX = P.cf2p ? C.IXX_P : C.IXX, IY = P.cf2p ? C.IYY_P : C.IYY, IZ = P.cf2p ? C.IZZ_P : C.IZZ;
+  P.Jd[0] = R(IX); P.Jd[1] = R(IY); P.Jd[2] = R(IZ);
+  P.Jinv[0] = R(1.0 / IX); P.Jinv[1] = R(1.0 / IY); P.Jinv[2] = R(1.0 / IZ);
+  P.L = R(C.L);
+  for (int m = 0; m < 4; ++m)
+    for (int k = 0; k < 3; ++k) P.MIX[m][k] = R(P.cf2p ? MIXER_P[m][k] : MIXER[m][k]);
   P.L_SQRT2 = R(C.L / std::sqrt(2.0));
   P.HOVER_RPM = R(C.HOVER_RPM);
   P.SPEED_LIMIT = R(0.03 * C.MAX_SPEED_KMH * (1000.0 / 3600.0));    // BRL:94-95
@@ -959,7 +978,8 @@ template <class R> int make_params(const qs_spec* s, Params<R>& P) {
   P.DRAG[0] = R(C.DRAG_XY); P.DRAG[1] = R(C.DRAG_XY); P.DRAG[2] = R(C.DRAG_Z);
   P.GND_COEFF = R(C.GND_EFF_COEFF); P.PROP_R = R(C.PROP_RADIUS); P.GND_CLIP = R(C.GND_EFF_H_CLIP);
   P.DW1 = R(C.DW1); P.DW2 = R(C.DW2); P.DW3 = R(C.DW3);
-  for (int m = 0; m < 4; ++m) { P.PROP_XY[m][0] = R(C.PROP_XY[m][0]); P.PROP_XY[m][1] = R(C.PROP_XY[m][1]); }
+  for (int m = 0; m < 4; ++m)
+    for (int k = 0; k < 2; ++k) P.PROP_XY[m][k] = R(P.cf2p ? C.PROP_XY_P[m][k] : C.PROP_XY[m][k]);
   P.sp_R = R(s->spiral_radius); P.sp_OMEGA = R(2 * M_PI / s->spiral_period); P.sp_VZ = R(s->height_rate);
   for (int i = 0; i < 3; ++i) P.sp_center[i] = R(s->target_center[i]);
   P.orig_xyz.resize(P.D * 3);

@@ -94,7 +94,8 @@ def _p(a):
 
 def make_spec(task="multihover", num_envs=1, num_drones=2, act="rpm", aux=(), physics="dyn", ctrl_freq=None, pyb_freq=240,
               precision=8, env_offset=0, episode_len_sec=None, initial_xyzs=None, autoreset=True,
-              spiral_radius=0.4, spiral_period=10.0, height_rate=0.05, target_center=(0.0, 0.0, 0.0)):
+              spiral_radius=0.4, spiral_period=10.0, height_rate=0.05, target_center=(0.0, 0.0, 0.0),
+              drone_model="cf2x"):
     s = QsSpec()
     s.task = TASK[task]
     s.num_envs = num_envs
@@ -105,7 +106,7 @@ def make_spec(task="multihover", num_envs=1, num_drones=2, act="rpm", aux=(), ph
     s.pyb_freq = pyb_freq
     s.ctrl_freq = ctrl_freq if ctrl_freq is not None else (48 if task == "spiral" else 30)
     s.precision = precision
-    s.flags = 0 if autoreset else 1
+    s.flags = (0 if autoreset else 1) | {"cf2x": 0, "cf2p": 4}[str(getattr(drone_model, "value", drone_model))]   # QS_FLAG_CF2P
     s.env_offset = env_offset
     s.episode_len_sec = episode_len_sec if episode_len_sec is not None else (12.0 if task == "spiral" else 8.0)
     keep = None

@@ -3,6 +3,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -21,7 +23,7 @@ def test_quadswarm_exports_every_declared_symbol():
         assert hasattr(lib, n), n
     assert set(names) <= set(_lib.EXPORTS)
     lib.qs_abi_version.restype = ctypes.c_int
-    assert lib.qs_abi_version() == 3
+    assert lib.qs_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_create_rejects_bad_spec_without_gpu_work():
@@ -37,6 +39,21 @@ def test_create_rejects_bad_spec_without_gpu_work():
     spec.ctrl_freq, spec.num_drones = 30, 7                         # default layout, D >= 6
     assert lib.qs_create(ctypes.byref(spec), 0, ctypes.byref(h)) == -1
     assert b"D >= 6" in lib.qs_last_error()
+    spec.num_drones, spec.flags = 2, L.FLAG_CF2P << 1               # a flag this ABI does not define
+    assert lib.qs_create(ctypes.byref(spec), 0, ctypes.byref(h)) == -1
+    assert b"bad flags" in lib.qs_last_error()
+
+
+def test_drone_models():
+    """CF2X and CF2P are accepted (QS_FLAG_CF2P); RACE, which has no DSL PID
+    (DSLPIDControl.py:34-36), is refused before any device work."""
+    from gym_pybullet_drones_amd.envs.swarm import QuadSwarm
+    from gym_pybullet_drones_amd.utils.enums import DroneModel
+    with pytest.raises(NotImplementedError):
+        QuadSwarm(num_envs=1, num_drones=2, drone_model=DroneModel.RACE)
+    import qs_oracle
+    s, _ = qs_oracle.make_spec(drone_model=DroneModel.CF2P)
+    assert s.flags & 4 and not qs_oracle.make_spec(drone_model="cf2x")[0].flags & 4
 
 
 def test_oracle_exports():

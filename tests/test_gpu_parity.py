@@ -63,6 +63,16 @@ CONFIGS = {
     "flock_rpm_d3_pyb": dict(task="flock", num_drones=3, act="rpm", physics="pyb"),
     "meetup_vel_d4": dict(task="meetup", num_drones=4, act="vel"),
     "leader_onedpid_d3_pyb": dict(task="leaderfollower", num_drones=3, act="one_d_pid", physics="pyb"),
+    # DroneModel.CF2P (the + configuration: cf2p.urdf inertia and props, BA:852-853 torques,
+    # PID:54-60 mixer), DYN / PYB, with the force modes that read the prop positions
+    "cf2p_mh_onedpid_d4": dict(task="multihover", num_drones=4, act="one_d_pid", drone_model="cf2p"),
+    "cf2p_mh_rpm_d4": dict(task="multihover", num_drones=4, act="rpm", drone_model="cf2p"),
+    "cf2p_mh_gnd_drag_d4": dict(task="multihover", num_drones=4, act="one_d_pid", aux=("gnd", "drag", "dw"),
+                                drone_model="cf2p"),
+    "cf2p_mh_vel_d4_pyb": dict(task="multihover", num_drones=4, act="vel", physics="pyb", drone_model="cf2p"),
+    "cf2p_spiral_vel_d5": dict(task="spiral", num_drones=5, act="vel", drone_model="cf2p"),
+    "cf2p_pyb_gnd_drag_dw_d4": dict(task="multihover", num_drones=4, act="one_d_pid", physics="pyb",
+                                    aux=("gnd", "drag", "dw"), drone_model="cf2p"),
 }
 
 
@@ -158,6 +168,11 @@ FREE_HORIZON_FP32 = {
     "pyb_dw_d4": dict(pos=24, vel=24),
     "mh_gnd_drag_d4": dict(pos=7, vel=7, rew=8),
     "pyb_gnd_drag_dw_d4": dict(pos=7, vel=7, rew=8),
+    # CF2P (the exact-fp32 oracle's horizons, seed 11: scripts/free_hz.py's oracle subject)
+    "cf2p_mh_gnd_drag_d4": dict(pos=7, vel=7, rew=8),
+    "cf2p_mh_vel_d4_pyb": dict(pos=19, quat=14, vel=17),
+    "cf2p_spiral_vel_d5": dict(quat=28, rew=17),
+    "cf2p_pyb_gnd_drag_dw_d4": dict(pos=7, vel=7, rew=8),   # (reward: one step past the state, as below)
 }
 
 
